@@ -1,0 +1,204 @@
+"""Throughput bench: rendered 256^2 faces/s (SDF + ngp Generator), 1..8 GPUs.
+
+Workload (BASELINE.json configs[1], eval.py's 5000-image generation): per step
+one Generator forward -- mapping MLP -> fused HIP renderer (64^2 rays x 24
+samples, hash grid, FiLM-SIREN on fp32 MFMA, compositing) -> StyleGAN2
+decoder to 256^2 (PyTorch-ROCm, fp32) -- on a batch of B random latents with
+random cameras, random-init weights (pretrained weights are not available
+offline), decoder noise drawn per step as in eval.py.  PNG encoding is not
+timed.  One process per GPU (torchrun); faces shard across ranks with no
+data-path collective (weak scaling): value = all faces / max-over-ranks time.
+
+Also reported: the dominant kernel's roofline (the fused field kernel, fp32
+MFMA bound) from HIP events recorded on the renderer's stream around that
+kernel during the timed steps, the hash-grid gather kernel's HBM-roofline
+fraction, and a CPU baseline (the oracle renderer + PyTorch-CPU decoder) on
+the host cores for a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+METRIC = "rendered faces/sec/GPU at 256² (SDF+ngp path); 1/2/4/8-GPU scaling"
+FLOP_PER_SAMPLE = 550912          # renderer MLP, SURVEY.md §8(d) / BASELINE.md §2
+GATHER_BYTES_PER_SAMPLE = 1024    # 16 levels x 8 corners x 2 x fp32
+MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBPS = 8000.0            # MI355X HBM3E peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=32, help="faces per step per GPU")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--traffic-json", default=str(REPO / "profiles" / "field_traffic.json"))
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def build_generator(sdfr, device, seed):
+    opt = sdfr.vol_render_opt(ngp=True)
+    torch.manual_seed(seed)
+    g = sdfr.Generator(opt.model, opt.rendering).to(device)
+    g.eval()
+    # per-ray sampling offsets from the device RNG (no host round trip per step)
+    g.renderer.rng_device = "device"
+    return g, opt
+
+
+def cpu_baseline(seconds):
+    """Oracle renderer (torch-CPU fp32 + C encoders) + PyTorch-CPU decoder, one face
+    per call as eval.py does, on the host cores; bounded to ~`seconds`."""
+    from oracle import oracle
+    from sdfr_loader import load
+    sdfr = load()
+    oracle.build()
+    opt = sdfr.vol_render_opt(ngp=True)
+    torch.manual_seed(1)
+    g = sdfr.Generator(opt.model, opt.rendering).eval()
+    sd = {k: v for k, v in g.state_dict().items() if k.startswith("renderer.")}
+    faces, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            z = torch.randn(1, 256)
+            cam, focal, near, far, _ = sdfr.generate_camera_params(64, "cpu", batch=1)
+            lat = g.style(z)
+            out = oracle.render_ngp(sd, cam.numpy(), focal.numpy(), near.numpy(), far.numpy(),
+                                    lat.numpy(), N=24, res=64, t_rand=torch.rand(1, 64, 64).numpy())
+            img, _ = g.decoder(out["features"], [lat])
+            faces += 1
+            el = time.perf_counter() - t0
+            if el >= seconds and faces >= 2:
+                break
+    return {"value": faces / el, "unit": "faces/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{faces} faces (64^2x24 oracle renderer + CPU decoder to 256^2), "
+                      f"1 face per call, {el:.1f}s"}
+
+
+def main():
+    args = parse()
+    world, rank, device = setup_dist(args)
+    from sdfr_loader import load
+    sdfr = load()
+    g, opt = build_generator(sdfr, device, args.seed)
+    B = args.batch
+    res = opt.model.renderer_spatial_output_dim
+    N = opt.rendering.N_samples
+    gen = torch.Generator(device=device)
+    gen.manual_seed(1000 + rank)
+
+    def step():
+        z = torch.randn(B, opt.model.style_dim, device=device, generator=gen)
+        cam, focal, near, far, _ = sdfr.generate_camera_params(
+            res, device, batch=B, azim_range=opt.camera.azim, elev_range=opt.camera.elev,
+            fov_ang=opt.camera.fov, dist_radius=opt.camera.dist_radius)
+        with torch.no_grad():
+            rgb, thumb = g([z], cam, focal, near, far, truncation=1, truncation_latent=None)
+        return rgb
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-step stage events on the renderer's stream
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    for e4 in evs:
+        for e in e4:
+            e.record()              # materialise the event handles before the timed loop
+    torch.cuda.synchronize()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        g.renderer.stage_events = evs[k]
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    g.renderer.stage_events = None
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    enc_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    field_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
+    render_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args.steps
+    samples = B * res * res * N
+    field_tflops = FLOP_PER_SAMPLE * samples / (field_ms * 1e-3) / 1e12
+    gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9
+    traffic = None
+    tj = Path(args.traffic_json)
+    if tj.exists():
+        try:
+            traffic = json.loads(tj.read_text()).get("bytes_per_launch_per_face")
+            traffic = None if traffic is None else traffic * B
+        except Exception:
+            traffic = None
+
+    faces = world * B * args.steps
+    line = {
+        "metric": METRIC,
+        "value": faces / elapsed,
+        "unit": "faces/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (random z, random cameras, random-init weights)",
+        "config": {"workload": "eval.py 5000-image generation (ffhq_256_sdf_ngp, configs[1])",
+                   "faces_per_step_per_gpu": B, "renderer": f"{res}x{res} rays x {N} samples",
+                   "output": "256x256 RGB", "parallelism": f"dp{world} (independent faces)"},
+        "roofline": {"kernel": "ngp_field_kernel (MLP on v_mfma_f32_16x16x4_f32 + compositing)",
+                     "bound": "mfma", "achieved": field_tflops, "peak": MFMA_F32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": field_tflops / MFMA_F32_PEAK_TFLOPS,
+                     "traffic": traffic},
+        "roofline_gather": {"kernel": "ngp_encode_kernel (sampling + 16-level hash-grid gather)",
+                            "bound": "hbm", "achieved": gather_gbps, "peak": HBM_PEAK_GBPS,
+                            "unit": "GB/s", "frac": gather_gbps / HBM_PEAK_GBPS},
+        "stage_ms_per_step": {"renderer_total": render_ms, "hash_grid": enc_ms,
+                              "field": field_ms},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,23 @@
+"""sdface-gan_amd: MI355X-native SDF + hash-grid renderer for SDFace-GAN.
+
+Import name: ``sdface_gan_amd`` (see ``sdfr_loader.py`` at the repository root;
+the directory name is not a valid Python identifier).
+
+Drop-in surface (reference: im2scene/sdf/models/):
+  Generator, VolumeFeatureRenderer, NGPSIRENGenerator, SirenGenerator,
+  FCGenerator, LinearLayer, FiLMSiren, get_encoder      (sdf_model.py)
+  GridEncoder, grid_encode                              (gridencoder/grid.py)
+  SHEncoder, sh_encode                                  (shencoder/sphere_harmonics.py)
+  generate_camera_params                                (sdf_utils.py:97-159)
+  SDFOptions, vol_render_opt                            (sdf_utils.py:447, training_utils.py:144)
+"""
+from . import _lib  # noqa: F401
+from .camera import generate_camera_params  # noqa: F401
+from .encoders import GridEncoder, SHEncoder, grid_encode, sh_encode  # noqa: F401
+from .generator import (Decoder, EqualLinear, FusedLeakyReLU, Generator,  # noqa: F401
+                        MappingLinear, ModulatedConv2d, fused_leaky_relu, upfirdn2d)
+from .options import AttrDict, SDFOptions, vol_render_opt  # noqa: F401
+from .renderer import (FCGenerator, FiLMSiren, LinearLayer, NGPSIRENGenerator,  # noqa: F401
+                       SirenGenerator, VolumeFeatureRenderer, get_encoder)
+
+__version__ = "0.1.0"

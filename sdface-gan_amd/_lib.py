@@ -1,0 +1,114 @@
+"""ctypes binding of libsdfr.so (the C ABI declared in include/sdfr.h).
+
+The library is built in-tree by ``make -C sdface-gan_amd`` (or
+``__graft_entry__.build()``) into ``sdface-gan_amd/lib/libsdfr.so``.  There is
+no fallback: if the library is missing or a call fails, a RuntimeError is
+raised naming the entry point and the library's own message.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("SDFR_LIB", PKG_DIR / "lib" / "libsdfr.so"))
+
+_vp = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_f32 = ctypes.c_float
+_int = ctypes.c_int
+
+SDFR_OK = 0
+SDFR_EINVAL = -1
+SDFR_ELAUNCH = -2
+SDFR_EUNSUPPORTED = -3
+ABI_VERSION = 1
+
+# every symbol include/sdfr.h declares (tests check the .so exports all of them)
+EXPORTS = (
+    "sdfr_abi_version", "sdfr_last_error",
+    "sdfr_grid_encode_forward", "sdfr_grid_encode_backward",
+    "sdfr_sh_encode_forward", "sdfr_sh_encode_backward",
+    "sdfr_render_ngp_workspace_bytes", "sdfr_render_ngp_forward",
+    "sdfr_render_ngp_encode_only",
+)
+
+
+class NgpWeights(ctypes.Structure):
+    """sdfr_ngp_weights (include/sdfr.h)."""
+    _fields_ = [
+        ("embeddings", _vp), ("offsets", _vp), ("num_levels", _u32),
+        ("log2_per_level_scale", _f32), ("base_resolution", _u32), ("bound", _f32),
+        ("input_w", _vp), ("input_b", _vp),
+        ("pts_w", _vp * 3), ("pts_b", _vp * 3), ("pts_gw", _vp * 3), ("pts_gb", _vp * 3),
+        ("pts_bw", _vp * 3), ("pts_bb", _vp * 3),
+        ("views_w", _vp), ("views_b", _vp),
+        ("views_gw", _vp), ("views_gb", _vp), ("views_bw", _vp), ("views_bb", _vp),
+        ("sigma_w", _vp), ("sigma_b", _vp), ("rgb_w", _vp), ("rgb_b", _vp),
+        ("sigmoid_beta", _vp),
+    ]
+
+
+class NgpRenderArgs(ctypes.Structure):
+    """sdfr_ngp_render_args (include/sdfr.h)."""
+    _fields_ = [
+        ("B", _u32), ("H", _u32), ("W", _u32), ("N", _u32),
+        ("cam", _vp), ("focal", _vp), ("near_", _vp), ("far_", _vp), ("styles", _vp),
+        ("pix_x", _vp), ("pix_y", _vp), ("t_vals", _vp), ("t_rand", _vp), ("sigma_noise", _vp),
+        ("t_rand_per_sample", _int), ("offset_sampling", _int), ("static_viewdirs", _int),
+        ("z_normalize", _int), ("force_background", _int), ("with_sdf", _int),
+        ("rgb", _vp), ("features", _vp), ("sdf", _vp), ("xyz", _vp), ("mask", _vp),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+        ("stage_events", _vp * 4),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    """Load libsdfr.so once; raise if it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(
+            f"sdface-gan_amd: HIP library {LIB_PATH} is missing; build it with "
+            "`make -C sdface-gan_amd` or `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(str(LIB_PATH))
+    L.sdfr_abi_version.restype = _int
+    L.sdfr_last_error.restype = ctypes.c_char_p
+    L.sdfr_grid_encode_forward.argtypes = [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _f32,
+                                           _u32, _vp, _u32, _int, _u32, _vp]
+    L.sdfr_grid_encode_backward.argtypes = [_vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32,
+                                            _f32, _u32, _vp, _vp, _u32, _int, _u32, _vp]
+    L.sdfr_sh_encode_forward.argtypes = [_vp, _vp, _u32, _u32, _u32, _vp, _vp]
+    L.sdfr_sh_encode_backward.argtypes = [_vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp]
+    L.sdfr_render_ngp_workspace_bytes.restype = ctypes.c_size_t
+    L.sdfr_render_ngp_workspace_bytes.argtypes = [_u32, _u32, _u32, _u32, _u32]
+    L.sdfr_render_ngp_forward.argtypes = [ctypes.POINTER(NgpWeights),
+                                          ctypes.POINTER(NgpRenderArgs), _vp]
+    L.sdfr_render_ngp_encode_only.argtypes = [ctypes.POINTER(NgpWeights),
+                                              ctypes.POINTER(NgpRenderArgs), _vp]
+    v = L.sdfr_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"libsdfr ABI {v} != expected {ABI_VERSION}; rebuild the library")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != SDFR_OK:
+        msg = lib().sdfr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)

@@ -1,0 +1,65 @@
+"""Camera sampling for the renderer: generate_camera_params (sdf_utils.py:97-159).
+
+Pure PyTorch on the caller's device, same argument meaning, same random draws
+(torch.randn / torch.rand on ``device``) and the same op order, so results are
+identical to the reference on the same device and seed.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def generate_camera_params(resolution, device, batch=1, locations=None, sweep=False,
+                           uniform=False, azim_range=0.3, elev_range=0.15, fov_ang=6,
+                           dist_radius=0.12):
+    """Returns (extrinsics [B,3,4] = [R^T | T], focal [B,1,1], near [B,1,1],
+    far [B,1,1], viewpoint [B,2] = (azim, elev))."""
+    if locations is not None:
+        azim = locations[:, 0].view(-1, 1)
+        elev = locations[:, 1].view(-1, 1)
+        dist = torch.ones(azim.shape[0], 1, device=device)
+        near, far = (dist - dist_radius).unsqueeze(-1), (dist + dist_radius).unsqueeze(-1)
+        fov = fov_ang * torch.ones(azim.shape[0], 1, device=device).view(-1, 1) * np.pi / 180
+        focal = 0.5 * resolution / torch.tan(fov).unsqueeze(-1)
+    elif sweep:
+        azim = (-azim_range + (2 * azim_range / 7) * torch.arange(8, device=device))
+        azim = azim.view(-1, 1).repeat(batch, 1)
+        elev = (-elev_range + 2 * elev_range *
+                torch.rand(batch, 1, device=device).repeat(1, 8).view(-1, 1))
+        dist = torch.ones(batch, 1, device=device).repeat(1, 8).view(-1, 1)
+        near, far = (dist - dist_radius).unsqueeze(-1), (dist + dist_radius).unsqueeze(-1)
+        fov = fov_ang * torch.ones(batch, 1, device=device).repeat(1, 8).view(-1, 1) * np.pi / 180
+        focal = 0.5 * resolution / torch.tan(fov).unsqueeze(-1)
+    else:
+        if uniform:
+            azim = -azim_range + 2 * azim_range * torch.rand(batch, 1, device=device)
+            elev = -elev_range + 2 * elev_range * torch.rand(batch, 1, device=device)
+        else:
+            azim = azim_range * torch.randn(batch, 1, device=device)
+            elev = elev_range * torch.randn(batch, 1, device=device)
+        dist = torch.ones(batch, 1, device=device)
+        near, far = (dist - dist_radius).unsqueeze(-1), (dist + dist_radius).unsqueeze(-1)
+        fov = fov_ang * torch.ones(batch, 1, device=device) * np.pi / 180
+        focal = 0.5 * resolution / torch.tan(fov).unsqueeze(-1)
+
+    viewpoint = torch.cat([azim, elev], 1)
+    x = torch.cos(elev) * torch.sin(azim)
+    y = torch.sin(elev)
+    z = torch.cos(elev) * torch.cos(azim)
+    camera_dir = torch.stack([x, y, z], dim=1).view(-1, 3)
+    camera_loc = dist * camera_dir
+
+    up = torch.tensor([[0, 1, 0]]).float().to(device) * torch.ones_like(dist)
+    z_axis = F.normalize(camera_dir, eps=1e-5)
+    x_axis = F.normalize(torch.cross(up, z_axis, dim=1), eps=1e-5)
+    y_axis = F.normalize(torch.cross(z_axis, x_axis, dim=1), eps=1e-5)
+    is_close = torch.isclose(x_axis, torch.tensor(0.0), atol=5e-3).all(dim=1, keepdim=True)
+    if is_close.any():
+        repl = F.normalize(torch.cross(y_axis, z_axis, dim=1), eps=1e-5)
+        x_axis = torch.where(is_close, repl, x_axis)
+    R = torch.cat((x_axis[:, None, :], y_axis[:, None, :], z_axis[:, None, :]), dim=1)
+    T = camera_loc[:, :, None]
+    extrinsics = torch.cat((R.transpose(1, 2), T), -1)
+    return extrinsics, focal, near, far, viewpoint

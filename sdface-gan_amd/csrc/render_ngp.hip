@@ -1,0 +1,700 @@
+// render_ngp.hip -- fused SDF + hash-grid volume renderer for MI355X (gfx950).
+//
+// Replaces VolumeFeatureRenderer.forward for rendering.type == "ngp"
+// (sdf_model.py:411-423 -> render :363 -> render_rays :310 ->
+// NGPSIRENGenerator.forward :1566 -> volume_integration :236) with three
+// launches on one stream:
+//
+//  1. ngp_prep_kernel   per-face FiLM gamma/beta (4 layers x 256, from the
+//                       renderer latent) and the MFMA-fragment packing of the
+//                       five dense weight matrices (1.07 MB, read once per call).
+//  2. ngp_encode_kernel ray generation + sampling (bit-exact vs. the reference
+//                       float chain) and the 16-level hash-grid gather, one
+//                       (sample, level) per thread, level-major grid so each
+//                       level's <= 4 MiB table stays in every XCD's L2.
+//                       Output [L][S][2] fp32 in "tile order" (16 rays of one
+//                       sample contiguous), exactly what stage 3 reads.
+//  3. ngp_field_kernel  the whole MLP on fp32 MFMA (v_mfma_f32_16x16x4_f32) +
+//                       SDF->density + front-to-back alpha compositing.  A wave
+//                       owns 16 rays and marches their samples in order; the
+//                       MFMA N dimension is the ray, so every per-ray quantity
+//                       (transmittance, colour/feature accumulators) is a
+//                       per-lane register and compositing needs no cross-lane
+//                       traffic.  Activations never leave registers: the
+//                       accumulator tile of layer l is, element for element,
+//                       the B operand of layer l+1 (K permuted consistently in
+//                       the packed weights).  Weights stream through a 3-slot
+//                       LDS ring (16 KB K-slices) shared by the 8 waves of the
+//                       workgroup; the [S,260] raw tensor the reference
+//                       materialises is never formed.
+//
+// Numerics: fp32 everywhere; MFMA f32 is an exact fmaf chain, so results
+// differ from the reference only by summation order (tolerances in
+// tests/test_gpu_render.py).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "sdfr_common.h"
+
+namespace sdfr {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t kW = 256;          // NGPSIRENGenerator width
+constexpr uint32_t kFeatIn = 32;      // 16 levels x 2
+constexpr uint32_t kViewsIn = 272;    // 256 + 16 SH
+constexpr uint32_t kSliceF4 = 1024;   // float4 per 16-wide K slice (16 t_out x 64 lanes)
+constexpr uint32_t kSlices = 2 + 16 * 3 + 17;   // 67 slices per sample step
+constexpr uint32_t kFilm = 4;         // FiLM layers: pts 0,1,2 + views
+constexpr uint32_t kTileRays = 16;    // rays per wave (MFMA N)
+
+// slice index -> (layer, t_in)
+__host__ __device__ constexpr uint32_t slice_base(uint32_t layer) {
+    return layer == 0 ? 0u : (layer == 4 ? 50u : 2u + 16u * (layer - 1));
+}
+
+// ----------------------------------------------------------------------------
+// 1. prep: FiLM vectors + packed weights
+// ----------------------------------------------------------------------------
+struct PrepArgs {
+    const float *styles;           // [B,256]
+    const float *gw[kFilm], *gb[kFilm], *bw[kFilm], *bb[kFilm];
+    const float *w[5];             // layer weights, row-major [256, K]
+    uint32_t K[5];
+    float *film;                   // [B][4][2][256]
+    f4 *packed;                    // [67][16][64]
+    uint32_t B;
+};
+
+// blocks [0, B*4*2): film rows (256 threads = 256 outputs)
+// blocks [B*8, B*8 + 67*4): packing, 256 float4 per block
+__global__ void __launch_bounds__(256) ngp_prep_kernel(const PrepArgs a) {
+    const uint32_t blk = blockIdx.x, j = threadIdx.x;
+    const uint32_t nfilm = a.B * kFilm * 2;
+    if (blk < nfilm) {
+        const uint32_t b = blk / (kFilm * 2), rem = blk % (kFilm * 2);
+        const uint32_t layer = rem >> 1, which = rem & 1;
+        const float *W = which ? a.bw[layer] : a.gw[layer];
+        const float *bias = which ? a.bb[layer] : a.gb[layer];
+        const float *st = a.styles + (size_t)b * kW;
+        const f4 *wr = reinterpret_cast<const f4 *>(W + (size_t)j * kW);
+        const f4 *sr = reinterpret_cast<const f4 *>(st);
+        float acc = 0.0f;
+#pragma unroll 8
+        for (uint32_t k = 0; k < kW / 4; ++k) {
+            const f4 w4 = wr[k], s4 = sr[k];
+            acc = __fmaf_rn(s4.x, w4.x, acc);
+            acc = __fmaf_rn(s4.y, w4.y, acc);
+            acc = __fmaf_rn(s4.z, w4.z, acc);
+            acc = __fmaf_rn(s4.w, w4.w, acc);
+        }
+        const float lin = __fadd_rn(acc, bias[j]);
+        // LinearLayer: std_init * linear + bias_init (sdf_model.py:39, 58-59)
+        const float v = which ? __fadd_rn(__fmul_rn(0.25f, lin), 0.0f)
+                              : __fadd_rn(__fmul_rn(15.0f, lin), 30.0f);
+        a.film[(((size_t)b * kFilm + layer) * 2 + which) * kW + j] = v;
+        return;
+    }
+    // packing: element (slice, t_out, lane) = W[16 t_out + (lane&15)][16 t_in + 4 (lane>>4) + r]
+    const uint32_t e = (blk - nfilm) * 256 + j;
+    if (e >= kSlices * kSliceF4) return;
+    const uint32_t slice = e / kSliceF4, rem = e % kSliceF4;
+    const uint32_t t_out = rem >> 6, lane = rem & 63;
+    uint32_t layer = 0;
+    if (slice >= 50) layer = 4;
+    else if (slice >= 2) layer = 1 + (slice - 2) / 16;
+    const uint32_t t_in = slice - slice_base(layer);
+    const uint32_t row = 16 * t_out + (lane & 15);
+    const uint32_t col = 16 * t_in + 4 * (lane >> 4);
+    const float *src = a.w[layer] + (size_t)row * a.K[layer] + col;
+    f4 v;
+    v.x = src[0]; v.y = src[1]; v.z = src[2]; v.w = src[3];
+    a.packed[e] = v;
+}
+
+// ----------------------------------------------------------------------------
+// shared ray / sample geometry
+// ----------------------------------------------------------------------------
+struct GeomArgs {
+    uint32_t B, H, W, N, tiles_per_face, total_tiles, S_total;
+    float half_res;
+    const float *cam, *focal, *near_, *far_, *pix_x, *pix_y;
+    SampleCfg sc;
+    int static_viewdirs, z_normalize;
+    float bound;
+};
+
+// tile-order sample id -> (face, ray-in-face, sample)
+struct SampleId {
+    uint32_t b, ray_local, s, n, tile;
+    bool valid;
+};
+
+__device__ __forceinline__ SampleId decode_sid(const GeomArgs &g, uint32_t sid) {
+    SampleId r;
+    r.n = sid & 15u;
+    const uint32_t rest = sid >> 4;
+    r.s = rest % g.N;
+    r.tile = rest / g.N;
+    r.b = r.tile / g.tiles_per_face;
+    r.ray_local = (r.tile % g.tiles_per_face) * kTileRays + r.n;
+    r.valid = r.tile < g.total_tiles && r.ray_local < g.H * g.W;
+    return r;
+}
+
+// ----------------------------------------------------------------------------
+// 2. encode: sampling + hash-grid gather
+// ----------------------------------------------------------------------------
+struct EncodeArgs {
+    GeomArgs g;
+    const float *emb;
+    const int32_t *offsets;
+    float *enc;                    // [L][S_total][2]
+    LevelTable lt;
+};
+
+__global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
+    const uint32_t sid = blockIdx.x * 256 + threadIdx.x;
+    if (sid >= a.g.S_total) return;
+    const uint32_t level = blockIdx.y;
+    LevelParam q = a.lt.p[level];
+    finish_level(q, a.offsets, level, 3, 0, 0);
+    float2 *out = reinterpret_cast<float2 *>(a.enc) + (size_t)level * a.g.S_total + sid;
+
+    const SampleId id = decode_sid(a.g, sid);
+    if (!id.valid) {
+        *out = make_float2(0.0f, 0.0f);
+        return;
+    }
+    const uint32_t y = id.ray_local / a.g.W, x = id.ray_local % a.g.W;
+    const uint32_t ray_index = (id.b * a.g.H + y) * a.g.W + x;
+    Ray ray;
+    make_ray(a.g.cam + (size_t)id.b * 12, a.g.focal[id.b], a.g.pix_x[x], a.g.pix_y[y],
+             a.g.half_res, ray);
+    const float nr = a.g.near_[id.b], fr = a.g.far_[id.b];
+    const float z = sample_z(a.g.sc, nr, fr, ray_index, id.s);
+    const float span = __fsub_rn(fr, nr);
+    float u[3];
+    bool oob = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));            // :343
+        const float np_ = a.g.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;  // :349
+        u[k] = __fdiv_rn(__fadd_rn(np_, a.g.bound), __fmul_rn(2.0f, a.g.bound));   // grid.py:149
+        if (u[k] < 0 || u[k] > 1) oob = true;
+    }
+    if (oob) {
+        *out = make_float2(0.0f, 0.0f);
+        return;
+    }
+    const float *grid = a.emb + (size_t)q.offset * 2;
+    LevelCoord<3, 2> lc;
+    level_coord<3, 2>(u, q, 0, 0, lc);
+    float res[2];
+    level_interp<3, 2>(grid, q, 0, lc, res);
+    *out = make_float2(res[0], res[1]);
+}
+
+// ----------------------------------------------------------------------------
+// 3. field: MLP on MFMA + compositing
+// ----------------------------------------------------------------------------
+struct FieldArgs {
+    GeomArgs g;
+    const float *enc;              // [L=16][S_total][2]
+    const f4 *packed;              // [67][1024]
+    const float *film;             // [B][4][2][256]
+    const float *bias[5];          // input, pts0..2, views
+    const float *sigma_w, *sigma_b, *rgb_w, *rgb_b, *sigmoid_beta;
+    const float *sigma_noise;      // [B,H,W,N] or null (no_sdf only)
+    int force_background, with_sdf;
+    float *rgb, *features, *sdf, *xyz, *mask;
+};
+
+constexpr int kWaves = 4;                       // 1 wave per SIMD, 512 VGPR+AGPR
+constexpr int kThreads = kWaves * 64;
+constexpr int kStageF4 = kSliceF4 / kThreads;   // float4 staged per thread per slice
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Branch-free sinf for |x| < 2^12 (FiLM arguments are O(100)): Cody-Waite
+// reduction by pi/2 with fma (3-part constant), minimax sin/cos on
+// [-pi/4, pi/4] (Cephes coefficients), quadrant select.  Max error ~1e-7
+// absolute; straight-line code so the compiler can interleave it with MFMA.
+__device__ __forceinline__ float sin_cw(float x) {
+    const float kf = __builtin_rintf(x * 0.636619772367581343f);
+    const int q = (int)kf;
+    float r = __fmaf_rn(-kf, 1.57079637050628662109375f, x);
+    r = __fmaf_rn(-kf, -4.37113900018624283e-8f, r);
+    r = __fmaf_rn(-kf, -1.71512451000597797e-15f, r);
+    const float r2 = r * r;
+    float ps = __fmaf_rn(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+    ps = __fmaf_rn(r2, ps, -1.6666654611e-1f);
+    const float sn = __fmaf_rn(r * r2, ps, r);
+    float pc = __fmaf_rn(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    pc = __fmaf_rn(r2, pc, 4.166664568298827e-2f);
+    const float cs = __fmaf_rn(r2 * r2, pc, __fmaf_rn(-0.5f, r2, 1.0f));
+    const float v = (q & 1) ? cs : sn;
+    return (q & 2) ? -v : v;
+}
+
+// SH degree 4 coefficients 4g..4g+3 of a unit direction (shencoder.cu:50-68)
+__device__ __forceinline__ f4 sh_quad(float x, float y, float z, uint32_t g) {
+    const float xy = __fmul_rn(x, y), xz = __fmul_rn(x, z), yz = __fmul_rn(y, z);
+    const float x2 = __fmul_rn(x, x), y2 = __fmul_rn(y, y), z2 = __fmul_rn(z, z);
+    f4 q0, q1, q2, q3;
+    q0.x = 0.28209479177387814f;
+    q0.y = __fmul_rn(-0.48860251190291987f, y);
+    q0.z = __fmul_rn(0.48860251190291987f, z);
+    q0.w = __fmul_rn(-0.48860251190291987f, x);
+    q1.x = __fmul_rn(1.0925484305920792f, xy);
+    q1.y = __fmul_rn(-1.0925484305920792f, yz);
+    q1.z = __fmaf_rn(0.94617469575755997f, z2, -0.31539156525251999f);
+    q1.w = __fmul_rn(-1.0925484305920792f, xz);
+    q2.x = __fmaf_rn(0.54627421529603959f, x2, -__fmul_rn(0.54627421529603959f, y2));
+    q2.y = __fmul_rn(__fmul_rn(0.59004358992664352f, y), __fmaf_rn(-3.0f, x2, y2));
+    q2.z = __fmul_rn(__fmul_rn(2.8906114426405538f, xy), z);
+    q2.w = __fmul_rn(__fmul_rn(0.45704579946446572f, y), __fmaf_rn(-5.0f, z2, 1.0f));
+    q3.x = __fmul_rn(__fmul_rn(0.3731763325901154f, z), __fmaf_rn(5.0f, z2, -3.0f));
+    q3.y = __fmul_rn(__fmul_rn(0.45704579946446572f, x), __fmaf_rn(-5.0f, z2, 1.0f));
+    q3.z = __fmul_rn(__fmul_rn(1.4453057213202769f, z), __fsub_rn(x2, y2));
+    q3.w = __fmul_rn(__fmul_rn(0.59004358992664352f, x), __fmaf_rn(3.0f, y2, -x2));
+    return g == 0 ? q0 : (g == 1 ? q1 : (g == 2 ? q2 : q3));
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// Streaming state for the weight ring: slot s of `lds` holds one K-slice.
+struct Ring {
+    f4 *lds;              // [3][kSliceF4]
+    const f4 *packed;
+    f4 st[kStageF4];      // staged next slice (global -> regs -> LDS)
+    uint32_t it;          // global slice iteration
+    uint32_t tid;
+};
+
+// One K-slice: stage slice it+1 into LDS, prefetch slice it+2, run the
+// 16 t_out x 4 MFMAs of slice `it` against the B operand quad, barrier.
+// A-operand quads are read four output tiles at a time, one group ahead,
+// and the four accumulators of a group are interleaved so no MFMA waits on
+// its predecessor (16x16x4 f32: 32-cycle issue, 40-cycle dependency).
+__device__ __forceinline__ void ring_step(Ring &R, f4 (&acc)[16], const f4 bq) {
+    const uint32_t cur = R.it % 3u, nxt = (R.it + 1u) % 3u;
+#pragma unroll
+    for (int i = 0; i < kStageF4; ++i) R.lds[nxt * kSliceF4 + R.tid + i * kThreads] = R.st[i];
+    const uint32_t pf = (R.it + 2u) % kSlices;
+#pragma unroll
+    for (int i = 0; i < kStageF4; ++i) R.st[i] = R.packed[pf * kSliceF4 + R.tid + i * kThreads];
+    const f4 *A = R.lds + cur * kSliceF4 + (R.tid & 63u);
+    f4 a[4], an[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = A[i * 64];
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+        if (grp < 3) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) an[i] = A[(4 * grp + 4 + i) * 64];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[4 * grp + i] = mfma4(a[i].x, bq.x, acc[4 * grp + i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[4 * grp + i] = mfma4(a[i].y, bq.y, acc[4 * grp + i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[4 * grp + i] = mfma4(a[i].z, bq.z, acc[4 * grp + i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[4 * grp + i] = mfma4(a[i].w, bq.w, acc[4 * grp + i]);
+        if (grp < 3) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = an[i];
+        }
+    }
+    __syncthreads();
+    ++R.it;
+}
+
+__device__ __forceinline__ void init_bias(f4 (&acc)[16], const float *bias, uint32_t g) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = *reinterpret_cast<const f4 *>(bias + 16 * t + 4 * g);
+}
+
+// sin(gamma * out + beta) with the reference's two roundings (sdf_model.py:67)
+__device__ __forceinline__ void film_act(f4 (&act)[16], const f4 (&acc)[16],
+                                         const float *gam, const float *bet, uint32_t g) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const f4 gm = *reinterpret_cast<const f4 *>(gam + 16 * t + 4 * g);
+        const f4 bt = *reinterpret_cast<const f4 *>(bet + 16 * t + 4 * g);
+        f4 v;
+        v.x = sin_cw(__fadd_rn(__fmul_rn(gm.x, acc[t].x), bt.x));
+        v.y = sin_cw(__fadd_rn(__fmul_rn(gm.y, acc[t].y), bt.y));
+        v.z = sin_cw(__fadd_rn(__fmul_rn(gm.z, acc[t].z), bt.z));
+        v.w = sin_cw(__fadd_rn(__fmul_rn(gm.w, acc[t].w), bt.w));
+        act[t] = v;
+    }
+}
+
+// sum over the 4 lane groups holding the same ray (lanes n, n+16, n+32, n+48)
+__device__ __forceinline__ float group_sum(float v) {
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+
+__device__ __forceinline__ float dot_feat(const f4 (&act)[16], const float *w, uint32_t g) {
+    float p = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const f4 wv = *reinterpret_cast<const f4 *>(w + 16 * t + 4 * g);
+        p = __fmaf_rn(act[t].x, wv.x, p);
+        p = __fmaf_rn(act[t].y, wv.y, p);
+        p = __fmaf_rn(act[t].z, wv.z, p);
+        p = __fmaf_rn(act[t].w, wv.w, p);
+    }
+    return group_sum(p);
+}
+
+__global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs a) {
+    __shared__ f4 ring_lds[3 * kSliceF4];   // 48 KB
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t n = lane & 15u, g = lane >> 4;
+    const GeomArgs &G = a.g;
+
+    uint32_t tile = blockIdx.x * kWaves + wave;
+    const bool tile_ok = tile < G.total_tiles;
+    if (!tile_ok) tile = G.total_tiles - 1;
+    const uint32_t b = tile / G.tiles_per_face;
+    uint32_t ray_local = (tile % G.tiles_per_face) * kTileRays + n;
+    const bool ray_ok = tile_ok && ray_local < G.H * G.W;
+    if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
+    const uint32_t py = ray_local / G.W, px = ray_local % G.W;
+    const uint32_t ray_index = (b * G.H + py) * G.W + px;
+
+    Ray ray;
+    make_ray(G.cam + (size_t)b * 12, G.focal[b], G.pix_x[px], G.pix_y[py], G.half_res, ray);
+    const float nr = G.near_[b], fr = G.far_[b];
+    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
+    f4 shq;
+    {
+        const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
+        const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
+        const float v2 = G.static_viewdirs ? ray.dir[2] : ray.d[2];
+        const float vn = norm3_torch(v0, v1, v2);
+        shq = sh_quad(__fdiv_rn(v0, vn), __fdiv_rn(v1, vn), __fdiv_rn(v2, vn), g);
+    }
+    const float beta_s = a.sigmoid_beta[0];
+    const float *film = a.film + (size_t)b * kFilm * 2 * kW;
+
+    Ring R;
+    R.lds = ring_lds;
+    R.packed = a.packed;
+    R.tid = tid;
+    R.it = 0;
+    // prologue: slice 0 -> slot 0, slice 1 -> regs
+#pragma unroll
+    for (int i = 0; i < kStageF4; ++i) R.lds[tid + i * kThreads] = a.packed[tid + i * kThreads];
+#pragma unroll
+    for (int i = 0; i < kStageF4; ++i) R.st[i] = a.packed[kSliceF4 + tid + i * kThreads];
+    __syncthreads();
+
+    f4 facc[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) facc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
+    float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
+
+    const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
+    float z = sample_z(G.sc, nr, fr, ray_index, 0);
+
+    for (uint32_t s = 0; s < G.N; ++s) {
+        const uint32_t sid = (tile * G.N + s) * kTileRays + n;
+        const float2 e0 = enc2[(size_t)(2 * g) * G.S_total + sid];
+        const float2 e1 = enc2[(size_t)(2 * g + 1) * G.S_total + sid];
+        const float2 e2 = enc2[(size_t)(8 + 2 * g) * G.S_total + sid];
+        const float2 e3 = enc2[(size_t)(9 + 2 * g) * G.S_total + sid];
+        const float z_next = (s + 1 < G.N) ? sample_z(G.sc, nr, fr, ray_index, s + 1) : 0.0f;
+
+        f4 acc[16], act[16];
+        // layer 0: input_linear (32 -> 256), LinearLayer(std 1, bias 0)
+        init_bias(acc, a.bias[0], g);
+        ring_step(R, acc, f4{e0.x, e0.y, e1.x, e1.y});
+        ring_step(R, acc, f4{e2.x, e2.y, e3.x, e3.y});
+#pragma unroll
+        for (int t = 0; t < 16; ++t) act[t] = acc[t];
+        // layers 1..3: FiLM SIREN 256 -> 256
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+            init_bias(acc, a.bias[1 + l], g);
+#pragma unroll
+            for (int t = 0; t < 16; ++t) ring_step(R, acc, act[t]);
+            film_act(act, acc, film + (l * 2 + 0) * kW, film + (l * 2 + 1) * kW, g);
+        }
+        // sigma_linear (256 -> 1)
+        const float sdf = __fadd_rn(dot_feat(act, a.sigma_w, g), a.sigma_b[0]);
+        // layer 4: views FiLM ([h, SH] 272 -> 256)
+        init_bias(acc, a.bias[4], g);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) ring_step(R, acc, act[t]);
+        ring_step(R, acc, shq);
+        film_act(act, acc, film + 6 * kW, film + 7 * kW, g);
+        // rgb_linear (256 -> 3)
+        const float r0 = __fadd_rn(dot_feat(act, a.rgb_w, g), a.rgb_b[0]);
+        const float r1 = __fadd_rn(dot_feat(act, a.rgb_w + kW, g), a.rgb_b[1]);
+        const float r2 = __fadd_rn(dot_feat(act, a.rgb_w + 2 * kW, g), a.rgb_b[2]);
+
+        // volume_integration (sdf_model.py:236-301), front to back
+        const float dist = (s + 1 < G.N) ? __fmul_rn(__fsub_rn(z_next, z), dnorm)
+                                         : __fmul_rn(1e10f, dnorm);
+        float alpha;
+        if (a.with_sdf) {
+            const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
+            alpha = 1.0f - expf(-sig * dist);
+        } else {
+            float raw = sdf;
+            if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + s];
+            const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+            alpha = 1.0f - expf(-sp * dist);
+        }
+        float w = alpha * T;
+        if (a.force_background && s + 1 == G.N) w = 1.0f - wsum;
+        T = T * ((1.0f - alpha) + 1e-10f);
+        wsum += w;
+        w_last = w;
+        racc0 = __fmaf_rn(w, sigmoidf_(r0), racc0);
+        racc1 = __fmaf_rn(w, sigmoidf_(r1), racc1);
+        racc2 = __fmaf_rn(w, sigmoidf_(r2), racc2);
+        if (a.xyz) {
+            xacc0 = __fmaf_rn(w, __fadd_rn(ray.o[0], __fmul_rn(ray.d[0], z)), xacc0);
+            xacc1 = __fmaf_rn(w, __fadd_rn(ray.o[1], __fmul_rn(ray.d[1], z)), xacc1);
+            xacc2 = __fmaf_rn(w, __fadd_rn(ray.o[2], __fmul_rn(ray.d[2], z)), xacc2);
+        }
+        if (a.features) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                facc[t].x = __fmaf_rn(w, act[t].x, facc[t].x);
+                facc[t].y = __fmaf_rn(w, act[t].y, facc[t].y);
+                facc[t].z = __fmaf_rn(w, act[t].z, facc[t].z);
+                facc[t].w = __fmaf_rn(w, act[t].w, facc[t].w);
+            }
+        }
+        if (a.sdf && ray_ok && g == 0) a.sdf[(size_t)ray_index * G.N + s] = sdf;
+        z = z_next;
+    }
+
+    if (!ray_ok) return;
+    const size_t HW = (size_t)G.H * G.W;
+    const size_t pix = (size_t)py * G.W + px;
+    if (g < 3) {
+        const float rc = g == 0 ? racc0 : (g == 1 ? racc1 : racc2);
+        a.rgb[((size_t)b * 3 + g) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, rc));
+        if (a.xyz) {
+            const float xc = g == 0 ? xacc0 : (g == 1 ? xacc1 : xacc2);
+            a.xyz[((size_t)b * 3 + g) * HW + pix] = xc;
+        }
+    } else if (a.mask) {
+        a.mask[(size_t)b * HW + pix] = w_last;
+    }
+    if (a.features) {
+        float *fb = a.features + (size_t)b * kW * HW + pix;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t j = 16 * t + 4 * g;
+            fb[(size_t)(j + 0) * HW] = facc[t].x;
+            fb[(size_t)(j + 1) * HW] = facc[t].y;
+            fb[(size_t)(j + 2) * HW] = facc[t].z;
+            fb[(size_t)(j + 3) * HW] = facc[t].w;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// host side
+// ----------------------------------------------------------------------------
+struct Workspace {
+    float *enc;
+    f4 *packed;
+    float *film;
+};
+
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t L,
+                        size_t *o_packed, size_t *o_film) {
+    const size_t tiles = (size_t)B * ((H * W + kTileRays - 1) / kTileRays);
+    const size_t S = tiles * N * kTileRays;
+    size_t off = align256(S * L * 2 * sizeof(float));
+    *o_packed = off;
+    off += align256((size_t)kSlices * kSliceF4 * sizeof(f4));
+    *o_film = off;
+    off += align256((size_t)B * kFilm * 2 * kW * sizeof(float));
+    return off;
+}
+
+static int validate(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a) {
+    if (!w || !a) return fail(SDFR_EINVAL, "render_ngp: null args");
+    if (w->num_levels != 16)
+        return fail(SDFR_EUNSUPPORTED, "render_ngp: fused path needs 16 levels x 2 features");
+    if (a->B == 0 || a->H == 0 || a->W == 0 || a->N == 0)
+        return fail(SDFR_EINVAL, "render_ngp: empty batch / image / sample count");
+    if (!a->cam || !a->focal || !a->near_ || !a->far_ || !a->styles || !a->pix_x ||
+        !a->pix_y || !a->t_vals || !a->rgb || !a->workspace)
+        return fail(SDFR_EINVAL, "render_ngp: required pointer is null");
+    const void *need[] = {w->embeddings, w->offsets, w->input_w, w->input_b, w->views_w,
+                          w->views_b, w->views_gw, w->views_gb, w->views_bw, w->views_bb,
+                          w->sigma_w, w->sigma_b, w->rgb_w, w->rgb_b, w->sigmoid_beta};
+    for (const void *p : need)
+        if (!p) return fail(SDFR_EINVAL, "render_ngp: weight pointer is null");
+    for (int l = 0; l < 3; ++l)
+        if (!w->pts_w[l] || !w->pts_b[l] || !w->pts_gw[l] || !w->pts_gb[l] || !w->pts_bw[l] ||
+            !w->pts_bb[l])
+            return fail(SDFR_EINVAL, "render_ngp: FiLM weight pointer is null");
+    size_t op, of;
+    if (a->workspace_bytes < ws_layout(a->B, a->H, a->W, a->N, 16, &op, &of))
+        return fail(SDFR_EINVAL, "render_ngp: workspace too small");
+    const uint64_t S = (uint64_t)a->B * ((a->H * a->W + 15) / 16) * a->N * 16;
+    if (S * 16 >= (1ull << 32))
+        return fail(SDFR_EINVAL, "render_ngp: too many samples per call (split the batch)");
+    return SDFR_OK;
+}
+
+static void fill_geom(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, GeomArgs &g) {
+    g.B = a->B;
+    g.H = a->H;
+    g.W = a->W;
+    g.N = a->N;
+    g.tiles_per_face = (a->H * a->W + kTileRays - 1) / kTileRays;
+    g.total_tiles = a->B * g.tiles_per_face;
+    g.S_total = g.total_tiles * a->N * kTileRays;
+    g.half_res = (float)a->W * 0.5f;   // get_rays uses out_im_res * .5 for both axes
+    g.cam = a->cam;
+    g.focal = a->focal;
+    g.near_ = a->near_;
+    g.far_ = a->far_;
+    g.pix_x = a->pix_x;
+    g.pix_y = a->pix_y;
+    g.sc.t_vals = a->t_vals;
+    g.sc.t_rand = a->t_rand;
+    g.sc.t_rand_per_sample = a->t_rand_per_sample;
+    g.sc.offset_sampling = a->offset_sampling;
+    g.sc.N = a->N;
+    g.static_viewdirs = a->static_viewdirs;
+    g.z_normalize = a->z_normalize;
+    g.bound = w->bound;
+}
+
+static void record_event(void *ev, hipStream_t st) {
+    if (ev) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev), st);
+}
+
+static int launch_prep(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, f4 *packed,
+                       float *film, hipStream_t st) {
+    PrepArgs p;
+    p.styles = a->styles;
+    for (int l = 0; l < 3; ++l) {
+        p.gw[l] = w->pts_gw[l];
+        p.gb[l] = w->pts_gb[l];
+        p.bw[l] = w->pts_bw[l];
+        p.bb[l] = w->pts_bb[l];
+        p.w[1 + l] = w->pts_w[l];
+        p.K[1 + l] = kW;
+    }
+    p.gw[3] = w->views_gw;
+    p.gb[3] = w->views_gb;
+    p.bw[3] = w->views_bw;
+    p.bb[3] = w->views_bb;
+    p.w[0] = w->input_w;
+    p.K[0] = kFeatIn;
+    p.w[4] = w->views_w;
+    p.K[4] = kViewsIn;
+    p.film = film;
+    p.packed = packed;
+    p.B = a->B;
+    const uint32_t blocks = a->B * kFilm * 2 + (kSlices * kSliceF4 + 255) / 256;
+    hipLaunchKernelGGL(ngp_prep_kernel, dim3(blocks), dim3(256), 0, st, p);
+    return check_launch("render_ngp: prep");
+}
+
+static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
+                         const GeomArgs &g, float *enc, hipStream_t st) {
+    EncodeArgs e;
+    e.g = g;
+    e.emb = w->embeddings;
+    e.offsets = w->offsets;
+    e.enc = enc;
+    make_level_table(16, w->log2_per_level_scale, w->base_resolution, e.lt);
+    hipLaunchKernelGGL(ngp_encode_kernel, dim3((g.S_total + 255) / 256, 16), dim3(256), 0, st, e);
+    return check_launch("render_ngp: encode");
+}
+
+}  // namespace sdfr
+
+using namespace sdfr;
+
+extern "C" {
+
+size_t sdfr_render_ngp_workspace_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t N,
+                                       uint32_t num_levels) {
+    size_t op, of;
+    return ws_layout(B, H, W, N, num_levels, &op, &of);
+}
+
+int sdfr_render_ngp_encode_only(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
+                                void *stream) {
+    int rc = validate(w, a);
+    if (rc) return rc;
+    GeomArgs g;
+    fill_geom(w, a, g);
+    return launch_encode(w, a, g, reinterpret_cast<float *>(a->workspace), (hipStream_t)stream);
+}
+
+int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
+                            void *stream) {
+    int rc = validate(w, a);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    size_t o_packed, o_film;
+    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film);
+    char *ws = reinterpret_cast<char *>(a->workspace);
+    float *enc = reinterpret_cast<float *>(ws);
+    f4 *packed = reinterpret_cast<f4 *>(ws + o_packed);
+    float *film = reinterpret_cast<float *>(ws + o_film);
+
+    GeomArgs g;
+    fill_geom(w, a, g);
+    record_event(a->stage_events[0], st);
+    if ((rc = launch_prep(w, a, packed, film, st))) return rc;
+    record_event(a->stage_events[1], st);
+    if ((rc = launch_encode(w, a, g, enc, st))) return rc;
+    record_event(a->stage_events[2], st);
+
+    FieldArgs f;
+    f.g = g;
+    f.enc = enc;
+    f.packed = packed;
+    f.film = film;
+    f.bias[0] = w->input_b;
+    for (int l = 0; l < 3; ++l) f.bias[1 + l] = w->pts_b[l];
+    f.bias[4] = w->views_b;
+    f.sigma_w = w->sigma_w;
+    f.sigma_b = w->sigma_b;
+    f.rgb_w = w->rgb_w;
+    f.rgb_b = w->rgb_b;
+    f.sigmoid_beta = w->sigmoid_beta;
+    f.sigma_noise = a->sigma_noise;
+    f.force_background = a->force_background;
+    f.with_sdf = a->with_sdf;
+    f.rgb = a->rgb;
+    f.features = a->features;
+    f.sdf = a->sdf;
+    f.xyz = a->xyz;
+    f.mask = a->mask;
+    const uint32_t blocks = (g.total_tiles + kWaves - 1) / kWaves;
+    hipLaunchKernelGGL(ngp_field_kernel, dim3(blocks), dim3(kThreads), 0, st, f);
+    if ((rc = check_launch("render_ngp: field"))) return rc;
+    record_event(a->stage_events[3], st);
+    return SDFR_OK;
+}
+
+}  // extern "C"

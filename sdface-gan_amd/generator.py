@@ -1,0 +1,422 @@
+"""Generator (mapping + fused renderer + StyleGAN2 decoder), drop-in API.
+
+Follows im2scene/sdf/models/sdf_model.py:
+  MappingLinear :437-466   Upsample/Blur :480-538    EqualLinear :579-611
+  ModulatedConv2d :614-701 NoiseInjection :704-792   StyledConv :795-818
+  ToRGB :821-843           Decoder :883-1056         Generator :1059-1216
+and the device-agnostic forms of the fused ops of sdf_op.py:105-120 / 259-314.
+
+The decoder stays on PyTorch-ROCm.  Its modulated convolution
+runs as ``conv(x * s, W) * demod`` -- one batched MIOpen convolution instead
+of the reference's per-face grouped convolution (same algebra, fp32).
+Geometry-aware noise projection (``project_noise``, pytorch3d) is not
+supported and raises.
+"""
+from __future__ import annotations
+
+import math
+import random
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .renderer import VolumeFeatureRenderer
+
+
+# ---------------------------------------------------------------------------
+# fused ops (sdf_op.py), device-agnostic
+# ---------------------------------------------------------------------------
+def fused_leaky_relu(input, bias=None, negative_slope=0.2, scale=2 ** 0.5):
+    if bias is not None:
+        shape = (1, bias.shape[0]) + (1,) * (input.dim() - bias.dim() - 1)
+        input = input + bias.view(shape)
+    return F.leaky_relu(input, negative_slope=0.2) * scale
+
+
+class FusedLeakyReLU(nn.Module):
+    def __init__(self, channel, bias=True, negative_slope=0.2, scale=2 ** 0.5):
+        super().__init__()
+        self.bias = nn.Parameter(torch.zeros(channel)) if bias else None
+        self.negative_slope = negative_slope
+        self.scale = scale
+
+    def forward(self, input):
+        return fused_leaky_relu(input, self.bias, self.negative_slope, self.scale)
+
+
+def upfirdn2d(input, kernel, up=1, down=1, pad=(0, 0)):
+    """Upsample (zero insertion) -> pad -> FIR (true convolution) -> downsample."""
+    b, c, h, w = input.shape
+    kh, kw = kernel.shape
+    p0, p1 = pad
+    x = input
+    if up > 1:
+        z = x.new_zeros(b, c, h, up, w, up)
+        z[:, :, :, 0, :, 0] = x
+        x = z.view(b, c, h * up, w * up)
+    x = F.pad(x, [max(p0, 0), max(p1, 0), max(p0, 0), max(p1, 0)])
+    x = x[:, :, max(-p0, 0):x.shape[2] - max(-p1, 0), max(-p0, 0):x.shape[3] - max(-p1, 0)]
+    wgt = torch.flip(kernel, [0, 1]).to(x.dtype).view(1, 1, kh, kw).expand(c, 1, kh, kw)
+    x = F.conv2d(x, wgt, groups=c)
+    if down > 1:
+        x = x[:, :, ::down, ::down]
+    return x
+
+
+def make_kernel(k):
+    k = torch.tensor(k, dtype=torch.float32)
+    if k.ndim == 1:
+        k = k[None, :] * k[:, None]
+    return k / k.sum()
+
+
+class Upsample(nn.Module):
+    def __init__(self, kernel, factor=2):
+        super().__init__()
+        self.factor = factor
+        self.register_buffer("kernel", make_kernel(kernel) * (factor ** 2))
+        p = self.kernel.shape[0] - factor
+        self.pad = ((p + 1) // 2 + factor - 1, p // 2)
+
+    def forward(self, input):
+        return upfirdn2d(input, self.kernel, up=self.factor, down=1, pad=self.pad)
+
+
+class Blur(nn.Module):
+    def __init__(self, kernel, pad, upsample_factor=1):
+        super().__init__()
+        k = make_kernel(kernel)
+        if upsample_factor > 1:
+            k = k * (upsample_factor ** 2)
+        self.register_buffer("kernel", k)
+        self.pad = pad
+
+    def forward(self, input):
+        return upfirdn2d(input, self.kernel, pad=self.pad)
+
+
+class PixelNorm(nn.Module):
+    def forward(self, input):
+        return input * torch.rsqrt(torch.mean(input ** 2, dim=1, keepdim=True) + 1e-8)
+
+
+class MappingLinear(nn.Module):
+    """Renderer mapping layer (sdf_model.py:437-466)."""
+
+    def __init__(self, in_dim, out_dim, bias=True, activation=None, is_last=False):
+        super().__init__()
+        std = 0.25 if is_last else 1
+        self.weight = nn.Parameter(std * nn.init.kaiming_normal_(
+            torch.empty(out_dim, in_dim), a=0.2, mode="fan_in", nonlinearity="leaky_relu"))
+        if bias:
+            lim = math.sqrt(1 / in_dim)
+            self.bias = nn.Parameter(nn.init.uniform_(torch.empty(out_dim), a=-lim, b=lim))
+        else:
+            self.bias = None
+        self.activation = activation
+
+    def forward(self, input):
+        if self.activation is not None:
+            return fused_leaky_relu(F.linear(input, self.weight), self.bias, scale=1)
+        return F.linear(input, self.weight, bias=self.bias)
+
+    def __repr__(self):
+        return f"{self.__class__.__name__}({self.weight.shape[1]}, {self.weight.shape[0]})"
+
+
+class EqualLinear(nn.Module):
+    def __init__(self, in_dim, out_dim, bias=True, bias_init=0, lr_mul=1, activation=None):
+        super().__init__()
+        self.weight = nn.Parameter(torch.randn(out_dim, in_dim).div_(lr_mul))
+        self.bias = nn.Parameter(torch.zeros(out_dim).fill_(bias_init)) if bias else None
+        self.activation = activation
+        self.scale = (1 / math.sqrt(in_dim)) * lr_mul
+        self.lr_mul = lr_mul
+
+    def forward(self, input):
+        if self.activation:
+            return fused_leaky_relu(F.linear(input, self.weight * self.scale),
+                                    self.bias * self.lr_mul)
+        return F.linear(input, self.weight * self.scale, bias=self.bias * self.lr_mul)
+
+    def __repr__(self):
+        return f"{self.__class__.__name__}({self.weight.shape[1]}, {self.weight.shape[0]})"
+
+
+class ModulatedConv2d(nn.Module):
+    def __init__(self, in_channel, out_channel, kernel_size, style_dim, demodulate=True,
+                 upsample=False, downsample=False, blur_kernel=(1, 3, 3, 1)):
+        super().__init__()
+        self.eps = 1e-8
+        self.kernel_size = kernel_size
+        self.in_channel = in_channel
+        self.out_channel = out_channel
+        self.upsample = upsample
+        self.downsample = downsample
+        if upsample:
+            factor = 2
+            p = (len(blur_kernel) - factor) - (kernel_size - 1)
+            self.blur = Blur(blur_kernel, pad=((p + 1) // 2 + factor - 1, p // 2 + 1),
+                             upsample_factor=factor)
+        if downsample:
+            factor = 2
+            p = (len(blur_kernel) - factor) + (kernel_size - 1)
+            self.blur = Blur(blur_kernel, pad=((p + 1) // 2, p // 2))
+        self.scale = 1 / math.sqrt(in_channel * kernel_size ** 2)
+        self.padding = kernel_size // 2
+        self.weight = nn.Parameter(torch.randn(1, out_channel, in_channel, kernel_size,
+                                               kernel_size))
+        self.modulation = EqualLinear(style_dim, in_channel, bias_init=1)
+        self.demodulate = demodulate
+
+    def __repr__(self):
+        return (f"{self.__class__.__name__}({self.in_channel}, {self.out_channel}, "
+                f"{self.kernel_size}, upsample={self.upsample}, downsample={self.downsample})")
+
+    def forward(self, input, style):
+        batch = input.shape[0]
+        s = self.modulation(style)                                   # [B, in]
+        w = self.scale * self.weight[0]                              # [out, in, k, k]
+        x = input * s.view(batch, -1, 1, 1)
+        if self.upsample:
+            out = F.conv_transpose2d(x, w.transpose(0, 1), padding=0, stride=2)
+        elif self.downsample:
+            out = F.conv2d(self.blur(x), w, padding=0, stride=2)
+        else:
+            out = F.conv2d(x, w, padding=self.padding)
+        if self.demodulate:
+            wsq = (w * w).sum([2, 3])                                # [out, in]
+            demod = torch.rsqrt((s * s) @ wsq.t() + 1e-8)            # [B, out]
+            out = out * demod.view(batch, -1, 1, 1)
+        if self.upsample:
+            out = self.blur(out)
+        return out
+
+
+class NoiseInjection(nn.Module):
+    def __init__(self, project=False):
+        super().__init__()
+        self.project = project
+        self.weight = nn.Parameter(torch.zeros(1))
+        self.prev_noise = None
+        self.mesh_fn = None
+        self.vert_noise = None
+
+    def forward(self, image, noise=None, transform=None, mesh_path=None):
+        batch, _, height, width = image.shape
+        if noise is None:
+            noise = image.new_empty(batch, 1, height, width).normal_()
+        elif self.project:
+            raise NotImplementedError("geometry-aware noise projection (pytorch3d) is not "
+                                      "part of this framework")
+        return image + self.weight * noise
+
+
+class StyledConv(nn.Module):
+    def __init__(self, in_channel, out_channel, kernel_size, style_dim, upsample=False,
+                 blur_kernel=(1, 3, 3, 1), project_noise=False):
+        super().__init__()
+        self.conv = ModulatedConv2d(in_channel, out_channel, kernel_size, style_dim,
+                                    upsample=upsample, blur_kernel=blur_kernel)
+        self.noise = NoiseInjection(project=project_noise)
+        self.bias = nn.Parameter(torch.zeros(1, out_channel, 1, 1))
+        self.activate = FusedLeakyReLU(out_channel)
+
+    def forward(self, input, style, noise=None, transform=None, mesh_path=None):
+        out = self.conv(input, style)
+        out = self.noise(out, noise=noise, transform=transform, mesh_path=mesh_path)
+        return self.activate(out)
+
+
+class ToRGB(nn.Module):
+    def __init__(self, in_channel, style_dim, upsample=True, blur_kernel=(1, 3, 3, 1)):
+        super().__init__()
+        self.upsample = Upsample(blur_kernel) if upsample else upsample
+        self.conv = ModulatedConv2d(in_channel, 3, 1, style_dim, demodulate=False)
+        self.bias = nn.Parameter(torch.zeros(1, 3, 1, 1))
+
+    def forward(self, input, style, skip=None):
+        out = self.conv(input, style) + self.bias
+        if skip is not None:
+            if self.upsample:
+                skip = self.upsample(skip)
+            out = out + skip
+        return out
+
+
+class Decoder(nn.Module):
+    """StyleGAN2 2D decoder, 64^2 x 256 features -> size^2 RGB (sdf_model.py:883-1056)."""
+
+    def __init__(self, model_opt, blur_kernel=(1, 3, 3, 1)):
+        super().__init__()
+        o = model_opt
+        self.size = o.size
+        self.style_dim = o.style_dim * 2
+        in_dim = self.style_dim if o.psp else self.style_dim // 2
+        layers = [PixelNorm(), EqualLinear(in_dim, self.style_dim, lr_mul=o.lr_mapping,
+                                           activation="fused_lrelu")]
+        for _ in range(4):
+            layers.append(EqualLinear(self.style_dim, self.style_dim, lr_mul=o.lr_mapping,
+                                      activation="fused_lrelu"))
+        self.style = nn.Sequential(*layers)
+        cm = o.channel_multiplier
+        self.channels = {4: 512, 8: 512, 16: 512, 32: 512, 64: 256 * cm, 128: 128 * cm,
+                         256: 64 * cm, 512: 32 * cm, 1024: 16 * cm}
+        dec_in = o.renderer_spatial_output_dim
+        self.log_size = int(math.log(self.size, 2))
+        self.log_in_size = int(math.log(dec_in, 2))
+        in_feat = o.feature_encoder_in_channels if not o.psp else self.style_dim
+        self.conv1 = StyledConv(in_feat, self.channels[dec_in], 3, self.style_dim,
+                                blur_kernel=blur_kernel, project_noise=o.project_noise)
+        self.to_rgb1 = ToRGB(self.channels[dec_in], self.style_dim, upsample=False)
+        self.num_layers = (self.log_size - self.log_in_size) * 2 + 1
+        self.convs = nn.ModuleList()
+        self.upsamples = nn.ModuleList()
+        self.to_rgbs = nn.ModuleList()
+        self.noises = nn.Module()
+        in_ch = self.channels[dec_in]
+        for idx in range(self.num_layers):
+            res = (idx + 2 * self.log_in_size + 1) // 2
+            self.noises.register_buffer(f"noise_{idx}", torch.randn(1, 1, 2 ** res, 2 ** res))
+        for i in range(self.log_in_size + 1, self.log_size + 1):
+            out_ch = self.channels[2 ** i]
+            self.convs.append(StyledConv(in_ch, out_ch, 3, self.style_dim, upsample=True,
+                                         blur_kernel=blur_kernel,
+                                         project_noise=o.project_noise))
+            self.convs.append(StyledConv(out_ch, out_ch, 3, self.style_dim,
+                                         blur_kernel=blur_kernel,
+                                         project_noise=o.project_noise))
+            self.to_rgbs.append(ToRGB(out_ch, self.style_dim))
+            in_ch = out_ch
+        self.n_latent = (self.log_size - self.log_in_size) * 2 + 2
+
+    def mean_latent(self, renderer_latent):
+        return self.style(renderer_latent).mean(0, keepdim=True)
+
+    def get_latent(self, input):
+        return self.style(input)
+
+    def styles_and_noise_forward(self, styles, noise, inject_index=None, truncation=1,
+                                 truncation_latent=None, input_is_latent=False,
+                                 randomize_noise=True):
+        if not input_is_latent:
+            styles = [self.style(s) for s in styles]
+        if noise is None:
+            noise = ([None] * self.num_layers if randomize_noise else
+                     [getattr(self.noises, f"noise_{i}") for i in range(self.num_layers)])
+        if truncation < 1:
+            styles = [truncation_latent[1] + truncation * (s - truncation_latent[1])
+                      for s in styles]
+        if len(styles) < 2:
+            inject_index = self.n_latent
+            latent = (styles[0].unsqueeze(1).repeat(1, inject_index, 1)
+                      if styles[0].ndim < 3 else styles[0])
+        else:
+            if inject_index is None:
+                inject_index = random.randint(1, self.n_latent - 1)
+            latent = torch.cat([styles[0].unsqueeze(1).repeat(1, inject_index, 1),
+                                styles[1].unsqueeze(1).repeat(1, self.n_latent - inject_index, 1)],
+                               1)
+        return latent, noise
+
+    def forward(self, features, styles, rgbd_in=None, transform=None, return_latents=False,
+                inject_index=None, truncation=1, truncation_latent=None, input_is_latent=False,
+                noise=None, randomize_noise=True, mesh_path=None):
+        latent, noise = self.styles_and_noise_forward(styles, noise, inject_index, truncation,
+                                                      truncation_latent, input_is_latent,
+                                                      randomize_noise)
+        out = self.conv1(features, latent[:, 0], noise=noise[0], transform=transform,
+                         mesh_path=mesh_path)
+        skip = self.to_rgb1(out, latent[:, 1], skip=rgbd_in)
+        i = 1
+        for c1, c2, n1, n2, to_rgb in zip(self.convs[::2], self.convs[1::2], noise[1::2],
+                                          noise[2::2], self.to_rgbs):
+            out = c1(out, latent[:, i], noise=n1, transform=transform, mesh_path=mesh_path)
+            out = c2(out, latent[:, i + 1], noise=n2, transform=transform, mesh_path=mesh_path)
+            skip = to_rgb(out, latent[:, i + 2], skip=skip)
+            i += 2
+        return skip, (latent if return_latents else None)
+
+
+def _has(o, k):
+    return k in o.keys() if hasattr(o, "keys") else hasattr(o, k)
+
+
+class Generator(nn.Module):
+    """Drop-in for sdf_model.py:1059-1216."""
+
+    def __init__(self, model_opt, renderer_opt, blur_kernel=(1, 3, 3, 1), ema=False,
+                 full_pipeline=True):
+        super().__init__()
+        self.size = model_opt.size
+        self.style_dim = model_opt.style_dim * 2 if model_opt.psp else model_opt.style_dim
+        self.num_layers = 1
+        self.train_renderer = not model_opt.freeze_renderer
+        self.full_pipeline = full_pipeline
+        model_opt.feature_encoder_in_channels = renderer_opt.width
+        self.is_train = not (ema or _has(model_opt, "is_test"))
+        self.style = nn.Sequential(*[MappingLinear(self.style_dim, self.style_dim,
+                                                   activation="fused_lrelu") for _ in range(3)])
+        self.renderer = VolumeFeatureRenderer(renderer_opt, style_dim=self.style_dim,
+                                              out_im_res=model_opt.renderer_spatial_output_dim)
+        if self.full_pipeline:
+            self.decoder = Decoder(model_opt, blur_kernel=blur_kernel)
+
+    def mean_latent(self, n_latent, device, z=None):
+        if z is None:
+            z = torch.randn(n_latent, self.style_dim, device=device)
+        renderer_latent = self.style(z)
+        renderer_latent_mean = renderer_latent.mean(0, keepdim=True)
+        decoder_latent_mean = (self.decoder.mean_latent(renderer_latent)
+                               if self.full_pipeline else None)
+        return [renderer_latent_mean, decoder_latent_mean]
+
+    def get_latent(self, input):
+        return self.style(input)
+
+    def styles_and_noise_forward(self, styles, inject_index=None, truncation=1,
+                                 truncation_latent=None, input_is_latent=False):
+        if not input_is_latent:
+            styles = [self.style(s) for s in styles]
+        if truncation < 1:
+            styles = [truncation_latent[0] + truncation * (s - truncation_latent[0])
+                      for s in styles]
+        return styles
+
+    def init_forward(self, styles, cam_poses, focals, near=0.88, far=1.12):
+        latent = self.styles_and_noise_forward(styles)
+        return self.renderer.mlp_init_pass(cam_poses, focals, near, far, styles=latent[0])
+
+    def forward(self, styles, cam_poses, focals, near=0.88, far=1.12, return_latents=False,
+                inject_index=None, truncation=1, truncation_latent=None, input_is_latent=False,
+                noise=None, randomize_noise=True, return_sdf=False, return_xyz=False,
+                return_eikonal=False, project_noise=False, mesh_path=None, t_rand=None):
+        with torch.set_grad_enabled(self.is_train and self.train_renderer):
+            latent = self.styles_and_noise_forward(styles, inject_index, truncation,
+                                                   truncation_latent, input_is_latent)
+            lat0 = latent[0][:, 0] if input_is_latent else latent[0]
+            thumb_rgb, features, sdf, mask, xyz, eikonal_term = self.renderer(
+                cam_poses, focals, near, far, styles=lat0, return_eikonal=return_eikonal,
+                t_rand=t_rand)
+        if self.full_pipeline:
+            rgb, decoder_latent = self.decoder(
+                features, latent, transform=cam_poses if project_noise else None,
+                return_latents=return_latents, inject_index=inject_index, truncation=truncation,
+                truncation_latent=truncation_latent, noise=noise,
+                input_is_latent=input_is_latent, randomize_noise=randomize_noise,
+                mesh_path=mesh_path)
+        else:
+            rgb = None
+        if return_latents:
+            return rgb, decoder_latent
+        out = (rgb, thumb_rgb)
+        if return_xyz:
+            out += (xyz,)
+        if return_sdf:
+            out += (sdf,)
+        if return_eikonal:
+            out += (eikonal_term,)
+        if return_xyz:
+            out += (mask,)
+        return out

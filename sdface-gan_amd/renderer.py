@@ -1,0 +1,558 @@
+"""Volume renderer: drop-in VolumeFeatureRenderer + its networks, MI355X path.
+
+Module / parameter names, constructor arguments, initialisation (including the
+order in which the CPU RNG is consumed) and forward signatures follow
+``im2scene/sdf/models/sdf_model.py``:
+
+  LinearLayer          :23-41     FiLMSiren          :44-69
+  SirenGenerator       :101-139   VolumeFeatureRenderer :143-423
+  get_encoder          :1512-1531 NGPSIRENGenerator  :1534-1596
+  FCGenerator          :1599-1670
+
+``VolumeFeatureRenderer.forward`` runs the fused HIP renderer
+(``sdfr_render_ngp_forward``: sampling + hash grid + MLP on MFMA + compositing)
+whenever the network is the ngp one and no gradient is required (eval.py,
+sdf_mesh.py, stage-2 training where the renderer is frozen).  When gradients
+are needed (stage-1 training, eikonal term) it runs the reference's op-by-op
+structure on the GPU, with the hash-grid and SH encoders on the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+import torch.autograd as autograd
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .encoders import GridEncoder, SHEncoder
+
+
+# ---------------------------------------------------------------------------
+# layers
+# ---------------------------------------------------------------------------
+class LinearLayer(nn.Module):
+    """SIREN linear layer: ``std_init * (x W^T + b) + bias_init`` (sdf_model.py:23-41)."""
+
+    def __init__(self, in_dim, out_dim, bias=True, bias_init=0, std_init=1, freq_init=False,
+                 is_first=False):
+        super().__init__()
+        if is_first:
+            w = torch.empty(out_dim, in_dim).uniform_(-1 / in_dim, 1 / in_dim)
+        elif freq_init:
+            lim = np.sqrt(6 / in_dim) / 25
+            w = torch.empty(out_dim, in_dim).uniform_(-lim, lim)
+        else:
+            w = 0.25 * nn.init.kaiming_normal_(torch.randn(out_dim, in_dim), a=0.2,
+                                               mode="fan_in", nonlinearity="leaky_relu")
+        self.weight = nn.Parameter(w)
+        lim = np.sqrt(1 / in_dim)
+        self.bias = nn.Parameter(nn.init.uniform_(torch.empty(out_dim), a=-lim, b=lim))
+        self.bias_init = bias_init
+        self.std_init = std_init
+
+    def forward(self, input):
+        return self.std_init * F.linear(input, self.weight, bias=self.bias) + self.bias_init
+
+
+class FiLMSiren(nn.Module):
+    """``sin(gamma(style) * (x W^T + b) + beta(style))`` (sdf_model.py:44-69)."""
+
+    def __init__(self, in_channel, out_channel, style_dim, is_first=False):
+        super().__init__()
+        self.in_channel = in_channel
+        self.out_channel = out_channel
+        if is_first:
+            w = torch.empty(out_channel, in_channel).uniform_(-1 / 3, 1 / 3)
+        else:
+            lim = np.sqrt(6 / in_channel) / 25
+            w = torch.empty(out_channel, in_channel).uniform_(-lim, lim)
+        self.weight = nn.Parameter(w)
+        lim = np.sqrt(1 / in_channel)
+        self.bias = nn.Parameter(nn.init.uniform_(torch.empty(out_channel), a=-lim, b=lim))
+        self.activation = torch.sin
+        self.gamma = LinearLayer(style_dim, out_channel, bias_init=30, std_init=15)
+        self.beta = LinearLayer(style_dim, out_channel, bias_init=0, std_init=0.25)
+
+    def forward(self, input, style):
+        batch, features = style.shape
+        out = F.linear(input, self.weight, bias=self.bias)
+        shape = (batch,) + (1,) * (input.dim() - 2) + (features,)
+        gamma = self.gamma(style).view(shape)
+        beta = self.beta(style).view(shape)
+        return self.activation(gamma * out + beta)
+
+
+# ---------------------------------------------------------------------------
+# networks
+# ---------------------------------------------------------------------------
+class SirenGenerator(nn.Module):
+    """FiLM-SIREN MLP, ``rendering.type == 'sdf'`` (sdf_model.py:101-139)."""
+
+    def __init__(self, D=8, W=256, style_dim=256, input_ch=3, input_ch_views=3, output_ch=4,
+                 output_features=True):
+        super().__init__()
+        self.D, self.W = D, W
+        self.input_ch, self.input_ch_views = input_ch, input_ch_views
+        self.style_dim = style_dim
+        self.output_features = output_features
+        layers = [FiLMSiren(3, W, style_dim=style_dim, is_first=True)]
+        layers += [FiLMSiren(W, W, style_dim=style_dim) for _ in range(D - 1)]
+        self.pts_linears = nn.ModuleList(layers)
+        self.views_linears = FiLMSiren(input_ch_views + W, W, style_dim=style_dim)
+        self.rgb_linear = LinearLayer(W, 3, freq_init=True)
+        self.sigma_linear = LinearLayer(W, 1, freq_init=True)
+
+    def forward(self, x, styles):
+        pts, views = torch.split(x, [self.input_ch, self.input_ch_views], dim=-1)
+        h = pts.contiguous()
+        for layer in self.pts_linears:
+            h = layer(h, styles)
+        sdf = self.sigma_linear(h)
+        feat = self.views_linears(torch.cat([h, views], -1), styles)
+        rgb = self.rgb_linear(feat)
+        out = torch.cat([rgb, sdf], -1)
+        return torch.cat([out, feat], -1) if self.output_features else out
+
+
+def get_encoder(encoding, input_dim=3, multires=6, degree=4, num_levels=16, level_dim=2,
+                base_resolution=16, log2_hashmap_size=19, desired_resolution=2048,
+                align_corners=False, **kwargs):
+    """(encoder module, output dim) as sdf_model.py:1512-1531."""
+    if encoding == "sphere_harmonics":
+        enc = SHEncoder(input_dim=input_dim, degree=degree)
+    elif encoding == "hashgrid":
+        enc = GridEncoder(input_dim=input_dim, num_levels=num_levels, level_dim=level_dim,
+                          base_resolution=base_resolution, log2_hashmap_size=log2_hashmap_size,
+                          desired_resolution=desired_resolution, gridtype="hash",
+                          align_corners=align_corners)
+    else:
+        raise NotImplementedError(
+            "Unknown encoding mode, choose from [None, frequency, sphere_harmonics, hashgrid, "
+            "tiledgrid]")
+    return enc, enc.output_dim
+
+
+class NGPSIRENGenerator(nn.Module):
+    """Hash-grid + FiLM-SIREN field, ``rendering.type == 'ngp'`` (sdf_model.py:1534-1596)."""
+
+    def __init__(self, D=2, W=256, style_dim=256, output_features=True):
+        super().__init__()
+        self.D, self.W = D, W
+        self.bound = 2
+        self.style_dim = style_dim
+        self.input_ch = 3
+        self.input_ch_views = 3
+        self.output_features = output_features
+        self.encoder, self.in_dim = get_encoder("hashgrid", desired_resolution=2048 * self.bound)
+        self.encoder_dir, self.in_dim_dir = get_encoder("sphere_harmonics")
+        # the reference aliases input_linear and rgb_linear here and re-creates
+        # rgb_linear below (sdf_model.py:1549, 1561); keep that RNG order and
+        # the module registration order (optimizer parameter order)
+        self.input_linear = LinearLayer(self.in_dim, self.W, freq_init=True)
+        self.rgb_linear = self.input_linear
+        layers = [FiLMSiren(self.W, self.W, style_dim=style_dim, is_first=True)]
+        layers += [FiLMSiren(self.W, self.W, style_dim=style_dim) for _ in range(self.D)]
+        self.pts_linears = nn.ModuleList(layers)
+        self.views_linears = FiLMSiren(self.in_dim_dir + self.W, self.W, style_dim=style_dim)
+        self.rgb_linear = LinearLayer(self.W, 3, freq_init=True)
+        self.sigma_linear = LinearLayer(W, 1, freq_init=True)
+
+    def forward(self, x, styles):
+        pts, views = torch.split(x, [self.input_ch, self.input_ch_views], dim=-1)
+        h = self.encoder(pts, bound=self.bound)
+        v = self.encoder_dir(views)
+        h = self.input_linear(h.contiguous())
+        for layer in self.pts_linears:
+            h = layer(h, styles)
+        sdf = self.sigma_linear(h)
+        feat = self.views_linears(torch.cat([h, v], -1), styles)
+        rgb = self.rgb_linear(feat)
+        out = torch.cat([rgb, sdf], -1)
+        return torch.cat([out, feat], -1) if self.output_features else out
+
+    def query_sdf(self, input_pts, styles):
+        # the reference returns the hash embedding here (sdf_model.py:1594-1596)
+        return self.encoder(input_pts, bound=self.bound)
+
+
+class FCGenerator(nn.Module):
+    """Positional-encoding ReLU MLP, ``rendering.fc == 1`` (sdf_model.py:1599-1670)."""
+
+    def __init__(self, D=8, W=256, style_dim=256, input_ch=3, input_ch_views=3, output_ch=4,
+                 output_features=True):
+        super().__init__()
+        self.D, self.W = D, W
+        self.input_ch, self.input_ch_views = input_ch, input_ch_views
+        self.style_dim = style_dim
+        self.output_features = output_features
+        self.n_freq_posenc = 10
+        self.n_freq_posenc_views = 4
+        dim_embed = 3 * self.n_freq_posenc * 2
+        dim_embed_view = 3 * self.n_freq_posenc_views * 2
+        self.x_in = nn.Linear(dim_embed, W)
+        self.style_in = nn.Linear(style_dim, W)
+        self.pts_linears = nn.ModuleList([nn.Linear(W, W) for _ in range(D - 1)])
+        self.views_linears = nn.Linear(dim_embed_view + W, W)
+        self.rgb_linear = nn.Linear(W, 3)
+        self.sigma_linear = nn.Linear(W, 1)
+
+    def transform_points(self, p, views=False):
+        p = p / 2
+        L = self.n_freq_posenc_views if views else self.n_freq_posenc
+        parts = []
+        for i in range(L):
+            parts.append(torch.cat([torch.sin((2 ** i) * np.pi * p),
+                                    torch.cos((2 ** i) * np.pi * p)], dim=-1))
+        return torch.cat(parts, dim=-1)
+
+    def forward(self, x, styles):
+        pts, views = torch.split(x, [self.input_ch, self.input_ch_views], dim=-1)
+        pts = self.transform_points(pts)
+        views = self.transform_points(views, True)
+        h = self.x_in(pts)
+        s = self.style_in(styles)
+        s = s.view((s.shape[0],) + (1,) * (h.dim() - 2) + (s.shape[-1],))
+        h = F.relu(h + s)
+        for layer in self.pts_linears:
+            h = F.relu(layer(h))
+        sdf = self.sigma_linear(h)
+        feat = self.views_linears(torch.cat([h, views], -1))
+        rgb = self.rgb_linear(feat)
+        out = torch.cat([rgb, sdf], -1)
+        return torch.cat([out, feat], -1) if self.output_features else out
+
+
+# ---------------------------------------------------------------------------
+# renderer
+# ---------------------------------------------------------------------------
+def _opt(opt, key, default=None):
+    try:
+        return opt[key]
+    except (KeyError, TypeError):
+        return getattr(opt, key, default)
+
+
+def _per_face(x, B, device):
+    t = torch.as_tensor(x, dtype=torch.float32, device=device).reshape(-1)
+    return (t.expand(B) if t.numel() == 1 else t).contiguous()
+
+
+class VolumeFeatureRenderer(nn.Module):
+    """Drop-in for sdf_model.py:143-423 (same options, buffers, outputs)."""
+
+    def __init__(self, opt, style_dim=256, out_im_res=64, mode="train"):
+        super().__init__()
+        self.test = mode != "train"
+        self.perturb = _opt(opt, "perturb")
+        self.offset_sampling = not _opt(opt, "no_offset_sampling")
+        self.N_samples = _opt(opt, "N_samples")
+        self.raw_noise_std = _opt(opt, "raw_noise_std")
+        self.return_xyz = _opt(opt, "return_xyz")
+        self.return_sdf = _opt(opt, "return_sdf")
+        self.static_viewdirs = _opt(opt, "static_viewdirs")
+        self.z_normalize = not _opt(opt, "no_z_normalize")
+        self.out_im_res = out_im_res
+        self.force_background = _opt(opt, "force_background")
+        self.with_sdf = not _opt(opt, "no_sdf")
+        keys = opt.keys() if hasattr(opt, "keys") else vars(opt).keys()
+        self.output_features = "no_features_output" not in keys
+        if self.with_sdf:
+            self.sigmoid_beta = nn.Parameter(0.1 * torch.ones(1))
+
+        lin = torch.linspace(0.5, self.out_im_res - 0.5, self.out_im_res)
+        i, j = torch.meshgrid(lin, lin, indexing="ij")
+        self.register_buffer("i", i.t().unsqueeze(0), persistent=False)
+        self.register_buffer("j", j.t().unsqueeze(0), persistent=False)
+        if self.offset_sampling:
+            t_vals = torch.linspace(0., 1. - 1 / self.N_samples, steps=self.N_samples)
+        else:
+            t_vals = torch.linspace(0., 1., steps=self.N_samples)
+        self.register_buffer("t_vals", t_vals.view(1, 1, 1, -1), persistent=False)
+        self.register_buffer("inf", torch.Tensor([1e10]), persistent=False)
+        self.register_buffer("zero_idx", torch.LongTensor([0]), persistent=False)
+        if self.test:
+            self.perturb = False
+            self.raw_noise_std = 0.
+
+        self.channel_dim = -1
+        self.samples_dim = 3
+        self.input_ch = 3
+        self.input_ch_views = 3
+        rtype = _opt(opt, "type")
+        self.feature_out_size = _opt(opt, "width") if rtype != "ngp" else style_dim
+        if rtype == "ngp":
+            self.network = NGPSIRENGenerator(D=2, W=style_dim, style_dim=style_dim,
+                                             output_features=self.output_features)
+        elif _opt(opt, "fc"):
+            self.network = FCGenerator(D=_opt(opt, "depth"), W=_opt(opt, "width"),
+                                       style_dim=style_dim, input_ch=self.input_ch, output_ch=4,
+                                       input_ch_views=self.input_ch_views,
+                                       output_features=self.output_features)
+        else:
+            self.network = SirenGenerator(D=_opt(opt, "depth"), W=_opt(opt, "width"),
+                                          style_dim=style_dim, input_ch=self.input_ch,
+                                          output_ch=4, input_ch_views=self.input_ch_views,
+                                          output_features=self.output_features)
+        # MI355X additions (not in the reference): where the per-ray sampling
+        # offsets are drawn ('cpu' = the reference's CPU RNG stream, 'device' =
+        # torch.cuda RNG, no host round trip) and a switch for the fused path.
+        self.rng_device = "cpu"
+        self.use_fused = True
+        # optional 4 torch.cuda.Event(enable_timing=True) recorded around the
+        # fused stages (prep | hash grid | field | end), see include/sdfr.h
+        self.stage_events = None
+
+    # ---------------------------------------------------------------- reference structure
+    def get_rays(self, focal, c2w):
+        dirs = torch.stack([(self.i - self.out_im_res * .5) / focal,
+                            -(self.j - self.out_im_res * .5) / focal,
+                            -torch.ones_like(self.i).expand(focal.shape[0], self.out_im_res,
+                                                            self.out_im_res)], -1)
+        rays_d = torch.sum(dirs[..., None, :] * c2w[:, None, None, :3, :3], -1)
+        rays_o = c2w[:, None, None, :3, -1].expand(rays_d.shape)
+        viewdirs = dirs if self.static_viewdirs else rays_d
+        return rays_o, rays_d, viewdirs
+
+    def get_eikonal_term(self, pts, sdf):
+        return autograd.grad(outputs=sdf, inputs=pts, grad_outputs=torch.ones_like(sdf),
+                             create_graph=True)[0]
+
+    def sdf_activation(self, input):
+        return torch.sigmoid(input / self.sigmoid_beta) / self.sigmoid_beta
+
+    def volume_integration(self, raw, z_vals, rays_d, pts, return_eikonal=False):
+        dists = z_vals[..., 1:] - z_vals[..., :-1]
+        rays_d_norm = torch.norm(rays_d.unsqueeze(self.samples_dim), dim=self.channel_dim)
+        dists = torch.cat([dists, self.inf.expand(rays_d_norm.shape)], self.channel_dim)
+        dists = dists * rays_d_norm
+        if self.output_features:
+            rgb, sdf, features = torch.split(raw, [3, 1, self.feature_out_size],
+                                             dim=self.channel_dim)
+        else:
+            rgb, sdf = torch.split(raw, [3, 1], dim=self.channel_dim)
+        noise = 0.
+        if self.raw_noise_std > 0.:
+            noise = torch.randn_like(sdf) * self.raw_noise_std
+        if self.with_sdf:
+            sigma = self.sdf_activation(-sdf)
+            eikonal_term = self.get_eikonal_term(pts, sdf) if return_eikonal else None
+            sigma = 1 - torch.exp(-sigma * dists.unsqueeze(self.channel_dim))
+        else:
+            eikonal_term = None
+            sigma = 1 - torch.exp(-F.softplus(sdf + noise) * dists.unsqueeze(self.channel_dim))
+        first = torch.ones_like(torch.index_select(sigma, self.samples_dim, self.zero_idx))
+        visibility = torch.cumprod(torch.cat([first, 1. - sigma + 1e-10], self.samples_dim),
+                                   self.samples_dim)[..., :-1, :]
+        weights = sigma * visibility
+        sdf_out = sdf if self.return_sdf else None
+        if self.force_background:
+            weights[..., -1, :] = 1 - weights[..., :-1, :].sum(self.samples_dim)
+        rgb_map = -1 + 2 * torch.sum(weights * torch.sigmoid(rgb), self.samples_dim)
+        feature_map = (torch.sum(weights * features, self.samples_dim)
+                       if self.output_features else None)
+        if self.return_xyz:
+            xyz = torch.sum(weights * pts, self.samples_dim)
+            mask = weights[..., -1, :]
+        else:
+            xyz = mask = None
+        return rgb_map, feature_map, sdf_out, mask, xyz, eikonal_term
+
+    def run_network(self, inputs, viewdirs, styles=None):
+        input_dirs = viewdirs.unsqueeze(self.samples_dim).expand(inputs.shape)
+        return self.network(torch.cat([inputs, input_dirs], self.channel_dim), styles=styles)
+
+    def _draw_t_rand(self, shape, device):
+        if self.rng_device == "cpu":
+            return torch.rand(shape).to(device)
+        return torch.rand(shape, device=device)
+
+    def render_rays(self, ray_batch, styles=None, return_eikonal=False, t_rand=None):
+        batch, h, w, _ = ray_batch.shape
+        split = [3, 3, 2]
+        if ray_batch.shape[-1] > 8:
+            rays_o, rays_d, bounds, viewdirs = torch.split(ray_batch, split + [3], dim=-1)
+        else:
+            rays_o, rays_d, bounds = torch.split(ray_batch, split, dim=-1)
+            viewdirs = None
+        near, far = torch.split(bounds, [1, 1], dim=-1)
+        z_vals = near * (1. - self.t_vals) + far * self.t_vals
+        if self.perturb > 0.:
+            if self.offset_sampling:
+                upper = torch.cat([z_vals[..., 1:], far], -1)
+                lower = z_vals.detach()
+                if t_rand is None:
+                    t_rand = self._draw_t_rand((batch, h, w), z_vals.device)
+                t_rand = t_rand.reshape(batch, h, w, 1)
+            else:
+                mids = .5 * (z_vals[..., 1:] + z_vals[..., :-1])
+                upper = torch.cat([mids, z_vals[..., -1:]], -1)
+                lower = torch.cat([z_vals[..., :1], mids], -1)
+                if t_rand is None:
+                    t_rand = self._draw_t_rand(z_vals.shape, z_vals.device)
+            z_vals = lower + (upper - lower) * t_rand
+        pts = rays_o.unsqueeze(3) + rays_d.unsqueeze(3) * z_vals.unsqueeze(-1)
+        if return_eikonal:
+            pts.requires_grad = True
+        normalized_pts = pts * 2 / ((far - near).unsqueeze(3)) if self.z_normalize else pts
+        raw = self.run_network(normalized_pts, viewdirs, styles=styles)
+        return self.volume_integration(raw, z_vals, rays_d, pts, return_eikonal=return_eikonal)
+
+    def render(self, focal, c2w, near, far, styles, c2w_staticcam=None, return_eikonal=False,
+               t_rand=None):
+        rays_o, rays_d, viewdirs = self.get_rays(focal, c2w)
+        viewdirs = viewdirs / torch.norm(viewdirs, dim=-1, keepdim=True)
+        near = near.unsqueeze(-1) * torch.ones_like(rays_d[..., :1])
+        far = far.unsqueeze(-1) * torch.ones_like(rays_d[..., :1])
+        rays = torch.cat([rays_o, rays_d, near, far], -1)
+        rays = torch.cat([rays, viewdirs], -1).float()
+        return self.render_rays(rays, styles=styles, return_eikonal=return_eikonal,
+                                t_rand=t_rand)
+
+    def mlp_init_pass(self, cam_poses, focal, near, far, styles=None):
+        rays_o, rays_d, viewdirs = self.get_rays(focal, cam_poses)
+        viewdirs = viewdirs / torch.norm(viewdirs, dim=-1, keepdim=True)
+        near = near.unsqueeze(-1) * torch.ones_like(rays_d[..., :1])
+        far = far.unsqueeze(-1) * torch.ones_like(rays_d[..., :1])
+        z_vals = near * (1. - self.t_vals) + far * self.t_vals
+        mids = .5 * (z_vals[..., 1:] + z_vals[..., :-1])
+        upper = torch.cat([mids, z_vals[..., -1:]], -1)
+        lower = torch.cat([z_vals[..., :1], mids], -1)
+        t_rand = self._draw_t_rand(z_vals.shape, z_vals.device)
+        z_vals = lower + (upper - lower) * t_rand
+        pts = rays_o.unsqueeze(3) + rays_d.unsqueeze(3) * z_vals.unsqueeze(-1)
+        normalized_pts = pts * 2 / ((far - near).unsqueeze(3)) if self.z_normalize else pts
+        raw = self.run_network(normalized_pts, viewdirs, styles=styles)
+        _, sdf = torch.split(raw[..., :4], [3, 1], dim=-1)
+        sdf = sdf.squeeze(-1)
+        target_values = pts.detach().norm(dim=-1) - ((far - near) / 4)
+        return sdf, target_values
+
+    # ---------------------------------------------------------------- fused HIP path
+    def _fused_ok(self, cam_poses, styles, return_eikonal):
+        if not (self.use_fused and isinstance(self.network, NGPSIRENGenerator)):
+            return False
+        if return_eikonal or not cam_poses.is_cuda or styles is None:
+            return False
+        if styles.dim() != 2 or styles.shape[1] != 256 or self.network.W != 256:
+            return False
+        if torch.is_grad_enabled() and (styles.requires_grad or any(
+                p.requires_grad for p in self.parameters())):
+            return False
+        return True
+
+    def _ngp_weight_struct(self):
+        net = self.network
+        P = lambda t: _lib.ptr(t)  # noqa: E731
+        w = _lib.NgpWeights()
+        w.embeddings = P(net.encoder.embeddings)
+        w.offsets = P(net.encoder.offsets)
+        w.num_levels = net.encoder.num_levels
+        w.log2_per_level_scale = float(np.log2(net.encoder.per_level_scale))
+        w.base_resolution = net.encoder.base_resolution
+        w.bound = float(net.bound)
+        w.input_w, w.input_b = P(net.input_linear.weight), P(net.input_linear.bias)
+        for l, layer in enumerate(net.pts_linears):
+            w.pts_w[l], w.pts_b[l] = P(layer.weight), P(layer.bias)
+            w.pts_gw[l], w.pts_gb[l] = P(layer.gamma.weight), P(layer.gamma.bias)
+            w.pts_bw[l], w.pts_bb[l] = P(layer.beta.weight), P(layer.beta.bias)
+        v = net.views_linears
+        w.views_w, w.views_b = P(v.weight), P(v.bias)
+        w.views_gw, w.views_gb = P(v.gamma.weight), P(v.gamma.bias)
+        w.views_bw, w.views_bb = P(v.beta.weight), P(v.beta.bias)
+        w.sigma_w, w.sigma_b = P(net.sigma_linear.weight), P(net.sigma_linear.bias)
+        w.rgb_w, w.rgb_b = P(net.rgb_linear.weight), P(net.rgb_linear.bias)
+        w.sigmoid_beta = P(self.sigmoid_beta) if self.with_sdf else None
+        return w
+
+    def _fused_check_params(self):
+        net = self.network
+        if len(net.pts_linears) != 3 or net.encoder.num_levels != 16 or \
+                net.encoder.level_dim != 2 or net.encoder_dir.degree != 4:
+            raise RuntimeError("fused ngp renderer supports the SDFace NGPSIRENGenerator only")
+        for p in self.parameters():
+            if not p.is_contiguous() or p.dtype != torch.float32:
+                raise RuntimeError("fused ngp renderer needs contiguous fp32 parameters")
+
+    def fused_forward(self, cam_poses, focal, near, far, styles, t_rand=None, encode_only=False):
+        """The whole ngp render on libsdfr (no autograd).  Returns the same tuple
+        as ``forward`` (rgb, features, sdf, mask, xyz, None)."""
+        self._fused_check_params()
+        dev = cam_poses.device
+        B = cam_poses.shape[0]
+        H = W = self.out_im_res
+        N = self.N_samples
+        cam = cam_poses.detach().float().contiguous()
+        focal = _per_face(focal, B, dev)
+        near = _per_face(near, B, dev)
+        far = _per_face(far, B, dev)
+        styles = styles.detach().float().contiguous()
+        per_sample = 0
+        if self.perturb > 0:
+            shape = (B, H, W) if self.offset_sampling else (B, H, W, N)
+            if t_rand is None:
+                t_rand = self._draw_t_rand(shape, dev)
+            t_rand = t_rand.to(device=dev, dtype=torch.float32).reshape(shape).contiguous()
+            per_sample = 0 if self.offset_sampling else 1
+        else:
+            t_rand = None
+        noise = None
+        if not self.with_sdf and self.raw_noise_std > 0:
+            noise = torch.randn(B, H, W, N, device=dev) * self.raw_noise_std
+        rgb = torch.empty(B, 3, H, W, device=dev)
+        features = torch.empty(B, 256, H, W, device=dev) if self.output_features else None
+        sdf = torch.empty(B, H, W, N, 1, device=dev) if self.return_sdf else None
+        xyz = torch.empty(B, 3, H, W, device=dev) if self.return_xyz else None
+        mask = torch.empty(B, 1, H, W, device=dev) if self.return_xyz else None
+        L = self.network.encoder.num_levels
+        ws_bytes = _lib.lib().sdfr_render_ngp_workspace_bytes(B, H, W, N, L)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        pix_x = self.i[0, 0, :].contiguous()
+        pix_y = self.j[0, :, 0].contiguous()
+        t_vals = self.t_vals.reshape(-1).contiguous()
+
+        a = _lib.NgpRenderArgs()
+        a.B, a.H, a.W, a.N = B, H, W, N
+        a.cam, a.focal, a.near_, a.far_ = (_lib.ptr(cam), _lib.ptr(focal), _lib.ptr(near),
+                                           _lib.ptr(far))
+        a.styles = _lib.ptr(styles)
+        a.pix_x, a.pix_y, a.t_vals = _lib.ptr(pix_x), _lib.ptr(pix_y), _lib.ptr(t_vals)
+        a.t_rand, a.sigma_noise = _lib.ptr(t_rand), _lib.ptr(noise)
+        a.t_rand_per_sample = per_sample
+        a.offset_sampling = int(self.offset_sampling)
+        a.static_viewdirs = int(bool(self.static_viewdirs))
+        a.z_normalize = int(self.z_normalize)
+        a.force_background = int(bool(self.force_background))
+        a.with_sdf = int(self.with_sdf)
+        a.rgb, a.features, a.sdf = _lib.ptr(rgb), _lib.ptr(features), _lib.ptr(sdf)
+        a.xyz, a.mask = _lib.ptr(xyz), _lib.ptr(mask)
+        a.workspace, a.workspace_bytes = _lib.ptr(ws), ws_bytes
+        if self.stage_events is not None:
+            for k, ev in enumerate(self.stage_events):
+                a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)
+        w = self._ngp_weight_struct()
+        fn = (_lib.lib().sdfr_render_ngp_encode_only if encode_only
+              else _lib.lib().sdfr_render_ngp_forward)
+        _lib.check(fn(ctypes.byref(w), ctypes.byref(a), _lib.stream_of(cam)),
+                   "sdfr_render_ngp_forward")
+        if encode_only:
+            return ws
+        return rgb, features, sdf, mask, xyz, None
+
+    # ---------------------------------------------------------------- API
+    def forward(self, cam_poses, focal, near, far, styles=None, return_eikonal=False,
+                t_rand=None):
+        if self._fused_ok(cam_poses, styles, return_eikonal):
+            return self.fused_forward(cam_poses, focal, near, far, styles, t_rand=t_rand)
+        rgb, features, sdf, mask, xyz, eikonal_term = self.render(
+            focal, c2w=cam_poses, near=near, far=far, styles=styles,
+            return_eikonal=return_eikonal, t_rand=t_rand)
+        rgb = rgb.permute(0, 3, 1, 2).contiguous()
+        if self.output_features:
+            features = features.permute(0, 3, 1, 2).contiguous()
+        if xyz is not None:
+            xyz = xyz.permute(0, 3, 1, 2).contiguous()
+            mask = mask.permute(0, 3, 1, 2).contiguous()
+        return rgb, features, sdf, mask, xyz, eikonal_term

@@ -1,0 +1,130 @@
+"""GPU parity: the HIP grid / SH encoder kernels against the C oracle.
+
+Index math and the trilinear accumulation follow the oracle's exact operation
+order, so forward outputs and dy_dx must be BIT-EXACT.  The table backward
+scatters with fp32 atomics (order-dependent), so it is compared with a
+tolerance; the input backward is a fixed-order reduction and is bit-exact.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden import weights as W
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _grid_gpu(sdfr, x, emb, offsets, pls, H=16, dydx=False, gridtype=0, align=False, interp=0):
+    lib = sdfr._lib
+    xt = torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+    et = torch.from_numpy(np.ascontiguousarray(emb)).to(DEV)
+    ot = torch.from_numpy(np.ascontiguousarray(offsets, dtype=np.int32)).to(DEV)
+    B, D = x.shape
+    L = len(offsets) - 1
+    C = emb.shape[1]
+    out = torch.empty(L, B, C, device=DEV)
+    dd = torch.empty(B, L * D * C, device=DEV) if dydx else None
+    lib.check(lib.lib().sdfr_grid_encode_forward(
+        lib.ptr(xt), lib.ptr(et), lib.ptr(ot), lib.ptr(out), B, D, C, L,
+        float(np.float32(np.log2(pls))), H, lib.ptr(dd), gridtype, int(align), interp,
+        lib.stream_of(xt)), "grid fwd")
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), (dd.cpu().numpy() if dydx else None)
+
+
+@pytest.fixture(scope="module")
+def table(oracle_mod):
+    offsets, pls = oracle_mod.grid_offsets()
+    return offsets, pls, W.det_table(int(offsets[-1]), 2, seed=7)
+
+
+def test_grid_forward_bit_exact_golden_inputs(sdfr, oracle_mod, golden_dir, table):
+    offsets, pls, emb = table
+    g = np.load(golden_dir / "encoders.npz")
+    x = g["grid_x"]
+    got, _ = _grid_gpu(sdfr, x, emb, offsets, pls)
+    ref, _ = oracle_mod.grid_encode_forward(x, emb, offsets, pls, 16)
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(got.transpose(1, 0, 2).reshape(len(x), -1), g["grid_out"])
+
+
+def test_grid_forward_bit_exact_large_and_dydx(sdfr, oracle_mod, table):
+    offsets, pls, emb = table
+    rng = np.random.default_rng(11)
+    x = rng.uniform(-0.05, 1.05, size=(200_003, 3)).astype(np.float32)   # ragged, some OOB
+    got, gd = _grid_gpu(sdfr, x, emb, offsets, pls, dydx=True)
+    ref, rd = oracle_mod.grid_encode_forward(x, emb, offsets, pls, 16, calc_dy_dx=True)
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(gd, rd)
+
+
+@pytest.mark.parametrize("D,C,gridtype,align,interp,log2h", [
+    (2, 4, 0, False, 0, 14),
+    (3, 1, 1, False, 0, 12),
+    (3, 8, 0, True, 1, 15),
+    (4, 2, 0, False, 0, 16),
+])
+def test_grid_forward_variants(sdfr, oracle_mod, D, C, gridtype, align, interp, log2h):
+    from oracle.oracle import grid_offsets
+    offsets, pls = grid_offsets(num_levels=8, level_dim=C, base_resolution=8,
+                                log2_hashmap_size=log2h, desired_resolution=256, input_dim=D,
+                                align_corners=align)
+    emb = W.det_uniform((int(offsets[-1]), C), -1, 1, 17)
+    rng = np.random.default_rng(D * 10 + C)
+    x = rng.uniform(0, 1, size=(5000, D)).astype(np.float32)
+    got, gd = _grid_gpu(sdfr, x, emb, offsets, pls, H=8, dydx=True, gridtype=gridtype,
+                        align=align, interp=interp)
+    ref, rd = oracle_mod.grid_encode_forward(x, emb, offsets, pls, 8, calc_dy_dx=True,
+                                             gridtype=gridtype, align_corners=align,
+                                             interp=interp)
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(gd, rd)
+
+
+def test_grid_backward(sdfr, oracle_mod, table):
+    offsets, pls, emb = table
+    rng = np.random.default_rng(5)
+    x = rng.uniform(0.2, 0.8, size=(4096, 3)).astype(np.float32)
+    xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    et = torch.nn.Parameter(torch.from_numpy(emb).to(DEV))
+    ot = torch.from_numpy(offsets).to(DEV)
+    out = sdfr.grid_encode(xt, et, ot, pls, 16, True, 0, False, 0)
+    grad = torch.from_numpy(rng.normal(size=out.shape).astype(np.float32)).to(DEV)
+    out.backward(grad)
+    _, dydx = oracle_mod.grid_encode_forward(x, emb, offsets, pls, 16, calc_dy_dx=True)
+    g_lbc = grad.view(4096, 16, 2).permute(1, 0, 2).contiguous().cpu().numpy()
+    ge, gi = oracle_mod.grid_encode_backward(g_lbc, x, emb, offsets, pls, 16, dy_dx=dydx)
+    # atomics: order-dependent fp32 sums; |sum| of a few dozen O(1) terms
+    np.testing.assert_allclose(et.grad.cpu().numpy(), ge, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(xt.grad.cpu().numpy(), gi)
+
+
+def test_grid_module_and_empty_batch(sdfr, table):
+    offsets, pls, emb = table
+    enc = sdfr.GridEncoder(desired_resolution=4096).to(DEV)
+    with torch.no_grad():
+        enc.embeddings.copy_(torch.from_numpy(emb))
+    x = torch.rand(2, 5, 3, device=DEV) * 2 - 1
+    assert enc(x, bound=2).shape == (2, 5, 32)
+    assert enc(torch.zeros(0, 3, device=DEV), bound=2).shape == (0, 32)
+
+
+def test_sh_forward_backward_bit_exact(sdfr, oracle_mod, golden_dir):
+    g = np.load(golden_dir / "encoders.npz")
+    rng = np.random.default_rng(9)
+    x = np.concatenate([g["sh_dirs"], rng.normal(size=(3001, 3)).astype(np.float32)])
+    xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    out = sdfr.sh_encode(xt, 4, True)
+    ref, dref = oracle_mod.sh_encode_forward(x, 4, calc_dy_dx=True)
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), ref)
+    np.testing.assert_array_equal(out.detach().cpu().numpy()[:1024], g["sh_out"])
+    grad = rng.normal(size=ref.shape).astype(np.float32)
+    out.backward(torch.from_numpy(grad).to(DEV))
+    np.testing.assert_array_equal(xt.grad.cpu().numpy(),
+                                  oracle_mod.sh_encode_backward(grad, x, 4, dref))
+    for deg in (1, 2, 3):
+        o = sdfr.sh_encode(torch.from_numpy(x).to(DEV), deg, False)
+        np.testing.assert_array_equal(o.cpu().numpy(), oracle_mod.sh_encode_forward(x, deg)[0])

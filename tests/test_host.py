@@ -1,0 +1,149 @@
+"""CPU: the C-ABI library, the drop-in module surface and the PyTorch parts."""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden import weights as W
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def header_symbols():
+    txt = (REPO / "include" / "sdfr.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char \*)\s*(sdfr_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol(sdfr):
+    lib = sdfr._lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 9
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(sdfr._lib.EXPORTS)
+    assert lib.sdfr_abi_version() == sdfr._lib.ABI_VERSION
+
+
+def test_argument_errors_mirror_reference(sdfr):
+    """Rejections happen before any launch, so they are checkable without a GPU."""
+    lib = sdfr._lib.lib()
+    nul = None
+    rc = lib.sdfr_grid_encode_forward(nul, nul, nul, nul, 4, 3, 3, 16, 0.5, 16, nul, 0, 0, 0, nul)
+    assert rc == sdfr._lib.SDFR_EINVAL
+    assert b"C must be 1, 2, 4, or 8" in lib.sdfr_last_error()
+    rc = lib.sdfr_grid_encode_forward(nul, nul, nul, nul, 4, 6, 2, 16, 0.5, 16, nul, 0, 0, 0, nul)
+    assert rc == sdfr._lib.SDFR_EINVAL
+    rc = lib.sdfr_sh_encode_forward(nul, nul, 4, 2, 4, nul, nul)
+    assert rc == sdfr._lib.SDFR_EINVAL and b"input dim == 3" in lib.sdfr_last_error()
+    rc = lib.sdfr_sh_encode_forward(nul, nul, 4, 3, 9, nul, nul)
+    assert rc == sdfr._lib.SDFR_EINVAL
+    rc = lib.sdfr_sh_encode_forward(nul, nul, 4, 3, 6, nul, nul)
+    assert rc == sdfr._lib.SDFR_EUNSUPPORTED
+    w, a = sdfr._lib.NgpWeights(), sdfr._lib.NgpRenderArgs()
+    rc = lib.sdfr_render_ngp_forward(ctypes.byref(w), ctypes.byref(a), nul)
+    assert rc in (sdfr._lib.SDFR_EINVAL, sdfr._lib.SDFR_EUNSUPPORTED)
+    with pytest.raises(RuntimeError, match="sdfr_render_ngp_forward"):
+        sdfr._lib.check(rc, "sdfr_render_ngp_forward")
+
+
+def test_workspace_size(sdfr):
+    lib = sdfr._lib.lib()
+    n = lib.sdfr_render_ngp_workspace_bytes(2, 64, 64, 24, 16)
+    enc = 2 * 4096 * 24 * 16 * 2 * 4
+    assert enc + 67 * 1024 * 16 <= n <= enc + 67 * 1024 * 16 + 2 * 8 * 256 * 4 + 1024
+
+
+def test_state_dict_matches_reference(sdfr, golden_dir):
+    opt = sdfr.vol_render_opt()
+    g = sdfr.Generator(opt.model, opt.rendering)
+    mine = {k: tuple(v.shape) for k, v in g.state_dict().items()}
+    ref = dict(W.golden_entries(golden_dir))
+    assert mine == ref
+
+
+def test_seeded_init_identical_to_reference(sdfr, golden_dir):
+    z = np.load(golden_dir / "init_stats.npz")
+    opt = sdfr.vol_render_opt()
+    torch.manual_seed(0)
+    g = sdfr.Generator(opt.model, opt.rendering)
+    sd = g.state_dict()
+    for k, st in zip(z["names"], z["stats"]):
+        v = sd[str(k)].double().reshape(-1)
+        mine = [v.sum().item(), (v * v).sum().item(), v[0].item(), v[-1].item()]
+        np.testing.assert_allclose(mine, st, rtol=1e-12, atol=1e-12, err_msg=str(k))
+    assert [k for k, _ in g.named_parameters()] == list(z["param_order"])
+
+
+def test_camera_matches_reference(sdfr, golden_dir):
+    g = np.load(golden_dir / "camera.npz")
+    for name, kw in [("gauss", {}), ("uniform", {"uniform": True}), ("sweep", {"sweep": True})]:
+        torch.manual_seed(123)
+        out = sdfr.generate_camera_params(64, "cpu", batch=5, **kw)
+        for k, v in zip(["ext", "focal", "near", "far", "vp"], out):
+            np.testing.assert_array_equal(v.numpy(), g[f"{name}_{k}"], err_msg=f"{name}_{k}")
+    out = sdfr.generate_camera_params(128, "cpu", batch=3,
+                                      locations=torch.from_numpy(g["loc_locations"]))
+    for k, v in zip(["ext", "focal", "near", "far", "vp"], out):
+        np.testing.assert_array_equal(v.numpy(), g[f"loc_{k}"])
+
+
+@pytest.fixture(scope="module")
+def det_generator(sdfr):
+    opt = sdfr.vol_render_opt()
+    g = sdfr.Generator(opt.model, opt.rendering)
+    W.det_init_(g)
+    return g.eval()
+
+
+def test_decoder_matches_reference(det_generator, golden_dir):
+    z = np.load(golden_dir / "generator.npz")
+    with torch.no_grad():
+        img, _ = det_generator.decoder(torch.from_numpy(z["dec_feats"]),
+                                       [torch.from_numpy(z["dec_latent"])],
+                                       randomize_noise=False)
+    # batched modulation conv(x*s, W)*demod vs the reference's per-face weights
+    np.testing.assert_allclose(img.numpy(), z["dec_img"], rtol=0, atol=2e-5)
+
+
+def test_mapping_and_mean_latent(det_generator, golden_dir):
+    z = np.load(golden_dir / "generator.npz")
+    with torch.no_grad():
+        lat = det_generator.style(torch.from_numpy(z["z"]))
+        np.testing.assert_array_equal(lat.numpy(), z["dec_latent"])
+        mean = det_generator.mean_latent(64, "cpu", z=torch.from_numpy(z["mean_z"]))
+    np.testing.assert_array_equal(mean[0].numpy(), z["mean_renderer"])
+    np.testing.assert_array_equal(mean[1].numpy(), z["mean_decoder"])
+
+
+def test_cpu_tensors_rejected_like_reference(sdfr):
+    enc = sdfr.GridEncoder(desired_resolution=4096)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        enc(torch.zeros(4, 3), bound=2)
+    sh = sdfr.SHEncoder()
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        sh(torch.zeros(4, 3))
+
+
+def test_options_defaults(sdfr):
+    opt = sdfr.vol_render_opt()
+    assert opt.rendering.N_samples == 24 and opt.rendering.perturb == 1.0
+    assert opt.model.renderer_spatial_output_dim == 64 and opt.model.size == 256
+    assert opt.camera.fov == 6 and opt.camera.dist_radius == 0.12
+    assert opt.rendering.type == "ngp" and opt.model.freeze_renderer
+    o1 = sdfr.vol_render_opt(train_renderer=True)
+    assert "no_features_output" in o1.rendering and o1.rendering.return_sdf
+
+
+def test_fused_path_selection(sdfr):
+    opt = sdfr.vol_render_opt()
+    r = sdfr.VolumeFeatureRenderer(opt.rendering, style_dim=256, out_im_res=8)
+    cam = torch.zeros(1, 3, 4)
+    st = torch.zeros(1, 256)
+    with torch.no_grad():
+        assert not r._fused_ok(cam, st, False)      # CPU tensors never take the HIP path
+    opt2 = sdfr.vol_render_opt(ngp=False)
+    r2 = sdfr.VolumeFeatureRenderer(opt2.rendering, style_dim=256, out_im_res=8)
+    assert isinstance(r2.network, sdfr.SirenGenerator)
