@@ -350,9 +350,9 @@ int sdfr_grid_encode_forward(const float *inputs, const float *embeddings,
         return fail(SDFR_EINVAL, "GridEncoding: C must be 1, 2, 4, or 8.");
     if (L == 0 || L > (uint32_t)kMaxLevels)
         return fail(SDFR_EINVAL, "GridEncoding: 1 <= L <= 64 levels supported.");
+    if (B == 0) return SDFR_OK;   // empty batch: nothing to launch (tensors may be NULL)
     if (!inputs || !embeddings || !offsets || !outputs)
         return fail(SDFR_EINVAL, "grid_encode_forward: null tensor pointer");
-    if (B == 0) return SDFR_OK;
     hipStream_t st = (hipStream_t)stream;
     LevelTable lt;
     make_level_table(L, S, H, lt);
@@ -375,11 +375,11 @@ int sdfr_grid_encode_backward(const float *grad, const float *inputs, const floa
         return fail(SDFR_EINVAL, "GridEncoding: C must be 1, 2, 4, or 8.");
     if (L == 0 || L > (uint32_t)kMaxLevels)
         return fail(SDFR_EINVAL, "GridEncoding: 1 <= L <= 64 levels supported.");
+    if (B == 0) return SDFR_OK;
     if (!grad || !inputs || !offsets || !grad_embeddings)
         return fail(SDFR_EINVAL, "grid_encode_backward: null tensor pointer");
     if ((dy_dx == nullptr) != (grad_inputs == nullptr))
         return fail(SDFR_EINVAL, "grid_encode_backward: dy_dx and grad_inputs go together");
-    if (B == 0) return SDFR_OK;
     hipStream_t st = (hipStream_t)stream;
     LevelTable lt;
     make_level_table(L, S, H, lt);
@@ -396,8 +396,8 @@ int sdfr_sh_encode_forward(const float *inputs, float *outputs, uint32_t B, uint
     if (D != 3) return fail(SDFR_EINVAL, "SH encoder only support input dim == 3");
     if (C < 1 || C > 8) return fail(SDFR_EINVAL, "SH encoder only supports degree in [1, 8]");
     if (C > 4) return fail(SDFR_EUNSUPPORTED, "sdfr: SH degree > 4 not implemented");
-    if (!inputs || !outputs) return fail(SDFR_EINVAL, "sh_encode_forward: null tensor pointer");
     if (B == 0) return SDFR_OK;
+    if (!inputs || !outputs) return fail(SDFR_EINVAL, "sh_encode_forward: null tensor pointer");
     hipLaunchKernelGGL(sh_fwd_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        inputs, outputs, dy_dx, B, C);
     return check_launch("sh_encode_forward");
@@ -409,9 +409,9 @@ int sdfr_sh_encode_backward(const float *grad, const float *inputs, uint32_t B, 
     if (D != 3) return fail(SDFR_EINVAL, "SH encoder only support input dim == 3");
     if (C < 1 || C > 8) return fail(SDFR_EINVAL, "SH encoder only supports degree in [1, 8]");
     if (C > 4) return fail(SDFR_EUNSUPPORTED, "sdfr: SH degree > 4 not implemented");
+    if (B == 0) return SDFR_OK;
     if (!grad || !dy_dx || !grad_inputs)
         return fail(SDFR_EINVAL, "sh_encode_backward: null tensor pointer");
-    if (B == 0) return SDFR_OK;
     hipLaunchKernelGGL(sh_bwd_kernel, dim3((B * 3 + 255) / 256), dim3(256), 0,
                        (hipStream_t)stream, grad, dy_dx, grad_inputs, B, C);
     return check_launch("sh_encode_backward");

@@ -212,6 +212,7 @@ struct FieldArgs {
     float *rgb, *features, *sdf, *xyz, *mask;
 };
 
+constexpr uint32_t kCst = 9 * kW;              // LDS constants: bias[5], sigma_w, rgb_w[3]
 constexpr int kWaves = 4;                       // 1 wave per SIMD, 512 VGPR+AGPR
 constexpr int kThreads = kWaves * 64;
 constexpr int kStageF4 = kSliceF4 / kThreads;   // float4 staged per thread per slice
@@ -276,12 +277,20 @@ struct Ring {
     uint32_t tid;
 };
 
+struct NoSide {
+    __device__ __forceinline__ void operator()() const {}
+};
+
 // One K-slice: stage slice it+1 into LDS, prefetch slice it+2, run the
 // 16 t_out x 4 MFMAs of slice `it` against the B operand quad, barrier.
 // A-operand quads are read four output tiles at a time, one group ahead,
 // and the four accumulators of a group are interleaved so no MFMA waits on
 // its predecessor (16x16x4 f32: 32-cycle issue, 40-cycle dependency).
-__device__ __forceinline__ void ring_step(Ring &R, f4 (&acc)[16], const f4 bq) {
+// `side` is register work (the previous layer's activation of one tile, the
+// compositing math...) placed in the same basic block as the MFMAs, so the
+// scheduler issues it in the MFMA shadow instead of after the layer.
+template <class Side>
+__device__ __forceinline__ void ring_step(Ring &R, f4 (&acc)[16], const f4 bq, Side &&side) {
     const uint32_t cur = R.it % 3u, nxt = (R.it + 1u) % 3u;
 #pragma unroll
     for (int i = 0; i < kStageF4; ++i) R.lds[nxt * kSliceF4 + R.tid + i * kThreads] = R.st[i];
@@ -311,8 +320,21 @@ __device__ __forceinline__ void ring_step(Ring &R, f4 (&acc)[16], const f4 bq) {
             for (int i = 0; i < 4; ++i) a[i] = an[i];
         }
     }
+    side();
     __syncthreads();
     ++R.it;
+}
+
+// One tile of a FiLM activation, in place: x = sin(gamma*x + beta) with the
+// reference's two roundings (sdf_model.py:67).
+__device__ __forceinline__ void film_tile(f4 &x, const float *gam, const float *bet, int t,
+                                          uint32_t g) {
+    const f4 gm = *reinterpret_cast<const f4 *>(gam + 16 * t + 4 * g);
+    const f4 bt = *reinterpret_cast<const f4 *>(bet + 16 * t + 4 * g);
+    x.x = sin_cw(__fadd_rn(__fmul_rn(gm.x, x.x), bt.x));
+    x.y = sin_cw(__fadd_rn(__fmul_rn(gm.y, x.y), bt.y));
+    x.z = sin_cw(__fadd_rn(__fmul_rn(gm.z, x.z), bt.z));
+    x.w = sin_cw(__fadd_rn(__fmul_rn(gm.w, x.w), bt.w));
 }
 
 __device__ __forceinline__ void init_bias(f4 (&acc)[16], const float *bias, uint32_t g) {
@@ -357,7 +379,8 @@ __device__ __forceinline__ float dot_feat(const f4 (&act)[16], const float *w, u
 }
 
 __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs a) {
-    __shared__ f4 ring_lds[3 * kSliceF4];   // 48 KB
+    __shared__ f4 ring_lds[3 * kSliceF4];   // 48 KB weight ring
+    __shared__ float cst[kCst];              // 9 KB biases + sigma/rgb rows
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t n = lane & 15u, g = lane >> 4;
     const GeomArgs &G = a.g;
@@ -384,7 +407,7 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
         const float vn = norm3_torch(v0, v1, v2);
         shq = sh_quad(__fdiv_rn(v0, vn), __fdiv_rn(v1, vn), __fdiv_rn(v2, vn), g);
     }
-    const float beta_s = a.sigmoid_beta[0];
+    const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
     const float *film = a.film + (size_t)b * kFilm * 2 * kW;
 
     Ring R;
@@ -392,6 +415,14 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
     R.packed = a.packed;
     R.tid = tid;
     R.it = 0;
+    // per-network constants (5 biases, sigma_linear and rgb_linear rows) in LDS
+    for (uint32_t i = tid; i < kCst; i += kThreads) {
+        float v;
+        if (i < 5 * kW) v = a.bias[i / kW][i % kW];
+        else if (i < 6 * kW) v = a.sigma_w[i - 5 * kW];
+        else v = a.rgb_w[i - 6 * kW];
+        cst[i] = v;
+    }
     // prologue: slice 0 -> slot 0, slice 1 -> regs
 #pragma unroll
     for (int i = 0; i < kStageF4; ++i) R.lds[tid + i * kThreads] = a.packed[tid + i * kThreads];
@@ -407,60 +438,100 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
 
     const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
     float z = sample_z(G.sc, nr, fr, ray_index, 0);
+    const float *f0g = film, *f0b = film + kW, *f1g = film + 2 * kW, *f1b = film + 3 * kW;
+    const float *f2g = film + 4 * kW, *f2b = film + 5 * kW, *f3g = film + 6 * kW,
+                *f3b = film + 7 * kW;
+    const float *bias_l = cst;                        // [5][256] in LDS
+    const float *sig_w = cst + 5 * kW, *rgb_w = cst + 6 * kW;
+    const float sig_b = a.sigma_b[0];
+    const float rgb_b0 = a.rgb_b[0], rgb_b1 = a.rgb_b[1], rgb_b2 = a.rgb_b[2];
+
+    // hash-grid features of sample 0 (levels 2g,2g+1 | 8+2g,9+2g of this lane group)
+    size_t sid = (size_t)(tile * G.N) * kTileRays + n;
+    float2 e0 = enc2[(2 * g) * (size_t)G.S_total + sid];
+    float2 e1 = enc2[(2 * g + 1) * (size_t)G.S_total + sid];
+    float2 e2 = enc2[(8 + 2 * g) * (size_t)G.S_total + sid];
+    float2 e3 = enc2[(9 + 2 * g) * (size_t)G.S_total + sid];
 
     for (uint32_t s = 0; s < G.N; ++s) {
-        const uint32_t sid = (tile * G.N + s) * kTileRays + n;
-        const float2 e0 = enc2[(size_t)(2 * g) * G.S_total + sid];
-        const float2 e1 = enc2[(size_t)(2 * g + 1) * G.S_total + sid];
-        const float2 e2 = enc2[(size_t)(8 + 2 * g) * G.S_total + sid];
-        const float2 e3 = enc2[(size_t)(9 + 2 * g) * G.S_total + sid];
+        const f4 in_lo = f4{e0.x, e0.y, e1.x, e1.y}, in_hi = f4{e2.x, e2.y, e3.x, e3.y};
         const float z_next = (s + 1 < G.N) ? sample_z(G.sc, nr, fr, ray_index, s + 1) : 0.0f;
-
-        f4 acc[16], act[16];
-        // layer 0: input_linear (32 -> 256), LinearLayer(std 1, bias 0)
-        init_bias(acc, a.bias[0], g);
-        ring_step(R, acc, f4{e0.x, e0.y, e1.x, e1.y});
-        ring_step(R, acc, f4{e2.x, e2.y, e3.x, e3.y});
+        float sdf = 0.0f, w = 0.0f;
+        f4 X[16], Y[16];
+        // Software pipeline: layer l accumulates into one register set while
+        // the previous layer's tiles are activated (sin) one slice ahead of
+        // their use as B operands, inside the MFMA stream.
+        // layer 0: input_linear (32 -> 256), identity LinearLayer -> X
+        init_bias(X, bias_l, g);
+        ring_step(R, X, in_lo, [&] {
+            if (s + 1 < G.N) {                        // prefetch the next sample's features
+                sid += kTileRays;
+                e0 = enc2[(2 * g) * (size_t)G.S_total + sid];
+                e1 = enc2[(2 * g + 1) * (size_t)G.S_total + sid];
+                e2 = enc2[(8 + 2 * g) * (size_t)G.S_total + sid];
+                e3 = enc2[(9 + 2 * g) * (size_t)G.S_total + sid];
+            }
+        });
+        ring_step(R, X, in_hi, NoSide{});
+        // layer 1: FiLM pts_linears.0 -> Y
+        init_bias(Y, bias_l + kW, g);
 #pragma unroll
-        for (int t = 0; t < 16; ++t) act[t] = acc[t];
-        // layers 1..3: FiLM SIREN 256 -> 256
+        for (int t = 0; t < 16; ++t)
+            ring_step(R, Y, X[t], [&] {
+                if (t == 15) film_tile(Y[0], f0g, f0b, 0, g);
+            });
+        // layer 2: FiLM pts_linears.1 -> X
+        init_bias(X, bias_l + 2 * kW, g);
 #pragma unroll
-        for (int l = 0; l < 3; ++l) {
-            init_bias(acc, a.bias[1 + l], g);
+        for (int t = 0; t < 16; ++t)
+            ring_step(R, X, Y[t], [&] {
+                if (t < 15) film_tile(Y[t + 1], f0g, f0b, t + 1, g);
+                else film_tile(X[0], f1g, f1b, 0, g);
+            });
+        // layer 3: FiLM pts_linears.2 -> Y
+        init_bias(Y, bias_l + 3 * kW, g);
 #pragma unroll
-            for (int t = 0; t < 16; ++t) ring_step(R, acc, act[t]);
-            film_act(act, acc, film + (l * 2 + 0) * kW, film + (l * 2 + 1) * kW, g);
-        }
-        // sigma_linear (256 -> 1)
-        const float sdf = __fadd_rn(dot_feat(act, a.sigma_w, g), a.sigma_b[0]);
-        // layer 4: views FiLM ([h, SH] 272 -> 256)
-        init_bias(acc, a.bias[4], g);
+        for (int t = 0; t < 16; ++t)
+            ring_step(R, Y, X[t], [&] {
+                if (t < 15) film_tile(X[t + 1], f1g, f1b, t + 1, g);
+                else film_tile(Y[0], f2g, f2b, 0, g);
+            });
+        // layer 4: views FiLM ([h3, SH] 272 -> 256) -> X; sigma_linear and the
+        // sample's compositing weight ride in the last h3 slice
+        init_bias(X, bias_l + 4 * kW, g);
 #pragma unroll
-        for (int t = 0; t < 16; ++t) ring_step(R, acc, act[t]);
-        ring_step(R, acc, shq);
-        film_act(act, acc, film + 6 * kW, film + 7 * kW, g);
-        // rgb_linear (256 -> 3)
-        const float r0 = __fadd_rn(dot_feat(act, a.rgb_w, g), a.rgb_b[0]);
-        const float r1 = __fadd_rn(dot_feat(act, a.rgb_w + kW, g), a.rgb_b[1]);
-        const float r2 = __fadd_rn(dot_feat(act, a.rgb_w + 2 * kW, g), a.rgb_b[2]);
-
-        // volume_integration (sdf_model.py:236-301), front to back
-        const float dist = (s + 1 < G.N) ? __fmul_rn(__fsub_rn(z_next, z), dnorm)
-                                         : __fmul_rn(1e10f, dnorm);
-        float alpha;
-        if (a.with_sdf) {
-            const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
-            alpha = 1.0f - expf(-sig * dist);
-        } else {
-            float raw = sdf;
-            if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + s];
-            const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
-            alpha = 1.0f - expf(-sp * dist);
-        }
-        float w = alpha * T;
-        if (a.force_background && s + 1 == G.N) w = 1.0f - wsum;
-        T = T * ((1.0f - alpha) + 1e-10f);
-        wsum += w;
+        for (int t = 0; t < 16; ++t)
+            ring_step(R, X, Y[t], [&] {
+                if (t < 15) {
+                    film_tile(Y[t + 1], f2g, f2b, t + 1, g);
+                } else {
+                    sdf = __fadd_rn(dot_feat(Y, sig_w, g), sig_b);
+                    // volume_integration (sdf_model.py:236-301), front to back
+                    const float dist = (s + 1 < G.N) ? __fmul_rn(__fsub_rn(z_next, z), dnorm)
+                                                     : __fmul_rn(1e10f, dnorm);
+                    float alpha;
+                    if (a.with_sdf) {
+                        const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
+                        alpha = 1.0f - expf(-sig * dist);
+                    } else {
+                        float raw = sdf;
+                        if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + s];
+                        const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+                        alpha = 1.0f - expf(-sp * dist);
+                    }
+                    w = alpha * T;
+                    if (a.force_background && s + 1 == G.N) w = 1.0f - wsum;
+                    T = T * ((1.0f - alpha) + 1e-10f);
+                    wsum += w;
+                }
+            });
+        ring_step(R, X, shq, NoSide{});
+        // colour features f = sin(gamma_v * . + beta_v); rgb_linear; compositing
+#pragma unroll
+        for (int t = 0; t < 16; ++t) film_tile(X[t], f3g, f3b, t, g);
+        const float r0 = __fadd_rn(dot_feat(X, rgb_w, g), rgb_b0);
+        const float r1 = __fadd_rn(dot_feat(X, rgb_w + kW, g), rgb_b1);
+        const float r2 = __fadd_rn(dot_feat(X, rgb_w + 2 * kW, g), rgb_b2);
         w_last = w;
         racc0 = __fmaf_rn(w, sigmoidf_(r0), racc0);
         racc1 = __fmaf_rn(w, sigmoidf_(r1), racc1);
@@ -473,10 +544,10 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
         if (a.features) {
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
-                facc[t].x = __fmaf_rn(w, act[t].x, facc[t].x);
-                facc[t].y = __fmaf_rn(w, act[t].y, facc[t].y);
-                facc[t].z = __fmaf_rn(w, act[t].z, facc[t].z);
-                facc[t].w = __fmaf_rn(w, act[t].w, facc[t].w);
+                facc[t].x = __fmaf_rn(w, X[t].x, facc[t].x);
+                facc[t].y = __fmaf_rn(w, X[t].y, facc[t].y);
+                facc[t].z = __fmaf_rn(w, X[t].z, facc[t].z);
+                facc[t].w = __fmaf_rn(w, X[t].w, facc[t].w);
             }
         }
         if (a.sdf && ray_ok && g == 0) a.sdf[(size_t)ray_index * G.N + s] = sdf;
@@ -543,9 +614,11 @@ static int validate(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a) {
         return fail(SDFR_EINVAL, "render_ngp: required pointer is null");
     const void *need[] = {w->embeddings, w->offsets, w->input_w, w->input_b, w->views_w,
                           w->views_b, w->views_gw, w->views_gb, w->views_bw, w->views_bb,
-                          w->sigma_w, w->sigma_b, w->rgb_w, w->rgb_b, w->sigmoid_beta};
+                          w->sigma_w, w->sigma_b, w->rgb_w, w->rgb_b};
     for (const void *p : need)
         if (!p) return fail(SDFR_EINVAL, "render_ngp: weight pointer is null");
+    if (a->with_sdf && !w->sigmoid_beta)
+        return fail(SDFR_EINVAL, "render_ngp: sigmoid_beta is required when with_sdf");
     for (int l = 0; l < 3; ++l)
         if (!w->pts_w[l] || !w->pts_b[l] || !w->pts_gw[l] || !w->pts_gb[l] || !w->pts_bw[l] ||
             !w->pts_bb[l])

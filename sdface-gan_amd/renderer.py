@@ -385,13 +385,14 @@ class VolumeFeatureRenderer(nn.Module):
                 lower = z_vals.detach()
                 if t_rand is None:
                     t_rand = self._draw_t_rand((batch, h, w), z_vals.device)
-                t_rand = t_rand.reshape(batch, h, w, 1)
+                t_rand = t_rand.to(z_vals.device).reshape(batch, h, w, 1)
             else:
                 mids = .5 * (z_vals[..., 1:] + z_vals[..., :-1])
                 upper = torch.cat([mids, z_vals[..., -1:]], -1)
                 lower = torch.cat([z_vals[..., :1], mids], -1)
                 if t_rand is None:
                     t_rand = self._draw_t_rand(z_vals.shape, z_vals.device)
+                t_rand = t_rand.to(z_vals.device).reshape(z_vals.shape)
             z_vals = lower + (upper - lower) * t_rand
         pts = rays_o.unsqueeze(3) + rays_d.unsqueeze(3) * z_vals.unsqueeze(-1)
         if return_eikonal:

@@ -18,21 +18,25 @@ from tests.golden import weights as W
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
-# max |HIP - reference| bounds (outputs are O(1): rgb in [-1,1], features = sum w*sin)
-TOL = {"rgb": 2e-4, "features": 2e-4, "sdf": 2e-4, "xyz": 2e-5, "mask": 2e-4}
-# and the mean |error| bound, which catches systematic drift a max bound can hide
-TOL_MEAN = 2e-6
+# (max, mean) |HIP - reference| bounds.  Measured on MI355X (round 1, all cases
+# below): features <= 2.9e-5 / 3.1e-6, rgb <= 4.2e-7 / 1e-7, sdf <= 9.4e-7 /
+# 1.7e-7, xyz <= 7.8e-8 / 1.0e-8, mask <= 4.2e-7 / 1.1e-7, 256^2 image
+# <= 1.7e-5 / 2.7e-6.  The mean bound catches systematic drift a max bound hides.
+TOL = {"rgb": (2e-6, 5e-7), "features": (1.2e-4, 1.5e-5), "sdf": (5e-6, 1e-6),
+       "xyz": (5e-7, 6e-8), "mask": (2e-6, 5e-7), "image": (1e-4, 1.5e-5),
+       # the op-by-op PyTorch-ROCm path (training / eikonal), not the HIP kernels
+       "module_rgb": (1e-3, 1e-4), "module_features": (2e-3, 2e-4)}
 
 _record = {}
 
 
-def _cmp(name, key, got, ref, tol=None):
+def _cmp(name, key, got, ref, tol_key=None):
     got = np.asarray(got, np.float64).reshape(np.shape(ref))
     err = np.abs(got - ref)
     _record[f"{name}:{key}"] = [float(err.max()), float(err.mean())]
-    tol = TOL[key] if tol is None else tol
-    assert err.max() <= tol, f"{name}:{key} max err {err.max():.3e} > {tol:.1e}"
-    assert err.mean() <= max(TOL_MEAN, tol / 50), f"{name}:{key} mean err {err.mean():.3e}"
+    tmax, tmean = TOL[tol_key or key]
+    assert err.max() <= tmax, f"{name}:{key} max err {err.max():.3e} > {tmax:.1e}"
+    assert err.mean() <= tmean, f"{name}:{key} mean err {err.mean():.3e} > {tmean:.1e}"
 
 
 def teardown_module(module):
@@ -54,7 +58,9 @@ def make_renderer(sdfr, sd, res, N, **flags):
     for k, v in flags.items():
         r[k] = v
     ren = sdfr.VolumeFeatureRenderer(r, style_dim=256, out_im_res=res)
-    ren.load_state_dict({k[len("renderer."):]: v for k, v in sd.items()}, strict=True)
+    own = ren.state_dict()
+    ren.load_state_dict({k[len("renderer."):]: v for k, v in sd.items()
+                         if k[len("renderer."):] in own}, strict=True)
     return ren.to(DEV).eval()
 
 
@@ -183,19 +189,26 @@ def test_out_of_bound_samples(sdfr, oracle_mod, renderer_sd):
     _cmp("oob", "features", feat.cpu().numpy(), o["features"].numpy())
 
 
-def test_fused_equals_unfused_module_path(sdfr, renderer_sd):
-    """The autograd path (HIP encoders + torch MLP) and the fused kernel agree."""
+def test_fused_equals_unfused_module_path(sdfr, oracle_mod, renderer_sd):
+    """The autograd path (HIP encoders + PyTorch-ROCm MLP/compositing ops) and the
+    fused kernel both match the oracle; the module path carries torch-ROCm's own
+    GEMM/transcendental rounding, hence its separate, looser bound."""
     ren = make_renderer(sdfr, renderer_sd, 16, 24)
     torch.manual_seed(8)
-    ext, focal, near, far, _ = sdfr.generate_camera_params(16, DEV, batch=2)
-    lat = torch.from_numpy(W.det_uniform((2, 256), -1, 1, 8)).to(DEV)
+    ext, focal, near, far, _ = sdfr.generate_camera_params(16, "cpu", batch=2)
+    lat = torch.from_numpy(W.det_uniform((2, 256), -1, 1, 8))
     tr = torch.rand(2, 16, 16)
+    args = [t.to(DEV) for t in (ext, focal, near, far)]
     with torch.no_grad():
-        f = ren(ext, focal, near, far, styles=lat, t_rand=tr)
+        f = ren(*args, styles=lat.to(DEV), t_rand=tr)
         ren.use_fused = False
-        u = ren(ext, focal, near, far, styles=lat, t_rand=tr)
-    _cmp("fused_vs_module", "rgb", f[0].cpu().numpy(), u[0].cpu().numpy())
-    _cmp("fused_vs_module", "features", f[1].cpu().numpy(), u[1].cpu().numpy())
+        u = ren(*args, styles=lat.to(DEV), t_rand=tr)
+    o = oracle_mod.render_ngp(renderer_sd, ext.numpy(), focal.numpy(), near.numpy(),
+                              far.numpy(), lat.numpy(), N=24, res=16, t_rand=tr.numpy())
+    _cmp("fused", "rgb", f[0].cpu().numpy(), o["rgb"].numpy())
+    _cmp("fused", "features", f[1].cpu().numpy(), o["features"].numpy())
+    _cmp("module", "rgb", u[0].cpu().numpy(), o["rgb"].numpy(), "module_rgb")
+    _cmp("module", "features", u[1].cpu().numpy(), o["features"].numpy(), "module_features")
 
 
 def test_generator_vs_reference_golden(sdfr, golden_dir):
@@ -208,9 +221,9 @@ def test_generator_vs_reference_golden(sdfr, golden_dir):
     with torch.no_grad():
         rgb, thumb = g([t("z")], t("ext"), t("focal"), t("near"), t("far"),
                        randomize_noise=False, t_rand=torch.from_numpy(z["t_rand"]))
-    _cmp("generator", "rgb", thumb.cpu().numpy(), z["thumb"])
+    _cmp("generator", "thumb", thumb.cpu().numpy(), z["thumb"], "rgb")
     # the 256^2 image goes through the PyTorch-ROCm decoder on top (MIOpen fp32)
-    _cmp("generator", "rgb", rgb.cpu().numpy(), z["rgb"], tol=2e-3)
+    _cmp("generator", "image", rgb.cpu().numpy(), z["rgb"])
 
 
 def test_batch_consistency(sdfr, renderer_sd):
