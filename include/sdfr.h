@@ -159,6 +159,19 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w,
 int sdfr_render_ngp_encode_only(const sdfr_ngp_weights *w,
                                 const sdfr_ngp_render_args *a, void *stream);
 
+/* Profiling hook: select an ablated build of the field kernel for the NEXT
+ * sdfr_render_ngp_forward calls (process-global).  0 = the product kernel;
+ * 1 no barrier, 2 no LDS A-operand reads, 4 no weight staging, 8 no
+ * activations, 15 MFMA only.  Non-zero variants produce wrong outputs and
+ * exist only to attribute kernel time ("Field kernel anatomy"). */
+int sdfr_debug_set_field_variant(int variant);
+
+/* Accuracy probe for the two device sin implementations the field kernel can
+ * use (software Cody-Waite + polynomial, hardware v_sin_f32 after reduction):
+ * out_cw[i] = sin_cw(x[i]), out_hw[i] = sin_hw(x[i]), n elements. */
+int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t n,
+                         void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,7 +31,7 @@ EXPORTS = (
     "sdfr_grid_encode_forward", "sdfr_grid_encode_backward",
     "sdfr_sh_encode_forward", "sdfr_sh_encode_backward",
     "sdfr_render_ngp_workspace_bytes", "sdfr_render_ngp_forward",
-    "sdfr_render_ngp_encode_only",
+    "sdfr_render_ngp_encode_only", "sdfr_debug_set_field_variant", "sdfr_debug_sin_probe",
 )
 
 
@@ -91,6 +91,8 @@ def lib():
                                           ctypes.POINTER(NgpRenderArgs), _vp]
     L.sdfr_render_ngp_encode_only.argtypes = [ctypes.POINTER(NgpWeights),
                                               ctypes.POINTER(NgpRenderArgs), _vp]
+    L.sdfr_debug_set_field_variant.argtypes = [_int]
+    L.sdfr_debug_sin_probe.argtypes = [_vp, _vp, _vp, _u32, _vp]
     v = L.sdfr_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"libsdfr ABI {v} != expected {ABI_VERSION}; rebuild the library")

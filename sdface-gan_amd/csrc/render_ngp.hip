@@ -242,6 +242,30 @@ __device__ __forceinline__ float sin_cw(float x) {
     return (q & 2) ? -v : v;
 }
 
+// sin via the hardware v_sin_f32 (argument in revolutions, |u| <= 0.5 after an
+// fma Cody-Waite reduction by 2pi): 6 VALU + 1 transcendental.  Accuracy is
+// measured against float64 by tests/test_gpu_encoders.py::test_sin_accuracy.
+__device__ __forceinline__ float sin_hw(float x) {
+    const float k = __builtin_rintf(x * 0.159154943091895336f);
+    float r = __fmaf_rn(-k, 6.28318548202514648f, x);
+    r = __fmaf_rn(-k, -1.74845553146951752e-7f, r);
+    return __builtin_amdgcn_sinf(r * 0.159154943091895336f);
+}
+
+// The FiLM activation's sin: hardware v_sin_f32 after reduction (max |err|
+// 3.7e-7 on |x| <= 200, measured; 1 transcendental + 6 VALU) instead of the
+// polynomial (9e-8, ~17 VALU).  Both errors sit an order of magnitude below
+// the fp32 summation-order differences of the MFMA GEMMs they feed.
+__device__ __forceinline__ float kSin(float x) { return sin_hw(x); }
+
+__global__ void sin_probe_kernel(const float *__restrict__ x, float *__restrict__ cw,
+                                 float *__restrict__ hw, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    cw[i] = sin_cw(x[i]);
+    hw[i] = sin_hw(x[i]);
+}
+
 // SH degree 4 coefficients 4g..4g+3 of a unit direction (shencoder.cu:50-68)
 __device__ __forceinline__ f4 sh_quad(float x, float y, float z, uint32_t g) {
     const float xy = __fmul_rn(x, y), xz = __fmul_rn(x, z), yz = __fmul_rn(y, z);
@@ -289,52 +313,74 @@ struct NoSide {
 // `side` is register work (the previous layer's activation of one tile, the
 // compositing math...) placed in the same basic block as the MFMAs, so the
 // scheduler issues it in the MFMA shadow instead of after the layer.
-template <class Side>
+// Ablation variants (profiling builds only, selected by
+// sdfr_debug_set_field_variant; V = 0 is the product): bit 0 drops the
+// barrier, bit 1 the LDS A-operand reads, bit 2 the ring staging, bit 3 the
+// activations.  Any V != 0 computes wrong results by construction.
+enum : int { ABL_BARRIER = 1, ABL_LDSREAD = 2, ABL_STAGE = 4, ABL_ACT = 8 };
+
+template <int V, class Side>
 __device__ __forceinline__ void ring_step(Ring &R, f4 (&acc)[16], const f4 bq, Side &&side) {
     const uint32_t cur = R.it % 3u, nxt = (R.it + 1u) % 3u;
-#pragma unroll
-    for (int i = 0; i < kStageF4; ++i) R.lds[nxt * kSliceF4 + R.tid + i * kThreads] = R.st[i];
-    const uint32_t pf = (R.it + 2u) % kSlices;
-#pragma unroll
-    for (int i = 0; i < kStageF4; ++i) R.st[i] = R.packed[pf * kSliceF4 + R.tid + i * kThreads];
+    // all 16 A-operand quads of this slice are read up front (one LDS latency
+    // per slice, nothing queued ahead of them in the LDS pipe), then 4
+    // accumulators are interleaved per MFMA group
     const f4 *A = R.lds + cur * kSliceF4 + (R.tid & 63u);
-    f4 a[4], an[4];
+    f4 a[16];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = A[i * 64];
+    for (int i = 0; i < 16; ++i) a[i] = (V & ABL_LDSREAD) ? bq * (float)(i + 1) : A[i * 64];
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
-        if (grp < 3) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) an[i] = A[(4 * grp + 4 + i) * 64];
-        }
+        for (int i = 0; i < 4; ++i)
+            acc[4 * grp + i] = mfma4(a[4 * grp + i].x, bq.x, acc[4 * grp + i]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[4 * grp + i] = mfma4(a[i].x, bq.x, acc[4 * grp + i]);
+        for (int i = 0; i < 4; ++i)
+            acc[4 * grp + i] = mfma4(a[4 * grp + i].y, bq.y, acc[4 * grp + i]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[4 * grp + i] = mfma4(a[i].y, bq.y, acc[4 * grp + i]);
+        for (int i = 0; i < 4; ++i)
+            acc[4 * grp + i] = mfma4(a[4 * grp + i].z, bq.z, acc[4 * grp + i]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[4 * grp + i] = mfma4(a[i].z, bq.z, acc[4 * grp + i]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[4 * grp + i] = mfma4(a[i].w, bq.w, acc[4 * grp + i]);
-        if (grp < 3) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = an[i];
-        }
+        for (int i = 0; i < 4; ++i)
+            acc[4 * grp + i] = mfma4(a[4 * grp + i].w, bq.w, acc[4 * grp + i]);
     }
     side();
-    __syncthreads();
+    if constexpr (!(V & ABL_STAGE)) {
+        // slice it+1 (loaded at the end of the previous slice, so it had this
+        // slice's whole MFMA body to land) -> LDS slot; then slice it+2 -> regs.
+        // Writing at the END keeps the LDS writes out of the way of this
+        // slice's A-operand reads.
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < kStageF4; ++i) R.lds[nxt * kSliceF4 + R.tid + i * kThreads] = R.st[i];
+        const uint32_t pf = (R.it + 2u) % kSlices;
+#pragma unroll
+        for (int i = 0; i < kStageF4; ++i)
+            R.st[i] = R.packed[pf * kSliceF4 + R.tid + i * kThreads];
+    }
+    if constexpr (!(V & ABL_BARRIER)) __syncthreads();
     ++R.it;
 }
 
+// Keep a register value's computation on this side of the next barrier: pure
+// VALU work is otherwise free to float past s_barrier to its first use (the
+// next slice), which would serialise it in front of that slice's MFMAs.
+__device__ __forceinline__ void pin(f4 &x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(float &x) { asm volatile("" : "+v"(x)); }
+
 // One tile of a FiLM activation, in place: x = sin(gamma*x + beta) with the
 // reference's two roundings (sdf_model.py:67).
+template <int V>
 __device__ __forceinline__ void film_tile(f4 &x, const float *gam, const float *bet, int t,
                                           uint32_t g) {
+    if constexpr ((V & ABL_ACT) != 0) return;
     const f4 gm = *reinterpret_cast<const f4 *>(gam + 16 * t + 4 * g);
     const f4 bt = *reinterpret_cast<const f4 *>(bet + 16 * t + 4 * g);
-    x.x = sin_cw(__fadd_rn(__fmul_rn(gm.x, x.x), bt.x));
-    x.y = sin_cw(__fadd_rn(__fmul_rn(gm.y, x.y), bt.y));
-    x.z = sin_cw(__fadd_rn(__fmul_rn(gm.z, x.z), bt.z));
-    x.w = sin_cw(__fadd_rn(__fmul_rn(gm.w, x.w), bt.w));
+    x.x = kSin(__fadd_rn(__fmul_rn(gm.x, x.x), bt.x));
+    x.y = kSin(__fadd_rn(__fmul_rn(gm.y, x.y), bt.y));
+    x.z = kSin(__fadd_rn(__fmul_rn(gm.z, x.z), bt.z));
+    x.w = kSin(__fadd_rn(__fmul_rn(gm.w, x.w), bt.w));
+    pin(x);
 }
 
 __device__ __forceinline__ void init_bias(f4 (&acc)[16], const float *bias, uint32_t g) {
@@ -378,9 +424,12 @@ __device__ __forceinline__ float dot_feat(const f4 (&act)[16], const float *w, u
     return group_sum(p);
 }
 
+template <int V>
 __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs a) {
     __shared__ f4 ring_lds[3 * kSliceF4];   // 48 KB weight ring
     __shared__ float cst[kCst];              // 9 KB biases + sigma/rgb rows
+    __shared__ float film_lds[kWaves][kFilm * 2 * kW];   // 32 KB: each wave's face
+    __shared__ f4 facc_lds[kWaves][16 * 64];              // 64 KB: feature accumulators
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t n = lane & 15u, g = lane >> 4;
     const GeomArgs &G = a.g;
@@ -408,7 +457,15 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
         shq = sh_quad(__fdiv_rn(v0, vn), __fdiv_rn(v1, vn), __fdiv_rn(v2, vn), g);
     }
     const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
-    const float *film = a.film + (size_t)b * kFilm * 2 * kW;
+    {
+        // this wave's face FiLM vectors (gamma/beta x 4 layers) -> LDS (own region,
+        // read back only by this wave: no barrier needed beyond the prologue one)
+        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * kFilm * 2 * kW);
+        f4 *dst = reinterpret_cast<f4 *>(film_lds[wave]);
+#pragma unroll
+        for (uint32_t i = lane; i < kFilm * 2 * kW / 4; i += 64) dst[i] = src[i];
+    }
+    const float *film = film_lds[wave];
 
     Ring R;
     R.lds = ring_lds;
@@ -430,9 +487,11 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
     for (int i = 0; i < kStageF4; ++i) R.st[i] = a.packed[kSliceF4 + tid + i * kThreads];
     __syncthreads();
 
-    f4 facc[16];
+    // composited features sum_s w_s f_s live in this wave's LDS region (lane-
+    // contiguous float4, conflict-free), not in 64 VGPRs per lane
+    f4 *facc = facc_lds[wave];
 #pragma unroll
-    for (int t = 0; t < 16; ++t) facc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int t = 0; t < 16; ++t) facc[t * 64 + lane] = f4{0.0f, 0.0f, 0.0f, 0.0f};
     float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
     float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
 
@@ -463,7 +522,7 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
         // their use as B operands, inside the MFMA stream.
         // layer 0: input_linear (32 -> 256), identity LinearLayer -> X
         init_bias(X, bias_l, g);
-        ring_step(R, X, in_lo, [&] {
+        ring_step<V>(R, X, in_lo, [&] {
             if (s + 1 < G.N) {                        // prefetch the next sample's features
                 sid += kTileRays;
                 e0 = enc2[(2 * g) * (size_t)G.S_total + sid];
@@ -472,38 +531,38 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
                 e3 = enc2[(9 + 2 * g) * (size_t)G.S_total + sid];
             }
         });
-        ring_step(R, X, in_hi, NoSide{});
+        ring_step<V>(R, X, in_hi, NoSide{});
         // layer 1: FiLM pts_linears.0 -> Y
         init_bias(Y, bias_l + kW, g);
 #pragma unroll
         for (int t = 0; t < 16; ++t)
-            ring_step(R, Y, X[t], [&] {
-                if (t == 15) film_tile(Y[0], f0g, f0b, 0, g);
+            ring_step<V>(R, Y, X[t], [&] {
+                if (t == 15) film_tile<V>(Y[0], f0g, f0b, 0, g);
             });
         // layer 2: FiLM pts_linears.1 -> X
         init_bias(X, bias_l + 2 * kW, g);
 #pragma unroll
         for (int t = 0; t < 16; ++t)
-            ring_step(R, X, Y[t], [&] {
-                if (t < 15) film_tile(Y[t + 1], f0g, f0b, t + 1, g);
-                else film_tile(X[0], f1g, f1b, 0, g);
+            ring_step<V>(R, X, Y[t], [&] {
+                if (t < 15) film_tile<V>(Y[t + 1], f0g, f0b, t + 1, g);
+                else film_tile<V>(X[0], f1g, f1b, 0, g);
             });
         // layer 3: FiLM pts_linears.2 -> Y
         init_bias(Y, bias_l + 3 * kW, g);
 #pragma unroll
         for (int t = 0; t < 16; ++t)
-            ring_step(R, Y, X[t], [&] {
-                if (t < 15) film_tile(X[t + 1], f1g, f1b, t + 1, g);
-                else film_tile(Y[0], f2g, f2b, 0, g);
+            ring_step<V>(R, Y, X[t], [&] {
+                if (t < 15) film_tile<V>(X[t + 1], f1g, f1b, t + 1, g);
+                else film_tile<V>(Y[0], f2g, f2b, 0, g);
             });
         // layer 4: views FiLM ([h3, SH] 272 -> 256) -> X; sigma_linear and the
         // sample's compositing weight ride in the last h3 slice
         init_bias(X, bias_l + 4 * kW, g);
 #pragma unroll
         for (int t = 0; t < 16; ++t)
-            ring_step(R, X, Y[t], [&] {
+            ring_step<V>(R, X, Y[t], [&] {
                 if (t < 15) {
-                    film_tile(Y[t + 1], f2g, f2b, t + 1, g);
+                    film_tile<V>(Y[t + 1], f2g, f2b, t + 1, g);
                 } else {
                     sdf = __fadd_rn(dot_feat(Y, sig_w, g), sig_b);
                     // volume_integration (sdf_model.py:236-301), front to back
@@ -525,10 +584,10 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
                     wsum += w;
                 }
             });
-        ring_step(R, X, shq, NoSide{});
+        ring_step<V>(R, X, shq, NoSide{});
         // colour features f = sin(gamma_v * . + beta_v); rgb_linear; compositing
 #pragma unroll
-        for (int t = 0; t < 16; ++t) film_tile(X[t], f3g, f3b, t, g);
+        for (int t = 0; t < 16; ++t) film_tile<V>(X[t], f3g, f3b, t, g);
         const float r0 = __fadd_rn(dot_feat(X, rgb_w, g), rgb_b0);
         const float r1 = __fadd_rn(dot_feat(X, rgb_w + kW, g), rgb_b1);
         const float r2 = __fadd_rn(dot_feat(X, rgb_w + 2 * kW, g), rgb_b2);
@@ -544,10 +603,12 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
         if (a.features) {
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
-                facc[t].x = __fmaf_rn(w, X[t].x, facc[t].x);
-                facc[t].y = __fmaf_rn(w, X[t].y, facc[t].y);
-                facc[t].z = __fmaf_rn(w, X[t].z, facc[t].z);
-                facc[t].w = __fmaf_rn(w, X[t].w, facc[t].w);
+                f4 v = facc[t * 64 + lane];
+                v.x = __fmaf_rn(w, X[t].x, v.x);
+                v.y = __fmaf_rn(w, X[t].y, v.y);
+                v.z = __fmaf_rn(w, X[t].z, v.z);
+                v.w = __fmaf_rn(w, X[t].w, v.w);
+                facc[t * 64 + lane] = v;
             }
         }
         if (a.sdf && ray_ok && g == 0) a.sdf[(size_t)ray_index * G.N + s] = sdf;
@@ -572,10 +633,11 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_kernel(const FieldArgs 
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const uint32_t j = 16 * t + 4 * g;
-            fb[(size_t)(j + 0) * HW] = facc[t].x;
-            fb[(size_t)(j + 1) * HW] = facc[t].y;
-            fb[(size_t)(j + 2) * HW] = facc[t].z;
-            fb[(size_t)(j + 3) * HW] = facc[t].w;
+            const f4 v = facc[t * 64 + lane];
+            fb[(size_t)(j + 0) * HW] = v.x;
+            fb[(size_t)(j + 1) * HW] = v.y;
+            fb[(size_t)(j + 2) * HW] = v.z;
+            fb[(size_t)(j + 3) * HW] = v.w;
         }
     }
 }
@@ -657,6 +719,25 @@ static void fill_geom(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, 
     g.bound = w->bound;
 }
 
+static int g_field_variant = 0;   // profiling ablations only (see ABL_*)
+
+static void launch_field(int v, dim3 grid, hipStream_t st, const FieldArgs &f) {
+    switch (v) {
+#define SDFR_FIELD_CASE(V)                                                                   \
+    case V:                                                                                  \
+        hipLaunchKernelGGL(ngp_field_kernel<V>, grid, dim3(kThreads), 0, st, f);             \
+        return;
+        SDFR_FIELD_CASE(1)
+        SDFR_FIELD_CASE(2)
+        SDFR_FIELD_CASE(4)
+        SDFR_FIELD_CASE(8)
+        SDFR_FIELD_CASE(15)
+#undef SDFR_FIELD_CASE
+        default:
+            hipLaunchKernelGGL(ngp_field_kernel<0>, grid, dim3(kThreads), 0, st, f);
+    }
+}
+
 static void record_event(void *ev, hipStream_t st) {
     if (ev) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev), st);
 }
@@ -706,6 +787,24 @@ static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *
 using namespace sdfr;
 
 extern "C" {
+
+int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t n,
+                         void *stream) {
+    if (n == 0) return SDFR_OK;
+    hipLaunchKernelGGL(sin_probe_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                       (hipStream_t)stream, x, out_cw, out_hw, n);
+    return check_launch("sin_probe");
+}
+
+int sdfr_debug_set_field_variant(int variant) {
+    const int ok[] = {0, 1, 2, 4, 8, 15};
+    for (int v : ok)
+        if (v == variant) {
+            g_field_variant = variant;
+            return SDFR_OK;
+        }
+    return fail(SDFR_EINVAL, "sdfr_debug_set_field_variant: variant must be 0,1,2,4,8,15");
+}
 
 size_t sdfr_render_ngp_workspace_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t N,
                                        uint32_t num_levels) {
@@ -764,7 +863,7 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     f.xyz = a->xyz;
     f.mask = a->mask;
     const uint32_t blocks = (g.total_tiles + kWaves - 1) / kWaves;
-    hipLaunchKernelGGL(ngp_field_kernel, dim3(blocks), dim3(kThreads), 0, st, f);
+    launch_field(g_field_variant, dim3(blocks), st, f);
     if ((rc = check_launch("render_ngp: field"))) return rc;
     record_event(a->stage_events[3], st);
     return SDFR_OK;

@@ -128,3 +128,18 @@ def test_sh_forward_backward_bit_exact(sdfr, oracle_mod, golden_dir):
     for deg in (1, 2, 3):
         o = sdfr.sh_encode(torch.from_numpy(x).to(DEV), deg, False)
         np.testing.assert_array_equal(o.cpu().numpy(), oracle_mod.sh_encode_forward(x, deg)[0])
+
+
+def test_device_sin_accuracy(sdfr):
+    """The field kernel's sin (hardware v_sin_f32 after an fma 2pi reduction) and
+    the polynomial alternative, against float64 over the FiLM argument range."""
+    lib = sdfr._lib
+    xs = ((torch.rand(1 << 20, dtype=torch.float64, generator=torch.Generator().manual_seed(0))
+           - 0.5) * 400).float()
+    xd = xs.to(DEV)
+    cw, hw = torch.empty_like(xd), torch.empty_like(xd)
+    lib.check(lib.lib().sdfr_debug_sin_probe(lib.ptr(xd), lib.ptr(cw), lib.ptr(hw), xd.numel(),
+                                             lib.stream_of(xd)), "sin probe")
+    ref = torch.sin(xs.double())
+    assert (cw.cpu().double() - ref).abs().max() < 2e-7
+    assert (hw.cpu().double() - ref).abs().max() < 1e-6
