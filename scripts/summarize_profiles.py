@@ -1,0 +1,93 @@
+"""Turn a gpu_profile.sh run (gpurun_out/prof_*) into the committed profiles/.
+
+  python scripts/summarize_profiles.py --tag round1 [--batch 32] [--src gpurun_out]
+
+Writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<tag>_traffic.json       per-kernel HBM bytes per launch from the FETCH_SIZE /
+                                    WRITE_SIZE passes, with the gfx950 correction
+  profiles/field_traffic.json       what bench.py reports as roofline.traffic
+
+Counter units and corrections (MI355X_MICROARCH.md, "HBM [CDNA4]"): FETCH_SIZE and
+WRITE_SIZE are in KiB; FETCH_SIZE reads exactly half the bytes of a wide coalesced
+streaming read on gfx950, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane
+stores.  The field kernel's reads are 16-B-per-lane streams (encoded samples, packed
+weights), so the doubling applies to it; the encode kernel's reads are 8-B gathers
+(uncalibrated width) and are reported both raw and doubled.
+"""
+import argparse
+import csv
+import json
+import shutil
+from collections import defaultdict
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+FIELD = "ngp_field_kernel"
+ENCODE = "ngp_encode_kernel"
+
+
+def counters(path):
+    per = defaultdict(list)
+    for f in sorted(Path(path).glob("*counter_collection.csv")):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                per[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
+
+
+def pick(d, key):
+    hits = [k for k in d if key in k]
+    return d[hits[0]] if hits else None
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--tag", required=True)
+    p.add_argument("--batch", type=int, default=32, help="faces per launch in the profiled bench")
+    p.add_argument("--src", default=str(REPO / "gpurun_out"))
+    a = p.parse_args()
+    src, dst = Path(a.src), REPO / "profiles"
+    dst.mkdir(exist_ok=True)
+
+    stats = next((src / "prof_trace").glob("*kernel_stats.csv"), None)
+    if stats is None:
+        raise SystemExit(f"no kernel_stats.csv under {src / 'prof_trace'}")
+    shutil.copy(stats, dst / f"{a.tag}_kernel_stats.csv")
+    durations = {}
+    with open(stats) as fh:
+        for row in csv.DictReader(fh):
+            durations[row["Name"]] = float(row["AverageNs"])
+
+    fetch, nf = counters(src / "prof_fetch")
+    write, nw = counters(src / "prof_write")
+    out = {"batch_faces_per_launch": a.batch, "unit": "bytes per launch",
+           "fetch_correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-stream undercount)",
+           "kernels": {}}
+    for name in sorted(set(fetch) | set(write)):
+        if "sdfr::" not in name:
+            continue
+        f = fetch.get(name)
+        w = write.get(name)
+        out["kernels"][name] = {
+            "fetch_bytes_raw": None if f is None else f * 1024,
+            "fetch_bytes_corrected": None if f is None else f * 1024 * 2,
+            "write_bytes": None if w is None else w * 1024,
+            "dispatches": {"fetch": nf.get(name), "write": nw.get(name)},
+            "avg_duration_ns": pick(durations, name.split("(")[0]),
+        }
+    (dst / f"{a.tag}_traffic.json").write_text(json.dumps(out, indent=1))
+
+    fk = next((v for k, v in out["kernels"].items() if FIELD in k), None)
+    if fk and fk["fetch_bytes_corrected"] is not None and fk["write_bytes"] is not None:
+        total = fk["fetch_bytes_corrected"] + fk["write_bytes"]
+        (dst / "field_traffic.json").write_text(json.dumps({
+            "kernel": FIELD, "source": f"profiles/{a.tag}_traffic.json",
+            "bytes_per_launch_per_face": total / a.batch,
+            "fetch_bytes_per_face": fk["fetch_bytes_corrected"] / a.batch,
+            "write_bytes_per_face": fk["write_bytes"] / a.batch}, indent=1))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
