@@ -172,6 +172,72 @@ int sdfr_debug_set_field_variant(int variant);
 int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t n,
                          void *stream);
 
+/* ---------------------------------------------------------------------------
+ * StyleGAN2 decoder ops (im2scene/sdf/models/sdf_op.py).
+ *
+ * sdfr_fused_bias_act <- fused_bias_act (fused_bias_act.cpp:11,
+ *   fused_bias_act_kernel.cu:18; callers sdf_op.py:29, :49, :64):
+ *   out[i] = f(x[i] + bias[(i / step_b) % size_b]) * scale over size_x floats,
+ *   f by (act, grad): (1,*) identity, (3,0) x>0 ? x : alpha*x,
+ *   (3,1) ref[i]>0 ? x : alpha*x, (*,2) 0.  bias NULL (size_b 0) = no bias;
+ *   ref may be NULL unless (act, grad) == (3, 1).  out may alias x.
+ * ------------------------------------------------------------------------- */
+int sdfr_fused_bias_act(float *out, const float *x, const float *bias, const float *ref,
+                        uint64_t size_x, uint32_t step_b, uint32_t size_b, int act,
+                        int grad, float alpha, float scale, void *stream);
+
+/* sdfr_upfirdn2d <- upfirdn2d (upfirdn2d.cpp:12, upfirdn2d_kernel.cu; caller
+ * sdf_op.py:230): input viewed as [major, in_h, in_w] (minor = 1), kernel
+ * [kernel_h, kernel_w] (device), out [major, out_h, out_w] with
+ *   out_h = (in_h*up_y + pad_y0 + pad_y1 - kernel_h) / down_y + 1  (same for w):
+ * zero-insertion upsample, pad (negative = crop), true convolution with the
+ * kernel, then keep every down-th sample (upfirdn2d_native, sdf_op.py:273). */
+int sdfr_upfirdn2d(float *out, const float *input, const float *kernel, uint32_t major,
+                   uint32_t in_h, uint32_t in_w, uint32_t kernel_h, uint32_t kernel_w,
+                   int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1,
+                   int pad_y0, int pad_y1, void *stream);
+
+/* Fused StyledConv / ToRGB epilogue (no reference counterpart: replaces the
+ * chain after each decoder convolution -- ModulatedConv2d demodulation and
+ * upsample blur (sdf_model.py:676-699), NoiseInjection (:704), FusedLeakyReLU
+ * (:818), ToRGB + skip Upsample (:821-843) -- with one pass over the
+ * activations).  Activations are NHWC (channels_last):
+ *   conv  [B,H,W,C], or [B,2H+1,2W+1,C] when blur_up (stride-2 transposed conv
+ *         output; blurred with outer(fir,fir), pad (1,1), as ModulatedConv2d.blur)
+ *   v     = lrelu((blur(conv) * demod[b,c] + noise_weight * noise[b,h,w])
+ *                 + bias[c], negative_slope) * act_scale
+ *   y     [B,H,W,C] = v * s_next[b,c] (the next conv's modulation; s_next NULL
+ *         -> v), or y NULL (not stored)
+ *   rgb   [B,3,H,W] (NCHW) = sum_c v * rgb_w[b,o,c] + rgb_b[o]
+ *         + upfirdn2d(skip, outer(fir,fir), up 2, pad (2,1)) when skip != NULL;
+ *         only when rgb_w != NULL, and not together with blur_up.
+ * C must be a multiple of 4; with rgb_w, C/4 must be a power of two <= 64 or
+ * a multiple of 64 (C <= 1024). */
+typedef struct sdfr_styled_epilogue_args {
+    uint32_t B, C, H, W;
+    const float *conv;
+    int blur_up;
+    float fir[4];                 /* separable taps; outer(fir,fir) = the 2-D kernel */
+    const float *demod;           /* [B,C] or NULL (no demodulation)               */
+    const float *noise;           /* [B,H,W] or NULL                               */
+    const float *noise_weight;    /* [1] NoiseInjection.weight (device)            */
+    const float *bias;            /* [C] FusedLeakyReLU.bias                       */
+    float negative_slope, act_scale;
+    const float *s_next;          /* [B,C] or NULL                                 */
+    float *y;                     /* [B,H,W,C] or NULL                             */
+    const float *rgb_w;           /* [B,3,C] modulated ToRGB weight or NULL        */
+    const float *rgb_b;           /* [3]                                           */
+    const float *skip;            /* [B,3,H/2,W/2] or NULL                         */
+    float *rgb;                   /* [B,3,H,W]                                     */
+} sdfr_styled_epilogue_args;
+
+int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *a, void *stream);
+
+/* Decoder input staging: y[b,h,w,c] = x[b,c,h,w] * s[b,c] (NCHW -> NHWC with
+ * the first ModulatedConv2d's modulation folded in).  C and H*W multiples of 4. */
+int sdfr_modulate_to_nhwc(float *y, const float *x, const float *s, uint32_t B, uint32_t C,
+                          uint32_t HW, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

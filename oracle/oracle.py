@@ -329,6 +329,79 @@ def render_ngp(sd, cam, focal, near, far, styles, *, N=24, res=64, t_rand=None,
 
 
 # --------------------------------------------------------------------------
+# StyleGAN2 decoder ops (im2scene/sdf/models/sdf_op.py), numpy
+# --------------------------------------------------------------------------
+def fused_bias_act(x, bias, ref, act, grad, alpha, scale):
+    """fused_bias_act_kernel.cu:18-47 in fp32: y = f(x + bias[dim 1]) * scale."""
+    x = np.asarray(x, np.float32)
+    if bias is not None and np.size(bias):
+        x = (x + np.asarray(bias, np.float32).reshape([1, -1] + [1] * (x.ndim - 2))).astype(
+            np.float32)
+    mode = act * 10 + grad
+    a = np.float32(alpha)
+    if mode == 30:
+        y = np.where(x > 0, x, x * a)
+    elif mode == 31:
+        y = np.where(np.asarray(ref, np.float32) > 0, x, x * a)
+    elif mode in (12, 32):
+        y = np.zeros_like(x)
+    else:
+        y = x
+    return (y * np.float32(scale)).astype(np.float32)
+
+
+def upfirdn2d(x, kernel, up_x, up_y, down_x, down_y, pad_x0, pad_x1, pad_y0, pad_y1):
+    """upfirdn2d_native (sdf_op.py:273-316) on [major, h, w], accumulated in float64:
+    zero-insertion upsample, pad / crop, true convolution with ``kernel``, decimate."""
+    x = np.asarray(x, np.float64)
+    k = np.asarray(kernel, np.float64)
+    m, h, w = x.shape
+    kh, kw = k.shape
+    u = np.zeros((m, h * up_y, w * up_x))
+    u[:, ::up_y, ::up_x] = x
+    u = np.pad(u, ((0, 0), (max(pad_y0, 0), max(pad_y1, 0)), (max(pad_x0, 0), max(pad_x1, 0))))
+    u = u[:, max(-pad_y0, 0):u.shape[1] - max(-pad_y1, 0),
+          max(-pad_x0, 0):u.shape[2] - max(-pad_x1, 0)]
+    oh, ow = u.shape[1] - kh + 1, u.shape[2] - kw + 1
+    kf = k[::-1, ::-1]
+    out = np.zeros((m, oh, ow))
+    for i in range(kh):
+        for j in range(kw):
+            out += u[:, i:i + oh, j:j + ow] * kf[i, j]
+    return out[:, ::down_y, ::down_x]
+
+
+def styled_epilogue(conv, *, kernel2d, bias, noise_weight, noise=None, demod=None,
+                    blur_up=False, s_next=None, rgb_w=None, rgb_b=None, skip=None,
+                    slope=0.2, scale=2 ** 0.5):
+    """What follows a decoder convolution in the reference, NCHW float64:
+    ModulatedConv2d demod + blur (sdf_model.py:676-699), NoiseInjection
+    (:704-792), FusedLeakyReLU (:818), ToRGB + Upsample of the skip (:821-843).
+    Returns (y = act * s_next, rgb)."""
+    c = np.asarray(conv, np.float64)
+    B, C = c.shape[:2]
+    if blur_up:   # Blur(pad=(1,1)) of the stride-2 transposed conv output
+        c = upfirdn2d(c.reshape(B * C, *c.shape[2:]), kernel2d, 1, 1, 1, 1, 1, 1, 1, 1)
+        c = c.reshape(B, C, *c.shape[1:])
+    H, W = c.shape[2:]
+    v = c * (1.0 if demod is None else np.asarray(demod, np.float64)[:, :, None, None])
+    if noise is not None:
+        v = v + float(noise_weight) * np.broadcast_to(np.asarray(noise, np.float64), (B, 1, H, W))
+    v = v + np.asarray(bias, np.float64).reshape(1, C, 1, 1)
+    v = np.where(v > 0, v, v * slope) * scale
+    y = v if s_next is None else v * np.asarray(s_next, np.float64)[:, :, None, None]
+    rgb = None
+    if rgb_w is not None:
+        rgb = np.einsum("bchw,boc->bohw", v, np.asarray(rgb_w, np.float64))
+        rgb = rgb + np.asarray(rgb_b, np.float64).reshape(1, 3, 1, 1)
+        if skip is not None:
+            s = np.asarray(skip, np.float64)
+            up = upfirdn2d(s.reshape(B * 3, *s.shape[2:]), kernel2d, 2, 2, 1, 1, 2, 1, 2, 1)
+            rgb = rgb + up.reshape(B, 3, H, W)
+    return y, rgb
+
+
+# --------------------------------------------------------------------------
 # deterministic, platform-independent weights (integer hash; no libm)
 # --------------------------------------------------------------------------
 def det_uniform(shape, lo, hi, seed):

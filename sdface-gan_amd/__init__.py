@@ -14,8 +14,10 @@ Drop-in surface (reference: im2scene/sdf/models/):
 from . import _lib  # noqa: F401
 from .camera import generate_camera_params  # noqa: F401
 from .encoders import GridEncoder, SHEncoder, grid_encode, sh_encode  # noqa: F401
-from .generator import (Decoder, EqualLinear, FusedLeakyReLU, Generator,  # noqa: F401
-                        MappingLinear, ModulatedConv2d, fused_leaky_relu, upfirdn2d)
+from . import decoder_ops  # noqa: F401
+from .generator import (Blur, Decoder, EqualLinear, FusedLeakyReLU, Generator,  # noqa: F401
+                        MappingLinear, ModulatedConv2d, NoiseInjection, PixelNorm, StyledConv,
+                        ToRGB, Upsample, fused_leaky_relu, make_kernel, upfirdn2d)
 from .options import AttrDict, SDFOptions, vol_render_opt  # noqa: F401
 from .renderer import (FCGenerator, FiLMSiren, LinearLayer, NGPSIRENGenerator,  # noqa: F401
                        SirenGenerator, VolumeFeatureRenderer, get_encoder)

@@ -32,6 +32,7 @@ EXPORTS = (
     "sdfr_sh_encode_forward", "sdfr_sh_encode_backward",
     "sdfr_render_ngp_workspace_bytes", "sdfr_render_ngp_forward",
     "sdfr_render_ngp_encode_only", "sdfr_debug_set_field_variant", "sdfr_debug_sin_probe",
+    "sdfr_fused_bias_act", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
 )
 
 
@@ -64,6 +65,17 @@ class NgpRenderArgs(ctypes.Structure):
     ]
 
 
+class StyledEpilogueArgs(ctypes.Structure):
+    """sdfr_styled_epilogue_args (include/sdfr.h)."""
+    _fields_ = [
+        ("B", _u32), ("C", _u32), ("H", _u32), ("W", _u32),
+        ("conv", _vp), ("blur_up", _int), ("fir", _f32 * 4),
+        ("demod", _vp), ("noise", _vp), ("noise_weight", _vp), ("bias", _vp),
+        ("negative_slope", _f32), ("act_scale", _f32),
+        ("s_next", _vp), ("y", _vp), ("rgb_w", _vp), ("rgb_b", _vp), ("skip", _vp), ("rgb", _vp),
+    ]
+
+
 _lib = None
 
 
@@ -93,6 +105,11 @@ def lib():
                                               ctypes.POINTER(NgpRenderArgs), _vp]
     L.sdfr_debug_set_field_variant.argtypes = [_int]
     L.sdfr_debug_sin_probe.argtypes = [_vp, _vp, _vp, _u32, _vp]
+    L.sdfr_fused_bias_act.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_uint64, _u32, _u32, _int, _int,
+                                      _f32, _f32, _vp]
+    L.sdfr_upfirdn2d.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32] + [_int] * 8 + [_vp]
+    L.sdfr_styled_epilogue.argtypes = [ctypes.POINTER(StyledEpilogueArgs), _vp]
+    L.sdfr_modulate_to_nhwc.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _vp]
     v = L.sdfr_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"libsdfr ABI {v} != expected {ABI_VERSION}; rebuild the library")

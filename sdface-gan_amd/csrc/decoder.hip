@@ -1,0 +1,451 @@
+// decoder.hip -- StyleGAN2 decoder ops for gfx950 (include/sdfr.h, "decoder ops").
+//
+// * sdfr_fused_bias_act / sdfr_upfirdn2d: drop-ins for the reference's two
+//   native ops (fused_bias_act_kernel.cu:18-47, upfirdn2d_kernel.cu), same
+//   argument meaning; element order of the arithmetic follows the reference
+//   (x + bias, activation, * scale) so the bias/activation op is bit-exact.
+// * sdfr_styled_epilogue: everything a StyledConv / ToRGB does after MIOpen's
+//   convolution, in one streaming pass over NHWC activations:
+//     [blur of the stride-2 transposed conv] -> demodulate -> + noise -> + bias
+//     -> leaky ReLU * sqrt(2) -> (store, pre-multiplied by the NEXT conv's
+//     modulation) and/or (1x1 ToRGB + upsampled skip).
+//   The decoder thereby touches each activation tensor once for reading and
+//   once for writing; the last layer's activations are never stored.
+// * sdfr_modulate_to_nhwc: renderer features (NCHW) -> NHWC times the first
+//   conv's modulation, an LDS-tiled transpose.
+//
+// All of these are HBM-streaming kernels: 16-B per lane accesses along the
+// contiguous axis, >= 8 waves per CU, no LDS except the transpose tile.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "sdfr_common.h"
+
+namespace sdfr {
+
+// ----------------------------------------------------------------------------
+// fused_bias_act (fused_bias_act_kernel.cu:18-47)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ float fba(float x, float ref, int mode, float alpha) {
+    switch (mode) {
+        case 30: return x > 0.0f ? x : x * alpha;
+        case 31: return ref > 0.0f ? x : x * alpha;
+        case 12:
+        case 32: return 0.0f;
+        default: return x;
+    }
+}
+
+__global__ __launch_bounds__(256) void fused_bias_act_kernel(
+    float *__restrict__ out, const float *__restrict__ x, const float *__restrict__ bias,
+    const float *__restrict__ ref, uint64_t n, uint32_t step_b, uint32_t size_b, int mode,
+    float alpha, float scale) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        float v = x[i];
+        if (bias) v = v + bias[(i / step_b) % size_b];
+        const float r = ref ? ref[i] : 0.0f;
+        out[i] = fba(v, r, mode, alpha) * scale;
+    }
+}
+
+// 4 consecutive elements share a bias entry (step_b % 4 == 0, n % 4 == 0)
+__global__ __launch_bounds__(256) void fused_bias_act_vec_kernel(
+    float4 *__restrict__ out, const float4 *__restrict__ x, const float *__restrict__ bias,
+    const float4 *__restrict__ ref, uint64_t n4, uint32_t step_b4, uint32_t size_b, int mode,
+    float alpha, float scale) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 v = x[i];
+        if (bias) {
+            const float b = bias[(i / step_b4) % size_b];
+            v.x = v.x + b; v.y = v.y + b; v.z = v.z + b; v.w = v.w + b;
+        }
+        const float4 r = ref ? ref[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 o;
+        o.x = fba(v.x, r.x, mode, alpha) * scale;
+        o.y = fba(v.y, r.y, mode, alpha) * scale;
+        o.z = fba(v.z, r.z, mode, alpha) * scale;
+        o.w = fba(v.w, r.w, mode, alpha) * scale;
+        out[i] = o;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// upfirdn2d (upfirdn2d_native semantics, sdf_op.py:273-316), one output / thread
+// ----------------------------------------------------------------------------
+struct UfdArgs {
+    float *out;
+    const float *in, *k;
+    uint32_t major, in_h, in_w, kh, kw, out_h, out_w;
+    int up_x, up_y, down_x, down_y, pad_x0, pad_y0;
+};
+
+__global__ __launch_bounds__(256) void upfirdn2d_kernel(UfdArgs a) {
+    const uint64_t total = (uint64_t)a.major * a.out_h * a.out_w;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const int uh = (int)a.in_h * a.up_y, uw = (int)a.in_w * a.up_x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        const uint32_t ox = (uint32_t)(t % a.out_w);
+        const uint32_t oy = (uint32_t)((t / a.out_w) % a.out_h);
+        const uint64_t m = t / ((uint64_t)a.out_w * a.out_h);
+        const float *src = a.in + m * a.in_h * a.in_w;
+        float acc = 0.0f;
+        for (uint32_t i = 0; i < a.kh; ++i) {
+            const int r = (int)(oy * a.down_y + i) - a.pad_y0;   // row in the upsampled image
+            if (r < 0 || r >= uh || r % a.up_y) continue;
+            const float *row = src + (uint64_t)(r / a.up_y) * a.in_w;
+            const float *krow = a.k + (uint64_t)(a.kh - 1 - i) * a.kw;
+            for (uint32_t j = 0; j < a.kw; ++j) {
+                const int c = (int)(ox * a.down_x + j) - a.pad_x0;
+                if (c < 0 || c >= uw || c % a.up_x) continue;
+                acc = fmaf(row[c / a.up_x], krow[a.kw - 1 - j], acc);
+            }
+        }
+        a.out[t] = acc;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// styled-conv epilogue
+// ----------------------------------------------------------------------------
+struct EpiArgs {
+    uint32_t B, C, H, W;
+    const float *conv;
+    float fir[4];
+    const float *demod, *noise, *noise_weight, *bias;
+    float slope, act_scale;
+    const float *s_next;
+    float *y;
+    const float *rgb_w, *rgb_b, *skip;
+    float *rgb;
+};
+
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+
+__device__ __forceinline__ float act1(float c, float dm, float nz, float b, float slope,
+                                      float scale) {
+    float v = c * dm;
+    v = v + nz;          // image + weight * noise (sdf_model.py NoiseInjection)
+    v = v + b;           // fused_bias_act: x + bias, lrelu, * scale
+    v = v > 0.0f ? v : v * slope;
+    return v * scale;
+}
+
+__device__ __forceinline__ float4 act4(float4 c, float4 dm, float nz, float4 b, float slope,
+                                       float scale) {
+    return make_float4(act1(c.x, dm.x, nz, b.x, slope, scale), act1(c.y, dm.y, nz, b.y, slope, scale),
+                       act1(c.z, dm.z, nz, b.z, slope, scale), act1(c.w, dm.w, nz, b.w, slope, scale));
+}
+
+// skip image upsampled by upfirdn2d(up=2, pad=(2,1), outer(fir,fir)) at (y, x)
+__device__ float skip_up(const float *__restrict__ img, uint32_t h2, uint32_t w2, int y, int x,
+                         const float *fir) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = y + i - 2;
+        if (r < 0 || (r & 1) || (r >> 1) >= (int)h2) continue;
+        float row = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = x + j - 2;
+            if (c < 0 || (c & 1) || (c >> 1) >= (int)w2) continue;
+            row = fmaf(img[(uint32_t)(r >> 1) * w2 + (uint32_t)(c >> 1)], fir[3 - j], row);
+        }
+        acc = fmaf(row, fir[3 - i], acc);
+    }
+    return acc;
+}
+
+constexpr uint32_t kEpiPixPerBlock = 64;
+
+// Plain epilogue: lanes of a wave split the C channels of PPW = 64/TPP pixels
+// (TPP threads x NQ float4 per pixel); the 1x1 ToRGB is a TPP-lane reduction.
+template <int NQ, bool RGB>
+__global__ __launch_bounds__(256) void epi_plain_kernel(EpiArgs a, uint32_t tpp_log2) {
+    const uint32_t TPP = 1u << tpp_log2;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t q = lane & (TPP - 1), g = lane >> tpp_log2;
+    const uint32_t ppw = 64u >> tpp_log2;
+    const uint32_t b = blockIdx.y;
+    const uint32_t HW = a.H * a.W, C = a.C;
+
+    float4 dm[NQ], bs[NQ], sn[NQ], rw[3][NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        const uint32_t c = 4 * (q + k * TPP);
+        dm[k] = a.demod ? ld4(a.demod + (size_t)b * C + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+        bs[k] = ld4(a.bias + c);
+        sn[k] = a.s_next ? ld4(a.s_next + (size_t)b * C + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+        if (RGB) {
+#pragma unroll
+            for (int o = 0; o < 3; ++o) rw[o][k] = ld4(a.rgb_w + ((size_t)b * 3 + o) * C + c);
+        }
+    }
+    const float nw = a.noise ? *a.noise_weight : 0.0f;
+    const uint32_t p0 = blockIdx.x * kEpiPixPerBlock;
+    for (uint32_t pp = wave * ppw + g; pp < kEpiPixPerBlock; pp += 4 * ppw) {
+        const uint32_t p = p0 + pp;
+        const bool live = p < HW;
+        float acc[3] = {0.f, 0.f, 0.f};
+        if (live) {
+            const float nz = a.noise ? nw * a.noise[(size_t)b * HW + p] : 0.0f;
+            const size_t base = ((size_t)b * HW + p) * C;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const uint32_t c = 4 * (q + k * TPP);
+                const float4 v = act4(ld4(a.conv + base + c), dm[k], nz, bs[k], a.slope,
+                                      a.act_scale);
+                if (a.y) {
+                    *reinterpret_cast<float4 *>(a.y + base + c) =
+                        make_float4(v.x * sn[k].x, v.y * sn[k].y, v.z * sn[k].z, v.w * sn[k].w);
+                }
+                if (RGB) {
+#pragma unroll
+                    for (int o = 0; o < 3; ++o) {
+                        acc[o] = fmaf(v.x, rw[o][k].x, acc[o]);
+                        acc[o] = fmaf(v.y, rw[o][k].y, acc[o]);
+                        acc[o] = fmaf(v.z, rw[o][k].z, acc[o]);
+                        acc[o] = fmaf(v.w, rw[o][k].w, acc[o]);
+                    }
+                }
+            }
+        }
+        if (RGB) {
+            for (uint32_t off = TPP >> 1; off; off >>= 1) {
+#pragma unroll
+                for (int o = 0; o < 3; ++o) acc[o] += __shfl_xor(acc[o], off, 64);
+            }
+            if (live && q == 0) {
+                const int yy = (int)(p / a.W), xx = (int)(p % a.W);
+#pragma unroll
+                for (int o = 0; o < 3; ++o) {
+                    float v = acc[o] + a.rgb_b[o];
+                    if (a.skip)
+                        v = v + skip_up(a.skip + ((size_t)b * 3 + o) * (HW / 4), a.H / 2, a.W / 2,
+                                        yy, xx, a.fir);
+                    a.rgb[((size_t)b * 3 + o) * HW + p] = v;
+                }
+            }
+        }
+    }
+}
+
+// Blur epilogue: thread = (face, row segment, column, channel quad); a sliding
+// window of 4 horizontally filtered input rows gives the 4x4 separable blur
+// with one new 16-B load per tap column per output row.
+constexpr uint32_t kBlurRows = 16;
+
+__global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg) {
+    const uint32_t Q = a.C >> 2;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t total = (uint64_t)a.B * nseg * a.W * Q;
+    if (t >= total) return;
+    const uint32_t q = (uint32_t)(t % Q);
+    const uint32_t ox = (uint32_t)((t / Q) % a.W);
+    const uint32_t seg = (uint32_t)((t / ((uint64_t)Q * a.W)) % nseg);
+    const uint32_t b = (uint32_t)(t / ((uint64_t)Q * a.W * nseg));
+    const uint32_t c = 4 * q;
+    const uint32_t Hi = a.H + 1, Wi = a.W + 1, C = a.C;
+    const float *src = a.conv + (size_t)b * Hi * Wi * C + c;
+    const float f0 = a.fir[3], f1 = a.fir[2], f2 = a.fir[1], f3 = a.fir[0];   // flipped taps
+
+    auto hrow = [&](int r) -> float4 {
+        float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < 0 || r >= (int)Hi) return h;
+        const float *row = src + (size_t)r * Wi * C;
+        const float fj[4] = {f0, f1, f2, f3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int cc = (int)ox + j - 1;
+            if (cc < 0 || cc >= (int)Wi) continue;
+            const float4 v = ld4(row + (size_t)cc * C);
+            h.x = fmaf(v.x, fj[j], h.x); h.y = fmaf(v.y, fj[j], h.y);
+            h.z = fmaf(v.z, fj[j], h.z); h.w = fmaf(v.w, fj[j], h.w);
+        }
+        return h;
+    };
+
+    const float4 dm = a.demod ? ld4(a.demod + (size_t)b * C + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 bs = ld4(a.bias + c);
+    const float4 sn = a.s_next ? ld4(a.s_next + (size_t)b * C + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float nw = a.noise ? *a.noise_weight : 0.0f;
+    const uint32_t y0 = seg * kBlurRows;
+    const uint32_t y1 = min(a.H, y0 + kBlurRows);
+    float4 h0 = hrow((int)y0 - 1), h1 = hrow((int)y0), h2 = hrow((int)y0 + 1);
+    for (uint32_t oy = y0; oy < y1; ++oy) {
+        const float4 h3 = hrow((int)oy + 2);
+        float4 s;
+        s.x = fmaf(h3.x, f3, fmaf(h2.x, f2, fmaf(h1.x, f1, h0.x * f0)));
+        s.y = fmaf(h3.y, f3, fmaf(h2.y, f2, fmaf(h1.y, f1, h0.y * f0)));
+        s.z = fmaf(h3.z, f3, fmaf(h2.z, f2, fmaf(h1.z, f1, h0.z * f0)));
+        s.w = fmaf(h3.w, f3, fmaf(h2.w, f2, fmaf(h1.w, f1, h0.w * f0)));
+        const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
+        const float nz = a.noise ? nw * a.noise[pix] : 0.0f;
+        const float4 v = act4(s, dm, nz, bs, a.slope, a.act_scale);
+        *reinterpret_cast<float4 *>(a.y + pix * C + c) =
+            make_float4(v.x * sn.x, v.y * sn.y, v.z * sn.z, v.w * sn.w);
+        h0 = h1; h1 = h2; h2 = h3;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// NCHW -> NHWC with modulation, 64 x 64 LDS tiles
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void modulate_nhwc_kernel(float *__restrict__ y,
+                                                            const float *__restrict__ x,
+                                                            const float *__restrict__ s,
+                                                            uint32_t C, uint32_t HW) {
+    __shared__ float tile[64][65];
+    const uint32_t b = blockIdx.z, c0 = blockIdx.y * 64, p0 = blockIdx.x * 64;
+    const uint32_t t = threadIdx.x;
+    // load: 16 threads x float4 cover 64 pixels of one channel; 16 channels per pass
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t cl = (t >> 4) + 16 * k, pl = 4 * (t & 15);
+        const uint32_t c = c0 + cl, p = p0 + pl;
+        if (c < C && p < HW) {
+            const float4 v = ld4(x + ((size_t)b * C + c) * HW + p);
+            const float sc = s[(size_t)b * C + c];
+            tile[cl][pl + 0] = v.x * sc; tile[cl][pl + 1] = v.y * sc;
+            tile[cl][pl + 2] = v.z * sc; tile[cl][pl + 3] = v.w * sc;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t pl = (t >> 4) + 16 * k, cl = 4 * (t & 15);
+        const uint32_t c = c0 + cl, p = p0 + pl;
+        if (c < C && p < HW) {
+            *reinterpret_cast<float4 *>(y + ((size_t)b * HW + p) * C + c) =
+                make_float4(tile[cl][pl], tile[cl + 1][pl], tile[cl + 2][pl], tile[cl + 3][pl]);
+        }
+    }
+}
+
+static uint32_t grid_for(uint64_t n, uint32_t per_block = 256) {
+    const uint64_t blocks = (n + per_block - 1) / per_block;
+    return (uint32_t)std::min<uint64_t>(blocks, 1u << 20);
+}
+
+static inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace sdfr
+
+using namespace sdfr;
+
+extern "C" {
+
+int sdfr_fused_bias_act(float *out, const float *x, const float *bias, const float *ref,
+                        uint64_t size_x, uint32_t step_b, uint32_t size_b, int act, int grad,
+                        float alpha, float scale, void *stream) {
+    if (size_x == 0) return SDFR_OK;
+    if (!out || !x) return fail(SDFR_EINVAL, "fused_bias_act: null tensor pointer");
+    if (bias && (size_b == 0 || step_b == 0))
+        return fail(SDFR_EINVAL, "fused_bias_act: bias needs size_b > 0 and step_b > 0");
+    if (act == 3 && grad == 1 && !ref)
+        return fail(SDFR_EINVAL, "fused_bias_act: grad mode 1 needs the reference output");
+    const int mode = act * 10 + grad;
+    if (!bias) size_b = 0;
+    hipStream_t st = (hipStream_t)stream;
+    const bool vec = size_x % 4 == 0 && (!bias || step_b % 4 == 0) && aligned16(out) &&
+                     aligned16(x) && (!ref || aligned16(ref));
+    if (vec) {
+        const uint64_t n4 = size_x / 4;
+        fused_bias_act_vec_kernel<<<grid_for(n4), 256, 0, st>>>(
+            reinterpret_cast<float4 *>(out), reinterpret_cast<const float4 *>(x), bias,
+            reinterpret_cast<const float4 *>(ref), n4, bias ? step_b / 4 : 1, size_b, mode, alpha,
+            scale);
+    } else {
+        fused_bias_act_kernel<<<grid_for(size_x), 256, 0, st>>>(out, x, bias, ref, size_x,
+                                                                 bias ? step_b : 1, size_b, mode,
+                                                                 alpha, scale);
+    }
+    return check_launch("fused_bias_act");
+}
+
+int sdfr_upfirdn2d(float *out, const float *input, const float *kernel, uint32_t major,
+                   uint32_t in_h, uint32_t in_w, uint32_t kernel_h, uint32_t kernel_w, int up_x,
+                   int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0,
+                   int pad_y1, void *stream) {
+    if (up_x < 1 || up_y < 1 || down_x < 1 || down_y < 1)
+        return fail(SDFR_EINVAL, "upfirdn2d: up and down factors must be >= 1");
+    if (kernel_h == 0 || kernel_w == 0) return fail(SDFR_EINVAL, "upfirdn2d: empty kernel");
+    const long oh = ((long)in_h * up_y + pad_y0 + pad_y1 - (long)kernel_h) / down_y + 1;
+    const long ow = ((long)in_w * up_x + pad_x0 + pad_x1 - (long)kernel_w) / down_x + 1;
+    if (oh <= 0 || ow <= 0) return fail(SDFR_EINVAL, "upfirdn2d: output size is not positive");
+    if (major == 0 || in_h == 0 || in_w == 0) return SDFR_OK;
+    if (!out || !input || !kernel) return fail(SDFR_EINVAL, "upfirdn2d: null tensor pointer");
+    UfdArgs a{out, input, kernel, major, in_h, in_w, kernel_h, kernel_w, (uint32_t)oh,
+              (uint32_t)ow, up_x, up_y, down_x, down_y, pad_x0, pad_y0};
+    upfirdn2d_kernel<<<grid_for((uint64_t)major * oh * ow), 256, 0, (hipStream_t)stream>>>(a);
+    return check_launch("upfirdn2d");
+}
+
+int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
+    if (!p) return fail(SDFR_EINVAL, "styled_epilogue: null args");
+    const sdfr_styled_epilogue_args &s = *p;
+    if (s.B == 0 || s.H == 0 || s.W == 0) return SDFR_OK;
+    if (s.C == 0 || s.C % 4) return fail(SDFR_EINVAL, "styled_epilogue: C must be a multiple of 4");
+    if (!s.conv || !s.bias || (s.noise && !s.noise_weight))
+        return fail(SDFR_EINVAL, "styled_epilogue: null tensor pointer");
+    const bool rgb = s.rgb_w != nullptr;
+    if (rgb && (!s.rgb || !s.rgb_b)) return fail(SDFR_EINVAL, "styled_epilogue: rgb output missing");
+    if (rgb && s.blur_up) return fail(SDFR_EINVAL, "styled_epilogue: ToRGB after a blur is not fused");
+    if (!rgb && !s.y) return fail(SDFR_EINVAL, "styled_epilogue: nothing to write");
+    if (s.skip && (s.H % 2 || s.W % 2)) return fail(SDFR_EINVAL, "styled_epilogue: odd size with skip");
+    for (const void *q : {(const void *)s.conv, (const void *)s.demod, (const void *)s.bias,
+                          (const void *)s.s_next, (const void *)s.y, (const void *)s.rgb_w})
+        if (q && !aligned16(q)) return fail(SDFR_EINVAL, "styled_epilogue: pointers must be 16-B aligned");
+    EpiArgs a{s.B, s.C, s.H, s.W, s.conv, {s.fir[0], s.fir[1], s.fir[2], s.fir[3]},
+              s.demod, s.noise, s.noise_weight, s.bias, s.negative_slope, s.act_scale,
+              s.s_next, s.y, s.rgb_w, s.rgb_b, s.skip, s.rgb};
+    hipStream_t st = (hipStream_t)stream;
+    if (s.blur_up) {
+        const uint32_t nseg = (s.H + kBlurRows - 1) / kBlurRows;
+        const uint64_t total = (uint64_t)s.B * nseg * s.W * (s.C / 4);
+        epi_blur_kernel<<<(uint32_t)((total + 255) / 256), 256, 0, st>>>(a, nseg);
+        return check_launch("styled_epilogue(blur)");
+    }
+    const uint32_t Q = s.C / 4;
+    const bool pow2 = (Q & (Q - 1)) == 0;
+    if (Q <= 64 ? !pow2 : (Q % 64 != 0))
+        return fail(SDFR_EUNSUPPORTED,
+                    "styled_epilogue: C/4 must be a power of two <= 64 or a multiple of 64");
+    uint32_t tpp_log2 = 6, nq = Q / 64;
+    if (Q <= 64) {
+        nq = 1;
+        tpp_log2 = 0;
+        while ((1u << tpp_log2) < Q) ++tpp_log2;
+    }
+    dim3 grid((s.H * s.W + kEpiPixPerBlock - 1) / kEpiPixPerBlock, s.B);
+#define EPI(NQ)                                                                          \
+    case NQ:                                                                             \
+        if (rgb) epi_plain_kernel<NQ, true><<<grid, 256, 0, st>>>(a, tpp_log2);          \
+        else epi_plain_kernel<NQ, false><<<grid, 256, 0, st>>>(a, tpp_log2);             \
+        break;
+    switch (nq) {
+        EPI(1)
+        EPI(2)
+        EPI(3)
+        EPI(4)
+        default: return fail(SDFR_EUNSUPPORTED, "styled_epilogue: C > 1024");
+    }
+#undef EPI
+    return check_launch("styled_epilogue");
+}
+
+int sdfr_modulate_to_nhwc(float *y, const float *x, const float *s, uint32_t B, uint32_t C,
+                          uint32_t HW, void *stream) {
+    if (B == 0 || C == 0 || HW == 0) return SDFR_OK;
+    if (!y || !x || !s) return fail(SDFR_EINVAL, "modulate_to_nhwc: null tensor pointer");
+    if (C % 4 || HW % 4) return fail(SDFR_EINVAL, "modulate_to_nhwc: C and H*W must be multiples of 4");
+    if (!aligned16(x) || !aligned16(y)) return fail(SDFR_EINVAL, "modulate_to_nhwc: pointers must be 16-B aligned");
+    dim3 grid((HW + 63) / 64, (C + 63) / 64, B);
+    modulate_nhwc_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(y, x, s, C, HW);
+    return check_launch("modulate_to_nhwc");
+}
+
+}  // extern "C"

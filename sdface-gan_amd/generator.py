@@ -6,9 +6,12 @@ Follows im2scene/sdf/models/sdf_model.py:
   ToRGB :821-843           Decoder :883-1056         Generator :1059-1216
 and the device-agnostic forms of the fused ops of sdf_op.py:105-120 / 259-314.
 
-The decoder stays on PyTorch-ROCm.  Its modulated convolution
-runs as ``conv(x * s, W) * demod`` -- one batched MIOpen convolution instead
-of the reference's per-face grouped convolution (same algebra, fp32).
+The decoder's convolutions stay on MIOpen.  Its modulated
+convolution runs as ``conv(x * s, W) * demod`` -- one batched convolution
+instead of the reference's per-face grouped convolution (same algebra, fp32).
+On the GPU, the bias/leaky-ReLU and upfirdn2d ops are the HIP kernels of
+decoder_ops.py; at inference (no grad) everything between two convolutions is
+one HIP epilogue over channels_last activations (``Decoder._fused_forward``).
 Geometry-aware noise projection (``project_noise``, pytorch3d) is not
 supported and raises.
 """
@@ -21,47 +24,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .decoder_ops import (FusedLeakyReLU, fused_leaky_relu, modulate_to_nhwc,  # noqa: F401
+                          separable_taps, styled_epilogue, upfirdn2d)
 from .renderer import VolumeFeatureRenderer
-
-
-# ---------------------------------------------------------------------------
-# fused ops (sdf_op.py), device-agnostic
-# ---------------------------------------------------------------------------
-def fused_leaky_relu(input, bias=None, negative_slope=0.2, scale=2 ** 0.5):
-    if bias is not None:
-        shape = (1, bias.shape[0]) + (1,) * (input.dim() - bias.dim() - 1)
-        input = input + bias.view(shape)
-    return F.leaky_relu(input, negative_slope=0.2) * scale
-
-
-class FusedLeakyReLU(nn.Module):
-    def __init__(self, channel, bias=True, negative_slope=0.2, scale=2 ** 0.5):
-        super().__init__()
-        self.bias = nn.Parameter(torch.zeros(channel)) if bias else None
-        self.negative_slope = negative_slope
-        self.scale = scale
-
-    def forward(self, input):
-        return fused_leaky_relu(input, self.bias, self.negative_slope, self.scale)
-
-
-def upfirdn2d(input, kernel, up=1, down=1, pad=(0, 0)):
-    """Upsample (zero insertion) -> pad -> FIR (true convolution) -> downsample."""
-    b, c, h, w = input.shape
-    kh, kw = kernel.shape
-    p0, p1 = pad
-    x = input
-    if up > 1:
-        z = x.new_zeros(b, c, h, up, w, up)
-        z[:, :, :, 0, :, 0] = x
-        x = z.view(b, c, h * up, w * up)
-    x = F.pad(x, [max(p0, 0), max(p1, 0), max(p0, 0), max(p1, 0)])
-    x = x[:, :, max(-p0, 0):x.shape[2] - max(-p1, 0), max(-p0, 0):x.shape[3] - max(-p1, 0)]
-    wgt = torch.flip(kernel, [0, 1]).to(x.dtype).view(1, 1, kh, kw).expand(c, 1, kh, kw)
-    x = F.conv2d(x, wgt, groups=c)
-    if down > 1:
-        x = x[:, :, ::down, ::down]
-    return x
 
 
 def make_kernel(k):
@@ -290,6 +255,8 @@ class Decoder(nn.Module):
             self.to_rgbs.append(ToRGB(out_ch, self.style_dim))
             in_ch = out_ch
         self.n_latent = (self.log_size - self.log_in_size) * 2 + 2
+        self.use_fused = True      # HIP epilogues on the inference path (GPU, no grad)
+        self._fir = None
 
     def mean_latent(self, renderer_latent):
         return self.style(renderer_latent).mean(0, keepdim=True)
@@ -326,6 +293,8 @@ class Decoder(nn.Module):
         latent, noise = self.styles_and_noise_forward(styles, noise, inject_index, truncation,
                                                       truncation_latent, input_is_latent,
                                                       randomize_noise)
+        if self._fused_ok(features, rgbd_in, transform):
+            return self._fused_forward(features, latent, noise), (latent if return_latents else None)
         out = self.conv1(features, latent[:, 0], noise=noise[0], transform=transform,
                          mesh_path=mesh_path)
         skip = self.to_rgb1(out, latent[:, 1], skip=rgbd_in)
@@ -337,6 +306,62 @@ class Decoder(nn.Module):
             skip = to_rgb(out, latent[:, i + 2], skip=skip)
             i += 2
         return skip, (latent if return_latents else None)
+
+    # -- fused inference path ------------------------------------------------
+    def _fused_ok(self, features, rgbd_in, transform):
+        if not (self.use_fused and features.is_cuda and rgbd_in is None and transform is None):
+            return False
+        if torch.is_grad_enabled() and (features.requires_grad or
+                                        any(p.requires_grad for p in self.parameters())):
+            return False
+        if self._fir is None:
+            fir = separable_taps(self.convs[0].conv.blur.kernel) if len(self.convs) else [0.0] * 4
+            ok = fir is not None and all(
+                torch.equal(t.upsample.kernel.cpu(), self.convs[0].conv.blur.kernel.cpu())
+                for t in self.to_rgbs)
+            self._fir = fir if ok else False
+        return self._fir is not False
+
+    def _fused_forward(self, features, latent, noise):
+        """Same computation as the module path, one MIOpen convolution plus one
+        sdfr_styled_epilogue per layer on channels_last activations; each
+        activation is pre-multiplied by the next layer's modulation and the
+        ToRGB layers are folded into the preceding epilogue."""
+        cl = torch.channels_last
+        B = features.shape[0]
+        seq = [self.conv1] + list(self.convs)
+        mods = [sc.conv.modulation(latent[:, i]) for i, sc in enumerate(seq)]
+        x = modulate_to_nhwc(features, mods[0])
+        rgb = None
+        for i, sc in enumerate(seq):
+            mc = sc.conv
+            w = mc.scale * mc.weight[0]
+            demod = (torch.rsqrt((mods[i] * mods[i]) @ (w * w).sum([2, 3]).t() + 1e-8)
+                     if mc.demodulate else None)
+            if mc.upsample:
+                out = F.conv_transpose2d(x, w.transpose(0, 1).contiguous(memory_format=cl),
+                                         stride=2)
+                H, W = out.shape[2] - 1, out.shape[3] - 1
+            else:
+                out = F.conv2d(x, w.contiguous(memory_format=cl), padding=mc.padding)
+                H, W = out.shape[2], out.shape[3]
+            n = noise[i] if noise[i] is not None else features.new_empty(B, 1, H, W).normal_()
+            last = i == len(seq) - 1
+            rgb_w = rgb_b = None
+            if i % 2 == 0:
+                to_rgb = self.to_rgb1 if i == 0 else self.to_rgbs[i // 2 - 1]
+                tc = to_rgb.conv
+                s_rgb = tc.modulation(latent[:, i + 1])
+                rgb_w = (tc.scale * tc.weight[0, :, :, 0, 0])[None] * s_rgb[:, None, :]
+                rgb_b = to_rgb.bias
+            x, rgb_new = styled_epilogue(
+                out, fir=self._fir, bias=sc.activate.bias, noise_weight=sc.noise.weight,
+                noise=n, demod=demod, blur_up=mc.upsample,
+                s_next=None if last else mods[i + 1], store_y=not last,
+                rgb_w=rgb_w, rgb_b=rgb_b, skip=rgb if i else None)
+            if rgb_new is not None:
+                rgb = rgb_new
+        return rgb
 
 
 def _has(o, k):
