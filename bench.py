@@ -34,6 +34,7 @@ METRIC = "rendered faces/sec/GPU at 256² (SDF+ngp path); 1/2/4/8-GPU scaling"
 FLOP_PER_SAMPLE = 550912          # renderer MLP, SURVEY.md §8(d) / BASELINE.md §2
 GATHER_BYTES_PER_SAMPLE = 1024    # 16 levels x 8 corners x 2 x fp32
 MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
+MFMA_F16_PEAK_TFLOPS = 2500.0     # MI355X dense fp16/bf16 MFMA peak (no sparsity)
 HBM_PEAK_GBPS = 8000.0            # MI355X HBM3E peak
 
 
@@ -45,6 +46,8 @@ def parse():
     p.add_argument("--batch", type=int, default=32, help="faces per step per GPU")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--field-precision", default="f16x3", choices=["f16x3", "fp32"],
+                   help="field-stage GEMM arithmetic (DESIGN.md section 5)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--traffic-json", default=str(REPO / "profiles" / "field_traffic.json"))
     return p.parse_args()
@@ -106,6 +109,7 @@ def main():
     from sdfr_loader import load
     sdfr = load()
     g, opt = build_generator(sdfr, device, args.seed)
+    g.renderer.field_precision = args.field_precision
     B = args.batch
     res = opt.model.renderer_spatial_output_dim
     N = opt.rendering.N_samples
@@ -155,14 +159,30 @@ def main():
     samples = B * res * res * N
     field_tflops = FLOP_PER_SAMPLE * samples / (field_ms * 1e-3) / 1e12
     gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9
+    f16x3 = args.field_precision == "f16x3"
+    field_kernel = "ngp_field_x_kernel" if f16x3 else "ngp_field_kernel"
     traffic = None
     tj = Path(args.traffic_json)
     if tj.exists():
         try:
-            traffic = json.loads(tj.read_text()).get("bytes_per_launch_per_face")
-            traffic = None if traffic is None else traffic * B
-        except Exception:
+            per = json.loads(tj.read_text())["kernels"][field_kernel]
+            traffic = per["bytes_per_launch_per_face"] * B
+        except (KeyError, ValueError, TypeError):
             traffic = None
+    if f16x3:
+        # fp32-accurate GEMMs as 3 fp16 MFMA terms: the attainable fp32-equivalent
+        # peak is the dense fp16 MFMA peak / 3
+        roof = {"kernel": "ngp_field_x_kernel (MLP as 3 split-fp16 v_mfma_f32_16x16x32_f16 "
+                          "terms per fp32 tile + compositing)",
+                "bound": "mfma", "achieved": field_tflops, "peak": MFMA_F16_PEAK_TFLOPS / 3,
+                "unit": "TFLOP/s", "frac": field_tflops / (MFMA_F16_PEAK_TFLOPS / 3),
+                "traffic": traffic, "mfma_dtype": "f16 (hi/lo split, fp32 accumulate)",
+                "mfma_issued_tflops": 3 * field_tflops, "mfma_peak_dtype": MFMA_F16_PEAK_TFLOPS}
+    else:
+        roof = {"kernel": "ngp_field_kernel (MLP on v_mfma_f32_16x16x4_f32 + compositing)",
+                "bound": "mfma", "achieved": field_tflops, "peak": MFMA_F32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": field_tflops / MFMA_F32_PEAK_TFLOPS,
+                "traffic": traffic, "mfma_dtype": "f32"}
 
     faces = world * B * args.steps
     line = {
@@ -180,11 +200,9 @@ def main():
         "data": "synthetic (random z, random cameras, random-init weights)",
         "config": {"workload": "eval.py 5000-image generation (ffhq_256_sdf_ngp, configs[1])",
                    "faces_per_step_per_gpu": B, "renderer": f"{res}x{res} rays x {N} samples",
-                   "output": "256x256 RGB", "parallelism": f"dp{world} (independent faces)"},
-        "roofline": {"kernel": "ngp_field_kernel (MLP on v_mfma_f32_16x16x4_f32 + compositing)",
-                     "bound": "mfma", "achieved": field_tflops, "peak": MFMA_F32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": field_tflops / MFMA_F32_PEAK_TFLOPS,
-                     "traffic": traffic},
+                   "output": "256x256 RGB", "parallelism": f"dp{world} (independent faces)",
+                   "field_precision": args.field_precision},
+        "roofline": roof,
         "roofline_gather": {"kernel": "ngp_encode_kernel (sampling + 16-level hash-grid gather)",
                             "bound": "hbm", "achieved": gather_gbps, "peak": HBM_PEAK_GBPS,
                             "unit": "GB/s", "frac": gather_gbps / HBM_PEAK_GBPS},

@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 1
+#define SDFR_ABI_VERSION 2
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -146,7 +146,16 @@ typedef struct sdfr_ngp_render_args {
      * [0] before the prep kernel, [1] before the hash-grid kernel,
      * [2] before the field (MLP + compositing) kernel, [3] after it. */
     void *stage_events[4];
+    /* Field-stage GEMM arithmetic (both accumulate in fp32):
+     * SDFR_FIELD_F16X3 (0, default) three v_mfma_f32_16x16x32_f16 per tile on a
+     *   hi/lo fp16 split of row-scaled weights and activations (fp32-level
+     *   accuracy);
+     * SDFR_FIELD_FP32 (1) v_mfma_f32_16x16x4_f32 (exact fp32 fma chain). */
+    int field_precision;
 } sdfr_ngp_render_args;
+
+#define SDFR_FIELD_F16X3 0
+#define SDFR_FIELD_FP32 1
 
 size_t sdfr_render_ngp_workspace_bytes(uint32_t B, uint32_t H, uint32_t W,
                                        uint32_t N, uint32_t num_levels);

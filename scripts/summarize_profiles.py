@@ -23,7 +23,7 @@ from collections import defaultdict
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
-FIELD = "ngp_field_kernel"
+FIELDS = ("ngp_field_kernel", "ngp_field_x_kernel")   # fp32 / f16x3 field kernels
 ENCODE = "ngp_encode_kernel"
 
 
@@ -78,14 +78,19 @@ def main():
         }
     (dst / f"{a.tag}_traffic.json").write_text(json.dumps(out, indent=1))
 
-    fk = next((v for k, v in out["kernels"].items() if FIELD in k), None)
-    if fk and fk["fetch_bytes_corrected"] is not None and fk["write_bytes"] is not None:
-        total = fk["fetch_bytes_corrected"] + fk["write_bytes"]
-        (dst / "field_traffic.json").write_text(json.dumps({
-            "kernel": FIELD, "source": f"profiles/{a.tag}_traffic.json",
-            "bytes_per_launch_per_face": total / a.batch,
-            "fetch_bytes_per_face": fk["fetch_bytes_corrected"] / a.batch,
-            "write_bytes_per_face": fk["write_bytes"] / a.batch}, indent=1))
+    tj = dst / "field_traffic.json"
+    prev = json.loads(tj.read_text()) if tj.exists() else {}
+    per = prev.get("kernels", {}) if isinstance(prev.get("kernels"), dict) else {}
+    for fname in FIELDS:
+        fk = next((v for k, v in out["kernels"].items() if f"::{fname}" in k), None)
+        if fk and fk["fetch_bytes_corrected"] is not None and fk["write_bytes"] is not None:
+            total = fk["fetch_bytes_corrected"] + fk["write_bytes"]
+            per[fname] = {"source": f"profiles/{a.tag}_traffic.json",
+                          "bytes_per_launch_per_face": total / a.batch,
+                          "fetch_bytes_per_face": fk["fetch_bytes_corrected"] / a.batch,
+                          "write_bytes_per_face": fk["write_bytes"] / a.batch}
+    tj.write_text(json.dumps({"unit": "HBM bytes per face per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+                              "kernels": per}, indent=1))
     print(json.dumps(out, indent=1))
 
 

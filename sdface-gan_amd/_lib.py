@@ -23,7 +23,9 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 1
+ABI_VERSION = 2
+FIELD_F16X3 = 0
+FIELD_FP32 = 1
 
 # every symbol include/sdfr.h declares (tests check the .so exports all of them)
 EXPORTS = (
@@ -61,7 +63,7 @@ class NgpRenderArgs(ctypes.Structure):
         ("z_normalize", _int), ("force_background", _int), ("with_sdf", _int),
         ("rgb", _vp), ("features", _vp), ("sdf", _vp), ("xyz", _vp), ("mask", _vp),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
-        ("stage_events", _vp * 4),
+        ("stage_events", _vp * 4), ("field_precision", _int),
     ]
 
 

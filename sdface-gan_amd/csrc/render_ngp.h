@@ -1,0 +1,119 @@
+// render_ngp.h -- pieces shared by the fused ngp renderer's kernels
+// (render_ngp.hip: prep, hash-grid encode, fp32-MFMA field kernel;
+//  field_f16x3.hip: split-fp16 MFMA field kernel).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "sdfr_common.h"
+
+namespace sdfr {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t kW = 256;          // NGPSIRENGenerator width
+constexpr uint32_t kFeatIn = 32;      // 16 levels x 2
+constexpr uint32_t kViewsIn = 272;    // 256 + 16 SH
+constexpr uint32_t kFilm = 4;         // FiLM layers: pts 0,1,2 + views
+constexpr uint32_t kTileRays = 16;    // rays per wave (MFMA N)
+
+// ----------------------------------------------------------------------------
+// shared ray / sample geometry
+// ----------------------------------------------------------------------------
+struct GeomArgs {
+    uint32_t B, H, W, N, tiles_per_face, total_tiles, S_total;
+    float half_res;
+    const float *cam, *focal, *near_, *far_, *pix_x, *pix_y;
+    SampleCfg sc;
+    int static_viewdirs, z_normalize;
+    float bound;
+};
+
+// tile-order sample id -> (face, ray-in-face, sample)
+struct SampleId {
+    uint32_t b, ray_local, s, n, tile;
+    bool valid;
+};
+
+__device__ __forceinline__ SampleId decode_sid(const GeomArgs &g, uint32_t sid) {
+    SampleId r;
+    r.n = sid & 15u;
+    const uint32_t rest = sid >> 4;
+    r.s = rest % g.N;
+    r.tile = rest / g.N;
+    r.b = r.tile / g.tiles_per_face;
+    r.ray_local = (r.tile % g.tiles_per_face) * kTileRays + r.n;
+    r.valid = r.tile < g.total_tiles && r.ray_local < g.H * g.W;
+    return r;
+}
+
+struct FieldArgs {
+    GeomArgs g;
+    const float *enc;              // [L=16][S_total][2]
+    const f4 *packed;              // [67][1024]
+    const float *film;             // [B][4][2][256]
+    const float *bias[5];          // input, pts0..2, views
+    const float *sigma_w, *sigma_b, *rgb_w, *rgb_b, *sigmoid_beta;
+    const float *sigma_noise;      // [B,H,W,N] or null (no_sdf only)
+    int force_background, with_sdf;
+    float *rgb, *features, *sdf, *xyz, *mask;
+};
+
+constexpr uint32_t kCst = 9 * kW;              // LDS constants: bias[5], sigma_w, rgb_w[3]
+constexpr int kWaves = 4;                       // 1 wave per SIMD, 512 VGPR+AGPR
+constexpr int kThreads = kWaves * 64;
+
+// sin via the hardware v_sin_f32 (argument in revolutions, |u| <= 0.5 after an
+// fma Cody-Waite reduction by 2pi): 6 VALU + 1 transcendental.  Accuracy is
+// measured against float64 by tests/test_gpu_encoders.py::test_sin_accuracy.
+__device__ __forceinline__ float sin_hw(float x) {
+    const float k = __builtin_rintf(x * 0.159154943091895336f);
+    float r = __fmaf_rn(-k, 6.28318548202514648f, x);
+    r = __fmaf_rn(-k, -1.74845553146951752e-7f, r);
+    return __builtin_amdgcn_sinf(r * 0.159154943091895336f);
+}
+
+// SH degree 4 coefficients 4g..4g+3 of a unit direction (shencoder.cu:50-68)
+__device__ __forceinline__ f4 sh_quad(float x, float y, float z, uint32_t g) {
+    const float xy = __fmul_rn(x, y), xz = __fmul_rn(x, z), yz = __fmul_rn(y, z);
+    const float x2 = __fmul_rn(x, x), y2 = __fmul_rn(y, y), z2 = __fmul_rn(z, z);
+    f4 q0, q1, q2, q3;
+    q0.x = 0.28209479177387814f;
+    q0.y = __fmul_rn(-0.48860251190291987f, y);
+    q0.z = __fmul_rn(0.48860251190291987f, z);
+    q0.w = __fmul_rn(-0.48860251190291987f, x);
+    q1.x = __fmul_rn(1.0925484305920792f, xy);
+    q1.y = __fmul_rn(-1.0925484305920792f, yz);
+    q1.z = __fmaf_rn(0.94617469575755997f, z2, -0.31539156525251999f);
+    q1.w = __fmul_rn(-1.0925484305920792f, xz);
+    q2.x = __fmaf_rn(0.54627421529603959f, x2, -__fmul_rn(0.54627421529603959f, y2));
+    q2.y = __fmul_rn(__fmul_rn(0.59004358992664352f, y), __fmaf_rn(-3.0f, x2, y2));
+    q2.z = __fmul_rn(__fmul_rn(2.8906114426405538f, xy), z);
+    q2.w = __fmul_rn(__fmul_rn(0.45704579946446572f, y), __fmaf_rn(-5.0f, z2, 1.0f));
+    q3.x = __fmul_rn(__fmul_rn(0.3731763325901154f, z), __fmaf_rn(5.0f, z2, -3.0f));
+    q3.y = __fmul_rn(__fmul_rn(0.45704579946446572f, x), __fmaf_rn(-5.0f, z2, 1.0f));
+    q3.z = __fmul_rn(__fmul_rn(1.4453057213202769f, z), __fsub_rn(x2, y2));
+    q3.w = __fmul_rn(__fmul_rn(0.59004358992664352f, x), __fmaf_rn(3.0f, y2, -x2));
+    return g == 0 ? q0 : (g == 1 ? q1 : (g == 2 ? q2 : q3));
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// sum over the 4 lane groups holding the same ray (lanes n, n+16, n+32, n+48)
+__device__ __forceinline__ float group_sum(float v) {
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+
+// Split-fp16 field path (field_f16x3.hip).  Its workspace region (`xws`,
+// f16x3_ws_bytes()) holds the packed fp16 fragments, row scales and scaled biases.
+size_t f16x3_ws_bytes(uint32_t B);
+int launch_xprep(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, char *xws,
+                 float *film, hipStream_t st);
+int launch_xfield(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, const GeomArgs &g,
+                  const float *enc, char *xws, const float *film, hipStream_t st);
+
+}  // namespace sdfr

@@ -36,19 +36,12 @@
 #include <cstdint>
 #include <string>
 
-#include "sdfr_common.h"
+#include "render_ngp.h"
 
 namespace sdfr {
 
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-constexpr uint32_t kW = 256;          // NGPSIRENGenerator width
-constexpr uint32_t kFeatIn = 32;      // 16 levels x 2
-constexpr uint32_t kViewsIn = 272;    // 256 + 16 SH
 constexpr uint32_t kSliceF4 = 1024;   // float4 per 16-wide K slice (16 t_out x 64 lanes)
 constexpr uint32_t kSlices = 2 + 16 * 3 + 17;   // 67 slices per sample step
-constexpr uint32_t kFilm = 4;         // FiLM layers: pts 0,1,2 + views
-constexpr uint32_t kTileRays = 16;    // rays per wave (MFMA N)
 
 // slice index -> (layer, t_in)
 __host__ __device__ constexpr uint32_t slice_base(uint32_t layer) {
@@ -115,36 +108,6 @@ __global__ void __launch_bounds__(256) ngp_prep_kernel(const PrepArgs a) {
 }
 
 // ----------------------------------------------------------------------------
-// shared ray / sample geometry
-// ----------------------------------------------------------------------------
-struct GeomArgs {
-    uint32_t B, H, W, N, tiles_per_face, total_tiles, S_total;
-    float half_res;
-    const float *cam, *focal, *near_, *far_, *pix_x, *pix_y;
-    SampleCfg sc;
-    int static_viewdirs, z_normalize;
-    float bound;
-};
-
-// tile-order sample id -> (face, ray-in-face, sample)
-struct SampleId {
-    uint32_t b, ray_local, s, n, tile;
-    bool valid;
-};
-
-__device__ __forceinline__ SampleId decode_sid(const GeomArgs &g, uint32_t sid) {
-    SampleId r;
-    r.n = sid & 15u;
-    const uint32_t rest = sid >> 4;
-    r.s = rest % g.N;
-    r.tile = rest / g.N;
-    r.b = r.tile / g.tiles_per_face;
-    r.ray_local = (r.tile % g.tiles_per_face) * kTileRays + r.n;
-    r.valid = r.tile < g.total_tiles && r.ray_local < g.H * g.W;
-    return r;
-}
-
-// ----------------------------------------------------------------------------
 // 2. encode: sampling + hash-grid gather
 // ----------------------------------------------------------------------------
 struct EncodeArgs {
@@ -200,21 +163,6 @@ __global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
 // ----------------------------------------------------------------------------
 // 3. field: MLP on MFMA + compositing
 // ----------------------------------------------------------------------------
-struct FieldArgs {
-    GeomArgs g;
-    const float *enc;              // [L=16][S_total][2]
-    const f4 *packed;              // [67][1024]
-    const float *film;             // [B][4][2][256]
-    const float *bias[5];          // input, pts0..2, views
-    const float *sigma_w, *sigma_b, *rgb_w, *rgb_b, *sigmoid_beta;
-    const float *sigma_noise;      // [B,H,W,N] or null (no_sdf only)
-    int force_background, with_sdf;
-    float *rgb, *features, *sdf, *xyz, *mask;
-};
-
-constexpr uint32_t kCst = 9 * kW;              // LDS constants: bias[5], sigma_w, rgb_w[3]
-constexpr int kWaves = 4;                       // 1 wave per SIMD, 512 VGPR+AGPR
-constexpr int kThreads = kWaves * 64;
 constexpr int kStageF4 = kSliceF4 / kThreads;   // float4 staged per thread per slice
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
@@ -242,16 +190,6 @@ __device__ __forceinline__ float sin_cw(float x) {
     return (q & 2) ? -v : v;
 }
 
-// sin via the hardware v_sin_f32 (argument in revolutions, |u| <= 0.5 after an
-// fma Cody-Waite reduction by 2pi): 6 VALU + 1 transcendental.  Accuracy is
-// measured against float64 by tests/test_gpu_encoders.py::test_sin_accuracy.
-__device__ __forceinline__ float sin_hw(float x) {
-    const float k = __builtin_rintf(x * 0.159154943091895336f);
-    float r = __fmaf_rn(-k, 6.28318548202514648f, x);
-    r = __fmaf_rn(-k, -1.74845553146951752e-7f, r);
-    return __builtin_amdgcn_sinf(r * 0.159154943091895336f);
-}
-
 // The FiLM activation's sin: hardware v_sin_f32 after reduction (max |err|
 // 3.7e-7 on |x| <= 200, measured; 1 transcendental + 6 VALU) instead of the
 // polynomial (9e-8, ~17 VALU).  Both errors sit an order of magnitude below
@@ -265,32 +203,6 @@ __global__ void sin_probe_kernel(const float *__restrict__ x, float *__restrict_
     cw[i] = sin_cw(x[i]);
     hw[i] = sin_hw(x[i]);
 }
-
-// SH degree 4 coefficients 4g..4g+3 of a unit direction (shencoder.cu:50-68)
-__device__ __forceinline__ f4 sh_quad(float x, float y, float z, uint32_t g) {
-    const float xy = __fmul_rn(x, y), xz = __fmul_rn(x, z), yz = __fmul_rn(y, z);
-    const float x2 = __fmul_rn(x, x), y2 = __fmul_rn(y, y), z2 = __fmul_rn(z, z);
-    f4 q0, q1, q2, q3;
-    q0.x = 0.28209479177387814f;
-    q0.y = __fmul_rn(-0.48860251190291987f, y);
-    q0.z = __fmul_rn(0.48860251190291987f, z);
-    q0.w = __fmul_rn(-0.48860251190291987f, x);
-    q1.x = __fmul_rn(1.0925484305920792f, xy);
-    q1.y = __fmul_rn(-1.0925484305920792f, yz);
-    q1.z = __fmaf_rn(0.94617469575755997f, z2, -0.31539156525251999f);
-    q1.w = __fmul_rn(-1.0925484305920792f, xz);
-    q2.x = __fmaf_rn(0.54627421529603959f, x2, -__fmul_rn(0.54627421529603959f, y2));
-    q2.y = __fmul_rn(__fmul_rn(0.59004358992664352f, y), __fmaf_rn(-3.0f, x2, y2));
-    q2.z = __fmul_rn(__fmul_rn(2.8906114426405538f, xy), z);
-    q2.w = __fmul_rn(__fmul_rn(0.45704579946446572f, y), __fmaf_rn(-5.0f, z2, 1.0f));
-    q3.x = __fmul_rn(__fmul_rn(0.3731763325901154f, z), __fmaf_rn(5.0f, z2, -3.0f));
-    q3.y = __fmul_rn(__fmul_rn(0.45704579946446572f, x), __fmaf_rn(-5.0f, z2, 1.0f));
-    q3.z = __fmul_rn(__fmul_rn(1.4453057213202769f, z), __fsub_rn(x2, y2));
-    q3.w = __fmul_rn(__fmul_rn(0.59004358992664352f, x), __fmaf_rn(3.0f, y2, -x2));
-    return g == 0 ? q0 : (g == 1 ? q1 : (g == 2 ? q2 : q3));
-}
-
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // Streaming state for the weight ring: slot s of `lds` holds one K-slice.
 struct Ring {
@@ -402,13 +314,6 @@ __device__ __forceinline__ void film_act(f4 (&act)[16], const f4 (&acc)[16],
         v.w = sin_cw(__fadd_rn(__fmul_rn(gm.w, acc[t].w), bt.w));
         act[t] = v;
     }
-}
-
-// sum over the 4 lane groups holding the same ray (lanes n, n+16, n+32, n+48)
-__device__ __forceinline__ float group_sum(float v) {
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    return v;
 }
 
 __device__ __forceinline__ float dot_feat(const f4 (&act)[16], const float *w, uint32_t g) {
@@ -653,8 +558,9 @@ struct Workspace {
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// enc [L][S][2] | packed fp32 fragments | film | split-fp16 region (field_f16x3.hip)
 static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t L,
-                        size_t *o_packed, size_t *o_film) {
+                        size_t *o_packed, size_t *o_film, size_t *o_x = nullptr) {
     const size_t tiles = (size_t)B * ((H * W + kTileRays - 1) / kTileRays);
     const size_t S = tiles * N * kTileRays;
     size_t off = align256(S * L * 2 * sizeof(float));
@@ -662,6 +568,8 @@ static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t
     off += align256((size_t)kSlices * kSliceF4 * sizeof(f4));
     *o_film = off;
     off += align256((size_t)B * kFilm * 2 * kW * sizeof(float));
+    if (o_x) *o_x = off;
+    off += align256(f16x3_ws_bytes(B));
     return off;
 }
 
@@ -671,6 +579,8 @@ static int validate(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a) {
         return fail(SDFR_EUNSUPPORTED, "render_ngp: fused path needs 16 levels x 2 features");
     if (a->B == 0 || a->H == 0 || a->W == 0 || a->N == 0)
         return fail(SDFR_EINVAL, "render_ngp: empty batch / image / sample count");
+    if (a->field_precision != SDFR_FIELD_F16X3 && a->field_precision != SDFR_FIELD_FP32)
+        return fail(SDFR_EINVAL, "render_ngp: field_precision must be 0 (f16x3) or 1 (fp32)");
     if (!a->cam || !a->focal || !a->near_ || !a->far_ || !a->styles || !a->pix_x ||
         !a->pix_y || !a->t_vals || !a->rgb || !a->workspace)
         return fail(SDFR_EINVAL, "render_ngp: required pointer is null");
@@ -826,8 +736,8 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     int rc = validate(w, a);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    size_t o_packed, o_film;
-    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film);
+    size_t o_packed, o_film, o_x;
+    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film, &o_x);
     char *ws = reinterpret_cast<char *>(a->workspace);
     float *enc = reinterpret_cast<float *>(ws);
     f4 *packed = reinterpret_cast<f4 *>(ws + o_packed);
@@ -836,6 +746,15 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     GeomArgs g;
     fill_geom(w, a, g);
     record_event(a->stage_events[0], st);
+    if (a->field_precision == SDFR_FIELD_F16X3) {
+        if ((rc = launch_xprep(w, a, ws + o_x, film, st))) return rc;
+        record_event(a->stage_events[1], st);
+        if ((rc = launch_encode(w, a, g, enc, st))) return rc;
+        record_event(a->stage_events[2], st);
+        if ((rc = launch_xfield(w, a, g, enc, ws + o_x, film, st))) return rc;
+        record_event(a->stage_events[3], st);
+        return SDFR_OK;
+    }
     if ((rc = launch_prep(w, a, packed, film, st))) return rc;
     record_event(a->stage_events[1], st);
     if ((rc = launch_encode(w, a, g, enc, st))) return rc;

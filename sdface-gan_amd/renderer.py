@@ -301,6 +301,10 @@ class VolumeFeatureRenderer(nn.Module):
         # torch.cuda RNG, no host round trip) and a switch for the fused path.
         self.rng_device = "cpu"
         self.use_fused = True
+        # field-stage GEMM arithmetic of the fused path: "f16x3" (three fp16 MFMA
+        # terms on row-scaled hi/lo splits, fp32-level accuracy) or "fp32"
+        # (v_mfma_f32_16x16x4_f32); include/sdfr.h, DESIGN.md section 5
+        self.field_precision = "f16x3"
         # optional 4 torch.cuda.Event(enable_timing=True) recorded around the
         # fused stages (prep | hash grid | field | end), see include/sdfr.h
         self.stage_events = None
@@ -530,6 +534,10 @@ class VolumeFeatureRenderer(nn.Module):
         a.rgb, a.features, a.sdf = _lib.ptr(rgb), _lib.ptr(features), _lib.ptr(sdf)
         a.xyz, a.mask = _lib.ptr(xyz), _lib.ptr(mask)
         a.workspace, a.workspace_bytes = _lib.ptr(ws), ws_bytes
+        if self.field_precision not in ("f16x3", "fp32"):
+            raise ValueError(f"field_precision must be 'f16x3' or 'fp32', "
+                             f"got {self.field_precision!r}")
+        a.field_precision = _lib.FIELD_FP32 if self.field_precision == "fp32" else _lib.FIELD_F16X3
         if self.stage_events is not None:
             for k, ev in enumerate(self.stage_events):
                 a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)

@@ -51,7 +51,10 @@ def renderer_sd(golden_dir):
     return W.det_state_dict(W.golden_entries(golden_dir), "renderer.")
 
 
-def make_renderer(sdfr, sd, res, N, **flags):
+PRECISIONS = ["f16x3", "fp32"]
+
+
+def make_renderer(sdfr, sd, res, N, precision="f16x3", **flags):
     opt = sdfr.vol_render_opt()
     r = opt.rendering
     r.N_samples = N
@@ -61,6 +64,7 @@ def make_renderer(sdfr, sd, res, N, **flags):
     own = ren.state_dict()
     ren.load_state_dict({k[len("renderer."):]: v for k, v in sd.items()
                          if k[len("renderer."):] in own}, strict=True)
+    ren.field_precision = precision
     return ren.to(DEV).eval()
 
 
@@ -78,16 +82,18 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("prec", PRECISIONS)
 @pytest.mark.parametrize("name,flags", CASES)
-def test_fused_render_vs_reference_golden(sdfr, golden_dir, renderer_sd, name, flags):
+def test_fused_render_vs_reference_golden(sdfr, golden_dir, renderer_sd, name, flags, prec):
     g = np.load(golden_dir / f"{name}.npz")
-    ren = make_renderer(sdfr, renderer_sd, int(g["res"]), int(g["n_samples"]), **flags)
+    ren = make_renderer(sdfr, renderer_sd, int(g["res"]), int(g["n_samples"]), prec, **flags)
     cam, focal, near, far, lat, tr = _inputs(g)
     with torch.no_grad():
         assert ren._fused_ok(cam, lat, False)
         rgb, feat, sdf, mask, xyz, eik = ren(cam, focal, near, far, styles=lat, t_rand=tr)
     torch.cuda.synchronize()
     assert eik is None
+    name = f"{name}_{prec}"
     _cmp(name, "rgb", rgb.cpu().numpy(), g["rgb"])
     _cmp(name, "features", feat.cpu().numpy(), g["features"])
     if "sdf" in g.files:
@@ -139,8 +145,9 @@ def test_encode_stage_bit_exact(sdfr, oracle_mod, golden_dir, renderer_sd, name)
     (2, 8, 16, dict(no_sdf=True)),                         # density branch (softplus)
     (1, 8, 1, {}),                                         # single sample per ray
 ])
-def test_fused_render_vs_oracle(sdfr, oracle_mod, renderer_sd, B, res, N, flags):
-    ren = make_renderer(sdfr, renderer_sd, res, N, **flags)
+@pytest.mark.parametrize("prec", PRECISIONS)
+def test_fused_render_vs_oracle(sdfr, oracle_mod, renderer_sd, B, res, N, flags, prec):
+    ren = make_renderer(sdfr, renderer_sd, res, N, prec, **flags)
     torch.manual_seed(B * 100 + res + N)
     ext, focal, near, far, _ = sdfr.generate_camera_params(res, "cpu", batch=B)
     lat = torch.from_numpy(W.det_uniform((B, 256), -1.5, 1.5, 5 + N))
@@ -159,7 +166,7 @@ def test_fused_render_vs_oracle(sdfr, oracle_mod, renderer_sd, B, res, N, flags)
         z_normalize=not flags.get("no_z_normalize", False),
         force_background=flags.get("force_background", False),
         with_sdf=not flags.get("no_sdf", False))
-    name = f"oracle_B{B}_r{res}_N{N}_{'_'.join(flags) or 'default'}"
+    name = f"oracle_B{B}_r{res}_N{N}_{'_'.join(flags) or 'default'}_{prec}"
     _cmp(name, "rgb", rgb.cpu().numpy(), o["rgb"].numpy())
     _cmp(name, "features", feat.cpu().numpy(), o["features"].numpy())
     if sdf is not None:
@@ -169,10 +176,11 @@ def test_fused_render_vs_oracle(sdfr, oracle_mod, renderer_sd, B, res, N, flags)
         _cmp(name, "mask", mask.cpu().numpy(), o["mask"].numpy())
 
 
-def test_out_of_bound_samples(sdfr, oracle_mod, renderer_sd):
+@pytest.mark.parametrize("prec", PRECISIONS)
+def test_out_of_bound_samples(sdfr, oracle_mod, renderer_sd, prec):
     """Camera far outside the unit volume: normalized points leave [0,1]^3 and the
     grid contributes exactly zero (gridencoder.cu:110-135)."""
-    ren = make_renderer(sdfr, renderer_sd, 8, 24)
+    ren = make_renderer(sdfr, renderer_sd, 8, 24, prec)
     torch.manual_seed(3)
     ext, focal, near, far, _ = sdfr.generate_camera_params(8, "cpu", batch=1)
     ext[:, :, 3] *= 3.0
@@ -185,8 +193,8 @@ def test_out_of_bound_samples(sdfr, oracle_mod, renderer_sd):
                               far.numpy(), lat.numpy(), N=24, res=8, t_rand=tr.numpy(),
                               return_intermediates=True)
     assert (o["enc"].abs().sum(-1) == 0).any()
-    _cmp("oob", "rgb", rgb.cpu().numpy(), o["rgb"].numpy())
-    _cmp("oob", "features", feat.cpu().numpy(), o["features"].numpy())
+    _cmp(f"oob_{prec}", "rgb", rgb.cpu().numpy(), o["rgb"].numpy())
+    _cmp(f"oob_{prec}", "features", feat.cpu().numpy(), o["features"].numpy())
 
 
 def test_fused_equals_unfused_module_path(sdfr, oracle_mod, renderer_sd):
@@ -226,9 +234,10 @@ def test_generator_vs_reference_golden(sdfr, golden_dir):
     _cmp("generator", "image", rgb.cpu().numpy(), z["rgb"])
 
 
-def test_batch_consistency(sdfr, renderer_sd):
+@pytest.mark.parametrize("prec", PRECISIONS)
+def test_batch_consistency(sdfr, renderer_sd, prec):
     """Faces are independent: rendering B faces at once == one at a time (bitwise)."""
-    ren = make_renderer(sdfr, renderer_sd, 16, 24)
+    ren = make_renderer(sdfr, renderer_sd, 16, 24, prec)
     torch.manual_seed(4)
     ext, focal, near, far, _ = sdfr.generate_camera_params(16, DEV, batch=3)
     lat = torch.from_numpy(W.det_uniform((3, 256), -1, 1, 4)).to(DEV)
