@@ -171,8 +171,10 @@ int sdfr_render_ngp_encode_only(const sdfr_ngp_weights *w,
 /* Profiling hook: select an ablated build of the field kernel for the NEXT
  * sdfr_render_ngp_forward calls (process-global).  0 = the product kernel;
  * 1 no barrier, 2 no LDS A-operand reads, 4 no weight staging, 8 no
- * activations, 15 MFMA only.  Non-zero variants produce wrong outputs and
- * exist only to attribute kernel time ("Field kernel anatomy"). */
+ * activations, 16 no compositing (f16x3 kernel), 15/31 MFMA only.  Non-zero
+ * variants produce wrong outputs, exist only to attribute kernel time
+ *  and are compiled only into `make ABLATION=1` builds;
+ * the product build accepts 0 only (SDFR_EINVAL otherwise). */
 int sdfr_debug_set_field_variant(int variant);
 
 /* Accuracy probe for the two device sin implementations the field kernel can

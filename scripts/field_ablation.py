@@ -16,10 +16,10 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from sdfr_loader import load  # noqa: E402
 
 VARIANTS = {0: "product", 1: "no barrier", 2: "no LDS A reads", 4: "no staging",
-            8: "no activations", 15: "MFMA only"}
+            8: "no activations", 16: "no compositing (f16x3)", 31: "MFMA only"}
 
 
-def main(B=32, rounds=5):
+def main(B=32, rounds=5, precision="f16x3"):
     sdfr = load()
     dev = "cuda:0"
     opt = sdfr.vol_render_opt()
@@ -27,6 +27,8 @@ def main(B=32, rounds=5):
     g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
     ren = g.renderer
     ren.rng_device = "device"
+    ren.field_precision = precision
+    print(f"field precision {precision}")
     ext, focal, near, far, _ = sdfr.generate_camera_params(64, dev, batch=B)
     lat = g.style(torch.randn(B, 256, device=dev))
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -85,4 +87,4 @@ def main(B=32, rounds=5):
 
 
 if __name__ == "__main__":
-    main()
+    main(precision=sys.argv[1] if len(sys.argv) > 1 else "f16x3")

@@ -1,0 +1,50 @@
+"""Median field-stage time of the fused renderer for each libsdfr.so variant given on
+the command line (each in its own subprocess; profiling aid, not a test).
+    python scripts/field_time.py sdface-gan_amd/lib_var/a/libsdfr.so ..."""
+import os
+import statistics
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+
+CHILD = r'''
+import statistics, sys, torch
+sys.path.insert(0, sys.argv[1])
+from sdfr_loader import load
+sdfr = load()
+dev = "cuda:0"; B = 32
+opt = sdfr.vol_render_opt()
+torch.manual_seed(0)
+g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
+ren = g.renderer; ren.rng_device = "device"; ren.field_precision = sys.argv[2]
+ext, focal, near, far, _ = sdfr.generate_camera_params(64, dev, batch=B)
+evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+for e in evs: e.record()
+ts = []
+with torch.no_grad():
+    lat = g.style(torch.randn(B, 256, device=dev))
+    for r in range(8):
+        ren.stage_events = evs
+        ren(ext, focal, near, far, styles=lat)
+        torch.cuda.synchronize()
+        if r >= 2: ts.append(evs[2].elapsed_time(evs[3]))
+med = statistics.median(ts)
+print(f"{med:.3f} ms  {550912 * B * 4096 * 24 / med / 1e9:.1f} TFLOP/s")
+'''
+
+
+def main():
+    prec = os.environ.get("PREC", "f16x3")
+    for lib in sys.argv[1:]:
+        env = dict(os.environ, SDFR_LIB=str(REPO / lib) if not lib.startswith("/") else lib)
+        out = subprocess.run([sys.executable, "-c", CHILD, str(REPO), prec], env=env,
+                             capture_output=True, text=True, timeout=240)
+        res = out.stdout.strip().splitlines()[-1] if out.returncode == 0 else \
+            f"FAILED rc={out.returncode}: {out.stderr.strip().splitlines()[-1:]}"
+        print(f"{lib:50s} {res}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

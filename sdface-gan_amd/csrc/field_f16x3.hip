@@ -41,6 +41,23 @@ constexpr uint32_t kXSlices = 2 + 16 * 3 + 18;   // half k-steps per pass
 constexpr int kXStage = kXSliceF4 / kThreads;    // float4 staged per thread per slice
 constexpr uint32_t kXCst = 10 * kW;              // bias_s[5], 1/su0, sigma_w, rgb_w[3]
 
+// Schedule options (compile-time; DESIGN.md section 5 records the measured choice):
+//   SDFR_X_PREFETCH  ring staged two slices ahead + next slice's first fragment
+//                    read before the barrier (1) / one slice ahead (0)
+//   SDFR_X_EPI       views layer output-group major with the compositing of tiles
+//                    0-7 in the MFMA shadow of tiles 8-15 (1) / after the layer (0)
+#ifndef SDFR_X_PREFETCH
+#define SDFR_X_PREFETCH 1
+#endif
+#ifndef SDFR_X_EPI
+#define SDFR_X_EPI 0
+#endif
+//   SDFR_X_BUFLOAD   ring staging loads as buffer_load (scalar slice offset, no
+//                    per-load 64-bit address VALU) (1) / global_load (0)
+#ifndef SDFR_X_BUFLOAD
+#define SDFR_X_BUFLOAD 1
+#endif
+
 __host__ __device__ constexpr uint32_t xslice_base(uint32_t layer) {
     return layer == 0 ? 0u : (layer == 4 ? 50u : 2u + 16u * (layer - 1));
 }
@@ -149,7 +166,10 @@ __global__ void __launch_bounds__(256) ngp_xprep_kernel(const XPrepArgs a) {
     if (slice >= 50) layer = 4;
     else if (slice >= 2) layer = 1 + (slice - 2) / 16;
     const uint32_t local = slice - xslice_base(layer);
-    const uint32_t q = local >> 1, h = local & 1;
+    // layers 0-3: k-step major (q, h); views layer: output-group major (h, q)
+    const bool hmajor = SDFR_X_EPI && layer == 4;
+    const uint32_t q = hmajor ? local % 9 : local >> 1;
+    const uint32_t h = hmajor ? local / 9 : local & 1;
     const uint32_t row = 16 * (8 * h + t8) + (lane & 15), g = lane >> 4;
     const uint32_t K = layer_k(layer);
     const float s = a.su[layer * kW + row];
@@ -189,10 +209,18 @@ struct XFieldArgs {
     float *rgb, *features, *sdf, *xyz, *mask;
 };
 
+// Weight ring: 3 LDS slots; during slice `it` the wave computes from slot it%3,
+// writes slice it+2 (held in registers since slice it-1) into slot (it+2)%3 --
+// the slot of slice it-1, which every wave finished reading before the barrier
+// that closed slice it-1 -- loads slice it+3 into registers, and reads the first
+// fragment pair of slice it+1 (already visible: written during it-1), so the
+// next slice's first MFMAs do not wait on LDS latency after the barrier.
 struct XRing {
     f4 *lds;              // [3][kXSliceF4]
     const f4 *packed;
-    f4 st[kXStage];       // staged next slice (global -> regs -> LDS)
+    f4 st[kXStage];       // slice it+2 (global -> regs -> LDS)
+    f4 pre_h, pre_l;      // first (hi, lo) A fragment of the current slice
+    __amdgpu_buffer_rsrc_t rsrc;   // the packed fragments (SDFR_X_BUFLOAD)
     uint32_t it;          // slice iteration (runs across passes)
     uint32_t tid;
 };
@@ -202,18 +230,29 @@ __device__ __forceinline__ void xpin(float &x) { asm volatile("" : "+v"(x)); }
 
 // One half k-step: 8 output tiles (8H .. 8H+7) x 2 sample columns x 3 split
 // terms = 48 MFMAs on one LDS ring slot, then `side` (register work issued in
-// the MFMA shadow), staging of slice it+1 into the next slot and of slice it+2
-// into registers, and the slice barrier.
-template <int H, class Side>
+// the MFMA shadow), the ring staging (XRing) and the slice barrier.
+// Ablation variants (profiling builds only, sdfr_debug_set_field_variant; V = 0
+// is the product): bit 0 drops the slice barrier, bit 1 the LDS A-fragment reads,
+// bit 2 the ring staging, bit 3 the per-layer activations, bit 4 the per-pass
+// compositing.  Any V != 0 computes wrong results by construction.
+template <int V, int H, class Side>
 __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], const f4 b0h,
                                       const f4 b0l, const f4 b1h, const f4 b1l, Side &&side) {
-    const uint32_t cur = R.it % 3u, nxt = (R.it + 1u) % 3u;
+    const uint32_t cur = R.it % 3u;
     const f4 *A = R.lds + cur * kXSliceF4 + (R.tid & 63u);
     f4 ah[8], al[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        ah[i] = A[(2 * i) * 64];
-        al[i] = A[(2 * i + 1) * 64];
+        if constexpr ((V & 2) != 0) {
+            ah[i] = b0h * (float)(i + 1);
+            al[i] = b1l * (float)(i + 1);
+        } else if (SDFR_X_PREFETCH && i == 0) {
+            ah[0] = R.pre_h;
+            al[0] = R.pre_l;
+        } else {
+            ah[i] = A[(2 * i) * 64];
+            al[i] = A[(2 * i + 1) * 64];
+        }
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -226,13 +265,31 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
         acc1[t] = mfma16(ah[i], b1h, acc1[t]);
     }
     side();
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((V & 4) == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t wslot = (R.it + 1u + SDFR_X_PREFETCH) % 3u;
 #pragma unroll
-    for (int i = 0; i < kXStage; ++i) R.lds[nxt * kXSliceF4 + R.tid + i * kThreads] = R.st[i];
-    const uint32_t pf = (R.it + 2u) % kXSlices;
+        for (int i = 0; i < kXStage; ++i)
+            R.lds[wslot * kXSliceF4 + R.tid + i * kThreads] = R.st[i];
+        const uint32_t pf = (R.it + 2u + SDFR_X_PREFETCH) % kXSlices;
 #pragma unroll
-    for (int i = 0; i < kXStage; ++i) R.st[i] = R.packed[pf * kXSliceF4 + R.tid + i * kThreads];
-    __syncthreads();
+        for (int i = 0; i < kXStage; ++i) {
+#if SDFR_X_BUFLOAD
+            R.st[i] = __builtin_bit_cast(
+                f4, __builtin_amdgcn_raw_buffer_load_b128(
+                        R.rsrc, (int)((R.tid + i * kThreads) * sizeof(f4)),
+                        (int)(pf * kXSliceF4 * sizeof(f4)), 0));
+#else
+            R.st[i] = R.packed[pf * kXSliceF4 + R.tid + i * kThreads];
+#endif
+        }
+    }
+    if constexpr ((V & 2) == 0 && SDFR_X_PREFETCH) {
+        const f4 *An = R.lds + ((R.it + 1u) % 3u) * kXSliceF4 + (R.tid & 63u);
+        R.pre_h = An[0];
+        R.pre_l = An[64];
+    }
+    if constexpr ((V & 1) == 0) __syncthreads();
     ++R.it;
 }
 
@@ -241,10 +298,15 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
 //   MODE 0: identity input layer, x * (1/su0)
 //   MODE 1: FiLM sin(gamma' x + beta) (sdf_model.py:67, two roundings)
 //   MODE 2: FiLM + partial sigma_linear dot product (the sdf head)
-template <int MODE>
+template <int MODE, int V>
 __device__ __forceinline__ void act_pair(f4 &za, f4 &zb, int q, const float *gam,
                                          const float *bet, const float *sw, float &sdfp,
                                          uint32_t g) {
+    if constexpr ((V & 8) != 0) {
+        xpin(za);
+        xpin(zb);
+        return;
+    }
     float v[8];
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -281,17 +343,17 @@ __device__ __forceinline__ void init_acc(f4 (&acc)[16], const float *bias, uint3
 // input pair (q+1) of each sample column is activated in the MFMA shadow; the
 // last k-step activates the first pair of this layer's own output (its tiles
 // 0-7 completed in the k-step's first half).
-template <class ActIn, class ActOut>
+template <int V, class ActIn, class ActOut>
 __device__ __forceinline__ void dense_layer(XRing &R, f4 (&in0)[16], f4 (&in1)[16],
                                             f4 (&out0)[16], f4 (&out1)[16], ActIn &&act_in,
                                             ActOut &&act_out) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int qn = q < 7 ? q + 1 : 7;
-        xstep<0>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1], [&] {
+        xstep<V, 0>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1], [&] {
             if (q < 7) act_in(in0[2 * qn], in0[2 * qn + 1], qn, 0);
         });
-        xstep<1>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1], [&] {
+        xstep<V, 1>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1], [&] {
             if (q < 7) {
                 act_in(in1[2 * qn], in1[2 * qn + 1], qn, 1);
             } else {
@@ -306,19 +368,24 @@ struct NoAct {
     __device__ __forceinline__ void operator()(f4 &, f4 &, int, int) const {}
 };
 
+template <int V>
 __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldArgs a) {
     __shared__ f4 ring_lds[3 * kXSliceF4];                // 48 KB weight ring
     __shared__ float cst[kXCst];                           // 10 KB constants
-    __shared__ float film_lds[kWaves][kFilm * 2 * kW];     // 32 KB: each wave's face
+    __shared__ float film_lds[kFilm * 2 * kW];             // 8 KB: the workgroup's face
     __shared__ f4 facc_lds[kWaves][16 * 64];               // 64 KB: feature accumulators
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t n = lane & 15u, g = lane >> 4;
     const GeomArgs &G = a.g;
 
-    uint32_t tile = blockIdx.x * kWaves + wave;
-    const bool tile_ok = tile < G.total_tiles;
-    if (!tile_ok) tile = G.total_tiles - 1;
-    const uint32_t b = tile / G.tiles_per_face;
+    // a workgroup's 4 waves own 4 consecutive tiles of ONE face (grid = faces x
+    // ceil(tiles_per_face / 4)), so the face's FiLM vectors are shared in LDS
+    const uint32_t wg_per_face = (G.tiles_per_face + kWaves - 1) / kWaves;
+    const uint32_t b = blockIdx.x / wg_per_face;
+    uint32_t tile_local = (blockIdx.x % wg_per_face) * kWaves + wave;
+    const bool tile_ok = tile_local < G.tiles_per_face;
+    if (!tile_ok) tile_local = G.tiles_per_face - 1;
+    const uint32_t tile = b * G.tiles_per_face + tile_local;
     uint32_t ray_local = (tile % G.tiles_per_face) * kTileRays + n;
     const bool ray_ok = tile_ok && ray_local < G.H * G.W;
     if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
@@ -350,15 +417,18 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
     const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
     {
         const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * kFilm * 2 * kW);
-        f4 *dst = reinterpret_cast<f4 *>(film_lds[wave]);
+        f4 *dst = reinterpret_cast<f4 *>(film_lds);
 #pragma unroll
-        for (uint32_t i = lane; i < kFilm * 2 * kW / 4; i += 64) dst[i] = src[i];
+        for (uint32_t i = tid; i < kFilm * 2 * kW / 4; i += kThreads) dst[i] = src[i];
     }
-    const float *film = film_lds[wave];
+    const float *film = film_lds;
 
     XRing R;
     R.lds = ring_lds;
     R.packed = a.packed;
+    R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<f4 *>(a.packed), 0,
+                                               (int)(kXSlices * kXSliceF4 * sizeof(f4)),
+                                               0x00020000);
     R.tid = tid;
     R.it = 0;
     // bias_s[5][256], 1/su of the input layer, sigma_linear row, rgb_linear rows
@@ -370,11 +440,15 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
         else v = a.rgb_w[i - 7 * kW];
         cst[i] = v;
     }
+    // prologue: slices 0 (.. 1) -> slots; the next slice -> registers
+    constexpr int kPro = 1 + SDFR_X_PREFETCH;
 #pragma unroll
-    for (int i = 0; i < kXStage; ++i) R.lds[tid + i * kThreads] = a.packed[tid + i * kThreads];
+    for (int i = 0; i < kPro * kXStage; ++i) R.lds[tid + i * kThreads] = a.packed[tid + i * kThreads];
 #pragma unroll
-    for (int i = 0; i < kXStage; ++i) R.st[i] = a.packed[kXSliceF4 + tid + i * kThreads];
+    for (int i = 0; i < kXStage; ++i) R.st[i] = a.packed[kPro * kXSliceF4 + tid + i * kThreads];
     __syncthreads();
+    R.pre_h = R.lds[lane];
+    R.pre_l = R.lds[64 + lane];
 
     f4 *facc = facc_lds[wave];
 #pragma unroll
@@ -426,48 +500,180 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
         float sdfp0 = 0.0f, sdfp1 = 0.0f;
         auto act_id = [&](f4 &za, f4 &zb, int q, int) {
             float dummy = 0.0f;
-            act_pair<0>(za, zb, q, inv_su0, nullptr, nullptr, dummy, g);
+            act_pair<0, V>(za, zb, q, inv_su0, nullptr, nullptr, dummy, g);
         };
         auto act_f0 = [&](f4 &za, f4 &zb, int q, int) {
             float dummy = 0.0f;
-            act_pair<1>(za, zb, q, f0g, f0b, nullptr, dummy, g);
+            act_pair<1, V>(za, zb, q, f0g, f0b, nullptr, dummy, g);
         };
         auto act_f1 = [&](f4 &za, f4 &zb, int q, int) {
             float dummy = 0.0f;
-            act_pair<1>(za, zb, q, f1g, f1b, nullptr, dummy, g);
+            act_pair<1, V>(za, zb, q, f1g, f1b, nullptr, dummy, g);
         };
         auto act_f2 = [&](f4 &za, f4 &zb, int q, int j) {
-            if (j == 0) act_pair<2>(za, zb, q, f2g, f2b, sig_w, sdfp0, g);
-            else act_pair<2>(za, zb, q, f2g, f2b, sig_w, sdfp1, g);
+            if (j == 0) act_pair<2, V>(za, zb, q, f2g, f2b, sig_w, sdfp0, g);
+            else act_pair<2, V>(za, zb, q, f2g, f2b, sig_w, sdfp1, g);
         };
 
-        // layer 0: input_linear (32 -> 256) -> X; next pass's features prefetched
+        // layer 0: input_linear (32 -> 256) -> X
         init_acc(X0, bias_l, g);
         init_acc(X1, bias_l, g);
-        xstep<0>(R, X0, X1, e0h, e0l, e1h, e1l, [&] {
-            if (p + 1 < npass) load_enc(2 * p + 2);
-        });
-        xstep<1>(R, X0, X1, e0h, e0l, e1h, e1l, [&] {
+        xstep<V, 0>(R, X0, X1, e0h, e0l, e1h, e1l, [] {});
+        xstep<V, 1>(R, X0, X1, e0h, e0l, e1h, e1l, [&] {
             act_id(X0[0], X0[1], 0, 0);
             act_id(X1[0], X1[1], 0, 1);
         });
         // layers 1-3: FiLM pts_linears.0..2
         init_acc(Y0, bias_l + kW, g);
         init_acc(Y1, bias_l + kW, g);
-        dense_layer(R, X0, X1, Y0, Y1, act_id, act_f0);
+        dense_layer<V>(R, X0, X1, Y0, Y1, act_id, act_f0);
         init_acc(X0, bias_l + 2 * kW, g);
         init_acc(X1, bias_l + 2 * kW, g);
-        dense_layer(R, Y0, Y1, X0, X1, act_f0, act_f1);
+        dense_layer<V>(R, Y0, Y1, X0, X1, act_f0, act_f1);
         init_acc(Y0, bias_l + 3 * kW, g);
         init_acc(Y1, bias_l + 3 * kW, g);
-        dense_layer(R, X0, X1, Y0, Y1, act_f1, act_f2);
+        dense_layer<V>(R, X0, X1, Y0, Y1, act_f1, act_f2);
+#if SDFR_X_EPI
+        // layer 4: views FiLM ([h3, SH] 272 -> 256) -> X, output-group major (the
+        // packing orders its 18 slices h-major): group 0 = tiles 0-7 over all 9
+        // k-steps, activating h3 pair q+1 of both columns in k-step q's shadow;
+        // group 1 = tiles 8-15, with the compositing of tiles 0-7 in its shadow.
+        init_acc(X0, bias_l + 4 * kW, g);
+        init_acc(X1, bias_l + 4 * kW, g);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int qn = q < 7 ? q + 1 : 7;
+            xstep<V, 0>(R, X0, X1, Y0[2 * q], Y0[2 * q + 1], Y1[2 * q], Y1[2 * q + 1], [&] {
+                if (q < 7) {
+                    act_f2(Y0[2 * qn], Y0[2 * qn + 1], qn, 0);
+                    act_f2(Y1[2 * qn], Y1[2 * qn + 1], qn, 1);
+                }
+            });
+        }
+#else
         // layer 4: views FiLM ([h3, SH] 272 -> 256) -> X; h3 pairs finish the sdf head
         init_acc(X0, bias_l + 4 * kW, g);
         init_acc(X1, bias_l + 4 * kW, g);
-        dense_layer(R, Y0, Y1, X0, X1, act_f2, NoAct{});
-        xstep<0>(R, X0, X1, shh, shl, shh, shl, [] {});
-        xstep<1>(R, X0, X1, shh, shl, shh, shl, [] {});
+        dense_layer<V>(R, Y0, Y1, X0, X1, act_f2, NoAct{});
+        xstep<V, 0>(R, X0, X1, shh, shl, shh, shl, [] {});
+        xstep<V, 1>(R, X0, X1, shh, shl, shh, shl, [] {});
+#endif
+#if SDFR_X_EPI
+        // volume_integration (sdf_model.py:236-301) weights of the pass's two
+        // samples, front to back; a sample past N gets weight 0 (no branch, so
+        // the compositing stays in the MFMA shadow)
+        const uint32_t s0 = 2 * p, s1 = 2 * p + 1;
+        const bool ok1 = s1 < G.N;
+        float sdf0 = 0.0f, sdf1 = 0.0f, w0 = 0.0f, w1 = 0.0f;
+        auto weights = [&] {
+            sdf0 = __fadd_rn(group_sum(sdfp0), sig_b);
+            sdf1 = __fadd_rn(group_sum(sdfp1), sig_b);
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                const uint32_t s = jj ? s1 : s0;
+                const uint32_t sc = s < G.N ? s : G.N - 1;
+                const float sdf = jj ? sdf1 : sdf0;
+                const float z = sample_z(G.sc, nr, fr, ray_index, sc);
+                const float dist =
+                    (sc + 1 < G.N)
+                        ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc + 1), z), dnorm)
+                        : __fmul_rn(1e10f, dnorm);
+                float alpha;
+                if (a.with_sdf) {
+                    const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
+                    alpha = 1.0f - expf(-sig * dist);
+                } else {
+                    float raw = sdf;
+                    if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc];
+                    const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+                    alpha = 1.0f - expf(-sp * dist);
+                }
+                float w = alpha * T;
+                if (a.force_background && sc + 1 == G.N) w = 1.0f - wsum;
+                const bool live = jj == 0 || ok1;
+                if (live) {
+                    T = T * ((1.0f - alpha) + 1e-10f);
+                    wsum += w;
+                }
+                if (jj) w1 = live ? w : 0.0f;
+                else w0 = w;
+            }
+            xpin(w0);
+            xpin(w1);
+        };
+        // colour features f = sin(gamma_v' x + beta_v) of tile t, rgb_linear
+        // partial dot products, feature compositing (sample s0 then s1)
+        float q00 = 0.0f, q01 = 0.0f, q02 = 0.0f, q10 = 0.0f, q11 = 0.0f, q12 = 0.0f;
+        auto epi_tile = [&](int t) {
+            if constexpr ((V & 16) != 0) {
+                racc0 += (X0[t][0] + X0[t][1]) + (X0[t][2] + X0[t][3]);
+                racc1 += (X1[t][0] + X1[t][1]) + (X1[t][2] + X1[t][3]);
+                return;
+            }
+            const int f0 = 16 * t + 4 * (int)g;
+            const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
+            const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
+            const f4 wr0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
+            const f4 wr1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
+            const f4 wr2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
+            f4 fa, fb;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                fa[r] = sin_hw(__fadd_rn(__fmul_rn(gm[r], X0[t][r]), bt[r]));
+                fb[r] = sin_hw(__fadd_rn(__fmul_rn(gm[r], X1[t][r]), bt[r]));
+                q00 = __fmaf_rn(fa[r], wr0[r], q00);
+                q01 = __fmaf_rn(fa[r], wr1[r], q01);
+                q02 = __fmaf_rn(fa[r], wr2[r], q02);
+                q10 = __fmaf_rn(fb[r], wr0[r], q10);
+                q11 = __fmaf_rn(fb[r], wr1[r], q11);
+                q12 = __fmaf_rn(fb[r], wr2[r], q12);
+            }
+            f4 v = facc[t * 64 + lane];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = __fmaf_rn(w0, fa[r], v[r]);
+                v[r] = __fmaf_rn(w1, fb[r], v[r]);
+            }
+            facc[t * 64 + lane] = v;
+            xpin(q00);
+            xpin(q10);
+        };
+#if SDFR_X_EPI
+        xstep<V, 0>(R, X0, X1, shh, shl, shh, shl, [&] { weights(); });
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            xstep<V, 1>(R, X0, X1, Y0[2 * q], Y0[2 * q + 1], Y1[2 * q], Y1[2 * q + 1],
+                        [&] { epi_tile(q); });
+        xstep<V, 1>(R, X0, X1, shh, shl, shh, shl, [] {});
+        // next pass's hash-grid features, in flight behind the exposed compositing
+        if (p + 1 < npass) load_enc(2 * p + 2);
+#pragma unroll
+        for (int t = 8; t < 16; ++t) epi_tile(t);
+#endif
 
+        // rgb head and the per-ray accumulators, sample s0 then s1
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            if (jj && !ok1) break;
+            const uint32_t s = jj ? s1 : s0;
+            const float w = jj ? w1 : w0;
+            const float r0 = __fadd_rn(group_sum(jj ? q10 : q00), rgb_b0);
+            const float r1 = __fadd_rn(group_sum(jj ? q11 : q01), rgb_b1);
+            const float r2 = __fadd_rn(group_sum(jj ? q12 : q02), rgb_b2);
+            w_last = w;
+            racc0 = __fmaf_rn(w, sigmoidf_(r0), racc0);
+            racc1 = __fmaf_rn(w, sigmoidf_(r1), racc1);
+            racc2 = __fmaf_rn(w, sigmoidf_(r2), racc2);
+            if (a.xyz) {
+                const float z = sample_z(G.sc, nr, fr, ray_index, s);
+                xacc0 = __fmaf_rn(w, __fadd_rn(ray.o[0], __fmul_rn(ray.d[0], z)), xacc0);
+                xacc1 = __fmaf_rn(w, __fadd_rn(ray.o[1], __fmul_rn(ray.d[1], z)), xacc1);
+                xacc2 = __fmaf_rn(w, __fadd_rn(ray.o[2], __fmul_rn(ray.d[2], z)), xacc2);
+            }
+            if (a.sdf && ray_ok && g == 0) a.sdf[(size_t)ray_index * G.N + s] = jj ? sdf1 : sdf0;
+        }
+#else
+        if (p + 1 < npass) load_enc(2 * p + 2);
         // compositing of the pass's two samples, front to back
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -539,6 +745,7 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
             }
             if (a.sdf && ray_ok && g == 0) a.sdf[(size_t)ray_index * G.N + s] = sdf;
         }
+#endif
     }
 
     if (!ray_ok) return;
@@ -643,8 +850,24 @@ int launch_xfield(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, cons
     f.sdf = a->sdf;
     f.xyz = a->xyz;
     f.mask = a->mask;
-    const uint32_t blocks = (g.total_tiles + kWaves - 1) / kWaves;
-    hipLaunchKernelGGL(ngp_field_x_kernel, dim3(blocks), dim3(kThreads), 0, st, f);
+    const uint32_t blocks = g.B * ((g.tiles_per_face + kWaves - 1) / kWaves);
+    switch (field_variant()) {
+#ifdef SDFR_ABLATION
+#define SDFR_XFIELD_CASE(V)                                                                  \
+    case V:                                                                                  \
+        hipLaunchKernelGGL(ngp_field_x_kernel<V>, dim3(blocks), dim3(kThreads), 0, st, f);   \
+        break;
+        SDFR_XFIELD_CASE(1)
+        SDFR_XFIELD_CASE(2)
+        SDFR_XFIELD_CASE(4)
+        SDFR_XFIELD_CASE(8)
+        SDFR_XFIELD_CASE(16)
+        SDFR_XFIELD_CASE(31)
+#undef SDFR_XFIELD_CASE
+#endif
+        default:
+            hipLaunchKernelGGL(ngp_field_x_kernel<0>, dim3(blocks), dim3(kThreads), 0, st, f);
+    }
     return check_launch("render_ngp: field (f16x3)");
 }
 

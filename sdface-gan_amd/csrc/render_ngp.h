@@ -65,14 +65,18 @@ constexpr uint32_t kCst = 9 * kW;              // LDS constants: bias[5], sigma_
 constexpr int kWaves = 4;                       // 1 wave per SIMD, 512 VGPR+AGPR
 constexpr int kThreads = kWaves * 64;
 
-// sin via the hardware v_sin_f32 (argument in revolutions, |u| <= 0.5 after an
-// fma Cody-Waite reduction by 2pi): 6 VALU + 1 transcendental.  Accuracy is
-// measured against float64 by tests/test_gpu_encoders.py::test_sin_accuracy.
+// sin via the hardware v_sin_f32, whose argument is in revolutions: x/(2pi)
+// = k + f with k = rint(x c_hi) and f = fma(x, c_hi, -k) + x c_lo (c_hi + c_lo =
+// 1/(2pi) to ~2^-50; x c_hi is exact inside the fma, so f carries one rounding,
+// |f| <= 0.5).  4 VALU + 1 transcendental; accuracy is measured against float64
+// by tests/test_gpu_encoders.py::test_sin_accuracy (|x| <= 200).
 __device__ __forceinline__ float sin_hw(float x) {
-    const float k = __builtin_rintf(x * 0.159154943091895336f);
-    float r = __fmaf_rn(-k, 6.28318548202514648f, x);
-    r = __fmaf_rn(-k, -1.74845553146951752e-7f, r);
-    return __builtin_amdgcn_sinf(r * 0.159154943091895336f);
+    constexpr float c_hi = 0.15915493667125702f;    // fl(1/(2pi))
+    constexpr float c_lo = 6.4206382432985265e-09f;  // 1/(2pi) - c_hi
+    const float k = __builtin_rintf(x * c_hi);
+    float f = __fmaf_rn(x, c_hi, -k);
+    f = __fmaf_rn(x, c_lo, f);
+    return __builtin_amdgcn_sinf(f);
 }
 
 // SH degree 4 coefficients 4g..4g+3 of a unit direction (shencoder.cu:50-68)
@@ -111,6 +115,7 @@ __device__ __forceinline__ float group_sum(float v) {
 // Split-fp16 field path (field_f16x3.hip).  Its workspace region (`xws`,
 // f16x3_ws_bytes()) holds the packed fp16 fragments, row scales and scaled biases.
 size_t f16x3_ws_bytes(uint32_t B);
+int field_variant();   // profiling ablation selected by sdfr_debug_set_field_variant
 int launch_xprep(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, char *xws,
                  float *film, hipStream_t st);
 int launch_xfield(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, const GeomArgs &g,

@@ -630,9 +630,11 @@ static void fill_geom(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, 
 }
 
 static int g_field_variant = 0;   // profiling ablations only (see ABL_*)
+int field_variant() { return g_field_variant; }
 
 static void launch_field(int v, dim3 grid, hipStream_t st, const FieldArgs &f) {
     switch (v) {
+#ifdef SDFR_ABLATION
 #define SDFR_FIELD_CASE(V)                                                                   \
     case V:                                                                                  \
         hipLaunchKernelGGL(ngp_field_kernel<V>, grid, dim3(kThreads), 0, st, f);             \
@@ -642,7 +644,10 @@ static void launch_field(int v, dim3 grid, hipStream_t st, const FieldArgs &f) {
         SDFR_FIELD_CASE(4)
         SDFR_FIELD_CASE(8)
         SDFR_FIELD_CASE(15)
+        SDFR_FIELD_CASE(16)
+        SDFR_FIELD_CASE(31)
 #undef SDFR_FIELD_CASE
+#endif
         default:
             hipLaunchKernelGGL(ngp_field_kernel<0>, grid, dim3(kThreads), 0, st, f);
     }
@@ -707,13 +712,18 @@ int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t 
 }
 
 int sdfr_debug_set_field_variant(int variant) {
-    const int ok[] = {0, 1, 2, 4, 8, 15};
+#ifdef SDFR_ABLATION
+    const int ok[] = {0, 1, 2, 4, 8, 15, 16, 31};
+#else
+    const int ok[] = {0};   // ablated kernels are only built with `make ABLATION=1`
+#endif
     for (int v : ok)
         if (v == variant) {
             g_field_variant = variant;
             return SDFR_OK;
         }
-    return fail(SDFR_EINVAL, "sdfr_debug_set_field_variant: variant must be 0,1,2,4,8,15");
+    return fail(SDFR_EINVAL,
+                "sdfr_debug_set_field_variant: variant must be 0,1,2,4,8,15,16,31");
 }
 
 size_t sdfr_render_ngp_workspace_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t N,
