@@ -1,0 +1,62 @@
+"""BASELINE configs[3]: sdf_mesh.py's SDF volume for marching cubes, on 1 GPU.
+
+Times the surface-extraction Generator (full_pipeline=False, return_sdf/xyz;
+sdf_mesh.py:244-252) at 128^2 rays x 128 samples (the reference setting) and at
+256^2 x 256 (a 256^3 volume, 16.8 M samples), one face per call as sdf_mesh.py
+does, plus align_volume; marching cubes (host, scikit-image) is excluded.
+Prints one JSON line per resolution."""
+import json
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from sdfr_loader import load  # noqa: E402
+
+
+def main(reps=5):
+    sdfr = load()
+    dev = "cuda:0"
+    for res in (128, 256):
+        opt = sdfr.vol_render_opt()
+        opt.model.renderer_spatial_output_dim = res
+        opt.rendering.N_samples = res
+        opt.rendering.return_sdf = True
+        opt.rendering.return_xyz = True
+        torch.manual_seed(0)
+        g = sdfr.Generator(opt.model, opt.rendering, full_pipeline=False).to(dev).eval()
+        g.renderer.rng_device = "device"
+        ext, focal, near, far, _ = sdfr.generate_camera_params(res, dev, batch=1)
+        z = torch.randn(1, 256, device=dev)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        for e in evs:
+            e.record()
+        g.renderer.stage_events = evs
+        times, field = [], []
+        with torch.no_grad():
+            for r in range(reps + 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                out = g([z], ext, focal, near, far, return_sdf=True, return_xyz=True)
+                vol = sdfr.align_volume(out[3])
+                torch.cuda.synchronize()
+                if r:
+                    times.append(time.perf_counter() - t0)
+                    field.append(evs[2].elapsed_time(evs[3]))
+        ms = sorted(times)[len(times) // 2] * 1e3
+        fms = sorted(field)[len(field) // 2]
+        samples = res * res * res
+        print(json.dumps({"config": f"sdf_mesh surface extraction {res}^2 rays x {res} samples "
+                                    f"({res}^3 SDF volume), 1 face per call",
+                          "ms_per_volume": ms, "volumes_per_s": 1e3 / ms,
+                          "field_ms": fms,
+                          "field_tflops": 550912 * samples / fms / 1e9,
+                          "volume_shape": list(vol.shape)}), flush=True)
+        del g, out, vol
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

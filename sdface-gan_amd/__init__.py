@@ -9,6 +9,8 @@ Drop-in surface (reference: im2scene/sdf/models/):
   GridEncoder, grid_encode                              (gridencoder/grid.py)
   SHEncoder, sh_encode                                  (shencoder/sphere_harmonics.py)
   generate_camera_params                                (sdf_utils.py:97-159)
+  align_volume, extract_mesh_with_marching_cubes,
+  xyz2mesh                                              (sdf_utils.py:164-223)
   SDFOptions, vol_render_opt                            (sdf_utils.py:447, training_utils.py:144)
 """
 from . import _lib  # noqa: F401
@@ -18,6 +20,7 @@ from . import decoder_ops  # noqa: F401
 from .generator import (Blur, Decoder, EqualLinear, FusedLeakyReLU, Generator,  # noqa: F401
                         MappingLinear, ModulatedConv2d, NoiseInjection, PixelNorm, StyledConv,
                         ToRGB, Upsample, fused_leaky_relu, make_kernel, upfirdn2d)
+from .mesh import align_volume, extract_mesh_with_marching_cubes, xyz2mesh  # noqa: F401
 from .options import AttrDict, SDFOptions, vol_render_opt  # noqa: F401
 from .renderer import (FCGenerator, FiLMSiren, LinearLayer, NGPSIRENGenerator,  # noqa: F401
                        SirenGenerator, VolumeFeatureRenderer, get_encoder)

@@ -294,6 +294,35 @@ def case_render(sdf_model, sdf_utils, name, B, res, n_samples, intermediates, se
     print(f"{name}.npz", rgb.shape)
 
 
+def case_mesh(sdf_model, sdf_utils):
+    """sdf_mesh.py's surface extractor (sdf_mesh.py:244-252: renderer at 128^2 rays x
+    128 samples, return_sdf/xyz, full_pipeline=False) on one face, plus
+    sdf_utils.align_volume (:164-184) on its SDF volume and on a small random one.
+    The 128^3 SDF is stored on every 8th pixel row/column (all samples)."""
+    g, opt = _generator(sdf_model, sdf_utils, res=128, n_samples=128, full_pipeline=False,
+                        return_sdf=True, return_xyz=True)
+    ext, focal, near, far, vp = _cams(sdf_utils, 1, 128, 51)
+    torch.manual_seed(52)
+    z = torch.randn(1, 256)
+    with torch.no_grad():
+        torch.manual_seed(53)
+        with _RandRecorder() as rr:
+            out = g([z], ext, focal, near, far, return_sdf=True, return_xyz=True)
+        _, thumb, xyz, sdf, mask = out
+        aligned = sdf_utils.align_volume(sdf)
+        torch.manual_seed(54)
+        vol = torch.randn(1, 12, 10, 16, 1)   # align_volume supports batch 1 only
+        vol_aligned = sdf_utils.align_volume(vol)
+    sub = slice(0, None, 8)
+    np.savez_compressed(OUT / "mesh128.npz", z=_t2n(z), ext=_t2n(ext), focal=_t2n(focal),
+                        near=_t2n(near), far=_t2n(far), t_rand=_t2n(rr.draws[0]),
+                        thumb=_t2n(thumb), xyz=_t2n(xyz), mask=_t2n(mask),
+                        sdf_sub=_t2n(sdf[:, sub, sub]), aligned_sub=_t2n(aligned[:, sub, sub]),
+                        vol=_t2n(vol), vol_aligned=_t2n(vol_aligned), res=np.int64(128),
+                        n_samples=np.int64(128))
+    print("mesh128.npz", sdf.shape, aligned.shape)
+
+
 def case_generator(sdf_model, sdf_utils):
     g, opt = _generator(sdf_model, sdf_utils, size=256, res=64, n_samples=24)
     ext, focal, near, far, vp = _cams(sdf_utils, 1, 64, 31)
@@ -346,6 +375,10 @@ def case_init_stats(sdf_model, sdf_utils):
 
 def main():
     sdf_model, sdf_utils = import_reference()
+    if len(sys.argv) > 1:                       # selected cases only, e.g. `mesh`
+        for name in sys.argv[1:]:
+            globals()[f"case_{name}"](sdf_model, sdf_utils)
+        return
     case_init_stats(sdf_model, sdf_utils)
     case_encoders()
     case_camera(sdf_utils)

@@ -149,3 +149,17 @@ def test_fused_path_selection(sdfr):
     opt2 = sdfr.vol_render_opt(ngp=False)
     r2 = sdfr.VolumeFeatureRenderer(opt2.rendering, style_dim=256, out_im_res=8)
     assert isinstance(r2.network, sdfr.SirenGenerator)
+
+
+def test_align_volume_matches_reference(sdfr, golden_dir):
+    """sdf_utils.align_volume on a random volume: same grid_sample, bit for bit."""
+    g = np.load(golden_dir / "mesh128.npz")
+    out = sdfr.align_volume(torch.from_numpy(g["vol"]))
+    np.testing.assert_array_equal(out.numpy(), g["vol_aligned"])
+
+
+def test_xyz2mesh_faces(sdfr):
+    xyz = torch.arange(3 * 4 * 5, dtype=torch.float32).reshape(1, 3, 4, 5)
+    res = sdfr.xyz2mesh(xyz)
+    verts, faces = res if isinstance(res, tuple) else (res.vertices, res.faces)
+    assert verts.shape == (20, 3) and faces.shape[1] == 3 and faces.max() < 20
