@@ -32,6 +32,7 @@ sys.path.insert(0, str(REPO))
 
 METRIC = "rendered faces/sec/GPU at 256² (SDF+ngp path); 1/2/4/8-GPU scaling"
 FLOP_PER_SAMPLE = 550912          # renderer MLP, SURVEY.md §8(d) / BASELINE.md §2
+FLOP_PER_SAMPLE_SIREN = 1053696   # SirenGenerator MLP, SURVEY.md §8(d)
 GATHER_BYTES_PER_SAMPLE = 1024    # 16 levels x 8 corners x 2 x fp32
 MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
 MFMA_F16_PEAK_TFLOPS = 2500.0     # MI355X dense fp16/bf16 MFMA peak (no sparsity)
@@ -48,6 +49,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--field-precision", default="f16x3", choices=["f16x3", "fp32"],
                    help="field-stage GEMM arithmetic (DESIGN.md section 5)")
+    p.add_argument("--net", default="ngp", choices=["ngp", "siren"],
+                   help="renderer network: ngp (headline, configs[1]) or siren "
+                        "(rendering.type 'sdf', configs[4]'s generator)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--traffic-json", default=str(REPO / "profiles" / "field_traffic.json"))
     return p.parse_args()
@@ -63,8 +67,8 @@ def setup_dist(args):
     return world, rank, torch.device("cuda", local)
 
 
-def build_generator(sdfr, device, seed):
-    opt = sdfr.vol_render_opt(ngp=True)
+def build_generator(sdfr, device, seed, ngp=True):
+    opt = sdfr.vol_render_opt(ngp=ngp)
     torch.manual_seed(seed)
     g = sdfr.Generator(opt.model, opt.rendering).to(device)
     g.eval()
@@ -73,16 +77,17 @@ def build_generator(sdfr, device, seed):
     return g, opt
 
 
-def cpu_baseline(seconds):
+def cpu_baseline(seconds, siren=False):
     """Oracle renderer (torch-CPU fp32 + C encoders) + PyTorch-CPU decoder, one face
     per call as eval.py does, on the host cores; bounded to ~`seconds`."""
     from oracle import oracle
     from sdfr_loader import load
     sdfr = load()
     oracle.build()
-    opt = sdfr.vol_render_opt(ngp=True)
+    opt = sdfr.vol_render_opt(ngp=not siren)
     torch.manual_seed(1)
     g = sdfr.Generator(opt.model, opt.rendering).eval()
+    render = oracle.render_siren if siren else oracle.render_ngp
     sd = {k: v for k, v in g.state_dict().items() if k.startswith("renderer.")}
     faces, t0 = 0, time.perf_counter()
     with torch.no_grad():
@@ -90,7 +95,7 @@ def cpu_baseline(seconds):
             z = torch.randn(1, 256)
             cam, focal, near, far, _ = sdfr.generate_camera_params(64, "cpu", batch=1)
             lat = g.style(z)
-            out = oracle.render_ngp(sd, cam.numpy(), focal.numpy(), near.numpy(), far.numpy(),
+            out = render(sd, cam.numpy(), focal.numpy(), near.numpy(), far.numpy(),
                                     lat.numpy(), N=24, res=64, t_rand=torch.rand(1, 64, 64).numpy())
             img, _ = g.decoder(out["features"], [lat])
             faces += 1
@@ -108,7 +113,8 @@ def main():
     world, rank, device = setup_dist(args)
     from sdfr_loader import load
     sdfr = load()
-    g, opt = build_generator(sdfr, device, args.seed)
+    siren = args.net == "siren"
+    g, opt = build_generator(sdfr, device, args.seed, ngp=not siren)
     g.renderer.field_precision = args.field_precision
     B = args.batch
     res = opt.model.renderer_spatial_output_dim
@@ -157,10 +163,12 @@ def main():
     field_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
     render_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args.steps
     samples = B * res * res * N
-    field_tflops = FLOP_PER_SAMPLE * samples / (field_ms * 1e-3) / 1e12
-    gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9
+    flop = FLOP_PER_SAMPLE_SIREN if siren else FLOP_PER_SAMPLE
+    field_tflops = flop * samples / (field_ms * 1e-3) / 1e12
+    gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9 if not siren else 0.0
     f16x3 = args.field_precision == "f16x3"
-    field_kernel = "ngp_field_x_kernel" if f16x3 else "ngp_field_kernel"
+    field_kernel = ("field_x_kernel<0, sdfr::SirenNet>" if siren else
+                    "field_x_kernel<0, sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
     traffic = None
     tj = Path(args.traffic_json)
     if tj.exists():
@@ -172,7 +180,7 @@ def main():
     if f16x3:
         # fp32-accurate GEMMs as 3 fp16 MFMA terms: the attainable fp32-equivalent
         # peak is the dense fp16 MFMA peak / 3
-        roof = {"kernel": "ngp_field_x_kernel (MLP as 3 split-fp16 v_mfma_f32_16x16x32_f16 "
+        roof = {"kernel": f"{field_kernel} (MLP as 3 split-fp16 v_mfma_f32_16x16x32_f16 "
                           "terms per fp32 tile + compositing)",
                 "bound": "mfma", "achieved": field_tflops, "peak": MFMA_F16_PEAK_TFLOPS / 3,
                 "unit": "TFLOP/s", "frac": field_tflops / (MFMA_F16_PEAK_TFLOPS / 3),
@@ -198,20 +206,23 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (random z, random cameras, random-init weights)",
-        "config": {"workload": "eval.py 5000-image generation (ffhq_256_sdf_ngp, configs[1])",
+        "config": {"workload": ("eval.py generation, SirenGenerator renderer (type 'sdf', "
+                                "configs[4]'s generator)") if siren else
+                               "eval.py 5000-image generation (ffhq_256_sdf_ngp, configs[1])",
                    "faces_per_step_per_gpu": B, "renderer": f"{res}x{res} rays x {N} samples",
                    "output": "256x256 RGB", "parallelism": f"dp{world} (independent faces)",
                    "field_precision": args.field_precision},
         "roofline": roof,
-        "roofline_gather": {"kernel": "ngp_encode_kernel (sampling + 16-level hash-grid gather)",
-                            "bound": "hbm", "achieved": gather_gbps, "peak": HBM_PEAK_GBPS,
-                            "unit": "GB/s", "frac": gather_gbps / HBM_PEAK_GBPS},
+        "roofline_gather": None if siren else {
+            "kernel": "ngp_encode_kernel (sampling + 16-level hash-grid gather)",
+            "bound": "hbm", "achieved": gather_gbps, "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": gather_gbps / HBM_PEAK_GBPS},
         "stage_ms_per_step": {"renderer_total": render_ms, "hash_grid": enc_ms,
                               "field": field_ms},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, siren)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -163,6 +163,34 @@ size_t sdfr_render_ngp_workspace_bytes(uint32_t B, uint32_t H, uint32_t W,
 int sdfr_render_ngp_forward(const sdfr_ngp_weights *w,
                             const sdfr_ngp_render_args *a, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Fused SIREN renderer forward (rendering.type == "sdf", SirenGenerator,
+ * sdf_model.py:101-139, BASELINE configs[4]): the same render chain as
+ * sdfr_render_ngp_forward with the network's 8 FiLM layers fed by the
+ * normalised sample points and the views layer by the unit view direction.
+ * Replaces VolumeFeatureRenderer.forward for type "sdf" (sdf_model.py:411-423);
+ * the reference has no native op here.  Takes the same render args
+ * (field_precision must be SDFR_FIELD_F16X3); workspace from
+ * sdfr_render_siren_workspace_bytes(B).  stage_events[1] == [2] (no encode stage).
+ * ------------------------------------------------------------------------- */
+typedef struct sdfr_siren_weights {
+    uint32_t depth;                     /* D (8)                                    */
+    uint32_t width;                     /* W (256)                                  */
+    const float *pts_w[8], *pts_b[8];   /* [256,3] (layer 0) / [256,256], [256]     */
+    const float *pts_gw[8], *pts_gb[8]; /* gamma LinearLayer [256,256], [256]       */
+    const float *pts_bw[8], *pts_bb[8]; /* beta  LinearLayer [256,256], [256]       */
+    const float *views_w, *views_b;     /* [256,259], [256]                         */
+    const float *views_gw, *views_gb, *views_bw, *views_bb;
+    const float *sigma_w, *sigma_b;     /* [1,256], [1]                             */
+    const float *rgb_w, *rgb_b;         /* [3,256], [3]                             */
+    const float *sigmoid_beta;          /* [1] (renderer.sigmoid_beta)              */
+} sdfr_siren_weights;
+
+size_t sdfr_render_siren_workspace_bytes(uint32_t B);
+
+int sdfr_render_siren_forward(const sdfr_siren_weights *w,
+                              const sdfr_ngp_render_args *a, void *stream);
+
 /* Profiling aid: enqueue only the hash-grid stage of the fused renderer
  * (writes the encoded samples into the workspace).  Same arguments. */
 int sdfr_render_ngp_encode_only(const sdfr_ngp_weights *w,

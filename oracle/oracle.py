@@ -296,13 +296,22 @@ def render_ngp(sd, cam, focal, near, far, styles, *, N=24, res=64, t_rand=None,
     feat = film(hv, net + "views_linears.")
     rgb_raw = 1 * _linear(feat, P(net + "rgb_linear.weight"), P(net + "rgb_linear.bias")) + 0
 
-    # volume_integration, sdf_model.py:236-301
+    out = _integrate(ray, sdf, rgb_raw, feat, P("sigmoid_beta"), with_sdf, force_background,
+                     output_features)
+    if return_intermediates:
+        out.update(ray)
+        out.update(enc=enc, sh=sh, rgb_raw=rgb_raw, feat_samples=feat)
+    return out
+
+
+def _integrate(ray, sdf, rgb_raw, feat, beta_s, with_sdf, force_background, output_features):
+    """volume_integration, sdf_model.py:236-301 (torch CPU fp32)."""
+    import torch
     z = torch.from_numpy(ray["z_vals"])
     dn = torch.from_numpy(ray["dnorm"])[..., None]
     dists = z[..., 1:] - z[..., :-1]
     dists = torch.cat([dists, torch.tensor([1e10]).expand(dn.shape)], -1)
     dists = dists * dn
-    beta_s = P("sigmoid_beta")
     if with_sdf:
         sigma = torch.sigmoid(-sdf / beta_s) / beta_s
         sigma = 1 - torch.exp(-sigma * dists.unsqueeze(-1))
@@ -318,14 +327,59 @@ def render_ngp(sd, cam, focal, near, far, styles, *, N=24, res=64, t_rand=None,
     pts = torch.from_numpy(ray["pts"])
     xyz = torch.sum(weights * pts, 3)
     mask = weights[..., -1, :]
-    out = dict(rgb=rgb_map.permute(0, 3, 1, 2).contiguous(),
-               features=feat_map.permute(0, 3, 1, 2).contiguous() if feat_map is not None else None,
-               sdf=sdf, mask=mask.permute(0, 3, 1, 2).contiguous(),
-               xyz=xyz.permute(0, 3, 1, 2).contiguous())
-    if return_intermediates:
-        out.update(ray)
-        out.update(enc=enc, sh=sh, rgb_raw=rgb_raw, weights=weights, feat_samples=feat)
-    return out
+    return dict(rgb=rgb_map.permute(0, 3, 1, 2).contiguous(),
+                features=feat_map.permute(0, 3, 1, 2).contiguous() if feat_map is not None
+                else None,
+                sdf=sdf, mask=mask.permute(0, 3, 1, 2).contiguous(),
+                xyz=xyz.permute(0, 3, 1, 2).contiguous(), weights=weights)
+
+
+def render_siren(sd, cam, focal, near, far, styles, *, N=24, res=64, t_rand=None,
+                 offset_sampling=True, static_viewdirs=False, z_normalize=True,
+                 force_background=False, output_features=True, with_sdf=True, depth=8,
+                 prefix="renderer."):
+    """fp32 CPU restatement of VolumeFeatureRenderer(type='sdf').forward: the ray /
+    sample chain of render_rays (sdf_model.py:310-351) feeding SirenGenerator
+    (sdf_model.py:101-139) with the normalised points and unit view directions,
+    then volume_integration.  Same arguments and outputs as render_ngp."""
+    import torch
+
+    def P(k):
+        v = sd[prefix + k]
+        return v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
+
+    cam = torch.as_tensor(cam, dtype=torch.float32).reshape(-1, 3, 4)
+    B = cam.shape[0]
+    near = np.asarray(near, np.float32).reshape(B)
+    far = np.asarray(far, np.float32).reshape(B)
+    ray = sample_rays(cam.numpy(), np.asarray(focal).reshape(B), near, far, res, res, N,
+                      t_rand=t_rand, offset_sampling=offset_sampling,
+                      static_viewdirs=static_viewdirs, z_normalize=z_normalize)
+    pts = torch.from_numpy(ray["pts"])
+    if z_normalize:                                           # sdf_model.py:348-349
+        span = torch.from_numpy(far - near).view(B, 1, 1, 1, 1)
+        x = pts * 2 / span
+    else:
+        x = pts
+    vd = torch.from_numpy(np.ascontiguousarray(
+        np.broadcast_to(ray["viewdirs"][:, :, :, None, :], (B, res, res, N, 3))))
+    sty = torch.as_tensor(styles, dtype=torch.float32)
+    net = "network."
+
+    def film(h, pre):
+        out = _linear(h, P(pre + "weight"), P(pre + "bias"))
+        gamma = 15 * _linear(sty, P(pre + "gamma.weight"), P(pre + "gamma.bias")) + 30
+        beta = 0.25 * _linear(sty, P(pre + "beta.weight"), P(pre + "beta.bias")) + 0
+        return torch.sin(gamma.view(B, 1, 1, 1, -1) * out + beta.view(B, 1, 1, 1, -1))
+
+    h = x
+    for i in range(depth):
+        h = film(h, f"{net}pts_linears.{i}.")
+    sdf = 1 * _linear(h, P(net + "sigma_linear.weight"), P(net + "sigma_linear.bias")) + 0
+    feat = film(torch.cat([h, vd], -1), net + "views_linears.")
+    rgb_raw = 1 * _linear(feat, P(net + "rgb_linear.weight"), P(net + "rgb_linear.bias")) + 0
+    return _integrate(ray, sdf, rgb_raw, feat, P("sigmoid_beta"), with_sdf, force_background,
+                      output_features)
 
 
 # --------------------------------------------------------------------------

@@ -23,7 +23,8 @@ from collections import defaultdict
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
-FIELDS = ("ngp_field_kernel", "ngp_field_x_kernel")   # fp32 / f16x3 field kernels
+# fp32 ngp / f16x3 ngp / f16x3 siren field kernels
+FIELDS = ("ngp_field_kernel", "field_x_kernel<0, sdfr::NgpNet>", "field_x_kernel<0, sdfr::SirenNet>")
 ENCODE = "ngp_encode_kernel"
 
 

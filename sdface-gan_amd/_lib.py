@@ -34,6 +34,7 @@ EXPORTS = (
     "sdfr_sh_encode_forward", "sdfr_sh_encode_backward",
     "sdfr_render_ngp_workspace_bytes", "sdfr_render_ngp_forward",
     "sdfr_render_ngp_encode_only", "sdfr_debug_set_field_variant", "sdfr_debug_sin_probe",
+    "sdfr_render_siren_workspace_bytes", "sdfr_render_siren_forward",
     "sdfr_fused_bias_act", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
 )
 
@@ -46,6 +47,19 @@ class NgpWeights(ctypes.Structure):
         ("input_w", _vp), ("input_b", _vp),
         ("pts_w", _vp * 3), ("pts_b", _vp * 3), ("pts_gw", _vp * 3), ("pts_gb", _vp * 3),
         ("pts_bw", _vp * 3), ("pts_bb", _vp * 3),
+        ("views_w", _vp), ("views_b", _vp),
+        ("views_gw", _vp), ("views_gb", _vp), ("views_bw", _vp), ("views_bb", _vp),
+        ("sigma_w", _vp), ("sigma_b", _vp), ("rgb_w", _vp), ("rgb_b", _vp),
+        ("sigmoid_beta", _vp),
+    ]
+
+
+class SirenWeights(ctypes.Structure):
+    """sdfr_siren_weights (include/sdfr.h)."""
+    _fields_ = [
+        ("depth", _u32), ("width", _u32),
+        ("pts_w", _vp * 8), ("pts_b", _vp * 8), ("pts_gw", _vp * 8), ("pts_gb", _vp * 8),
+        ("pts_bw", _vp * 8), ("pts_bb", _vp * 8),
         ("views_w", _vp), ("views_b", _vp),
         ("views_gw", _vp), ("views_gb", _vp), ("views_bw", _vp), ("views_bb", _vp),
         ("sigma_w", _vp), ("sigma_b", _vp), ("rgb_w", _vp), ("rgb_b", _vp),
@@ -106,6 +120,10 @@ def lib():
     L.sdfr_render_ngp_encode_only.argtypes = [ctypes.POINTER(NgpWeights),
                                               ctypes.POINTER(NgpRenderArgs), _vp]
     L.sdfr_debug_set_field_variant.argtypes = [_int]
+    L.sdfr_render_siren_workspace_bytes.restype = ctypes.c_size_t
+    L.sdfr_render_siren_workspace_bytes.argtypes = [_u32]
+    L.sdfr_render_siren_forward.argtypes = [ctypes.POINTER(SirenWeights),
+                                            ctypes.POINTER(NgpRenderArgs), _vp]
     L.sdfr_debug_sin_probe.argtypes = [_vp, _vp, _vp, _u32, _vp]
     L.sdfr_fused_bias_act.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_uint64, _u32, _u32, _int, _int,
                                       _f32, _f32, _vp]

@@ -1,10 +1,16 @@
-// field_f16x3.hip -- the fused renderer's field stage on split-fp16 MFMA.
+// field_f16x3.hip -- the fused renderer's field stage on split-fp16 MFMA, for
+// both SDFace networks:
 //
-// Same job as ngp_field_kernel (render_ngp.hip): NGPSIRENGenerator's five
-// dense layers (sdf_model.py:1566-1592) + SDF->density + front-to-back alpha
-// compositing (volume_integration, :236-301) for 16 rays per wave, but every
-// fp32 GEMM tile runs as three v_mfma_f32_16x16x32_f16 on a hi/lo fp16 split
-// of both operands:
+//   NgpNet    NGPSIRENGenerator (sdf_model.py:1534-1592): hash-grid features (32)
+//             -> input_linear -> 3 FiLM layers -> sigma | [h3, SH(16)] -> views
+//             FiLM -> rgb.  Inputs come from the hash-grid encode kernel.
+//   SirenNet  SirenGenerator (sdf_model.py:101-139): normalised points (3) -> 8
+//             FiLM layers -> sigma | [h7, viewdir(3)] -> views FiLM -> rgb.
+//             Points are formed in-kernel from the ray (bit-exact chain).
+//
+// followed by SDF->density and front-to-back alpha compositing
+// (volume_integration, :236-301), 16 rays per wave.  Every fp32 GEMM tile runs
+// as three v_mfma_f32_16x16x32_f16 on a hi/lo fp16 split of both operands:
 //
 //     W.x = W_hi.x_hi + W_hi.x_lo + W_lo.x_hi   (+ W_lo.x_lo, dropped: 2^-22 rel.)
 //
@@ -13,19 +19,19 @@
 // Accuracy (scripts/probe_split_f16.hip, measured on MI355X): a 256-deep dot
 // product is as accurate as the fp32 fma chain PROVIDED the fp16 lo parts do
 // not go subnormal -- so every weight row is scaled by a power of two su
-// (max |w| su in [0.5,1), ngp_xscale_kernel).  Power-of-two scaling commutes
-// with rounding, so it is undone exactly: biases enter pre-scaled, the FiLM
-// gamma is divided by su (gamma' x_scaled == gamma x, bit for bit), and the
-// identity input layer multiplies by 1/su.
+// (max |w| su in [0.5,1), xscale_kernel).  Power-of-two scaling commutes with
+// rounding, so it is undone exactly: biases enter pre-scaled, the FiLM gamma is
+// divided by su (gamma' x_scaled == gamma x, bit for bit), and NGP's identity
+// input layer multiplies by 1/su.
 //
 // Work unit: a wave owns 16 rays and evaluates TWO samples per pass (MFMA
 // N = 2 x 16), so each A fragment read from LDS feeds 6 MFMAs and the weight
-// stream (1.1 MB per pass, shared by the 4 waves of a workgroup through a
-// 3-slot LDS ring) is amortised over 128 ray-samples.  The accumulator of
-// layer l is the B operand of layer l+1 with no lane movement: after a pair of
-// 16-row tiles (2q, 2q+1) is activated, its 8 values per lane are split in
-// place into (hi, lo) fp16x8, which is exactly the k-step q fragment (the
-// packed weights permute K to match, ngp_xprep_kernel).
+// stream (1.1 MB ngp / 2.1 MB siren per pass, shared by the 4 waves of a
+// workgroup through a 3-slot LDS ring) is amortised over 128 ray-samples.  The
+// accumulator of layer l is the B operand of layer l+1 with no lane movement:
+// after a pair of 16-row tiles (2q, 2q+1) is activated, its 8 values per lane
+// are split in place into (hi, lo) fp16x8, which is exactly the k-step q
+// fragment (the packed weights permute K to match, xprep_kernel).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -37,32 +43,66 @@ namespace sdfr {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 t_out][hi,lo][64 lanes] x 16 B
-constexpr uint32_t kXSlices = 2 + 16 * 3 + 18;   // half k-steps per pass
 constexpr int kXStage = kXSliceF4 / kThreads;    // float4 staged per thread per slice
-constexpr uint32_t kXCst = 10 * kW;              // bias_s[5], 1/su0, sigma_w, rgb_w[3]
 
 // Schedule options (compile-time; DESIGN.md section 5 records the measured choice):
 //   SDFR_X_PREFETCH  ring staged two slices ahead + next slice's first fragment
 //                    read before the barrier (1) / one slice ahead (0)
-//   SDFR_X_EPI       views layer output-group major with the compositing of tiles
-//                    0-7 in the MFMA shadow of tiles 8-15 (1) / after the layer (0)
+//   SDFR_X_BUFLOAD   ring staging loads as buffer_load (scalar slice offset, no
+//                    per-load 64-bit address VALU) (1) / global_load (0)
 #ifndef SDFR_X_PREFETCH
 #define SDFR_X_PREFETCH 1
 #endif
-#ifndef SDFR_X_EPI
-#define SDFR_X_EPI 0
-#endif
-//   SDFR_X_BUFLOAD   ring staging loads as buffer_load (scalar slice offset, no
-//                    per-load 64-bit address VALU) (1) / global_load (0)
 #ifndef SDFR_X_BUFLOAD
 #define SDFR_X_BUFLOAD 1
 #endif
 
-__host__ __device__ constexpr uint32_t xslice_base(uint32_t layer) {
-    return layer == 0 ? 0u : (layer == 4 ? 50u : 2u + 16u * (layer - 1));
+// ----------------------------------------------------------------------------
+// network policies.  Weight matrices ("layers") in order: layer 0, the dense
+// 256x256 layers, the views layer.  Slices: 2 per k-step of 32 input features
+// (8 output tiles each); layer 0 has one k-step, dense layers 8, views 9.
+// ----------------------------------------------------------------------------
+struct NgpNet {
+    static constexpr bool kSiren = false;
+    static constexpr int kLayers = 5;          // input_linear, pts_linears.0-2, views
+    static constexpr int kFilmN = 4;           // FiLM: pts_linears.0-2, views
+    static constexpr int kHidden = 3;          // dense layers after layer 0
+    static constexpr uint32_t kSlices = 2 + 16 * 3 + 18;
+    __host__ __device__ static constexpr uint32_t K(int l) {
+        return l == 0 ? kFeatIn : (l == 4 ? kViewsIn : kW);
+    }
+    __host__ __device__ static constexpr int film_layer(int f) { return f + 1; }
+};
+struct SirenNet {
+    static constexpr bool kSiren = true;
+    static constexpr int kLayers = 9;          // pts_linears.0-7, views
+    static constexpr int kFilmN = 9;
+    static constexpr int kHidden = 7;
+    static constexpr uint32_t kSlices = 2 + 16 * 7 + 18;
+    __host__ __device__ static constexpr uint32_t K(int l) {
+        return l == 0 ? 3u : (l == 8 ? kW + 3 : kW);
+    }
+    __host__ __device__ static constexpr int film_layer(int f) { return f; }
+};
+constexpr int kMaxLayers = 9;
+
+template <class Net>
+__host__ __device__ constexpr uint32_t xslice_base(int l) {
+    return l == 0 ? 0u : (l == Net::kLayers - 1 ? 2u + 16u * Net::kHidden : 2u + 16u * (l - 1));
 }
-__host__ __device__ constexpr uint32_t layer_k(uint32_t layer) {
-    return layer == 0 ? kFeatIn : (layer == 4 ? kViewsIn : kW);
+
+// K index of element j of lane group g in k-step q of layer l (-1 = zero pad).
+template <class Net>
+__device__ __forceinline__ int xperm_k(int l, uint32_t q, uint32_t g, uint32_t j) {
+    if (l == 0) {
+        if constexpr (Net::kSiren) return (g == 0 && j < 3) ? (int)j : -1;   // xyz
+        return (int)(8 * g + j);                                           // 32 features
+    }
+    if (l == Net::kLayers - 1 && q == 8) {
+        if constexpr (Net::kSiren) return (g == 0 && j < 3) ? (int)(kW + j) : -1;   // viewdir
+        return g < 2 ? (int)(kW + 8 * g + j) : -1;                                // SH 0-15
+    }
+    return (int)(16 * (2 * q + (j >> 2)) + 4 * g + (j & 3));
 }
 
 __device__ __forceinline__ h8 as_h8(f4 v) { return __builtin_bit_cast(h8, v); }
@@ -83,18 +123,19 @@ __device__ __forceinline__ void split8(const float (&v)[8], f4 &hi, f4 &lo) {
 }
 
 // ----------------------------------------------------------------------------
-// prep 1: per-row power-of-two scales and scaled biases
+// prep 1: per-row power-of-two scales and scaled biases (one block per layer)
 // ----------------------------------------------------------------------------
 struct XScaleArgs {
-    const float *w[5];
-    const float *b[5];
-    float *su;       // [5][256]
-    float *bias_s;   // [5][256]
+    const float *w[kMaxLayers];
+    const float *b[kMaxLayers];
+    uint32_t K[kMaxLayers];
+    float *su;       // [layers][256]
+    float *bias_s;   // [layers][256]
 };
 
-__global__ void __launch_bounds__(256) ngp_xscale_kernel(const XScaleArgs a) {
+__global__ void __launch_bounds__(256) xscale_kernel(const XScaleArgs a) {
     const uint32_t layer = blockIdx.x, row = threadIdx.x;
-    const uint32_t K = layer_k(layer);
+    const uint32_t K = a.K[layer];
     const float *wr = a.w[layer] + (size_t)row * K;
     float m = 0.0f;
     for (uint32_t k = 0; k < K; ++k) m = fmaxf(m, fabsf(wr[k]));
@@ -114,30 +155,25 @@ __global__ void __launch_bounds__(256) ngp_xscale_kernel(const XScaleArgs a) {
 // ----------------------------------------------------------------------------
 struct XPrepArgs {
     const float *styles;           // [B,256]
-    const float *gw[kFilm], *gb[kFilm], *bw[kFilm], *bb[kFilm];
-    const float *w[5];
-    const float *su;               // [5][256]
-    float *film;                   // [B][4][2][256]
-    f4 *packed;                    // [68][8][2][64] fp16x8
+    const float *gw[kMaxLayers], *gb[kMaxLayers], *bw[kMaxLayers], *bb[kMaxLayers];
+    const float *w[kMaxLayers];
+    const float *su;               // [layers][256]
+    float *film;                   // [B][films][2][256]
+    f4 *packed;                    // [slices][8][2][64] fp16x8
     uint32_t B;
 };
 
-// K index of element j of lane group g in k-step q of `layer` (-1 = zero pad).
-__device__ __forceinline__ int xperm_k(uint32_t layer, uint32_t q, uint32_t g, uint32_t j) {
-    if (layer == 0) return (int)(8 * g + j);
-    if (layer == 4 && q == 8) return g < 2 ? (int)(kW + 8 * g + j) : -1;
-    return (int)(16 * (2 * q + (j >> 2)) + 4 * g + (j & 3));
-}
-
-// blocks [0, B*8): FiLM rows; then packing, one (slice, t8, lane) per thread
-__global__ void __launch_bounds__(256) ngp_xprep_kernel(const XPrepArgs a) {
+// blocks [0, B*films*2): FiLM rows; then packing, one (slice, t8, lane) per thread
+template <class Net>
+__global__ void __launch_bounds__(256) xprep_kernel(const XPrepArgs a) {
+    constexpr int NF = Net::kFilmN;
     const uint32_t blk = blockIdx.x, j = threadIdx.x;
-    const uint32_t nfilm = a.B * kFilm * 2;
+    const uint32_t nfilm = a.B * NF * 2;
     if (blk < nfilm) {
-        const uint32_t b = blk / (kFilm * 2), rem = blk % (kFilm * 2);
-        const uint32_t layer = rem >> 1, which = rem & 1;
-        const float *W = which ? a.bw[layer] : a.gw[layer];
-        const float *bias = which ? a.bb[layer] : a.gb[layer];
+        const uint32_t b = blk / (NF * 2), rem = blk % (NF * 2);
+        const uint32_t f = rem >> 1, which = rem & 1;
+        const float *W = which ? a.bw[f] : a.gw[f];
+        const float *bias = which ? a.bb[f] : a.gb[f];
         const f4 *wr = reinterpret_cast<const f4 *>(W + (size_t)j * kW);
         const f4 *sr = reinterpret_cast<const f4 *>(a.styles + (size_t)b * kW);
         float acc = 0.0f;
@@ -151,43 +187,33 @@ __global__ void __launch_bounds__(256) ngp_xprep_kernel(const XPrepArgs a) {
         }
         const float lin = __fadd_rn(acc, bias[j]);
         // LinearLayer: std_init * linear + bias_init (sdf_model.py:39, 58-59); the
-        // gamma of network layer `layer+1` absorbs that layer's row scale exactly
+        // gamma absorbs the row scale of the layer it modulates, exactly
         const float v = which ? __fadd_rn(__fmul_rn(0.25f, lin), 0.0f)
                               : __fdiv_rn(__fadd_rn(__fmul_rn(15.0f, lin), 30.0f),
-                                          a.su[(layer + 1) * kW + j]);
-        a.film[(((size_t)b * kFilm + layer) * 2 + which) * kW + j] = v;
+                                          a.su[Net::film_layer(f) * kW + j]);
+        a.film[(((size_t)b * NF + f) * 2 + which) * kW + j] = v;
         return;
     }
     const uint32_t e = (blk - nfilm) * 256 + j;
-    if (e >= kXSlices * 512) return;
+    if (e >= Net::kSlices * 512) return;
     const uint32_t slice = e / 512, rem = e % 512;
     const uint32_t t8 = rem >> 6, lane = rem & 63;
-    uint32_t layer = 0;
-    if (slice >= 50) layer = 4;
+    int layer = 0;
+    if (slice >= xslice_base<Net>(Net::kLayers - 1)) layer = Net::kLayers - 1;
     else if (slice >= 2) layer = 1 + (slice - 2) / 16;
-    const uint32_t local = slice - xslice_base(layer);
-    // layers 0-3: k-step major (q, h); views layer: output-group major (h, q)
-    const bool hmajor = SDFR_X_EPI && layer == 4;
-    const uint32_t q = hmajor ? local % 9 : local >> 1;
-    const uint32_t h = hmajor ? local / 9 : local & 1;
+    const uint32_t local = slice - xslice_base<Net>(layer);
+    const uint32_t q = local >> 1, h = local & 1;
     const uint32_t row = 16 * (8 * h + t8) + (lane & 15), g = lane >> 4;
-    const uint32_t K = layer_k(layer);
+    const uint32_t K = Net::K(layer);
     const float s = a.su[layer * kW + row];
     float v[8];
 #pragma unroll
     for (uint32_t jj = 0; jj < 8; ++jj) {
-        const int k = xperm_k(layer, q, g, jj);
+        const int k = xperm_k<Net>(layer, q, g, jj);
         v[jj] = k < 0 ? 0.0f : __fmul_rn(a.w[layer][(size_t)row * K + k], s);
     }
     f4 hi, lo;
-    h8 H, L;
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-        H[jj] = (_Float16)v[jj];
-        L[jj] = (_Float16)__fsub_rn(v[jj], (float)H[jj]);
-    }
-    hi = __builtin_bit_cast(f4, H);
-    lo = __builtin_bit_cast(f4, L);
+    split8(v, hi, lo);
     f4 *dst = a.packed + (size_t)slice * kXSliceF4 + t8 * 128 + lane;
     dst[0] = hi;
     dst[64] = lo;
@@ -198,27 +224,28 @@ __global__ void __launch_bounds__(256) ngp_xprep_kernel(const XPrepArgs a) {
 // ----------------------------------------------------------------------------
 struct XFieldArgs {
     GeomArgs g;
-    const float *enc;              // [L=16][S_total][2]
-    const f4 *packed;              // [68][1024]
-    const float *film;             // [B][4][2][256], gamma pre-divided by su
-    const float *su;               // [5][256]
-    const float *bias_s;           // [5][256]
+    const float *enc;              // ngp: [L=16][S_total][2]; siren: unused
+    const f4 *packed;              // [slices][1024]
+    const float *film;             // [B][films][2][256], gamma pre-divided by su
+    const float *su;               // [layers][256]
+    const float *bias_s;           // [layers][256]
     const float *sigma_w, *sigma_b, *rgb_w, *rgb_b, *sigmoid_beta;
     const float *sigma_noise;      // [B,H,W,N] or null (no_sdf only)
     int force_background, with_sdf;
     float *rgb, *features, *sdf, *xyz, *mask;
 };
 
-// Weight ring: 3 LDS slots; during slice `it` the wave computes from slot it%3,
-// writes slice it+2 (held in registers since slice it-1) into slot (it+2)%3 --
-// the slot of slice it-1, which every wave finished reading before the barrier
-// that closed slice it-1 -- loads slice it+3 into registers, and reads the first
-// fragment pair of slice it+1 (already visible: written during it-1), so the
-// next slice's first MFMAs do not wait on LDS latency after the barrier.
+// Weight ring: 3 LDS slots.  With SDFR_X_PREFETCH, during slice `it` the wave
+// computes from slot it%3, writes slice it+2 (held in registers since slice
+// it-1) into slot (it+2)%3 -- the slot of slice it-1, which every wave finished
+// reading before the barrier that closed slice it-1 -- loads slice it+3 into
+// registers, and reads the first fragment pair of slice it+1 (already visible:
+// written during it-1), so the next slice's first MFMAs do not wait on LDS
+// latency after the barrier.
 struct XRing {
     f4 *lds;              // [3][kXSliceF4]
     const f4 *packed;
-    f4 st[kXStage];       // slice it+2 (global -> regs -> LDS)
+    f4 st[kXStage];       // the slice staged through registers
     f4 pre_h, pre_l;      // first (hi, lo) A fragment of the current slice
     __amdgpu_buffer_rsrc_t rsrc;   // the packed fragments (SDFR_X_BUFLOAD)
     uint32_t it;          // slice iteration (runs across passes)
@@ -235,7 +262,7 @@ __device__ __forceinline__ void xpin(float &x) { asm volatile("" : "+v"(x)); }
 // is the product): bit 0 drops the slice barrier, bit 1 the LDS A-fragment reads,
 // bit 2 the ring staging, bit 3 the per-layer activations, bit 4 the per-pass
 // compositing.  Any V != 0 computes wrong results by construction.
-template <int V, int H, class Side>
+template <int V, class Net, int H, class Side>
 __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], const f4 b0h,
                                       const f4 b0l, const f4 b1h, const f4 b1l, Side &&side) {
     const uint32_t cur = R.it % 3u;
@@ -271,7 +298,7 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
 #pragma unroll
         for (int i = 0; i < kXStage; ++i)
             R.lds[wslot * kXSliceF4 + R.tid + i * kThreads] = R.st[i];
-        const uint32_t pf = (R.it + 2u + SDFR_X_PREFETCH) % kXSlices;
+        const uint32_t pf = (R.it + 2u + SDFR_X_PREFETCH) % Net::kSlices;
 #pragma unroll
         for (int i = 0; i < kXStage; ++i) {
 #if SDFR_X_BUFLOAD
@@ -295,8 +322,8 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
 
 // Activate tile pair (2q, 2q+1) of one sample column in place and split it
 // into the (hi, lo) B fragment of k-step q.
-//   MODE 0: identity input layer, x * (1/su0)
-//   MODE 1: FiLM sin(gamma' x + beta) (sdf_model.py:67, two roundings)
+//   MODE 0: identity layer, x * (1/su)            (ngp input_linear)
+//   MODE 1: FiLM sin(gamma' x + beta)              (sdf_model.py:67, two roundings)
 //   MODE 2: FiLM + partial sigma_linear dot product (the sdf head)
 template <int MODE, int V>
 __device__ __forceinline__ void act_pair(f4 &za, f4 &zb, int q, const float *gam,
@@ -343,24 +370,26 @@ __device__ __forceinline__ void init_acc(f4 (&acc)[16], const float *bias, uint3
 // input pair (q+1) of each sample column is activated in the MFMA shadow; the
 // last k-step activates the first pair of this layer's own output (its tiles
 // 0-7 completed in the k-step's first half).
-template <int V, class ActIn, class ActOut>
+template <int V, class Net, class ActIn, class ActOut>
 __device__ __forceinline__ void dense_layer(XRing &R, f4 (&in0)[16], f4 (&in1)[16],
                                             f4 (&out0)[16], f4 (&out1)[16], ActIn &&act_in,
                                             ActOut &&act_out) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int qn = q < 7 ? q + 1 : 7;
-        xstep<V, 0>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1], [&] {
-            if (q < 7) act_in(in0[2 * qn], in0[2 * qn + 1], qn, 0);
-        });
-        xstep<V, 1>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1], [&] {
-            if (q < 7) {
-                act_in(in1[2 * qn], in1[2 * qn + 1], qn, 1);
-            } else {
-                act_out(out0[0], out0[1], 0, 0);
-                act_out(out1[0], out1[1], 0, 1);
-            }
-        });
+        xstep<V, Net, 0>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1],
+                         [&] {
+                             if (q < 7) act_in(in0[2 * qn], in0[2 * qn + 1], qn, 0);
+                         });
+        xstep<V, Net, 1>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1],
+                         [&] {
+                             if (q < 7) {
+                                 act_in(in1[2 * qn], in1[2 * qn + 1], qn, 1);
+                             } else {
+                                 act_out(out0[0], out0[1], 0, 0);
+                                 act_out(out1[0], out1[1], 0, 1);
+                             }
+                         });
     }
 }
 
@@ -368,11 +397,12 @@ struct NoAct {
     __device__ __forceinline__ void operator()(f4 &, f4 &, int, int) const {}
 };
 
-template <int V>
-__global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldArgs a) {
-    __shared__ f4 ring_lds[3 * kXSliceF4];                // 48 KB weight ring
-    __shared__ float cst[kXCst];                           // 10 KB constants
-    __shared__ float film_lds[kFilm * 2 * kW];             // 8 KB: the workgroup's face
+template <int V, class Net>
+__global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a) {
+    constexpr int NL = Net::kLayers, NF = Net::kFilmN;
+    __shared__ f4 ring_lds[3 * kXSliceF4];                 // 48 KB weight ring
+    __shared__ float cst[(NL + 5) * kW];                   // bias_s[NL], 1/su0, sigma_w, rgb_w[3]
+    __shared__ float film_lds[NF * 2 * kW];                // the workgroup's face
     __shared__ f4 facc_lds[kWaves][16 * 64];               // 64 KB: feature accumulators
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t n = lane & 15u, g = lane >> 4;
@@ -386,7 +416,7 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
     const bool tile_ok = tile_local < G.tiles_per_face;
     if (!tile_ok) tile_local = G.tiles_per_face - 1;
     const uint32_t tile = b * G.tiles_per_face + tile_local;
-    uint32_t ray_local = (tile % G.tiles_per_face) * kTileRays + n;
+    uint32_t ray_local = tile_local * kTileRays + n;
     const bool ray_ok = tile_ok && ray_local < G.H * G.W;
     if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
     const uint32_t py = ray_local / G.W, px = ray_local % G.W;
@@ -395,49 +425,58 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
     Ray ray;
     make_ray(G.cam + (size_t)b * 12, G.focal[b], G.pix_x[px], G.pix_y[py], G.half_res, ray);
     const float nr = G.near_[b], fr = G.far_[b];
+    const float span = __fsub_rn(fr, nr);
     const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
-    // SH k-step fragment (identical for both sample columns): lanes g = 0, 1
-    // hold SH 0-7 / 8-15, g = 2, 3 the zero padding of K = 272 -> 288
-    f4 shh, shl;
+    // the views layer's last k-step fragment (identical for both sample columns):
+    // ngp: lanes g = 0, 1 hold SH 0-7 / 8-15 (K 272 -> 288); siren: lane group 0
+    // holds the unit view direction (K 259 -> 288); the rest is zero padding
+    f4 vxh, vxl;
     {
         const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
         const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
         const float v2 = G.static_viewdirs ? ray.dir[2] : ray.d[2];
         const float vn = norm3_torch(v0, v1, v2);
         const float ux = __fdiv_rn(v0, vn), uy = __fdiv_rn(v1, vn), uz = __fdiv_rn(v2, vn);
-        const f4 qa = sh_quad(ux, uy, uz, (2 * g) & 3), qb = sh_quad(ux, uy, uz, (2 * g + 1) & 3);
         float v[8];
+        if constexpr (Net::kSiren) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            v[r] = g < 2 ? qa[r] : 0.0f;
-            v[4 + r] = g < 2 ? qb[r] : 0.0f;
+            for (int r = 0; r < 8; ++r) v[r] = 0.0f;
+            if (g == 0) {
+                v[0] = ux;
+                v[1] = uy;
+                v[2] = uz;
+            }
+        } else {
+            const f4 qa = sh_quad(ux, uy, uz, (2 * g) & 3), qb = sh_quad(ux, uy, uz, (2 * g + 1) & 3);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = g < 2 ? qa[r] : 0.0f;
+                v[4 + r] = g < 2 ? qb[r] : 0.0f;
+            }
         }
-        split8(v, shh, shl);
+        split8(v, vxh, vxl);
     }
     const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
     {
-        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * kFilm * 2 * kW);
+        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * NF * 2 * kW);
         f4 *dst = reinterpret_cast<f4 *>(film_lds);
-#pragma unroll
-        for (uint32_t i = tid; i < kFilm * 2 * kW / 4; i += kThreads) dst[i] = src[i];
+        for (uint32_t i = tid; i < NF * 2 * kW / 4; i += kThreads) dst[i] = src[i];
     }
-    const float *film = film_lds;
 
     XRing R;
     R.lds = ring_lds;
     R.packed = a.packed;
     R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<f4 *>(a.packed), 0,
-                                               (int)(kXSlices * kXSliceF4 * sizeof(f4)),
+                                               (int)(Net::kSlices * kXSliceF4 * sizeof(f4)),
                                                0x00020000);
     R.tid = tid;
     R.it = 0;
-    // bias_s[5][256], 1/su of the input layer, sigma_linear row, rgb_linear rows
-    for (uint32_t i = tid; i < kXCst; i += kThreads) {
+    for (uint32_t i = tid; i < (NL + 5) * kW; i += kThreads) {
         float v;
-        if (i < 5 * kW) v = a.bias_s[i];
-        else if (i < 6 * kW) v = __fdiv_rn(1.0f, a.su[i - 5 * kW]);
-        else if (i < 7 * kW) v = a.sigma_w[i - 6 * kW];
-        else v = a.rgb_w[i - 7 * kW];
+        if (i < NL * kW) v = a.bias_s[i];
+        else if (i < (NL + 1) * kW) v = __fdiv_rn(1.0f, a.su[i - NL * kW]);
+        else if (i < (NL + 2) * kW) v = a.sigma_w[i - (NL + 1) * kW];
+        else v = a.rgb_w[i - (NL + 2) * kW];
         cst[i] = v;
     }
     // prologue: slices 0 (.. 1) -> slots; the next slice -> registers
@@ -456,30 +495,47 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
     float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
     float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
 
-    const float *bias_l = cst;                     // [5][256] (scaled)
-    const float *inv_su0 = cst + 5 * kW;
-    const float *sig_w = cst + 6 * kW, *rgb_w = cst + 7 * kW;
-    const float *f0g = film, *f0b = film + kW, *f1g = film + 2 * kW, *f1b = film + 3 * kW;
-    const float *f2g = film + 4 * kW, *f2b = film + 5 * kW, *f3g = film + 6 * kW,
-                *f3b = film + 7 * kW;
+    const float *bias_l = cst;                     // [NL][256] (scaled)
+    const float *inv_su0 = cst + NL * kW;
+    const float *sig_w = cst + (NL + 1) * kW, *rgb_w = cst + (NL + 2) * kW;
+    auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
+    auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
     const float sig_b = a.sigma_b[0];
     const float rgb_b0 = a.rgb_b[0], rgb_b1 = a.rgb_b[1], rgb_b2 = a.rgb_b[2];
 
-    // hash-grid features: lane group g holds levels 4g..4g+3 (K = 8g..8g+7)
+    // layer-0 inputs of the pass's two samples:
+    //   ngp   the hash-grid features, lane group g holds levels 4g..4g+3 (K 8g..8g+7)
+    //   siren the normalised point (sdf_model.py:343-349) in lane group 0
     const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
     const size_t tile_sid = (size_t)(tile * G.N) * kTileRays + n;
     float2 en[2][4];
-    auto load_enc = [&](uint32_t s0) {
+    auto load_inputs = [&](uint32_t s0) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             uint32_t s = s0 + j;
             if (s >= G.N) s = G.N - 1;
-            const size_t sid = tile_sid + (size_t)s * kTileRays;
+            if constexpr (Net::kSiren) {
+                const float z = sample_z(G.sc, nr, fr, ray_index, s);
+                float np_[3];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) en[j][c] = enc2[(4 * g + c) * (size_t)G.S_total + sid];
+                for (int k = 0; k < 3; ++k) {
+                    const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));
+                    np_[k] = G.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;
+                }
+                const bool g0 = g == 0;
+                en[j][0] = make_float2(g0 ? np_[0] : 0.0f, g0 ? np_[1] : 0.0f);
+                en[j][1] = make_float2(g0 ? np_[2] : 0.0f, 0.0f);
+                en[j][2] = make_float2(0.0f, 0.0f);
+                en[j][3] = make_float2(0.0f, 0.0f);
+            } else {
+                const size_t sid = tile_sid + (size_t)s * kTileRays;
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    en[j][c] = enc2[(4 * g + c) * (size_t)G.S_total + sid];
+            }
         }
     };
-    load_enc(0);
+    load_inputs(0);
 
     const uint32_t npass = (G.N + 1) / 2;
     for (uint32_t p = 0; p < npass; ++p) {
@@ -498,188 +554,89 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
             split8(v1, e1h, e1l);
         }
         float sdfp0 = 0.0f, sdfp1 = 0.0f;
-        auto act_id = [&](f4 &za, f4 &zb, int q, int) {
-            float dummy = 0.0f;
-            act_pair<0, V>(za, zb, q, inv_su0, nullptr, nullptr, dummy, g);
+        // activation of layer l's output: ngp layer 0 is the identity input_linear,
+        // every other layer is a FiLM with film index film_layer^-1(l); the last
+        // hidden layer also feeds the sdf head
+        auto act_film = [&](int f) {
+            return [&, f](f4 &za, f4 &zb, int q, int) {
+                float dummy = 0.0f;
+                act_pair<1, V>(za, zb, q, fg(f), fb(f), nullptr, dummy, g);
+            };
         };
-        auto act_f0 = [&](f4 &za, f4 &zb, int q, int) {
-            float dummy = 0.0f;
-            act_pair<1, V>(za, zb, q, f0g, f0b, nullptr, dummy, g);
+        auto act_sdf = [&](int f) {
+            return [&, f](f4 &za, f4 &zb, int q, int j) {
+                if (j == 0) act_pair<2, V>(za, zb, q, fg(f), fb(f), sig_w, sdfp0, g);
+                else act_pair<2, V>(za, zb, q, fg(f), fb(f), sig_w, sdfp1, g);
+            };
         };
-        auto act_f1 = [&](f4 &za, f4 &zb, int q, int) {
-            float dummy = 0.0f;
-            act_pair<1, V>(za, zb, q, f1g, f1b, nullptr, dummy, g);
-        };
-        auto act_f2 = [&](f4 &za, f4 &zb, int q, int j) {
-            if (j == 0) act_pair<2, V>(za, zb, q, f2g, f2b, sig_w, sdfp0, g);
-            else act_pair<2, V>(za, zb, q, f2g, f2b, sig_w, sdfp1, g);
+        auto act_l0 = [&](f4 &za, f4 &zb, int q, int j) {
+            if constexpr (Net::kSiren) {
+                act_film(0)(za, zb, q, j);
+            } else {
+                float dummy = 0.0f;
+                act_pair<0, V>(za, zb, q, inv_su0, nullptr, nullptr, dummy, g);
+            }
         };
 
-        // layer 0: input_linear (32 -> 256) -> X
+        // layer 0 (32 -> 256 ngp / 3 -> 256 siren) -> X
         init_acc(X0, bias_l, g);
         init_acc(X1, bias_l, g);
-        xstep<V, 0>(R, X0, X1, e0h, e0l, e1h, e1l, [] {});
-        xstep<V, 1>(R, X0, X1, e0h, e0l, e1h, e1l, [&] {
-            act_id(X0[0], X0[1], 0, 0);
-            act_id(X1[0], X1[1], 0, 1);
+        xstep<V, Net, 0>(R, X0, X1, e0h, e0l, e1h, e1l, [] {});
+        xstep<V, Net, 1>(R, X0, X1, e0h, e0l, e1h, e1l, [&] {
+            act_l0(X0[0], X0[1], 0, 0);
+            act_l0(X1[0], X1[1], 0, 1);
         });
-        // layers 1-3: FiLM pts_linears.0..2
-        init_acc(Y0, bias_l + kW, g);
-        init_acc(Y1, bias_l + kW, g);
-        dense_layer<V>(R, X0, X1, Y0, Y1, act_id, act_f0);
-        init_acc(X0, bias_l + 2 * kW, g);
-        init_acc(X1, bias_l + 2 * kW, g);
-        dense_layer<V>(R, Y0, Y1, X0, X1, act_f0, act_f1);
-        init_acc(Y0, bias_l + 3 * kW, g);
-        init_acc(Y1, bias_l + 3 * kW, g);
-        dense_layer<V>(R, X0, X1, Y0, Y1, act_f1, act_f2);
-#if SDFR_X_EPI
-        // layer 4: views FiLM ([h3, SH] 272 -> 256) -> X, output-group major (the
-        // packing orders its 18 slices h-major): group 0 = tiles 0-7 over all 9
-        // k-steps, activating h3 pair q+1 of both columns in k-step q's shadow;
-        // group 1 = tiles 8-15, with the compositing of tiles 0-7 in its shadow.
-        init_acc(X0, bias_l + 4 * kW, g);
-        init_acc(X1, bias_l + 4 * kW, g);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int qn = q < 7 ? q + 1 : 7;
-            xstep<V, 0>(R, X0, X1, Y0[2 * q], Y0[2 * q + 1], Y1[2 * q], Y1[2 * q + 1], [&] {
-                if (q < 7) {
-                    act_f2(Y0[2 * qn], Y0[2 * qn + 1], qn, 0);
-                    act_f2(Y1[2 * qn], Y1[2 * qn + 1], qn, 1);
-                }
-            });
+        if constexpr (Net::kSiren) {
+            // pts_linears.1-7 (X->Y, then (Y->X, X->Y) x 3); film f modulates layer f
+            init_acc(Y0, bias_l + 1 * kW, g);
+            init_acc(Y1, bias_l + 1 * kW, g);
+            dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_l0, act_film(1));
+            for (int l = 2; l < 6; l += 2) {                  // layers 2-5
+                init_acc(X0, bias_l + l * kW, g);
+                init_acc(X1, bias_l + l * kW, g);
+                dense_layer<V, Net>(R, Y0, Y1, X0, X1, act_film(l - 1), act_film(l));
+                init_acc(Y0, bias_l + (l + 1) * kW, g);
+                init_acc(Y1, bias_l + (l + 1) * kW, g);
+                dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_film(l), act_film(l + 1));
+            }
+            init_acc(X0, bias_l + 6 * kW, g);
+            init_acc(X1, bias_l + 6 * kW, g);
+            dense_layer<V, Net>(R, Y0, Y1, X0, X1, act_film(5), act_film(6));
+            init_acc(Y0, bias_l + 7 * kW, g);
+            init_acc(Y1, bias_l + 7 * kW, g);
+            dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_film(6), act_sdf(7));
+        } else {
+            // pts_linears.0-2: film f modulates layer f+1
+            init_acc(Y0, bias_l + kW, g);
+            init_acc(Y1, bias_l + kW, g);
+            dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_l0, act_film(0));
+            init_acc(X0, bias_l + 2 * kW, g);
+            init_acc(X1, bias_l + 2 * kW, g);
+            dense_layer<V, Net>(R, Y0, Y1, X0, X1, act_film(0), act_film(1));
+            init_acc(Y0, bias_l + 3 * kW, g);
+            init_acc(Y1, bias_l + 3 * kW, g);
+            dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_film(1), act_sdf(2));
         }
-#else
-        // layer 4: views FiLM ([h3, SH] 272 -> 256) -> X; h3 pairs finish the sdf head
-        init_acc(X0, bias_l + 4 * kW, g);
-        init_acc(X1, bias_l + 4 * kW, g);
-        dense_layer<V>(R, Y0, Y1, X0, X1, act_f2, NoAct{});
-        xstep<V, 0>(R, X0, X1, shh, shl, shh, shl, [] {});
-        xstep<V, 1>(R, X0, X1, shh, shl, shh, shl, [] {});
-#endif
-#if SDFR_X_EPI
-        // volume_integration (sdf_model.py:236-301) weights of the pass's two
-        // samples, front to back; a sample past N gets weight 0 (no branch, so
-        // the compositing stays in the MFMA shadow)
-        const uint32_t s0 = 2 * p, s1 = 2 * p + 1;
-        const bool ok1 = s1 < G.N;
-        float sdf0 = 0.0f, sdf1 = 0.0f, w0 = 0.0f, w1 = 0.0f;
-        auto weights = [&] {
-            sdf0 = __fadd_rn(group_sum(sdfp0), sig_b);
-            sdf1 = __fadd_rn(group_sum(sdfp1), sig_b);
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-                const uint32_t s = jj ? s1 : s0;
-                const uint32_t sc = s < G.N ? s : G.N - 1;
-                const float sdf = jj ? sdf1 : sdf0;
-                const float z = sample_z(G.sc, nr, fr, ray_index, sc);
-                const float dist =
-                    (sc + 1 < G.N)
-                        ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc + 1), z), dnorm)
-                        : __fmul_rn(1e10f, dnorm);
-                float alpha;
-                if (a.with_sdf) {
-                    const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
-                    alpha = 1.0f - expf(-sig * dist);
-                } else {
-                    float raw = sdf;
-                    if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc];
-                    const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
-                    alpha = 1.0f - expf(-sp * dist);
-                }
-                float w = alpha * T;
-                if (a.force_background && sc + 1 == G.N) w = 1.0f - wsum;
-                const bool live = jj == 0 || ok1;
-                if (live) {
-                    T = T * ((1.0f - alpha) + 1e-10f);
-                    wsum += w;
-                }
-                if (jj) w1 = live ? w : 0.0f;
-                else w0 = w;
-            }
-            xpin(w0);
-            xpin(w1);
-        };
-        // colour features f = sin(gamma_v' x + beta_v) of tile t, rgb_linear
-        // partial dot products, feature compositing (sample s0 then s1)
-        float q00 = 0.0f, q01 = 0.0f, q02 = 0.0f, q10 = 0.0f, q11 = 0.0f, q12 = 0.0f;
-        auto epi_tile = [&](int t) {
-            if constexpr ((V & 16) != 0) {
-                racc0 += (X0[t][0] + X0[t][1]) + (X0[t][2] + X0[t][3]);
-                racc1 += (X1[t][0] + X1[t][1]) + (X1[t][2] + X1[t][3]);
-                return;
-            }
-            const int f0 = 16 * t + 4 * (int)g;
-            const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
-            const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
-            const f4 wr0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
-            const f4 wr1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
-            const f4 wr2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
-            f4 fa, fb;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                fa[r] = sin_hw(__fadd_rn(__fmul_rn(gm[r], X0[t][r]), bt[r]));
-                fb[r] = sin_hw(__fadd_rn(__fmul_rn(gm[r], X1[t][r]), bt[r]));
-                q00 = __fmaf_rn(fa[r], wr0[r], q00);
-                q01 = __fmaf_rn(fa[r], wr1[r], q01);
-                q02 = __fmaf_rn(fa[r], wr2[r], q02);
-                q10 = __fmaf_rn(fb[r], wr0[r], q10);
-                q11 = __fmaf_rn(fb[r], wr1[r], q11);
-                q12 = __fmaf_rn(fb[r], wr2[r], q12);
-            }
-            f4 v = facc[t * 64 + lane];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[r] = __fmaf_rn(w0, fa[r], v[r]);
-                v[r] = __fmaf_rn(w1, fb[r], v[r]);
-            }
-            facc[t * 64 + lane] = v;
-            xpin(q00);
-            xpin(q10);
-        };
-#if SDFR_X_EPI
-        xstep<V, 0>(R, X0, X1, shh, shl, shh, shl, [&] { weights(); });
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            xstep<V, 1>(R, X0, X1, Y0[2 * q], Y0[2 * q + 1], Y1[2 * q], Y1[2 * q + 1],
-                        [&] { epi_tile(q); });
-        xstep<V, 1>(R, X0, X1, shh, shl, shh, shl, [] {});
-        // next pass's hash-grid features, in flight behind the exposed compositing
-        if (p + 1 < npass) load_enc(2 * p + 2);
-#pragma unroll
-        for (int t = 8; t < 16; ++t) epi_tile(t);
-#endif
+        // views FiLM ([h_last, SH | viewdir] -> 256) -> X; h_last pairs finish the sdf head
+        init_acc(X0, bias_l + (NL - 1) * kW, g);
+        init_acc(X1, bias_l + (NL - 1) * kW, g);
+        dense_layer<V, Net>(R, Y0, Y1, X0, X1, act_sdf(NF - 2), NoAct{});
+        xstep<V, Net, 0>(R, X0, X1, vxh, vxl, vxh, vxl, [] {});
+        xstep<V, Net, 1>(R, X0, X1, vxh, vxl, vxh, vxl, [] {});
 
-        // rgb head and the per-ray accumulators, sample s0 then s1
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            if (jj && !ok1) break;
-            const uint32_t s = jj ? s1 : s0;
-            const float w = jj ? w1 : w0;
-            const float r0 = __fadd_rn(group_sum(jj ? q10 : q00), rgb_b0);
-            const float r1 = __fadd_rn(group_sum(jj ? q11 : q01), rgb_b1);
-            const float r2 = __fadd_rn(group_sum(jj ? q12 : q02), rgb_b2);
-            w_last = w;
-            racc0 = __fmaf_rn(w, sigmoidf_(r0), racc0);
-            racc1 = __fmaf_rn(w, sigmoidf_(r1), racc1);
-            racc2 = __fmaf_rn(w, sigmoidf_(r2), racc2);
-            if (a.xyz) {
-                const float z = sample_z(G.sc, nr, fr, ray_index, s);
-                xacc0 = __fmaf_rn(w, __fadd_rn(ray.o[0], __fmul_rn(ray.d[0], z)), xacc0);
-                xacc1 = __fmaf_rn(w, __fadd_rn(ray.o[1], __fmul_rn(ray.d[1], z)), xacc1);
-                xacc2 = __fmaf_rn(w, __fadd_rn(ray.o[2], __fmul_rn(ray.d[2], z)), xacc2);
-            }
-            if (a.sdf && ray_ok && g == 0) a.sdf[(size_t)ray_index * G.N + s] = jj ? sdf1 : sdf0;
-        }
-#else
-        if (p + 1 < npass) load_enc(2 * p + 2);
+        if (p + 1 < npass) load_inputs(2 * p + 2);
+        const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
         // compositing of the pass's two samples, front to back
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const uint32_t s = 2 * p + j;
             if (s >= G.N) break;
             f4 (&Xj)[16] = j ? X1 : X0;
+            if constexpr ((V & 16) != 0) {
+#pragma unroll
+                for (int t = 0; t < 16; ++t) racc0 += (Xj[t][0] + Xj[t][1]) + (Xj[t][2] + Xj[t][3]);
+                continue;
+            }
             const float sdf = __fadd_rn(group_sum(j ? sdfp1 : sdfp0), sig_b);
             const float z = sample_z(G.sc, nr, fr, ray_index, s);
             const float dist = (s + 1 < G.N)
@@ -745,7 +702,6 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
             }
             if (a.sdf && ray_ok && g == 0) a.sdf[(size_t)ray_index * G.N + s] = sdf;
         }
-#endif
     }
 
     if (!ray_ok) return;
@@ -762,15 +718,15 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
         a.mask[(size_t)b * HW + pix] = w_last;
     }
     if (a.features) {
-        float *fb = a.features + (size_t)b * kW * HW + pix;
+        float *fbp = a.features + (size_t)b * kW * HW + pix;
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const uint32_t jf = 16 * t + 4 * g;
             const f4 v = facc[t * 64 + lane];
-            fb[(size_t)(jf + 0) * HW] = v.x;
-            fb[(size_t)(jf + 1) * HW] = v.y;
-            fb[(size_t)(jf + 2) * HW] = v.z;
-            fb[(size_t)(jf + 3) * HW] = v.w;
+            fbp[(size_t)(jf + 0) * HW] = v.x;
+            fbp[(size_t)(jf + 1) * HW] = v.y;
+            fbp[(size_t)(jf + 2) * HW] = v.z;
+            fbp[(size_t)(jf + 3) * HW] = v.w;
         }
     }
 }
@@ -778,70 +734,71 @@ __global__ void __launch_bounds__(kThreads, 1) ngp_field_x_kernel(const XFieldAr
 // ----------------------------------------------------------------------------
 // host
 // ----------------------------------------------------------------------------
-// workspace tail used by this path: packed [68][1024] f4 | su [5][256] | bias_s [5][256]
-size_t f16x3_ws_bytes(uint32_t B) {
-    (void)B;
-    return (size_t)kXSlices * kXSliceF4 * sizeof(f4) + 2 * 5 * kW * sizeof(float);
+template <class Net>
+static size_t xws_bytes() {
+    return (size_t)Net::kSlices * kXSliceF4 * sizeof(f4) + 2 * Net::kLayers * kW * sizeof(float);
 }
 
-static const float *xbias(const sdfr_ngp_weights *w, int l) {
-    return l == 0 ? w->input_b : (l == 4 ? w->views_b : w->pts_b[l - 1]);
-}
-static const float *xweight(const sdfr_ngp_weights *w, int l) {
-    return l == 0 ? w->input_w : (l == 4 ? w->views_w : w->pts_w[l - 1]);
-}
+// workspace region of this path: packed [slices][1024] f4 | su [L][256] | bias_s [L][256]
+size_t f16x3_ws_bytes(int net) { return net ? xws_bytes<SirenNet>() : xws_bytes<NgpNet>(); }
 
-int launch_xprep(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, char *xws,
-                 float *film, hipStream_t st) {
+// The network's tensors in policy order (layer 0, dense layers, views; FiLM sets).
+struct NetPtrs {
+    const float *w[kMaxLayers], *b[kMaxLayers];
+    const float *gw[kMaxLayers], *gb[kMaxLayers], *bw[kMaxLayers], *bb[kMaxLayers];
+    const float *sigma_w, *sigma_b, *rgb_w, *rgb_b, *sigmoid_beta;
+};
+
+template <class Net>
+static int launch_xprep(const NetPtrs &P, const sdfr_ngp_render_args *a, char *xws, float *film,
+                        hipStream_t st) {
     f4 *packed = reinterpret_cast<f4 *>(xws);
-    float *su = reinterpret_cast<float *>(xws + (size_t)kXSlices * kXSliceF4 * sizeof(f4));
-    float *bias_s = su + 5 * kW;
+    float *su = reinterpret_cast<float *>(xws + (size_t)Net::kSlices * kXSliceF4 * sizeof(f4));
+    float *bias_s = su + Net::kLayers * kW;
     XScaleArgs sa;
-    for (int l = 0; l < 5; ++l) {
-        sa.w[l] = xweight(w, l);
-        sa.b[l] = xbias(w, l);
+    for (int l = 0; l < Net::kLayers; ++l) {
+        sa.w[l] = P.w[l];
+        sa.b[l] = P.b[l];
+        sa.K[l] = Net::K(l);
     }
     sa.su = su;
     sa.bias_s = bias_s;
-    hipLaunchKernelGGL(ngp_xscale_kernel, dim3(5), dim3(256), 0, st, sa);
-    int rc = check_launch("render_ngp: xscale");
+    hipLaunchKernelGGL(xscale_kernel, dim3(Net::kLayers), dim3(256), 0, st, sa);
+    int rc = check_launch("render: xscale");
     if (rc) return rc;
     XPrepArgs p;
     p.styles = a->styles;
-    for (int l = 0; l < 3; ++l) {
-        p.gw[l] = w->pts_gw[l];
-        p.gb[l] = w->pts_gb[l];
-        p.bw[l] = w->pts_bw[l];
-        p.bb[l] = w->pts_bb[l];
+    for (int f = 0; f < Net::kFilmN; ++f) {
+        p.gw[f] = P.gw[f];
+        p.gb[f] = P.gb[f];
+        p.bw[f] = P.bw[f];
+        p.bb[f] = P.bb[f];
     }
-    p.gw[3] = w->views_gw;
-    p.gb[3] = w->views_gb;
-    p.bw[3] = w->views_bw;
-    p.bb[3] = w->views_bb;
-    for (int l = 0; l < 5; ++l) p.w[l] = xweight(w, l);
+    for (int l = 0; l < Net::kLayers; ++l) p.w[l] = P.w[l];
     p.su = su;
     p.film = film;
     p.packed = packed;
     p.B = a->B;
-    const uint32_t blocks = a->B * kFilm * 2 + (kXSlices * 512 + 255) / 256;
-    hipLaunchKernelGGL(ngp_xprep_kernel, dim3(blocks), dim3(256), 0, st, p);
-    return check_launch("render_ngp: xprep");
+    const uint32_t blocks = a->B * Net::kFilmN * 2 + (Net::kSlices * 512 + 255) / 256;
+    hipLaunchKernelGGL(xprep_kernel<Net>, dim3(blocks), dim3(256), 0, st, p);
+    return check_launch("render: xprep");
 }
 
-int launch_xfield(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, const GeomArgs &g,
-                  const float *enc, char *xws, const float *film, hipStream_t st) {
+template <class Net>
+static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const GeomArgs &g,
+                         const float *enc, char *xws, const float *film, hipStream_t st) {
     XFieldArgs f;
     f.g = g;
     f.enc = enc;
     f.packed = reinterpret_cast<const f4 *>(xws);
-    f.su = reinterpret_cast<const float *>(xws + (size_t)kXSlices * kXSliceF4 * sizeof(f4));
-    f.bias_s = f.su + 5 * kW;
+    f.su = reinterpret_cast<const float *>(xws + (size_t)Net::kSlices * kXSliceF4 * sizeof(f4));
+    f.bias_s = f.su + Net::kLayers * kW;
     f.film = film;
-    f.sigma_w = w->sigma_w;
-    f.sigma_b = w->sigma_b;
-    f.rgb_w = w->rgb_w;
-    f.rgb_b = w->rgb_b;
-    f.sigmoid_beta = w->sigmoid_beta;
+    f.sigma_w = P.sigma_w;
+    f.sigma_b = P.sigma_b;
+    f.rgb_w = P.rgb_w;
+    f.rgb_b = P.rgb_b;
+    f.sigmoid_beta = P.sigmoid_beta;
     f.sigma_noise = a->sigma_noise;
     f.force_background = a->force_background;
     f.with_sdf = a->with_sdf;
@@ -855,7 +812,7 @@ int launch_xfield(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, cons
 #ifdef SDFR_ABLATION
 #define SDFR_XFIELD_CASE(V)                                                                  \
     case V:                                                                                  \
-        hipLaunchKernelGGL(ngp_field_x_kernel<V>, dim3(blocks), dim3(kThreads), 0, st, f);   \
+        hipLaunchKernelGGL((field_x_kernel<V, Net>), dim3(blocks), dim3(kThreads), 0, st, f); \
         break;
         SDFR_XFIELD_CASE(1)
         SDFR_XFIELD_CASE(2)
@@ -866,9 +823,132 @@ int launch_xfield(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, cons
 #undef SDFR_XFIELD_CASE
 #endif
         default:
-            hipLaunchKernelGGL(ngp_field_x_kernel<0>, dim3(blocks), dim3(kThreads), 0, st, f);
+            hipLaunchKernelGGL((field_x_kernel<0, Net>), dim3(blocks), dim3(kThreads), 0, st, f);
     }
-    return check_launch("render_ngp: field (f16x3)");
+    return check_launch("render: field (f16x3)");
+}
+
+static NetPtrs ngp_ptrs(const sdfr_ngp_weights *w) {
+    NetPtrs P{};
+    P.w[0] = w->input_w;
+    P.b[0] = w->input_b;
+    for (int l = 0; l < 3; ++l) {
+        P.w[1 + l] = w->pts_w[l];
+        P.b[1 + l] = w->pts_b[l];
+        P.gw[l] = w->pts_gw[l];
+        P.gb[l] = w->pts_gb[l];
+        P.bw[l] = w->pts_bw[l];
+        P.bb[l] = w->pts_bb[l];
+    }
+    P.w[4] = w->views_w;
+    P.b[4] = w->views_b;
+    P.gw[3] = w->views_gw;
+    P.gb[3] = w->views_gb;
+    P.bw[3] = w->views_bw;
+    P.bb[3] = w->views_bb;
+    P.sigma_w = w->sigma_w;
+    P.sigma_b = w->sigma_b;
+    P.rgb_w = w->rgb_w;
+    P.rgb_b = w->rgb_b;
+    P.sigmoid_beta = w->sigmoid_beta;
+    return P;
+}
+
+int launch_xprep_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, char *xws,
+                     float *film, hipStream_t st) {
+    return launch_xprep<NgpNet>(ngp_ptrs(w), a, xws, film, st);
+}
+
+int launch_xfield_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
+                      const GeomArgs &g, const float *enc, char *xws, const float *film,
+                      hipStream_t st) {
+    return launch_xfield<NgpNet>(ngp_ptrs(w), a, g, enc, xws, film, st);
+}
+
+// ----------------------------------------------------------------------------
+// SIREN entry points
+// ----------------------------------------------------------------------------
+static size_t align256x(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// film [B][9][2][256] | split-fp16 region
+static size_t siren_ws_layout(uint32_t B, size_t *o_x) {
+    size_t off = align256x((size_t)B * SirenNet::kFilmN * 2 * kW * sizeof(float));
+    if (o_x) *o_x = off;
+    return off + align256x(xws_bytes<SirenNet>());
+}
+
+static int siren_validate(const sdfr_siren_weights *w, const sdfr_ngp_render_args *a) {
+    if (!w || !a) return fail(SDFR_EINVAL, "render_siren: null args");
+    if (w->depth != 8 || w->width != 256)
+        return fail(SDFR_EUNSUPPORTED, "render_siren: fused path needs depth 8, width 256");
+    if (a->field_precision != SDFR_FIELD_F16X3)
+        return fail(SDFR_EUNSUPPORTED, "render_siren: only field_precision 0 (f16x3)");
+    if (a->B == 0 || a->H == 0 || a->W == 0 || a->N == 0)
+        return fail(SDFR_EINVAL, "render_siren: empty batch / image / sample count");
+    if (!a->cam || !a->focal || !a->near_ || !a->far_ || !a->styles || !a->pix_x ||
+        !a->pix_y || !a->t_vals || !a->rgb || !a->workspace)
+        return fail(SDFR_EINVAL, "render_siren: required pointer is null");
+    for (int l = 0; l < 8; ++l)
+        if (!w->pts_w[l] || !w->pts_b[l] || !w->pts_gw[l] || !w->pts_gb[l] || !w->pts_bw[l] ||
+            !w->pts_bb[l])
+            return fail(SDFR_EINVAL, "render_siren: FiLM weight pointer is null");
+    const void *need[] = {w->views_w, w->views_b, w->views_gw, w->views_gb, w->views_bw,
+                          w->views_bb, w->sigma_w, w->sigma_b, w->rgb_w, w->rgb_b};
+    for (const void *p : need)
+        if (!p) return fail(SDFR_EINVAL, "render_siren: weight pointer is null");
+    if (a->with_sdf && !w->sigmoid_beta)
+        return fail(SDFR_EINVAL, "render_siren: sigmoid_beta is required when with_sdf");
+    if (a->workspace_bytes < siren_ws_layout(a->B, nullptr))
+        return fail(SDFR_EINVAL, "render_siren: workspace too small");
+    return SDFR_OK;
 }
 
 }  // namespace sdfr
+
+using namespace sdfr;
+
+extern "C" {
+
+size_t sdfr_render_siren_workspace_bytes(uint32_t B) { return siren_ws_layout(B, nullptr); }
+
+int sdfr_render_siren_forward(const sdfr_siren_weights *w, const sdfr_ngp_render_args *a,
+                              void *stream) {
+    int rc = siren_validate(w, a);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    size_t o_x;
+    siren_ws_layout(a->B, &o_x);
+    char *ws = reinterpret_cast<char *>(a->workspace);
+    float *film = reinterpret_cast<float *>(ws);
+    NetPtrs P{};
+    for (int l = 0; l < 8; ++l) {
+        P.w[l] = w->pts_w[l];
+        P.b[l] = w->pts_b[l];
+        P.gw[l] = w->pts_gw[l];
+        P.gb[l] = w->pts_gb[l];
+        P.bw[l] = w->pts_bw[l];
+        P.bb[l] = w->pts_bb[l];
+    }
+    P.w[8] = w->views_w;
+    P.b[8] = w->views_b;
+    P.gw[8] = w->views_gw;
+    P.gb[8] = w->views_gb;
+    P.bw[8] = w->views_bw;
+    P.bb[8] = w->views_bb;
+    P.sigma_w = w->sigma_w;
+    P.sigma_b = w->sigma_b;
+    P.rgb_w = w->rgb_w;
+    P.rgb_b = w->rgb_b;
+    P.sigmoid_beta = w->sigmoid_beta;
+    GeomArgs g;
+    fill_geom_args(a, 1.0f, g);
+    record_event(a->stage_events[0], st);
+    if ((rc = launch_xprep<SirenNet>(P, a, ws + o_x, film, st))) return rc;
+    record_event(a->stage_events[1], st);
+    record_event(a->stage_events[2], st);
+    if ((rc = launch_xfield<SirenNet>(P, a, g, nullptr, ws + o_x, film, st))) return rc;
+    record_event(a->stage_events[3], st);
+    return SDFR_OK;
+}
+
+}  // extern "C"

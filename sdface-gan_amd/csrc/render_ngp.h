@@ -113,12 +113,16 @@ __device__ __forceinline__ float group_sum(float v) {
 }
 
 // Split-fp16 field path (field_f16x3.hip).  Its workspace region (`xws`,
-// f16x3_ws_bytes()) holds the packed fp16 fragments, row scales and scaled biases.
-size_t f16x3_ws_bytes(uint32_t B);
+// f16x3_ws_bytes(net): 0 = ngp, 1 = siren) holds the packed fp16 fragments, row
+// scales and scaled biases.
+size_t f16x3_ws_bytes(int net);
 int field_variant();   // profiling ablation selected by sdfr_debug_set_field_variant
-int launch_xprep(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, char *xws,
-                 float *film, hipStream_t st);
-int launch_xfield(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, const GeomArgs &g,
-                  const float *enc, char *xws, const float *film, hipStream_t st);
+int launch_xprep_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, char *xws,
+                     float *film, hipStream_t st);
+int launch_xfield_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
+                      const GeomArgs &g, const float *enc, char *xws, const float *film,
+                      hipStream_t st);
+void fill_geom_args(const sdfr_ngp_render_args *a, float bound, GeomArgs &g);
+void record_event(void *ev, hipStream_t st);
 
 }  // namespace sdfr

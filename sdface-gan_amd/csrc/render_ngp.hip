@@ -569,7 +569,7 @@ static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t
     *o_film = off;
     off += align256((size_t)B * kFilm * 2 * kW * sizeof(float));
     if (o_x) *o_x = off;
-    off += align256(f16x3_ws_bytes(B));
+    off += align256(f16x3_ws_bytes(0));
     return off;
 }
 
@@ -605,6 +605,10 @@ static int validate(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a) {
 }
 
 static void fill_geom(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, GeomArgs &g) {
+    fill_geom_args(a, w->bound, g);
+}
+
+void fill_geom_args(const sdfr_ngp_render_args *a, float bound, GeomArgs &g) {
     g.B = a->B;
     g.H = a->H;
     g.W = a->W;
@@ -626,7 +630,11 @@ static void fill_geom(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, 
     g.sc.N = a->N;
     g.static_viewdirs = a->static_viewdirs;
     g.z_normalize = a->z_normalize;
-    g.bound = w->bound;
+    g.bound = bound;
+}
+
+void record_event(void *ev, hipStream_t st) {
+    if (ev) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev), st);
 }
 
 static int g_field_variant = 0;   // profiling ablations only (see ABL_*)
@@ -653,9 +661,6 @@ static void launch_field(int v, dim3 grid, hipStream_t st, const FieldArgs &f) {
     }
 }
 
-static void record_event(void *ev, hipStream_t st) {
-    if (ev) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev), st);
-}
 
 static int launch_prep(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, f4 *packed,
                        float *film, hipStream_t st) {
@@ -757,11 +762,11 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     fill_geom(w, a, g);
     record_event(a->stage_events[0], st);
     if (a->field_precision == SDFR_FIELD_F16X3) {
-        if ((rc = launch_xprep(w, a, ws + o_x, film, st))) return rc;
+        if ((rc = launch_xprep_ngp(w, a, ws + o_x, film, st))) return rc;
         record_event(a->stage_events[1], st);
         if ((rc = launch_encode(w, a, g, enc, st))) return rc;
         record_event(a->stage_events[2], st);
-        if ((rc = launch_xfield(w, a, g, enc, ws + o_x, film, st))) return rc;
+        if ((rc = launch_xfield_ngp(w, a, g, enc, ws + o_x, film, st))) return rc;
         record_event(a->stage_events[3], st);
         return SDFR_OK;
     }

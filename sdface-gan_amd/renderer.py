@@ -437,7 +437,13 @@ class VolumeFeatureRenderer(nn.Module):
 
     # ---------------------------------------------------------------- fused HIP path
     def _fused_ok(self, cam_poses, styles, return_eikonal):
-        if not (self.use_fused and isinstance(self.network, NGPSIRENGenerator)):
+        if not self.use_fused:
+            return False
+        siren = isinstance(self.network, SirenGenerator)
+        if not (isinstance(self.network, NGPSIRENGenerator) or siren):
+            return False
+        if siren and (self.field_precision != "f16x3" or self.network.D != 8 or
+                      len(self.network.pts_linears) != 8):
             return False
         if return_eikonal or not cam_poses.is_cuda or styles is None:
             return False
@@ -472,9 +478,31 @@ class VolumeFeatureRenderer(nn.Module):
         w.sigmoid_beta = P(self.sigmoid_beta) if self.with_sdf else None
         return w
 
+    def _siren_weight_struct(self):
+        net = self.network
+        P = lambda t: _lib.ptr(t)  # noqa: E731
+        w = _lib.SirenWeights()
+        w.depth, w.width = net.D, net.W
+        for l, layer in enumerate(net.pts_linears):
+            w.pts_w[l], w.pts_b[l] = P(layer.weight), P(layer.bias)
+            w.pts_gw[l], w.pts_gb[l] = P(layer.gamma.weight), P(layer.gamma.bias)
+            w.pts_bw[l], w.pts_bb[l] = P(layer.beta.weight), P(layer.beta.bias)
+        v = net.views_linears
+        w.views_w, w.views_b = P(v.weight), P(v.bias)
+        w.views_gw, w.views_gb = P(v.gamma.weight), P(v.gamma.bias)
+        w.views_bw, w.views_bb = P(v.beta.weight), P(v.beta.bias)
+        w.sigma_w, w.sigma_b = P(net.sigma_linear.weight), P(net.sigma_linear.bias)
+        w.rgb_w, w.rgb_b = P(net.rgb_linear.weight), P(net.rgb_linear.bias)
+        w.sigmoid_beta = P(self.sigmoid_beta) if self.with_sdf else None
+        return w
+
     def _fused_check_params(self):
         net = self.network
-        if len(net.pts_linears) != 3 or net.encoder.num_levels != 16 or \
+        if isinstance(net, SirenGenerator):
+            if net.D != 8 or net.W != 256 or net.input_ch_views != 3:
+                raise RuntimeError("fused siren renderer supports the SDFace SirenGenerator "
+                                   "(D=8, W=256) only")
+        elif len(net.pts_linears) != 3 or net.encoder.num_levels != 16 or \
                 net.encoder.level_dim != 2 or net.encoder_dir.degree != 4:
             raise RuntimeError("fused ngp renderer supports the SDFace NGPSIRENGenerator only")
         for p in self.parameters():
@@ -511,8 +539,12 @@ class VolumeFeatureRenderer(nn.Module):
         sdf = torch.empty(B, H, W, N, 1, device=dev) if self.return_sdf else None
         xyz = torch.empty(B, 3, H, W, device=dev) if self.return_xyz else None
         mask = torch.empty(B, 1, H, W, device=dev) if self.return_xyz else None
-        L = self.network.encoder.num_levels
-        ws_bytes = _lib.lib().sdfr_render_ngp_workspace_bytes(B, H, W, N, L)
+        siren = isinstance(self.network, SirenGenerator)
+        if siren:
+            ws_bytes = _lib.lib().sdfr_render_siren_workspace_bytes(B)
+        else:
+            L = self.network.encoder.num_levels
+            ws_bytes = _lib.lib().sdfr_render_ngp_workspace_bytes(B, H, W, N, L)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         pix_x = self.i[0, 0, :].contiguous()
         pix_y = self.j[0, :, 0].contiguous()
@@ -541,6 +573,14 @@ class VolumeFeatureRenderer(nn.Module):
         if self.stage_events is not None:
             for k, ev in enumerate(self.stage_events):
                 a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)
+        if siren:
+            if encode_only:
+                raise RuntimeError("the siren renderer has no hash-grid encode stage")
+            w = self._siren_weight_struct()
+            _lib.check(_lib.lib().sdfr_render_siren_forward(ctypes.byref(w), ctypes.byref(a),
+                                                            _lib.stream_of(cam)),
+                       "sdfr_render_siren_forward")
+            return rgb, features, sdf, mask, xyz, None
         w = self._ngp_weight_struct()
         fn = (_lib.lib().sdfr_render_ngp_encode_only if encode_only
               else _lib.lib().sdfr_render_ngp_forward)

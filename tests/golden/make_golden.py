@@ -323,6 +323,22 @@ def case_mesh(sdf_model, sdf_utils):
     print("mesh128.npz", sdf.shape, aligned.shape)
 
 
+def case_siren(sdf_model, sdf_utils):
+    """rendering.type == 'sdf' (SirenGenerator, 100 % reference code on CPU)."""
+    case_render(sdf_model, sdf_utils, "render_siren_small", B=2, res=8, n_samples=24,
+                intermediates=False, seed=61, type="sdf")
+    case_render(sdf_model, sdf_utils, "render_siren_mesh_opts", B=1, res=8, n_samples=32,
+                intermediates=False, seed=71, type="sdf", static_viewdirs=True,
+                force_background=True, perturb=0, return_sdf=True, return_xyz=True)
+    case_render(sdf_model, sdf_utils, "render_siren_face32", B=1, res=32, n_samples=24,
+                intermediates=False, seed=81, type="sdf", return_sdf=True, return_xyz=True)
+    g, _ = _generator(sdf_model, sdf_utils, res=8, n_samples=24, full_pipeline=False, type="sdf")
+    sd = g.state_dict()
+    shapes = np.array([repr((k, tuple(sd[k].shape))) for k in sorted(sd)])
+    np.savez_compressed(OUT / "state_dict_keys_siren.npz", entries=shapes)
+    print("state_dict_keys_siren.npz", len(shapes), "keys")
+
+
 def case_generator(sdf_model, sdf_utils):
     g, opt = _generator(sdf_model, sdf_utils, size=256, res=64, n_samples=24)
     ext, focal, near, far, vp = _cams(sdf_utils, 1, 64, 31)
@@ -390,6 +406,8 @@ def main():
     case_render(sdf_model, sdf_utils, "render_face64", B=1, res=64, n_samples=24,
                 intermediates=False, seed=41, return_sdf=True, return_xyz=True)
     case_generator(sdf_model, sdf_utils)
+    case_mesh(sdf_model, sdf_utils)
+    case_siren(sdf_model, sdf_utils)
 
 
 if __name__ == "__main__":

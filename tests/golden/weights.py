@@ -47,8 +47,8 @@ def init_range(name: str, shape):
             return _u(0.25 * KAIMING_LRELU_STD / math.sqrt(fan_in))
         if name.endswith("gamma.bias") or name.endswith("beta.bias"):
             return (-1 / 16, 1 / 16)
-        if name.endswith("pts_linears.0.weight") and shape[-1] == 256:
-            return (-1 / 3, 1 / 3)
+        if name.endswith("pts_linears.0.weight") and shape[-1] in (256, 3):
+            return (-1 / 3, 1 / 3)          # FiLMSiren(is_first=True), ngp and siren
         if name.endswith(".weight"):
             a = math.sqrt(6 / fan_in) / 25
             return (-a, a)
@@ -123,7 +123,9 @@ def det_state_dict(entries, prefix=""):
     return sd
 
 
-def golden_entries(golden_dir):
+def golden_entries(golden_dir, siren=False):
+    """(name, shape) of the reference Generator's state dict: the ngp one, or with
+    siren=True the SirenGenerator renderer's (full_pipeline=False)."""
     import ast
-    z = np.load(golden_dir / "state_dict_keys.npz")
+    z = np.load(golden_dir / ("state_dict_keys_siren.npz" if siren else "state_dict_keys.npz"))
     return [ast.literal_eval(str(e)) for e in z["entries"]]

@@ -249,3 +249,94 @@ def test_batch_consistency(sdfr, renderer_sd, prec):
                       styles=lat[b:b + 1], t_rand=tr[b:b + 1])
             assert torch.equal(one[0], full[0][b:b + 1])
             assert torch.equal(one[1], full[1][b:b + 1])
+
+
+# ---------------------------------------------------------------- SIREN (type "sdf")
+@pytest.fixture(scope="module")
+def siren_sd(golden_dir):
+    return W.det_state_dict(W.golden_entries(golden_dir, siren=True), "renderer.")
+
+
+def make_siren(sdfr, sd, res, N, **flags):
+    opt = sdfr.vol_render_opt(ngp=False)
+    r = opt.rendering
+    r.N_samples = N
+    for k, v in flags.items():
+        r[k] = v
+    ren = sdfr.VolumeFeatureRenderer(r, style_dim=256, out_im_res=res)
+    own = ren.state_dict()
+    ren.load_state_dict({k[len("renderer."):]: v for k, v in sd.items()
+                         if k[len("renderer."):] in own}, strict=True)
+    return ren.to(DEV).eval()
+
+
+SIREN_CASES = [
+    ("render_siren_small", {}),
+    ("render_siren_mesh_opts", dict(static_viewdirs=True, force_background=True, perturb=0,
+                                    return_sdf=True, return_xyz=True)),
+    ("render_siren_face32", dict(return_sdf=True, return_xyz=True)),
+]
+
+
+@pytest.mark.parametrize("name,flags", SIREN_CASES)
+def test_fused_siren_vs_reference_golden(sdfr, golden_dir, siren_sd, name, flags):
+    """The fused SIREN kernel (sdfr_render_siren_forward) against the reference's
+    own SirenGenerator renderer on the same inputs."""
+    g = np.load(golden_dir / f"{name}.npz")
+    ren = make_siren(sdfr, siren_sd, int(g["res"]), int(g["n_samples"]), **flags)
+    cam, focal, near, far, lat, tr = _inputs(g)
+    with torch.no_grad():
+        assert ren._fused_ok(cam, lat, False)
+        rgb, feat, sdf, mask, xyz, eik = ren(cam, focal, near, far, styles=lat, t_rand=tr)
+    torch.cuda.synchronize()
+    _cmp(name, "rgb", rgb.cpu().numpy(), g["rgb"])
+    _cmp(name, "features", feat.cpu().numpy(), g["features"])
+    if "sdf" in g.files:
+        _cmp(name, "sdf", sdf.cpu().numpy(), g["sdf"])
+        _cmp(name, "xyz", xyz.cpu().numpy(), g["xyz"])
+        _cmp(name, "mask", mask.cpu().numpy(), g["mask"])
+
+
+@pytest.mark.parametrize("B,res,N,flags", [
+    (3, 10, 7, {}),                                        # ragged tiles, odd N
+    (2, 8, 24, dict(no_offset_sampling=True)),
+    (2, 8, 24, dict(no_z_normalize=True, return_xyz=True)),
+    (2, 8, 16, dict(no_sdf=True)),
+])
+def test_fused_siren_vs_oracle(sdfr, oracle_mod, siren_sd, B, res, N, flags):
+    ren = make_siren(sdfr, siren_sd, res, N, **flags)
+    torch.manual_seed(B * 100 + res + N + 1)
+    ext, focal, near, far, _ = sdfr.generate_camera_params(res, "cpu", batch=B)
+    lat = torch.from_numpy(W.det_uniform((B, 256), -1.5, 1.5, 9 + N))
+    tr = torch.rand((B, res, res, N) if flags.get("no_offset_sampling") else (B, res, res))
+    with torch.no_grad():
+        rgb, feat, sdf, mask, xyz, _ = ren(ext.to(DEV), focal.to(DEV), near.to(DEV),
+                                           far.to(DEV), styles=lat.to(DEV), t_rand=tr)
+    torch.cuda.synchronize()
+    o = oracle_mod.render_siren(
+        siren_sd, ext.numpy(), focal.numpy(), near.numpy(), far.numpy(), lat.numpy(), N=N,
+        res=res, t_rand=tr.numpy(), offset_sampling=not flags.get("no_offset_sampling", False),
+        z_normalize=not flags.get("no_z_normalize", False),
+        with_sdf=not flags.get("no_sdf", False))
+    name = f"siren_oracle_B{B}_r{res}_N{N}_{'_'.join(flags) or 'default'}"
+    _cmp(name, "rgb", rgb.cpu().numpy(), o["rgb"].numpy())
+    _cmp(name, "features", feat.cpu().numpy(), o["features"].numpy())
+    if xyz is not None:
+        _cmp(name, "xyz", xyz.cpu().numpy(), o["xyz"].numpy())
+        _cmp(name, "mask", mask.cpu().numpy(), o["mask"].numpy())
+
+
+def test_siren_fused_equals_module_path(sdfr, siren_sd):
+    """Fused kernel vs. the op-by-op PyTorch-ROCm SirenGenerator on the same GPU
+    inputs (module-path bound: torch-ROCm's own GEMM / sin rounding)."""
+    ren = make_siren(sdfr, siren_sd, 16, 24)
+    torch.manual_seed(12)
+    ext, focal, near, far, _ = sdfr.generate_camera_params(16, DEV, batch=2)
+    lat = torch.from_numpy(W.det_uniform((2, 256), -1, 1, 12)).to(DEV)
+    tr = torch.rand(2, 16, 16)
+    with torch.no_grad():
+        f = ren(ext, focal, near, far, styles=lat, t_rand=tr)
+        ren.use_fused = False
+        u = ren(ext, focal, near, far, styles=lat, t_rand=tr)
+    _cmp("siren_module", "rgb", f[0].cpu().numpy(), u[0].cpu().numpy(), "module_rgb")
+    _cmp("siren_module", "features", f[1].cpu().numpy(), u[1].cpu().numpy(), "module_features")

@@ -66,6 +66,13 @@ def test_state_dict_matches_reference(sdfr, golden_dir):
     assert mine == ref
 
 
+def test_siren_state_dict_matches_reference(sdfr, golden_dir):
+    opt = sdfr.vol_render_opt(ngp=False)
+    g = sdfr.Generator(opt.model, opt.rendering, full_pipeline=False)
+    mine = {k: tuple(v.shape) for k, v in g.state_dict().items()}
+    assert mine == dict(W.golden_entries(golden_dir, siren=True))
+
+
 def test_seeded_init_identical_to_reference(sdfr, golden_dir):
     z = np.load(golden_dir / "init_stats.npz")
     opt = sdfr.vol_render_opt()

@@ -165,6 +165,25 @@ def test_renderer_restatement_matches_reference(oracle_mod, golden_dir, name, kw
                                       _grid_ref(oracle_mod, g["grid_in"]))
 
 
+@pytest.mark.parametrize("name,kw", [
+    ("render_siren_small", {}),
+    ("render_siren_mesh_opts", dict(static_viewdirs=True, force_background=True)),
+    ("render_siren_face32", {}),
+])
+def test_siren_restatement_matches_reference(oracle_mod, golden_dir, name, kw):
+    """oracle.render_siren (the CPU checker of the fused SIREN kernel) against the
+    reference's own SirenGenerator renderer on the same inputs."""
+    g = np.load(golden_dir / f"{name}.npz")
+    sd = W.det_state_dict(W.golden_entries(golden_dir, siren=True), "renderer.")
+    tr = g["t_rand"] if g["t_rand"].size else None
+    out = oracle_mod.render_siren(sd, g["ext"], g["focal"], g["near"], g["far"], g["latent"],
+                                  N=int(g["n_samples"]), res=int(g["res"]), t_rand=tr, **kw)
+    for k in ["rgb", "features", "sdf", "xyz", "mask"]:
+        if k in g.files:
+            a = out[k].numpy().reshape(g[k].shape)
+            np.testing.assert_allclose(a, g[k], rtol=0, atol=2e-7, err_msg=k)
+
+
 def _grid_ref(oracle_mod, grid_in):
     offsets, pls = oracle_mod.grid_offsets()
     emb = W.det_table(int(offsets[-1]), 2, seed=7)
