@@ -22,6 +22,7 @@ from .generator import (Blur, Decoder, EqualLinear, FusedLeakyReLU, Generator,  
                         ToRGB, Upsample, fused_leaky_relu, make_kernel, upfirdn2d)
 from .mesh import align_volume, extract_mesh_with_marching_cubes, xyz2mesh  # noqa: F401
 from .options import AttrDict, SDFOptions, vol_render_opt  # noqa: F401
+from . import training  # noqa: F401  (stage-2 DDP trainer, Discriminator, losses)
 from .renderer import (FCGenerator, FiLMSiren, LinearLayer, NGPSIRENGenerator,  # noqa: F401
                        SirenGenerator, VolumeFeatureRenderer, get_encoder)
 
