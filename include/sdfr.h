@@ -277,6 +277,27 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *a, void *stream);
 int sdfr_modulate_to_nhwc(float *y, const float *x, const float *s, uint32_t B, uint32_t C,
                           uint32_t HW, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Decoder 3x3 convolutions on split-fp16 MFMA (no reference counterpart: they
+ * replace the MIOpen convolutions of ModulatedConv2d on the fused decoder path,
+ * sdf_model.py:676-699, batched form conv(x * s, w) * demod).
+ *
+ * sdfr_conv_pack_weights: w [Cout][Cin][3][3] (ModulatedConv2d.weight[0]) times
+ *   scale -> su [Cout] (per-row power-of-two scale, written) and the packed hi/lo
+ *   fp16 fragments (sdfr_conv_pack_bytes(Cout, Cin) - 4*Cout bytes).
+ * sdfr_conv3x3_f16x3: NHWC fp32 in, NHWC fp32 out, result multiplied by su[o]
+ *   (the caller folds 1/su into the demodulation -- exact, powers of two):
+ *   transposed = 0: out [B,H,W,Cout] = conv2d(x, w, padding 1);
+ *   transposed = 1: out [B,2H+1,2W+1,Cout] = conv_transpose2d(x, w^T, stride 2)
+ *   (x [B,H,W,Cin]).  Cout % 128 == 0, Cin % 32 == 0.
+ * ------------------------------------------------------------------------- */
+size_t sdfr_conv_pack_bytes(uint32_t Cout, uint32_t Cin);
+int sdfr_conv_pack_weights(const float *w, float scale, uint32_t Cout, uint32_t Cin,
+                           void *packed, float *su, void *stream);
+int sdfr_conv3x3_f16x3(float *out, const float *x, const void *packed, uint32_t B,
+                       uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
+                       int transposed, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

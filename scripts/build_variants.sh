@@ -4,7 +4,7 @@
 #   scripts/build_variants.sh name1 "-DFOO=1" name2 "-DFOO=0 -DBAR=1" ...
 set -eu
 cd "$(dirname "$0")/../sdface-gan_amd"
-make -s build/encoders.o build/render_ngp.o build/decoder.o
+make -s build/encoders.o build/render_ngp.o build/decoder.o build/conv_f16x3.o
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall"
 pids=()
 while [ $# -ge 2 ]; do
@@ -12,7 +12,7 @@ while [ $# -ge 2 ]; do
   mkdir -p lib_var/$name
   ( /opt/rocm/bin/hipcc $FLAGS $defs -c csrc/field_f16x3.hip -o lib_var/$name/field_f16x3.o &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib_var/$name/libsdfr.so \
-        build/encoders.o build/render_ngp.o lib_var/$name/field_f16x3.o build/decoder.o &&
+        build/encoders.o build/render_ngp.o lib_var/$name/field_f16x3.o build/decoder.o build/conv_f16x3.o &&
     echo "built $name ($defs)" ) &
   pids+=($!)
 done

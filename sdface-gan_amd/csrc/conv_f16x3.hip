@@ -1,0 +1,320 @@
+// conv_f16x3.hip -- the StyleGAN2 decoder's 3x3 convolutions on split-fp16 MFMA.
+//
+// Replaces the two convolution forms of ModulatedConv2d on the fused decoder
+// path (sdf_model.py:676-699, applied as conv(x * s, w) * demod -- the batched
+// form of the reference's per-face modulated weights, see generator.py):
+//   regular     out[b,y,x,o]   = sum_{i,ky,kx} x[b,y+ky-1,x+kx-1,i] w[o,i,ky,kx]   (pad 1)
+//   transposed  out[b,2a+ky,2c+kx,o] += x[b,a,c,i] w[o,i,ky,kx]   (conv_transpose2d,
+//               stride 2, output (2H+1) x (2W+1), before the upsampling blur)
+// as implicit GEMMs over NHWC activations: M = output channels (A = weights),
+// N = output pixels (B = activations), K = input channels x taps.  Every fp32
+// tile product is W_hi.x_hi + W_hi.x_lo + W_lo.x_hi on v_mfma_f32_16x16x32_f16
+// with fp32 accumulation (the field kernel's scheme):
+// 5.3x the fp32 MFMA rate at fp32-level accuracy.  Weights are row-scaled by a
+// power of two su[o] so their fp16 lo parts stay normal; the caller folds 1/su
+// into the demodulation (exact).  A transposed conv is four implicit GEMMs, one
+// per output parity class (oy & 1, ox & 1), each over its own tap subset.
+//
+// Workgroup: 128 output channels x 128 output pixels, 4 waves of 64 x 64, K in
+// steps of 32 input channels at one tap; weight fragments (pre-packed hi/lo)
+// and activations (fp32 -> hi/lo split while staging) are double-buffered in
+// 64 KB of LDS, one barrier per K-step; two workgroups per CU.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "sdfr_common.h"
+
+namespace sdfr {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCT = 128;        // output channels per workgroup
+constexpr int kPT = 128;        // output pixels per workgroup
+constexpr int kStepF4 = 1024;   // f4 per operand per K-step (16 KB)
+
+__device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a),
+                                                  __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
+
+// ----------------------------------------------------------------------------
+// weight packing: w [Cout][Cin][3][3] * scale -> su [Cout], fragments
+// [tap 9][Cin/32][Cout/128][8 m-tiles][hi, lo][64 lanes] fp16x8, lane (m, g)
+// holding w[o = 16 mt + m][i = 32 c + 8 g + j][tap], j = 0..7
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) conv_scale_kernel(const float *__restrict__ w, float scale,
+                                                         uint32_t Cin, float *__restrict__ su) {
+    const uint32_t o = blockIdx.x;
+    float m = 0.0f;
+    for (uint32_t k = threadIdx.x; k < Cin * 9; k += 256)
+        m = fmaxf(m, fabsf(__fmul_rn(w[(size_t)o * Cin * 9 + k], scale)));
+    __shared__ float red[256];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (uint32_t s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        float v = 1.0f;
+        const float mx = red[0];
+        if (mx > 0.0f && mx < 3.0e38f) {
+            int ex;
+            (void)frexpf(mx, &ex);
+            ex = ex < -100 ? -100 : (ex > 100 ? 100 : ex);
+            v = ldexpf(1.0f, -ex);
+        }
+        su[o] = v;
+    }
+}
+
+__global__ void __launch_bounds__(256) conv_pack_kernel(const float *__restrict__ w, float scale,
+                                                        uint32_t Cin, uint32_t Cout,
+                                                        const float *__restrict__ su,
+                                                        f4 *__restrict__ packed) {
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;        // one (tap, c, cb, mt, lane)
+    const uint32_t nC = Cin / 32, nB = Cout / kCT;
+    const uint32_t total = 9 * nC * nB * 8 * 64;
+    if (e >= total) return;
+    const uint32_t lane = e & 63, mt = (e >> 6) & 7;
+    uint32_t r = e >> 9;
+    const uint32_t cb = r % nB;
+    r /= nB;
+    const uint32_t c = r % nC, tap = r / nC;
+    const uint32_t o = cb * kCT + mt * 16 + (lane & 15), g = lane >> 4;
+    const float s = su[o];
+    h8 H, L;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t i = c * 32 + 8 * g + j;
+        const float v = __fmul_rn(__fmul_rn(w[((size_t)o * Cin + i) * 9 + tap], scale), s);
+        H[j] = (_Float16)v;
+        L[j] = (_Float16)__fsub_rn(v, (float)H[j]);
+    }
+    f4 *dst = packed + ((size_t)(e >> 6) * 2) * 64 + lane;   // [.. mt][hi,lo][lane]
+    dst[0] = __builtin_bit_cast(f4, H);
+    dst[64] = __builtin_bit_cast(f4, L);
+}
+
+// ----------------------------------------------------------------------------
+// implicit GEMM
+// ----------------------------------------------------------------------------
+struct ConvArgs {
+    const float *x;                // [B, Hin, Win, Cin]
+    const f4 *wpk;                 // packed fragments (above)
+    float *out;                    // [B, Hf, Wf, Cout]
+    uint32_t B, Hin, Win, Cin, Cout;
+    uint32_t Hc, Wc;               // this launch's output grid
+    uint32_t Hf, Wf;               // full output image
+    uint32_t sy, py, px;           // output pixel (a, c) -> (sy a + py, sy c + px)
+    uint32_t ntaps;
+    int dy[9], dx[9];              // input pixel = (a + dy, c + dx)
+    uint32_t tap[9];               // packed weight tap (3 ky + kx)
+};
+
+__global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
+    __shared__ f4 As[2][kStepF4];   // [mt 8][hi,lo][64]
+    __shared__ f4 Bs[2][kStepF4];   // [nt 8][hi,lo][64]
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t wm = wave & 1u, wn = wave >> 1;
+    const uint32_t cb = blockIdx.y;
+    const uint32_t npix = a.B * a.Hc * a.Wc;
+    const uint32_t pix0 = blockIdx.x * kPT;
+    const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT;
+    const uint32_t nk = nC * a.ntaps;
+
+    // staging pixels of this thread: pl = (tid >> 3) + 32 i, channels 4 (tid & 7) .. +3
+    const uint32_t q = tid & 7u;
+    int sb[4], sa[4], sc[4];
+    bool sv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t P = pix0 + (tid >> 3) + 32 * i;
+        sv[i] = P < npix;
+        const uint32_t Pc = sv[i] ? P : 0;
+        const uint32_t hw = a.Hc * a.Wc;
+        sb[i] = (int)(Pc / hw);
+        const uint32_t rem = Pc % hw;
+        sa[i] = (int)(rem / a.Wc);
+        sc[i] = (int)(rem % a.Wc);
+    }
+    // B-fragment slot of this thread's 4 channels: n-tile, lane (g, n), half
+    const uint32_t g_b = q >> 1, half = q & 1u;
+
+    f4 wst[4], xst[4];
+    auto load_step = [&](uint32_t ks) {
+        const uint32_t c = ks / a.ntaps, t = ks % a.ntaps;
+        const f4 *wsrc = a.wpk + ((size_t)(a.tap[t] * nC + c) * nB + cb) * kStepF4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wst[i] = wsrc[tid + 256 * i];
+        const int dy = a.dy[t], dx = a.dx[t];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int iy = sa[i] + dy, ix = sc[i] + dx;
+            const bool ok = sv[i] && iy >= 0 && iy < (int)a.Hin && ix >= 0 && ix < (int)a.Win;
+            f4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (ok)
+                v = *reinterpret_cast<const f4 *>(
+                    a.x + (((size_t)sb[i] * a.Hin + iy) * a.Win + ix) * a.Cin + c * 32 + 4 * q);
+            xst[i] = v;
+        }
+    };
+    auto store_step = [&](uint32_t buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) As[buf][tid + 256 * i] = wst[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            h4 hv, lv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                hv[r] = (_Float16)xst[i][r];
+                lv[r] = (_Float16)__fsub_rn(xst[i][r], (float)hv[r]);
+            }
+            const uint32_t pl = (tid >> 3) + 32 * i;
+            const uint32_t nt = pl >> 4, n = pl & 15u;
+            const uint32_t l = g_b * 16 + n;
+            char *base = reinterpret_cast<char *>(&Bs[buf][(nt * 2) * 64 + l]) + half * 8;
+            *reinterpret_cast<h4 *>(base) = hv;
+            *reinterpret_cast<h4 *>(base + 64 * sizeof(f4)) = lv;
+        }
+    };
+
+    f4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    load_step(0);
+    store_step(0);
+    __syncthreads();
+    for (uint32_t ks = 0; ks < nk; ++ks) {
+        const uint32_t buf = ks & 1u;
+        if (ks + 1 < nk) load_step(ks + 1);
+        f4 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ah[i] = As[buf][((4 * wm + i) * 2) * 64 + lane];
+            al[i] = As[buf][((4 * wm + i) * 2 + 1) * 64 + lane];
+            bh[i] = Bs[buf][((4 * wn + i) * 2) * 64 + lane];
+            bl[i] = Bs[buf][((4 * wn + i) * 2 + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[i][j] = mfma16(al[i], bh[j], acc[i][j]);
+                acc[i][j] = mfma16(ah[i], bl[j], acc[i][j]);
+                acc[i][j] = mfma16(ah[i], bh[j], acc[i][j]);
+            }
+        if (ks + 1 < nk) store_step(buf ^ 1u);
+        __syncthreads();
+    }
+
+    // epilogue: lane (n, g) of tile (i, j) holds channels 16 mt + 4 g .. +3 of pixel 16 nt + n
+    const uint32_t n = lane & 15u, g = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t P = pix0 + (4 * wn + j) * 16 + n;
+        if (P >= npix) continue;
+        const uint32_t hw = a.Hc * a.Wc;
+        const uint32_t b = P / hw, rem = P % hw;
+        const uint32_t oy = a.sy * (rem / a.Wc) + a.py, ox = a.sy * (rem % a.Wc) + a.px;
+        float *dst = a.out + (((size_t)b * a.Hf + oy) * a.Wf + ox) * a.Cout + cb * kCT + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<f4 *>(dst + (4 * wm + i) * 16) = acc[i][j];
+    }
+}
+
+}  // namespace
+}  // namespace sdfr
+
+using namespace sdfr;
+
+extern "C" {
+
+size_t sdfr_conv_pack_bytes(uint32_t Cout, uint32_t Cin) {
+    return (size_t)9 * Cin * Cout * 2 * sizeof(_Float16) + (size_t)Cout * sizeof(float);
+}
+
+int sdfr_conv_pack_weights(const float *w, float scale, uint32_t Cout, uint32_t Cin,
+                           void *packed, float *su, void *stream) {
+    if (!w || !packed || !su) return fail(SDFR_EINVAL, "conv_pack_weights: null pointer");
+    if (Cout == 0 || Cout % kCT || Cin == 0 || Cin % 32)
+        return fail(SDFR_EINVAL, "conv_pack_weights: Cout % 128 and Cin % 32 must be 0");
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(conv_scale_kernel, dim3(Cout), dim3(256), 0, st, w, scale, Cin, su);
+    int rc = check_launch("conv_pack_weights: scale");
+    if (rc) return rc;
+    const uint32_t total = 9 * (Cin / 32) * (Cout / kCT) * 8 * 64;
+    hipLaunchKernelGGL(conv_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, scale,
+                       Cin, Cout, su, reinterpret_cast<f4 *>(packed));
+    return check_launch("conv_pack_weights: pack");
+}
+
+int sdfr_conv3x3_f16x3(float *out, const float *x, const void *packed, uint32_t B, uint32_t H,
+                       uint32_t W, uint32_t Cin, uint32_t Cout, int transposed, void *stream) {
+    if (!out || !x || !packed) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
+    if (B == 0 || H == 0 || W == 0 || Cout % kCT || Cin % 32 || Cin == 0 || Cout == 0)
+        return fail(SDFR_EINVAL, "conv3x3_f16x3: bad shape (Cout % 128, Cin % 32)");
+    hipStream_t st = (hipStream_t)stream;
+    ConvArgs a{};
+    a.x = x;
+    a.wpk = reinterpret_cast<const f4 *>(packed);
+    a.out = out;
+    a.B = B;
+    a.Hin = H;
+    a.Win = W;
+    a.Cin = Cin;
+    a.Cout = Cout;
+    auto launch = [&]() {
+        const uint32_t npix = B * a.Hc * a.Wc;
+        hipLaunchKernelGGL(conv_x_kernel, dim3((npix + kPT - 1) / kPT, Cout / kCT), dim3(256), 0,
+                           st, a);
+        return check_launch("conv3x3_f16x3");
+    };
+    if (!transposed) {
+        a.Hc = a.Hf = H;
+        a.Wc = a.Wf = W;
+        a.sy = 1;
+        a.py = a.px = 0;
+        a.ntaps = 9;
+        for (int t = 0; t < 9; ++t) {
+            a.dy[t] = t / 3 - 1;
+            a.dx[t] = t % 3 - 1;
+            a.tap[t] = t;
+        }
+        return launch();
+    }
+    // conv_transpose2d, stride 2: out (2a + ky, 2c + kx) <- x (a, c).  Parity class
+    // (py, px): output (2a' + py, 2c' + px) takes ky in {0, 2} (py = 0, input row
+    // a' - ky/2) or ky = 1 (py = 1, input row a'), likewise for x.
+    a.Hf = 2 * H + 1;
+    a.Wf = 2 * W + 1;
+    a.sy = 2;
+    for (uint32_t py = 0; py < 2; ++py)
+        for (uint32_t px = 0; px < 2; ++px) {
+            a.py = py;
+            a.px = px;
+            a.Hc = py ? H : H + 1;
+            a.Wc = px ? W : W + 1;
+            uint32_t nt = 0;
+            for (int ky = (int)py; ky < 3; ky += 2)
+                for (int kx = (int)px; kx < 3; kx += 2) {
+                    a.dy[nt] = -(ky >> 1);
+                    a.dx[nt] = -(kx >> 1);
+                    a.tap[nt] = (uint32_t)(ky * 3 + kx);
+                    ++nt;
+                }
+            a.ntaps = nt;
+            const int rc = launch();
+            if (rc) return rc;
+        }
+    return SDFR_OK;
+}
+
+}  // extern "C"

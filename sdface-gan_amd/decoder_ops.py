@@ -294,3 +294,35 @@ def styled_epilogue(conv, *, fir, bias, noise_weight, noise=None, demod=None, bl
     a.rgb = _lib.ptr(rgb)
     _lib.check(_lib.lib().sdfr_styled_epilogue(a, _lib.stream_of(conv)), "styled_epilogue")
     return y, rgb
+
+
+# ---------------------------------------------------------------------------
+# decoder convolutions on split-fp16 MFMA (csrc/conv_f16x3.hip)
+# ---------------------------------------------------------------------------
+def conv_pack_weights(weight, scale):
+    """ModulatedConv2d weight [Cout, Cin, 3, 3] * scale -> (packed fragments, su [Cout]).
+    The convolution result comes out multiplied by su (fold 1/su into demod)."""
+    _require_cuda(weight)
+    w = weight.detach().float().contiguous()
+    Cout, Cin = w.shape[0], w.shape[1]
+    nbytes = _lib.lib().sdfr_conv_pack_bytes(Cout, Cin) - 4 * Cout
+    packed = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+    su = torch.empty(Cout, dtype=torch.float32, device=w.device)
+    _lib.check(_lib.lib().sdfr_conv_pack_weights(_lib.ptr(w), float(scale), Cout, Cin,
+                                                 _lib.ptr(packed), _lib.ptr(su),
+                                                 _lib.stream_of(w)), "conv_pack_weights")
+    return packed, su
+
+
+def conv3x3_f16x3(x, packed, Cout, transposed=False):
+    """x channels_last [B, Cin, H, W] -> channels_last [B, Cout, H, W] (conv2d, pad 1) or
+    [B, Cout, 2H+1, 2W+1] (conv_transpose2d stride 2), scaled by su (conv_pack_weights)."""
+    _require_cuda(x)
+    B, Cin, H, W = x.shape
+    x = x.contiguous(memory_format=torch.channels_last)
+    Ho, Wo = (2 * H + 1, 2 * W + 1) if transposed else (H, W)
+    out = torch.empty(B, Cout, Ho, Wo, device=x.device, memory_format=torch.channels_last)
+    _lib.check(_lib.lib().sdfr_conv3x3_f16x3(_lib.ptr(out), _lib.ptr(x), _lib.ptr(packed), B, H,
+                                             W, Cin, Cout, int(bool(transposed)),
+                                             _lib.stream_of(x)), "conv3x3_f16x3")
+    return out

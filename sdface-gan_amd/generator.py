@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .decoder_ops import conv3x3_f16x3, conv_pack_weights  # noqa: E402
 from .decoder_ops import (FusedLeakyReLU, fused_leaky_relu, modulate_to_nhwc,  # noqa: F401
                           separable_taps, styled_epilogue, upfirdn2d)
 from .renderer import VolumeFeatureRenderer
@@ -256,7 +257,11 @@ class Decoder(nn.Module):
             in_ch = out_ch
         self.n_latent = (self.log_size - self.log_in_size) * 2 + 2
         self.use_fused = True      # HIP epilogues on the inference path (GPU, no grad)
+        # convolutions of the fused path: "f16x3" (split-fp16 MFMA implicit GEMM,
+        # csrc/conv_f16x3.hip) or "miopen" (F.conv2d / conv_transpose2d, fp32)
+        self.conv_impl = "f16x3"
         self._fir = None
+        self._packs = {}
 
     def mean_latent(self, renderer_latent):
         return self.style(renderer_latent).mean(0, keepdim=True)
@@ -322,6 +327,15 @@ class Decoder(nn.Module):
             self._fir = fir if ok else False
         return self._fir is not False
 
+    def _pack(self, i, mc):
+        """Packed split-fp16 weights of layer i, rebuilt when the weight changes."""
+        key = (mc.weight.data_ptr(), mc.weight._version, mc.weight.device)
+        hit = self._packs.get(i)
+        if hit is None or hit[0] != key:
+            hit = (key,) + conv_pack_weights(mc.weight[0], mc.scale)
+            self._packs[i] = hit
+        return hit[1], hit[2]
+
     def _fused_forward(self, features, latent, noise):
         """Same computation as the module path, one MIOpen convolution plus one
         sdfr_styled_epilogue per layer on channels_last activations; each
@@ -338,12 +352,19 @@ class Decoder(nn.Module):
             w = mc.scale * mc.weight[0]
             demod = (torch.rsqrt((mods[i] * mods[i]) @ (w * w).sum([2, 3]).t() + 1e-8)
                      if mc.demodulate else None)
-            if mc.upsample:
+            if self.conv_impl == "f16x3" and mc.kernel_size == 3 and mc.demodulate and \
+                    w.shape[0] % 128 == 0 and w.shape[1] % 32 == 0:
+                packed, su = self._pack(i, mc)
+                out = conv3x3_f16x3(x, packed, w.shape[0], transposed=mc.upsample)
+                demod = demod / su            # result carries su (power of two): exact
+            elif mc.upsample:
                 out = F.conv_transpose2d(x, w.transpose(0, 1).contiguous(memory_format=cl),
                                          stride=2)
-                H, W = out.shape[2] - 1, out.shape[3] - 1
             else:
                 out = F.conv2d(x, w.contiguous(memory_format=cl), padding=mc.padding)
+            if mc.upsample:
+                H, W = out.shape[2] - 1, out.shape[3] - 1
+            else:
                 H, W = out.shape[2], out.shape[3]
             n = noise[i] if noise[i] is not None else features.new_empty(B, 1, H, W).normal_()
             last = i == len(seq) - 1

@@ -177,12 +177,48 @@ def test_modulate_to_nhwc_bit_exact(ops, C, H):
     np.testing.assert_array_equal(y.cpu().numpy(), (x * s[:, :, None, None]).numpy())
 
 
-def test_decoder_fused_equals_module_path(sdfr):
+@pytest.mark.parametrize("B,Cin,Cout,H,W,transposed", [
+    (2, 32, 128, 5, 7, False),        # ragged pixel tiles, border taps
+    (1, 256, 256, 16, 16, False),
+    (3, 64, 128, 6, 5, True),         # all four parity classes, ragged
+    (1, 512, 256, 8, 8, True),
+])
+def test_conv3x3_f16x3_vs_fp64(ops, B, Cin, Cout, H, W, transposed):
+    """Split-fp16 implicit-GEMM conv against float64; its error must be of the same
+    order as PyTorch-ROCm's own fp32 convolution of the same inputs."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(B * 7 + Cin + H)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(1, Cout, Cin, 3, 3, generator=g)
+    scale = 1 / math.sqrt(Cin * 9)
+    w32 = (scale * w[0]).float()
+    packed, su = ops.conv_pack_weights(w[0].to(DEV), scale)
+    out = ops.conv3x3_f16x3(x.to(DEV).contiguous(memory_format=torch.channels_last), packed,
+                            Cout, transposed=transposed)
+    got = (out / su.view(1, -1, 1, 1)).cpu().double()
+    if transposed:
+        ref = F.conv_transpose2d(x.double(), w32.double().transpose(0, 1), stride=2)
+        r32 = F.conv_transpose2d(x.to(DEV), w32.to(DEV).transpose(0, 1).contiguous(), stride=2)
+    else:
+        ref = F.conv2d(x.double(), w32.double(), padding=1)
+        r32 = F.conv2d(x.to(DEV), w32.to(DEV), padding=1)
+    assert got.shape == ref.shape
+    assert torch.all(su == torch.exp2(torch.round(torch.log2(su))))      # powers of two
+    e16 = float((got - ref).abs().max())
+    e32 = float((r32.cpu().double() - ref).abs().max())
+    name = f"conv_f16x3_B{B}_{Cin}x{Cout}_{H}x{W}_{'T' if transposed else 'N'}"
+    _record[name] = [e16, e32]
+    assert e16 <= 4 * e32 + 1e-6, (e16, e32)
+
+
+@pytest.mark.parametrize("conv_impl", ["f16x3", "miopen"])
+def test_decoder_fused_equals_module_path(sdfr, conv_impl):
     """Same weights, latents and noise: HIP-epilogue decoder == op-by-op decoder."""
     opt = sdfr.vol_render_opt()
     opt.model.feature_encoder_in_channels = opt.rendering.width   # as Generator.__init__ sets it
     torch.manual_seed(0)
     dec = sdfr.Decoder(opt.model).to(DEV).eval()
+    dec.conv_impl = conv_impl
     with torch.no_grad():
         for m in dec.modules():
             if isinstance(m, sdfr.NoiseInjection):
@@ -201,6 +237,6 @@ def test_decoder_fused_equals_module_path(sdfr):
         dec.use_fused = True
     assert fused.shape == mod.shape == (B, 3, 256, 256)
     scale = float(mod.abs().max())
-    _record["decoder_fused_vs_module_scale"] = scale
-    _close("decoder_fused_vs_module", fused.cpu(), mod.cpu(), 1e-4 * max(1.0, scale),
+    _record[f"decoder_fused_vs_module_scale_{conv_impl}"] = scale
+    _close(f"decoder_fused_vs_module_{conv_impl}", fused.cpu(), mod.cpu(), 1e-4 * max(1.0, scale),
            1e-5 * max(1.0, scale))
