@@ -16,9 +16,12 @@
 // per output parity class (oy & 1, ox & 1), each over its own tap subset.
 //
 // Workgroup: 128 output channels x 128 output pixels, 4 waves of 64 x 64, K in
-// steps of 32 input channels at one tap; weight fragments (pre-packed hi/lo)
-// and activations (fp32 -> hi/lo split while staging) are double-buffered in
-// 64 KB of LDS, one barrier per K-step; two workgroups per CU.
+// steps of 32 input channels at one tap.  Both operands arrive already split
+// (weights pre-packed in fragment order; activations as the hi/lo fp16 planes the
+// previous epilogue writes) and are staged global -> LDS by LDS-DMA
+// (buffer_load ... lds: no VGPRs, no VALU; the buffer range check zero-fills the
+// padding taps), double-buffered in 64 KB of LDS, one barrier per K-step, two
+// workgroups per CU.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -104,7 +107,7 @@ __global__ void __launch_bounds__(256) conv_pack_kernel(const float *__restrict_
 // implicit GEMM
 // ----------------------------------------------------------------------------
 struct ConvArgs {
-    const float *x;                // [B, Hin, Win, Cin]
+    const _Float16 *xh, *xl;       // [B, Hin, Win, Cin] hi / lo planes
     const f4 *wpk;                 // packed fragments (above)
     float *out;                    // [B, Hf, Wf, Cout]
     uint32_t B, Hin, Win, Cin, Cout;
@@ -115,6 +118,8 @@ struct ConvArgs {
     int dy[9], dx[9];              // input pixel = (a + dy, c + dx)
     uint32_t tap[9];               // packed weight tap (3 ky + kx)
 };
+
+typedef __attribute__((address_space(3))) void lds_void;
 
 __global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
     __shared__ f4 As[2][kStepF4];   // [mt 8][hi,lo][64]
@@ -127,59 +132,57 @@ __global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
     const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT;
     const uint32_t nk = nC * a.ntaps;
 
-    // staging pixels of this thread: pl = (tid >> 3) + 32 i, channels 4 (tid & 7) .. +3
-    const uint32_t q = tid & 7u;
-    int sb[4], sa[4], sc[4];
-    bool sv[4];
+    // LDS-DMA sources.  Weights: the K-step's 16 KB block is contiguous; wave w
+    // moves its 1-KB pieces 4w .. 4w+3.  Activations: wave w moves the hi and lo
+    // fragments of n-tiles 2w, 2w+1; lane (g = lane >> 4, n = lane & 15) fetches
+    // channels 8g .. 8g+7 of pixel 16 nt + n (16 B), so the LDS image is
+    // lane-linear = the fragment layout.
+    const uint32_t xbytes = a.B * a.Hin * a.Win * a.Cin * 2;
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<f4 *>(a.wpk), 0, (int)(9u * nC * nB * kStepF4 * 16u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(a.xh), 0, (int)xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rl =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(a.xl), 0, (int)xbytes, 0x00020000);
+    const uint32_t g8 = 8 * (lane >> 4);
+    int pb[2], pa[2], pc[2];
+    bool pv[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t P = pix0 + (tid >> 3) + 32 * i;
-        sv[i] = P < npix;
-        const uint32_t Pc = sv[i] ? P : 0;
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t P = pix0 + (2 * wave + k) * 16 + (lane & 15u);
+        pv[k] = P < npix;
+        const uint32_t Pc = pv[k] ? P : 0;
         const uint32_t hw = a.Hc * a.Wc;
-        sb[i] = (int)(Pc / hw);
+        pb[k] = (int)(Pc / hw);
         const uint32_t rem = Pc % hw;
-        sa[i] = (int)(rem / a.Wc);
-        sc[i] = (int)(rem % a.Wc);
+        pa[k] = (int)(rem / a.Wc);
+        pc[k] = (int)(rem % a.Wc);
     }
-    // B-fragment slot of this thread's 4 channels: n-tile, lane (g, n), half
-    const uint32_t g_b = q >> 1, half = q & 1u;
 
-    f4 wst[4], xst[4];
-    auto load_step = [&](uint32_t ks) {
+    auto issue_step = [&](uint32_t ks, uint32_t buf) {
         const uint32_t c = ks / a.ntaps, t = ks % a.ntaps;
-        const f4 *wsrc = a.wpk + ((size_t)(a.tap[t] * nC + c) * nB + cb) * kStepF4;
+        const uint32_t wbase = ((a.tap[t] * nC + c) * nB + cb) * kStepF4 * 16u;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) wst[i] = wsrc[tid + 256 * i];
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t piece = 4 * wave + k;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rw, (lds_void *)&As[buf][piece * 64], 16, (int)(lane * 16u),
+                (int)(wbase + piece * 1024u), 0, 0);
+        }
         const int dy = a.dy[t], dx = a.dx[t];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int iy = sa[i] + dy, ix = sc[i] + dx;
-            const bool ok = sv[i] && iy >= 0 && iy < (int)a.Hin && ix >= 0 && ix < (int)a.Win;
-            f4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (ok)
-                v = *reinterpret_cast<const f4 *>(
-                    a.x + (((size_t)sb[i] * a.Hin + iy) * a.Win + ix) * a.Cin + c * 32 + 4 * q);
-            xst[i] = v;
-        }
-    };
-    auto store_step = [&](uint32_t buf) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) As[buf][tid + 256 * i] = wst[i];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            h4 hv, lv;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                hv[r] = (_Float16)xst[i][r];
-                lv[r] = (_Float16)__fsub_rn(xst[i][r], (float)hv[r]);
-            }
-            const uint32_t pl = (tid >> 3) + 32 * i;
-            const uint32_t nt = pl >> 4, n = pl & 15u;
-            const uint32_t l = g_b * 16 + n;
-            char *base = reinterpret_cast<char *>(&Bs[buf][(nt * 2) * 64 + l]) + half * 8;
-            *reinterpret_cast<h4 *>(base) = hv;
-            *reinterpret_cast<h4 *>(base + 64 * sizeof(f4)) = lv;
+        for (int k = 0; k < 2; ++k) {
+            const int iy = pa[k] + dy, ix = pc[k] + dx;
+            const bool ok = pv[k] && iy >= 0 && iy < (int)a.Hin && ix >= 0 && ix < (int)a.Win;
+            const uint32_t off =
+                ok ? ((((uint32_t)pb[k] * a.Hin + (uint32_t)iy) * a.Win + (uint32_t)ix) * a.Cin +
+                      c * 32 + g8) * 2u
+                   : 0x7FFFFFF0u;                      // past num_records: zero fill
+            const uint32_t nt = 2 * wave + k;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (lds_void *)&Bs[buf][(nt * 2) * 64], 16,
+                                                     (int)off, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_void *)&Bs[buf][(nt * 2 + 1) * 64],
+                                                     16, (int)off, 0, 0, 0);
         }
     };
 
@@ -189,12 +192,13 @@ __global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
-    load_step(0);
-    store_step(0);
+    issue_step(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (uint32_t ks = 0; ks < nk; ++ks) {
         const uint32_t buf = ks & 1u;
-        if (ks + 1 < nk) load_step(ks + 1);
+        // the other buffer was last read in step ks-1, closed by the barrier below it
+        if (ks + 1 < nk) issue_step(ks + 1, buf ^ 1u);
         f4 ah[4], al[4], bh[4], bl[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -211,7 +215,7 @@ __global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
                 acc[i][j] = mfma16(ah[i], bl[j], acc[i][j]);
                 acc[i][j] = mfma16(ah[i], bh[j], acc[i][j]);
             }
-        if (ks + 1 < nk) store_step(buf ^ 1u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // step ks+1's DMA has landed
         __syncthreads();
     }
 
@@ -256,14 +260,18 @@ int sdfr_conv_pack_weights(const float *w, float scale, uint32_t Cout, uint32_t 
     return check_launch("conv_pack_weights: pack");
 }
 
-int sdfr_conv3x3_f16x3(float *out, const float *x, const void *packed, uint32_t B, uint32_t H,
-                       uint32_t W, uint32_t Cin, uint32_t Cout, int transposed, void *stream) {
-    if (!out || !x || !packed) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
+int sdfr_conv3x3_f16x3(float *out, const void *x_hi, const void *x_lo, const void *packed,
+                       uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
+                       int transposed, void *stream) {
+    if (!out || !x_hi || !x_lo || !packed) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
     if (B == 0 || H == 0 || W == 0 || Cout % kCT || Cin % 32 || Cin == 0 || Cout == 0)
         return fail(SDFR_EINVAL, "conv3x3_f16x3: bad shape (Cout % 128, Cin % 32)");
+    if ((uint64_t)B * H * W * Cin * 2 >= (1ull << 31) || 9ull * Cin * Cout * 4 >= (1ull << 31))
+        return fail(SDFR_EINVAL, "conv3x3_f16x3: tensor too large for 32-bit offsets (split B)");
     hipStream_t st = (hipStream_t)stream;
     ConvArgs a{};
-    a.x = x;
+    a.xh = reinterpret_cast<const _Float16 *>(x_hi);
+    a.xl = reinterpret_cast<const _Float16 *>(x_lo);
     a.wpk = reinterpret_cast<const f4 *>(packed);
     a.out = out;
     a.B = B;

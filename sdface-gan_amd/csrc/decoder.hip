@@ -120,7 +120,27 @@ struct EpiArgs {
     float *y;
     const float *rgb_w, *rgb_b, *skip;
     float *rgb;
+    _Float16 *yh, *yl;     // split fp16 output planes (instead of y) or null
 };
+
+typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+
+// y (pre-multiplied by the next modulation) as fp32, or as the round-to-nearest
+// hi/lo fp16 split the split-fp16 convolution consumes (conv_f16x3.hip)
+__device__ __forceinline__ void store_y(const EpiArgs &a, size_t idx, float4 v) {
+    if (a.yh) {
+        h4v h, l;
+        h[0] = (_Float16)v.x; h[1] = (_Float16)v.y; h[2] = (_Float16)v.z; h[3] = (_Float16)v.w;
+        l[0] = (_Float16)(v.x - (float)h[0]);
+        l[1] = (_Float16)(v.y - (float)h[1]);
+        l[2] = (_Float16)(v.z - (float)h[2]);
+        l[3] = (_Float16)(v.w - (float)h[3]);
+        *reinterpret_cast<h4v *>(a.yh + idx) = h;
+        *reinterpret_cast<h4v *>(a.yl + idx) = l;
+    } else {
+        *reinterpret_cast<float4 *>(a.y + idx) = v;
+    }
+}
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
@@ -162,7 +182,8 @@ __device__ float skip_up(const float *__restrict__ img, uint32_t h2, uint32_t w2
 constexpr uint32_t kEpiPixPerBlock = 64;
 
 // Plain epilogue: lanes of a wave split the C channels of PPW = 64/TPP pixels
-// (TPP threads x NQ float4 per pixel); the 1x1 ToRGB is a TPP-lane reduction.
+// (TPP threads x NQ float4 per pixel, TPP <= 16 so a wave works on >= 4 pixels
+// at once); the 1x1 ToRGB is a TPP-lane reduction (log2 TPP shuffle steps).
 template <int NQ, bool RGB>
 __global__ __launch_bounds__(256) void epi_plain_kernel(EpiArgs a, uint32_t tpp_log2) {
     const uint32_t TPP = 1u << tpp_log2;
@@ -198,10 +219,9 @@ __global__ __launch_bounds__(256) void epi_plain_kernel(EpiArgs a, uint32_t tpp_
                 const uint32_t c = 4 * (q + k * TPP);
                 const float4 v = act4(ld4(a.conv + base + c), dm[k], nz, bs[k], a.slope,
                                       a.act_scale);
-                if (a.y) {
-                    *reinterpret_cast<float4 *>(a.y + base + c) =
-                        make_float4(v.x * sn[k].x, v.y * sn[k].y, v.z * sn[k].z, v.w * sn[k].w);
-                }
+                if (a.y || a.yh)
+                    store_y(a, base + c,
+                            make_float4(v.x * sn[k].x, v.y * sn[k].y, v.z * sn[k].z, v.w * sn[k].w));
                 if (RGB) {
 #pragma unroll
                     for (int o = 0; o < 3; ++o) {
@@ -285,8 +305,7 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg)
         const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
         const float nz = a.noise ? nw * a.noise[pix] : 0.0f;
         const float4 v = act4(s, dm, nz, bs, a.slope, a.act_scale);
-        *reinterpret_cast<float4 *>(a.y + pix * C + c) =
-            make_float4(v.x * sn.x, v.y * sn.y, v.z * sn.z, v.w * sn.w);
+        store_y(a, pix * C + c, make_float4(v.x * sn.x, v.y * sn.y, v.z * sn.z, v.w * sn.w));
         h0 = h1; h1 = h2; h2 = h3;
     }
 }
@@ -295,6 +314,8 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg)
 // NCHW -> NHWC with modulation, 64 x 64 LDS tiles
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void modulate_nhwc_kernel(float *__restrict__ y,
+                                                            _Float16 *__restrict__ yh,
+                                                            _Float16 *__restrict__ yl,
                                                             const float *__restrict__ x,
                                                             const float *__restrict__ s,
                                                             uint32_t C, uint32_t HW) {
@@ -319,8 +340,21 @@ __global__ __launch_bounds__(256) void modulate_nhwc_kernel(float *__restrict__ 
         const uint32_t pl = (t >> 4) + 16 * k, cl = 4 * (t & 15);
         const uint32_t c = c0 + cl, p = p0 + pl;
         if (c < C && p < HW) {
-            *reinterpret_cast<float4 *>(y + ((size_t)b * HW + p) * C + c) =
+            const float4 v =
                 make_float4(tile[cl][pl], tile[cl + 1][pl], tile[cl + 2][pl], tile[cl + 3][pl]);
+            const size_t idx = ((size_t)b * HW + p) * C + c;
+            if (yh) {
+                h4v h, l;
+                h[0] = (_Float16)v.x; h[1] = (_Float16)v.y; h[2] = (_Float16)v.z; h[3] = (_Float16)v.w;
+                l[0] = (_Float16)(v.x - (float)h[0]);
+                l[1] = (_Float16)(v.y - (float)h[1]);
+                l[2] = (_Float16)(v.z - (float)h[2]);
+                l[3] = (_Float16)(v.w - (float)h[3]);
+                *reinterpret_cast<h4v *>(yh + idx) = h;
+                *reinterpret_cast<h4v *>(yl + idx) = l;
+            } else {
+                *reinterpret_cast<float4 *>(y + idx) = v;
+            }
         }
     }
 }
@@ -394,14 +428,17 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
     const bool rgb = s.rgb_w != nullptr;
     if (rgb && (!s.rgb || !s.rgb_b)) return fail(SDFR_EINVAL, "styled_epilogue: rgb output missing");
     if (rgb && s.blur_up) return fail(SDFR_EINVAL, "styled_epilogue: ToRGB after a blur is not fused");
-    if (!rgb && !s.y) return fail(SDFR_EINVAL, "styled_epilogue: nothing to write");
+    if (!rgb && !s.y && !s.y_hi) return fail(SDFR_EINVAL, "styled_epilogue: nothing to write");
+    if (s.y && s.y_hi) return fail(SDFR_EINVAL, "styled_epilogue: y and y_hi/y_lo are exclusive");
+    if (!s.y_hi != !s.y_lo) return fail(SDFR_EINVAL, "styled_epilogue: y_hi and y_lo go together");
     if (s.skip && (s.H % 2 || s.W % 2)) return fail(SDFR_EINVAL, "styled_epilogue: odd size with skip");
     for (const void *q : {(const void *)s.conv, (const void *)s.demod, (const void *)s.bias,
                           (const void *)s.s_next, (const void *)s.y, (const void *)s.rgb_w})
         if (q && !aligned16(q)) return fail(SDFR_EINVAL, "styled_epilogue: pointers must be 16-B aligned");
     EpiArgs a{s.B, s.C, s.H, s.W, s.conv, {s.fir[0], s.fir[1], s.fir[2], s.fir[3]},
               s.demod, s.noise, s.noise_weight, s.bias, s.negative_slope, s.act_scale,
-              s.s_next, s.y, s.rgb_w, s.rgb_b, s.skip, s.rgb};
+              s.s_next, s.y, s.rgb_w, s.rgb_b, s.skip, s.rgb,
+              reinterpret_cast<_Float16 *>(s.y_hi), reinterpret_cast<_Float16 *>(s.y_lo)};
     hipStream_t st = (hipStream_t)stream;
     if (s.blur_up) {
         const uint32_t nseg = (s.H + kBlurRows - 1) / kBlurRows;
@@ -414,11 +451,17 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
     if (Q <= 64 ? !pow2 : (Q % 64 != 0))
         return fail(SDFR_EUNSUPPORTED,
                     "styled_epilogue: C/4 must be a power of two <= 64 or a multiple of 64");
-    uint32_t tpp_log2 = 6, nq = Q / 64;
-    if (Q <= 64) {
-        nq = 1;
-        tpp_log2 = 0;
+    // TPP = min(Q, 16) lanes per pixel, NQ = Q / TPP float4 each (<= 8: C <= 512);
+    // wider channels (Q a multiple of 64) use a whole wave per pixel, NQ = Q / 64
+    uint32_t tpp_log2 = 0, nq = 1;
+    if (Q <= 16) {
         while ((1u << tpp_log2) < Q) ++tpp_log2;
+    } else if (Q <= 128) {
+        tpp_log2 = 4;
+        nq = Q / 16;
+    } else {
+        tpp_log2 = 6;
+        nq = Q / 64;
     }
     dim3 grid((s.H * s.W + kEpiPixPerBlock - 1) / kEpiPixPerBlock, s.B);
 #define EPI(NQ)                                                                          \
@@ -431,21 +474,38 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
         EPI(2)
         EPI(3)
         EPI(4)
+        EPI(8)
         default: return fail(SDFR_EUNSUPPORTED, "styled_epilogue: C > 1024");
     }
 #undef EPI
     return check_launch("styled_epilogue");
 }
 
+static int modulate_common(float *y, void *yh, void *yl, const float *x, const float *s,
+                           uint32_t B, uint32_t C, uint32_t HW, void *stream) {
+    if (B == 0 || C == 0 || HW == 0) return SDFR_OK;
+    if ((!y && !yh) || !x || !s || (yh && !yl))
+        return fail(SDFR_EINVAL, "modulate_to_nhwc: null tensor pointer");
+    if (C % 4 || HW % 4) return fail(SDFR_EINVAL, "modulate_to_nhwc: C and H*W must be multiples of 4");
+    if (!aligned16(x) || (y && !aligned16(y)))
+        return fail(SDFR_EINVAL, "modulate_to_nhwc: pointers must be 16-B aligned");
+    dim3 grid((HW + 63) / 64, (C + 63) / 64, B);
+    modulate_nhwc_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(
+        y, reinterpret_cast<_Float16 *>(yh), reinterpret_cast<_Float16 *>(yl), x, s, C, HW);
+    return check_launch("modulate_to_nhwc");
+}
+
 int sdfr_modulate_to_nhwc(float *y, const float *x, const float *s, uint32_t B, uint32_t C,
                           uint32_t HW, void *stream) {
-    if (B == 0 || C == 0 || HW == 0) return SDFR_OK;
-    if (!y || !x || !s) return fail(SDFR_EINVAL, "modulate_to_nhwc: null tensor pointer");
-    if (C % 4 || HW % 4) return fail(SDFR_EINVAL, "modulate_to_nhwc: C and H*W must be multiples of 4");
-    if (!aligned16(x) || !aligned16(y)) return fail(SDFR_EINVAL, "modulate_to_nhwc: pointers must be 16-B aligned");
-    dim3 grid((HW + 63) / 64, (C + 63) / 64, B);
-    modulate_nhwc_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(y, x, s, C, HW);
-    return check_launch("modulate_to_nhwc");
+    if (!y && B && C && HW) return fail(SDFR_EINVAL, "modulate_to_nhwc: null tensor pointer");
+    return modulate_common(y, nullptr, nullptr, x, s, B, C, HW, stream);
+}
+
+int sdfr_modulate_to_nhwc_split(void *y_hi, void *y_lo, const float *x, const float *s,
+                                uint32_t B, uint32_t C, uint32_t HW, void *stream) {
+    if ((!y_hi || !y_lo) && B && C && HW)
+        return fail(SDFR_EINVAL, "modulate_to_nhwc_split: null tensor pointer");
+    return modulate_common(nullptr, y_hi, y_lo, x, s, B, C, HW, stream);
 }
 
 }  // extern "C"

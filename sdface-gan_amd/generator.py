@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .decoder_ops import conv3x3_f16x3, conv_pack_weights  # noqa: E402
+from .decoder_ops import conv3x3_f16x3, conv_pack_weights, modulate_to_nhwc_split  # noqa: E402
 from .decoder_ops import (FusedLeakyReLU, fused_leaky_relu, modulate_to_nhwc,  # noqa: F401
                           separable_taps, styled_epilogue, upfirdn2d)
 from .renderer import VolumeFeatureRenderer
@@ -327,6 +327,12 @@ class Decoder(nn.Module):
             self._fir = fir if ok else False
         return self._fir is not False
 
+    def _conv_x(self, mc):
+        """Does this ModulatedConv2d run on the split-fp16 implicit GEMM?"""
+        _, cout, cin, k, _ = mc.weight.shape
+        return (self.conv_impl == "f16x3" and k == 3 and mc.demodulate and not mc.downsample
+                and cout % 128 == 0 and cin % 32 == 0)
+
     def _pack(self, i, mc):
         """Packed split-fp16 weights of layer i, rebuilt when the weight changes."""
         key = (mc.weight.data_ptr(), mc.weight._version, mc.weight.device)
@@ -345,15 +351,15 @@ class Decoder(nn.Module):
         B = features.shape[0]
         seq = [self.conv1] + list(self.convs)
         mods = [sc.conv.modulation(latent[:, i]) for i, sc in enumerate(seq)]
-        x = modulate_to_nhwc(features, mods[0])
+        split = [self._conv_x(sc.conv) for sc in seq]     # layer i's input as hi/lo planes
+        x = (modulate_to_nhwc_split if split[0] else modulate_to_nhwc)(features, mods[0])
         rgb = None
         for i, sc in enumerate(seq):
             mc = sc.conv
             w = mc.scale * mc.weight[0]
             demod = (torch.rsqrt((mods[i] * mods[i]) @ (w * w).sum([2, 3]).t() + 1e-8)
                      if mc.demodulate else None)
-            if self.conv_impl == "f16x3" and mc.kernel_size == 3 and mc.demodulate and \
-                    w.shape[0] % 128 == 0 and w.shape[1] % 32 == 0:
+            if split[i]:
                 packed, su = self._pack(i, mc)
                 out = conv3x3_f16x3(x, packed, w.shape[0], transposed=mc.upsample)
                 demod = demod / su            # result carries su (power of two): exact
@@ -379,7 +385,8 @@ class Decoder(nn.Module):
                 out, fir=self._fir, bias=sc.activate.bias, noise_weight=sc.noise.weight,
                 noise=n, demod=demod, blur_up=mc.upsample,
                 s_next=None if last else mods[i + 1], store_y=not last,
-                rgb_w=rgb_w, rgb_b=rgb_b, skip=rgb if i else None)
+                rgb_w=rgb_w, rgb_b=rgb_b, skip=rgb if i else None,
+                split_y=not last and split[i + 1])
             if rgb_new is not None:
                 rgb = rgb_new
         return rgb

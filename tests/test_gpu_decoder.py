@@ -167,6 +167,30 @@ def test_styled_epilogue_rejects_bad_channels(ops):
                             rgb_b=torch.zeros(3, device=DEV), store_y=False)
 
 
+def test_split_planes_bit_exact(ops):
+    """modulate_to_nhwc_split and the epilogue's split y write exactly the
+    round-to-nearest (hi, lo) fp16 split of their fp32 result."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 64, 8, 12, generator=g)
+    s = torch.rand(2, 64, generator=g) + 0.5
+    hi, lo = ops.modulate_to_nhwc_split(x.to(DEV), s.to(DEV))
+    ref = (x * s[:, :, None, None]).permute(0, 2, 3, 1).contiguous()
+    rh = ref.half()
+    np.testing.assert_array_equal(hi.cpu().numpy(), rh.numpy())
+    np.testing.assert_array_equal(lo.cpu().numpy(), (ref - rh.float()).half().numpy())
+    conv = torch.randn(2, 64, 8, 12, generator=g).to(DEV).contiguous(
+        memory_format=torch.channels_last)
+    kw = dict(fir=[0.125, 0.375, 0.375, 0.125], bias=torch.randn(64, device=DEV),
+              noise_weight=torch.full((1,), 0.1, device=DEV),
+              noise=torch.randn(2, 1, 8, 12, device=DEV), demod=torch.rand(2, 64, device=DEV),
+              s_next=torch.rand(2, 64, device=DEV))
+    y, _ = ops.styled_epilogue(conv, **kw)
+    (yh, yl), _ = ops.styled_epilogue(conv, split_y=True, **kw)
+    ref = y.permute(0, 2, 3, 1).contiguous().cpu()
+    np.testing.assert_array_equal(yh.cpu().numpy(), ref.half().numpy())
+    np.testing.assert_array_equal(yl.cpu().numpy(), (ref - ref.half().float()).half().numpy())
+
+
 @pytest.mark.parametrize("C,H", [(256, 64), (36, 5), (128, 20)])
 def test_modulate_to_nhwc_bit_exact(ops, C, H):
     g = torch.Generator().manual_seed(C)
@@ -193,8 +217,7 @@ def test_conv3x3_f16x3_vs_fp64(ops, B, Cin, Cout, H, W, transposed):
     scale = 1 / math.sqrt(Cin * 9)
     w32 = (scale * w[0]).float()
     packed, su = ops.conv_pack_weights(w[0].to(DEV), scale)
-    out = ops.conv3x3_f16x3(x.to(DEV).contiguous(memory_format=torch.channels_last), packed,
-                            Cout, transposed=transposed)
+    out = ops.conv3x3_f16x3(ops.split_nhwc(x.to(DEV)), packed, Cout, transposed=transposed)
     got = (out / su.view(1, -1, 1, 1)).cpu().double()
     if transposed:
         ref = F.conv_transpose2d(x.double(), w32.double().transpose(0, 1), stride=2)
