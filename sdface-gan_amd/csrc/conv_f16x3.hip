@@ -15,13 +15,14 @@
 // into the demodulation (exact).  A transposed conv is four implicit GEMMs, one
 // per output parity class (oy & 1, ox & 1), each over its own tap subset.
 //
-// Workgroup: 128 output channels x 128 output pixels, 4 waves of 64 x 64, K in
-// steps of 32 input channels at one tap.  Both operands arrive already split
-// (weights pre-packed in fragment order; activations as the hi/lo fp16 planes the
-// previous epilogue writes) and are staged global -> LDS by LDS-DMA
-// (buffer_load ... lds: no VGPRs, no VALU; the buffer range check zero-fills the
-// padding taps), double-buffered in 64 KB of LDS, one barrier per K-step, two
-// workgroups per CU.
+// Workgroup: 128 output channels x 256 output pixels, 8 waves of 64 x 64 (two per
+// SIMD), K in steps of 32 input channels at one tap.  Both operands arrive
+// already split (weights pre-packed in fragment order; activations as the hi/lo
+// fp16 planes the previous epilogue writes) and are staged global -> LDS by
+// LDS-DMA (buffer_load ... lds: no VGPRs, no VALU; the buffer range check
+// zero-fills the padding taps) through a 3-stage ring of 48 KB stages: two
+// K-steps stay in flight behind a counted vmcnt and a raw barrier, one
+// workgroup per CU.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -36,8 +37,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 
 constexpr int kCT = 128;        // output channels per workgroup
-constexpr int kPT = 128;        // output pixels per workgroup
-constexpr int kStepF4 = 1024;   // f4 per operand per K-step (16 KB)
+constexpr int kPT = 256;        // output pixels per workgroup
+constexpr int kStepF4 = 1024;   // f4 of weight fragments per K-step (16 KB)
+constexpr int kStages = 3;      // LDS-DMA ring depth (two K-steps in flight)
 
 __device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a),
@@ -119,12 +121,43 @@ struct ConvArgs {
     uint32_t tap[9];               // packed weight tap (3 ky + kx)
 };
 
-typedef __attribute__((address_space(3))) void lds_void;
+typedef int v4i __attribute__((ext_vector_type(4)));
 
-__global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
-    __shared__ f4 As[2][kStepF4];   // [mt 8][hi,lo][64]
-    __shared__ f4 Bs[2][kStepF4];   // [nt 8][hi,lo][64]
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+// Buffer resource over [base, base + bytes) (gfx950 raw buffer, range-checked).
+__device__ __forceinline__ v4i make_rsrc(const void *base, uint32_t bytes) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    v4i r;
+    r.x = (int)(uint32_t)b;
+    r.y = (int)(uint32_t)(b >> 32);
+    r.z = (int)bytes;
+    r.w = 0x00020000;
+    return r;
+}
+
+// One LDS-DMA piece: 64 lanes x 16 B from rsrc at (voff + soff) to LDS byte
+// address lds (wave-uniform base + 16 lane).  Inline asm, so hipcc neither
+// tracks it in its own s_waitcnt bookkeeping (no vmcnt(0) drain in front of
+// every ds_read of the ring) nor reserves M0 across it; completion is counted
+// explicitly by the ring below.  Offsets past num_records read zeros.
+__device__ __forceinline__ void dma16(v4i rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
+        : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)reinterpret_cast<uintptr_t>(p);
+}
+
+__global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
+    __shared__ f4 As[kStages][kStepF4];       // [mt 8][hi,lo][64]
+    __shared__ f4 Bs[kStages][2 * kStepF4];   // [nt 16][hi,lo][64]
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
     const uint32_t wm = wave & 1u, wn = wave >> 1;
     const uint32_t cb = blockIdx.y;
     const uint32_t npix = a.B * a.Hc * a.Wc;
@@ -132,18 +165,15 @@ __global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
     const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT;
     const uint32_t nk = nC * a.ntaps;
 
-    // LDS-DMA sources.  Weights: the K-step's 16 KB block is contiguous; wave w
-    // moves its 1-KB pieces 4w .. 4w+3.  Activations: wave w moves the hi and lo
-    // fragments of n-tiles 2w, 2w+1; lane (g = lane >> 4, n = lane & 15) fetches
-    // channels 8g .. 8g+7 of pixel 16 nt + n (16 B), so the LDS image is
-    // lane-linear = the fragment layout.
+    // LDS-DMA sources (6 pieces of 1 KB per wave per K-step).  Weights: the K-step's
+    // 16 KB block is contiguous; wave w moves pieces 2w, 2w+1.  Activations: wave w
+    // moves the hi and lo fragments of n-tiles 2w, 2w+1; lane (g = lane >> 4,
+    // n = lane & 15) fetches channels 8g .. 8g+7 of pixel 16 nt + n (16 B), so the
+    // LDS image is lane-linear = the fragment layout.
     const uint32_t xbytes = a.B * a.Hin * a.Win * a.Cin * 2;
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<f4 *>(a.wpk), 0, (int)(9u * nC * nB * kStepF4 * 16u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rh =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(a.xh), 0, (int)xbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rl =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(a.xl), 0, (int)xbytes, 0x00020000);
+    const v4i rw = make_rsrc(a.wpk, 9u * nC * nB * kStepF4 * 16u);
+    const v4i rh = make_rsrc(a.xh, xbytes);
+    const v4i rl = make_rsrc(a.xl, xbytes);
     const uint32_t g8 = 8 * (lane >> 4);
     int pb[2], pa[2], pc[2];
     bool pv[2];
@@ -163,11 +193,9 @@ __global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
         const uint32_t c = ks / a.ntaps, t = ks % a.ntaps;
         const uint32_t wbase = ((a.tap[t] * nC + c) * nB + cb) * kStepF4 * 16u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t piece = 4 * wave + k;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rw, (lds_void *)&As[buf][piece * 64], 16, (int)(lane * 16u),
-                (int)(wbase + piece * 1024u), 0, 0);
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t piece = 2 * wave + k;
+            dma16(rw, lane * 16u, wbase + piece * 1024u, lds_addr(&As[buf][piece * 64]));
         }
         const int dy = a.dy[t], dx = a.dx[t];
 #pragma unroll
@@ -179,10 +207,8 @@ __global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
                       c * 32 + g8) * 2u
                    : 0x7FFFFFF0u;                      // past num_records: zero fill
             const uint32_t nt = 2 * wave + k;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (lds_void *)&Bs[buf][(nt * 2) * 64], 16,
-                                                     (int)off, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_void *)&Bs[buf][(nt * 2 + 1) * 64],
-                                                     16, (int)off, 0, 0, 0);
+            dma16(rh, off, 0u, lds_addr(&Bs[buf][(nt * 2) * 64]));
+            dma16(rl, off, 0u, lds_addr(&Bs[buf][(nt * 2 + 1) * 64]));
         }
     };
 
@@ -192,20 +218,25 @@ __global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
+    // ring: step ks in stage ks % 3; steps ks+1, ks+2 in flight while ks computes.
+    // Stage (ks+2) % 3 last held step ks-1, whose reads every wave completed before
+    // the barrier that closed step ks-1.
     issue_step(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (nk > 1) issue_step(1, 1);
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    uint32_t cur = 0;
     for (uint32_t ks = 0; ks < nk; ++ks) {
-        const uint32_t buf = ks & 1u;
-        // the other buffer was last read in step ks-1, closed by the barrier below it
-        if (ks + 1 < nk) issue_step(ks + 1, buf ^ 1u);
+        const bool more = ks + 2 < nk;
+        if (more) issue_step(ks + 2, cur == 0 ? 2u : cur - 1);
         f4 ah[4], al[4], bh[4], bl[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            ah[i] = As[buf][((4 * wm + i) * 2) * 64 + lane];
-            al[i] = As[buf][((4 * wm + i) * 2 + 1) * 64 + lane];
-            bh[i] = Bs[buf][((4 * wn + i) * 2) * 64 + lane];
-            bl[i] = Bs[buf][((4 * wn + i) * 2 + 1) * 64 + lane];
+            ah[i] = As[cur][((4 * wm + i) * 2) * 64 + lane];
+            al[i] = As[cur][((4 * wm + i) * 2 + 1) * 64 + lane];
+            bh[i] = Bs[cur][((4 * wn + i) * 2) * 64 + lane];
+            bl[i] = Bs[cur][((4 * wn + i) * 2 + 1) * 64 + lane];
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -215,8 +246,12 @@ __global__ void __launch_bounds__(256, 2) conv_x_kernel(const ConvArgs a) {
                 acc[i][j] = mfma16(ah[i], bl[j], acc[i][j]);
                 acc[i][j] = mfma16(ah[i], bh[j], acc[i][j]);
             }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // step ks+1's DMA has landed
-        __syncthreads();
+        // step ks+1 must have landed (only ks+2's 6 pieces may stay in flight), and
+        // this wave's fragment reads of stage `cur` must be done, before the barrier
+        if (more) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        cur = cur == 2 ? 0 : cur + 1;
     }
 
     // epilogue: lane (n, g) of tile (i, j) holds channels 16 mt + 4 g .. +3 of pixel 16 nt + n
@@ -281,7 +316,7 @@ int sdfr_conv3x3_f16x3(float *out, const void *x_hi, const void *x_lo, const voi
     a.Cout = Cout;
     auto launch = [&]() {
         const uint32_t npix = B * a.Hc * a.Wc;
-        hipLaunchKernelGGL(conv_x_kernel, dim3((npix + kPT - 1) / kPT, Cout / kCT), dim3(256), 0,
+        hipLaunchKernelGGL(conv_x_kernel, dim3((npix + kPT - 1) / kPT, Cout / kCT), dim3(512), 0,
                            st, a);
         return check_launch("conv3x3_f16x3");
     };
