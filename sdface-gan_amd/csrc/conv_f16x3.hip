@@ -108,15 +108,34 @@ __global__ void __launch_bounds__(256) conv_pack_kernel(const float *__restrict_
 // ----------------------------------------------------------------------------
 // implicit GEMM
 // ----------------------------------------------------------------------------
+#ifndef CONV_REGDB
+#define CONV_REGDB 1      // fragments of step ks+1 read into a second register set mid-step
+#endif
+#ifndef CONV_XCD
+#define CONV_XCD 1
+#endif
+#ifndef CONV_ABL
+#define CONV_ABL 0        // timing ablations (wrong results): 1 L2-resident x, 2 no staging, 3 + no barrier
+#endif
+
+// One output-pixel class: the plain convolution has one (every pixel, 9 taps); the
+// stride-2 transposed one has four parity classes (4, 2, 2 and 1 taps) that share
+// one launch, heaviest first, so their tails overlap.
+struct ConvClass {
+    uint32_t Hc, Wc;               // the class's output grid
+    uint32_t py, px;               // output pixel (a, c) -> (sy a + py, sy c + px)
+    uint32_t ntaps, t0;            // its taps: dy/dx/tap[t0 .. t0 + ntaps)
+    uint32_t tile0, ntiles;        // workgroups [tile0, tile0 + pad8(ntiles)) of the grid
+};
+
 struct ConvArgs {
     const _Float16 *xh, *xl;       // [B, Hin, Win, Cin] hi / lo planes
     const f4 *wpk;                 // packed fragments (above)
     float *out;                    // [B, Hf, Wf, Cout]
     uint32_t B, Hin, Win, Cin, Cout;
-    uint32_t Hc, Wc;               // this launch's output grid
-    uint32_t Hf, Wf;               // full output image
-    uint32_t sy, py, px;           // output pixel (a, c) -> (sy a + py, sy c + px)
-    uint32_t ntaps;
+    uint32_t Hf, Wf, sy;           // full output image, class stride
+    uint32_t ncls;
+    ConvClass cls[4];
     int dy[9], dx[9];              // input pixel = (a + dy, c + dx)
     uint32_t tap[9];               // packed weight tap (3 ky + kx)
 };
@@ -159,11 +178,30 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
     const uint32_t wm = wave & 1u, wn = wave >> 1;
-    const uint32_t cb = blockIdx.y;
-    const uint32_t npix = a.B * a.Hc * a.Wc;
-    const uint32_t pix0 = blockIdx.x * kPT;
+    // this workgroup's class (ranges start at multiples of 8: blockIdx.x % 8 is the XCD)
+    uint32_t ci = 0;
+    for (uint32_t i = 1; i < a.ncls; ++i)
+        if (blockIdx.x >= a.cls[i].tile0) ci = i;
+    const ConvClass &cl = a.cls[ci];
+    const uint32_t Hc = cl.Hc, Wc = cl.Wc, py = cl.py, px = cl.px;
+    const uint32_t ntaps = cl.ntaps, t0 = cl.t0, ntiles = cl.ntiles;
+    const uint32_t npix = a.B * Hc * Wc;
     const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT;
-    const uint32_t nk = nC * a.ntaps;
+    const uint32_t loc = blockIdx.x - cl.tile0;
+#if CONV_XCD
+    // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs; give
+    // each XCD one contiguous run of the class's tiles, with the Cout block fastest,
+    // so the tiles that re-read an activation row (the other Cout blocks of the same
+    // pixels, the rows above and below through the taps) run on the same XCD at
+    // about the same time and hit its L2.
+    const uint32_t tile = (loc & 7u) * ((ntiles + 7) >> 3) + (loc >> 3);
+#else
+    const uint32_t tile = loc;
+#endif
+    if (tile >= ntiles) return;                       // padding slot (whole workgroup)
+    const uint32_t cb = tile % nB;
+    const uint32_t pix0 = (tile / nB) * kPT;
+    const uint32_t nk = nC * ntaps;
 
     // LDS-DMA sources (6 pieces of 1 KB per wave per K-step).  Weights: the K-step's
     // 16 KB block is contiguous; wave w moves pieces 2w, 2w+1.  Activations: wave w
@@ -182,15 +220,15 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
         const uint32_t P = pix0 + (2 * wave + k) * 16 + (lane & 15u);
         pv[k] = P < npix;
         const uint32_t Pc = pv[k] ? P : 0;
-        const uint32_t hw = a.Hc * a.Wc;
+        const uint32_t hw = Hc * Wc;
         pb[k] = (int)(Pc / hw);
         const uint32_t rem = Pc % hw;
-        pa[k] = (int)(rem / a.Wc);
-        pc[k] = (int)(rem % a.Wc);
+        pa[k] = (int)(rem / Wc);
+        pc[k] = (int)(rem % Wc);
     }
 
     auto issue_step = [&](uint32_t ks, uint32_t buf) {
-        const uint32_t c = ks / a.ntaps, t = ks % a.ntaps;
+        const uint32_t c = ks / ntaps, t = t0 + ks % ntaps;
         const uint32_t wbase = ((a.tap[t] * nC + c) * nB + cb) * kStepF4 * 16u;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -202,10 +240,14 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
         for (int k = 0; k < 2; ++k) {
             const int iy = pa[k] + dy, ix = pc[k] + dx;
             const bool ok = pv[k] && iy >= 0 && iy < (int)a.Hin && ix >= 0 && ix < (int)a.Win;
+#if CONV_ABL == 1   // ablation: activations from a tiny L2-resident window
+            const uint32_t off = ((lane & 15u) * a.Cin + c * 32 + g8) * 2u + 0 * (ok ? 1u : 0u);
+#else
             const uint32_t off =
                 ok ? ((((uint32_t)pb[k] * a.Hin + (uint32_t)iy) * a.Win + (uint32_t)ix) * a.Cin +
                       c * 32 + g8) * 2u
                    : 0x7FFFFFF0u;                      // past num_records: zero fill
+#endif
             const uint32_t nt = 2 * wave + k;
             dma16(rh, off, 0u, lds_addr(&Bs[buf][(nt * 2) * 64]));
             dma16(rl, off, 0u, lds_addr(&Bs[buf][(nt * 2 + 1) * 64]));
@@ -218,7 +260,64 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
-    // ring: step ks in stage ks % 3; steps ks+1, ks+2 in flight while ks computes.
+    // Fragments of one K-step: [0..3] A hi, [4..7] A lo, [8..11] B hi, [12..15] B lo.
+    auto read_frags = [&](f4 (&R)[16], uint32_t st) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            R[i] = As[st][((4 * wm + i) * 2) * 64 + lane];
+            R[4 + i] = As[st][((4 * wm + i) * 2 + 1) * 64 + lane];
+            R[8 + i] = Bs[st][((4 * wn + i) * 2) * 64 + lane];
+            R[12 + i] = Bs[st][((4 * wn + i) * 2 + 1) * 64 + lane];
+        }
+    };
+    // rows i0 .. i0+nr-1 of the wave's 4 x 4 tiles; per A fragment the three split
+    // terms sweep the 4 B fragments (consecutive MFMAs never share an accumulator)
+    auto mfma_rows = [&](const f4 (&R)[16], int i0, int nr) {
+#pragma unroll
+        for (int i = i0; i < i0 + nr; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[4 + i], R[8 + j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[i], R[12 + j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[i], R[8 + j], acc[i][j]);
+        }
+    };
+
+#if CONV_REGDB
+    // Ring: step ks lives in stage ks % 3 and is read into registers half a step
+    // early.  Half-way through step ks (rows 0-1 done) the wave waits for its pieces
+    // of step ks+1 (ks+2's 6 may stay in flight), drains its LDS reads and meets the
+    // others at a raw barrier: after it step ks+1 is in LDS everywhere and nobody
+    // reads stage ks % 3 any more, so step ks+3 is issued into it and step ks+1's
+    // fragments are read while rows 2-3 of step ks compute.
+    auto step = [&](uint32_t ks, const f4 (&R)[16], f4 (&Rn)[16]) {
+        mfma_rows(R, 0, 2);
+        if (ks + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const uint32_t st = ks % 3u;
+        if (ks + 3 < nk) issue_step(ks + 3, st);
+        if (ks + 1 < nk) read_frags(Rn, st == 2 ? 0u : st + 1);
+        mfma_rows(R, 2, 2);
+    };
+    issue_step(0, 0);
+    if (nk > 1) issue_step(1, 1);
+    if (nk > 2) issue_step(2, 2);
+    if (nk > 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    f4 R0[16], R1[16];
+    read_frags(R0, 0);
+    uint32_t ks = 0;
+    for (; ks + 1 < nk; ks += 2) {
+        step(ks, R0, R1);
+        step(ks + 1, R1, R0);
+    }
+    if (ks < nk) step(ks, R0, R1);
+#else
+    // Ring: step ks in stage ks % 3; steps ks+1, ks+2 in flight while ks computes.
     // Stage (ks+2) % 3 last held step ks-1, whose reads every wave completed before
     // the barrier that closed step ks-1.
     issue_step(0, 0);
@@ -229,30 +328,26 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     uint32_t cur = 0;
     for (uint32_t ks = 0; ks < nk; ++ks) {
         const bool more = ks + 2 < nk;
+#if CONV_ABL == 2 || CONV_ABL == 3   // ablation: no staging in the loop (stale LDS)
+        (void)more;
+#else
         if (more) issue_step(ks + 2, cur == 0 ? 2u : cur - 1);
-        f4 ah[4], al[4], bh[4], bl[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            ah[i] = As[cur][((4 * wm + i) * 2) * 64 + lane];
-            al[i] = As[cur][((4 * wm + i) * 2 + 1) * 64 + lane];
-            bh[i] = Bs[cur][((4 * wn + i) * 2) * 64 + lane];
-            bl[i] = Bs[cur][((4 * wn + i) * 2 + 1) * 64 + lane];
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                acc[i][j] = mfma16(al[i], bh[j], acc[i][j]);
-                acc[i][j] = mfma16(ah[i], bl[j], acc[i][j]);
-                acc[i][j] = mfma16(ah[i], bh[j], acc[i][j]);
-            }
+#endif
+        f4 R[16];
+        read_frags(R, cur);
+        mfma_rows(R, 0, 4);
         // step ks+1 must have landed (only ks+2's 6 pieces may stay in flight), and
         // this wave's fragment reads of stage `cur` must be done, before the barrier
+#if CONV_ABL == 3   // ablation: no staging, no barrier
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
         if (more) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+#endif
         cur = cur == 2 ? 0 : cur + 1;
     }
+#endif
 
     // epilogue: lane (n, g) of tile (i, j) holds channels 16 mt + 4 g .. +3 of pixel 16 nt + n
     const uint32_t n = lane & 15u, g = lane >> 4;
@@ -260,9 +355,9 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     for (int j = 0; j < 4; ++j) {
         const uint32_t P = pix0 + (4 * wn + j) * 16 + n;
         if (P >= npix) continue;
-        const uint32_t hw = a.Hc * a.Wc;
+        const uint32_t hw = Hc * Wc;
         const uint32_t b = P / hw, rem = P % hw;
-        const uint32_t oy = a.sy * (rem / a.Wc) + a.py, ox = a.sy * (rem % a.Wc) + a.px;
+        const uint32_t oy = a.sy * (rem / Wc) + py, ox = a.sy * (rem % Wc) + px;
         float *dst = a.out + (((size_t)b * a.Hf + oy) * a.Wf + ox) * a.Cout + cb * kCT + 4 * g;
 #pragma unroll
         for (int i = 0; i < 4; ++i) *reinterpret_cast<f4 *>(dst + (4 * wm + i) * 16) = acc[i][j];
@@ -314,50 +409,54 @@ int sdfr_conv3x3_f16x3(float *out, const void *x_hi, const void *x_lo, const voi
     a.Win = W;
     a.Cin = Cin;
     a.Cout = Cout;
-    auto launch = [&]() {
-        const uint32_t npix = B * a.Hc * a.Wc;
-        hipLaunchKernelGGL(conv_x_kernel, dim3((npix + kPT - 1) / kPT, Cout / kCT), dim3(512), 0,
-                           st, a);
-        return check_launch("conv3x3_f16x3");
+    // classes (heaviest first) -> contiguous workgroup ranges padded to multiples of 8
+    uint32_t grid = 0, ntap = 0;
+    auto add_class = [&](uint32_t Hc, uint32_t Wc, uint32_t py, uint32_t px, uint32_t nt) {
+        ConvClass &c = a.cls[a.ncls++];
+        c.Hc = Hc;
+        c.Wc = Wc;
+        c.py = py;
+        c.px = px;
+        c.t0 = ntap - nt;
+        c.ntaps = nt;
+        c.tile0 = grid;
+        c.ntiles = (B * Hc * Wc + kPT - 1) / kPT * (Cout / kCT);
+        grid += (c.ntiles + 7) & ~7u;
     };
     if (!transposed) {
-        a.Hc = a.Hf = H;
-        a.Wc = a.Wf = W;
+        a.Hf = H;
+        a.Wf = W;
         a.sy = 1;
-        a.py = a.px = 0;
-        a.ntaps = 9;
         for (int t = 0; t < 9; ++t) {
             a.dy[t] = t / 3 - 1;
             a.dx[t] = t % 3 - 1;
             a.tap[t] = t;
         }
-        return launch();
+        ntap = 9;
+        add_class(H, W, 0, 0, 9);
+    } else {
+        // conv_transpose2d, stride 2: out (2a + ky, 2c + kx) <- x (a, c).  Parity class
+        // (py, px): output (2a' + py, 2c' + px) takes ky in {0, 2} (py = 0, input row
+        // a' - ky/2) or ky = 1 (py = 1, input row a'), likewise for x.
+        a.Hf = 2 * H + 1;
+        a.Wf = 2 * W + 1;
+        a.sy = 2;
+        for (uint32_t py = 0; py < 2; ++py)
+            for (uint32_t px = 0; px < 2; ++px) {
+                uint32_t nt = 0;
+                for (int ky = (int)py; ky < 3; ky += 2)
+                    for (int kx = (int)px; kx < 3; kx += 2) {
+                        a.dy[ntap] = -(ky >> 1);
+                        a.dx[ntap] = -(kx >> 1);
+                        a.tap[ntap] = (uint32_t)(ky * 3 + kx);
+                        ++ntap;
+                        ++nt;
+                    }
+                add_class(py ? H : H + 1, px ? W : W + 1, py, px, nt);
+            }
     }
-    // conv_transpose2d, stride 2: out (2a + ky, 2c + kx) <- x (a, c).  Parity class
-    // (py, px): output (2a' + py, 2c' + px) takes ky in {0, 2} (py = 0, input row
-    // a' - ky/2) or ky = 1 (py = 1, input row a'), likewise for x.
-    a.Hf = 2 * H + 1;
-    a.Wf = 2 * W + 1;
-    a.sy = 2;
-    for (uint32_t py = 0; py < 2; ++py)
-        for (uint32_t px = 0; px < 2; ++px) {
-            a.py = py;
-            a.px = px;
-            a.Hc = py ? H : H + 1;
-            a.Wc = px ? W : W + 1;
-            uint32_t nt = 0;
-            for (int ky = (int)py; ky < 3; ky += 2)
-                for (int kx = (int)px; kx < 3; kx += 2) {
-                    a.dy[nt] = -(ky >> 1);
-                    a.dx[nt] = -(kx >> 1);
-                    a.tap[nt] = (uint32_t)(ky * 3 + kx);
-                    ++nt;
-                }
-            a.ntaps = nt;
-            const int rc = launch();
-            if (rc) return rc;
-        }
-    return SDFR_OK;
+    hipLaunchKernelGGL(conv_x_kernel, dim3(grid), dim3(512), 0, st, a);
+    return check_launch("conv3x3_f16x3");
 }
 
 }  // extern "C"
