@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 3
+#define SDFR_ABI_VERSION 4
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -268,9 +268,9 @@ typedef struct sdfr_styled_epilogue_args {
     const float *rgb_b;           /* [3]                                           */
     const float *skip;            /* [B,3,H/2,W/2] or NULL                         */
     float *rgb;                   /* [B,3,H,W]                                     */
-    /* instead of y: the round-to-nearest fp16 split y = hi + lo as two [B,H,W,C]
-     * fp16 planes (the input format of sdfr_conv3x3_f16x3), or both NULL */
-    void *y_hi, *y_lo;
+    /* instead of y: the round-to-nearest fp16 split y = hi + lo in the split-NHWC
+     * layout below (the input format of sdfr_conv3x3_f16x3), or NULL */
+    void *y_split;
 } sdfr_styled_epilogue_args;
 
 int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *a, void *stream);
@@ -279,9 +279,13 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *a, void *stream);
  * the first ModulatedConv2d's modulation folded in).  C and H*W multiples of 4. */
 int sdfr_modulate_to_nhwc(float *y, const float *x, const float *s, uint32_t B, uint32_t C,
                           uint32_t HW, void *stream);
-/* The same with y written as the hi/lo fp16 split planes [B,H,W,C] each. */
-int sdfr_modulate_to_nhwc_split(void *y_hi, void *y_lo, const float *x, const float *s,
-                                uint32_t B, uint32_t C, uint32_t HW, void *stream);
+/* The same with y written in the split-NHWC layout (C % 8 == 0).
+ *
+ * Split-NHWC: the round-to-nearest fp16 split x = hi + lo of an NHWC fp32 tensor,
+ * fp16 [B,H,W,C/8,2,8]: per pixel and group of 8 channels, 8 hi then 8 lo
+ * halves (32 channels of one pixel = one 128-B line). */
+int sdfr_modulate_to_nhwc_split(void *y_split, const float *x, const float *s, uint32_t B,
+                                uint32_t C, uint32_t HW, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Decoder 3x3 convolutions on split-fp16 MFMA (no reference counterpart: they
@@ -291,9 +295,9 @@ int sdfr_modulate_to_nhwc_split(void *y_hi, void *y_lo, const float *x, const fl
  * sdfr_conv_pack_weights: w [Cout][Cin][3][3] (ModulatedConv2d.weight[0]) times
  *   scale -> su [Cout] (per-row power-of-two scale, written) and the packed hi/lo
  *   fp16 fragments (sdfr_conv_pack_bytes(Cout, Cin) - 4*Cout bytes).
- * sdfr_conv3x3_f16x3: input as the hi/lo fp16 split of an NHWC fp32 tensor (two
- *   [B,H,W,Cin] fp16 planes, x = x_hi + x_lo, as written by the *_split / y_hi
- *   outputs above), NHWC fp32 out, result multiplied by su[o]
+ * sdfr_conv3x3_f16x3: input in the split-NHWC layout ([B,H,W,Cin/8,2,8] fp16, as
+ *   written by the *_split / y_split outputs above), NHWC fp32 out, result
+ *   multiplied by su[o]
  *   (the caller folds 1/su into the demodulation -- exact, powers of two):
  *   transposed = 0: out [B,H,W,Cout] = conv2d(x, w, padding 1);
  *   transposed = 1: out [B,2H+1,2W+1,Cout] = conv_transpose2d(x, w^T, stride 2)
@@ -302,7 +306,7 @@ int sdfr_modulate_to_nhwc_split(void *y_hi, void *y_lo, const float *x, const fl
 size_t sdfr_conv_pack_bytes(uint32_t Cout, uint32_t Cin);
 int sdfr_conv_pack_weights(const float *w, float scale, uint32_t Cout, uint32_t Cin,
                            void *packed, float *su, void *stream);
-int sdfr_conv3x3_f16x3(float *out, const void *x_hi, const void *x_lo, const void *packed,
+int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
                        uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
                        int transposed, void *stream);
 

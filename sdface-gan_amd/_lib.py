@@ -23,7 +23,7 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 3
+ABI_VERSION = 4
 FIELD_F16X3 = 0
 FIELD_FP32 = 1
 
@@ -91,7 +91,7 @@ class StyledEpilogueArgs(ctypes.Structure):
         ("demod", _vp), ("noise", _vp), ("noise_weight", _vp), ("bias", _vp),
         ("negative_slope", _f32), ("act_scale", _f32),
         ("s_next", _vp), ("y", _vp), ("rgb_w", _vp), ("rgb_b", _vp), ("skip", _vp), ("rgb", _vp),
-        ("y_hi", _vp), ("y_lo", _vp),
+        ("y_split", _vp),
     ]
 
 
@@ -133,11 +133,11 @@ def lib():
     L.sdfr_upfirdn2d.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32] + [_int] * 8 + [_vp]
     L.sdfr_styled_epilogue.argtypes = [ctypes.POINTER(StyledEpilogueArgs), _vp]
     L.sdfr_modulate_to_nhwc.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _vp]
-    L.sdfr_modulate_to_nhwc_split.argtypes = [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp]
+    L.sdfr_modulate_to_nhwc_split.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _vp]
     L.sdfr_conv_pack_bytes.restype = ctypes.c_size_t
     L.sdfr_conv_pack_bytes.argtypes = [_u32, _u32]
     L.sdfr_conv_pack_weights.argtypes = [_vp, _f32, _u32, _u32, _vp, _vp, _vp]
-    L.sdfr_conv3x3_f16x3.argtypes = [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _int, _vp]
+    L.sdfr_conv3x3_f16x3.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _int, _vp]
     v = L.sdfr_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"libsdfr ABI {v} != expected {ABI_VERSION}; rebuild the library")

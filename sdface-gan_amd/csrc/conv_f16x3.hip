@@ -17,12 +17,13 @@
 //
 // Workgroup: 128 output channels x 256 output pixels, 8 waves of 64 x 64 (two per
 // SIMD), K in steps of 32 input channels at one tap.  Both operands arrive
-// already split (weights pre-packed in fragment order; activations as the hi/lo
-// fp16 planes the previous epilogue writes) and are staged global -> LDS by
-// LDS-DMA (buffer_load ... lds: no VGPRs, no VALU; the buffer range check
-// zero-fills the padding taps) through a 3-stage ring of 48 KB stages: two
-// K-steps stay in flight behind a counted vmcnt and a raw barrier, one
-// workgroup per CU.
+// already split (weights pre-packed in fragment order; activations in the
+// split-NHWC layout the previous epilogue writes, 32 channels of a pixel's hi and
+// lo = one 128-B line) and are staged global -> LDS by LDS-DMA (buffer_load ...
+// lds: no VGPRs, no VALU; the buffer range check zero-fills the padding taps)
+// through a 3-stage ring of 48 KB stages: two K-steps stay in flight behind a
+// counted vmcnt and a raw barrier, one workgroup per CU.  The workgroup order is
+// XCD-aware, and the four parity classes of a transposed conv share one launch.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -129,7 +130,7 @@ struct ConvClass {
 };
 
 struct ConvArgs {
-    const _Float16 *xh, *xl;       // [B, Hin, Win, Cin] hi / lo planes
+    const _Float16 *xs;            // split-NHWC [B, Hin, Win, Cin/8, 2, 8]
     const f4 *wpk;                 // packed fragments (above)
     float *out;                    // [B, Hf, Wf, Cout]
     uint32_t B, Hin, Win, Cin, Cout;
@@ -204,20 +205,22 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     const uint32_t nk = nC * ntaps;
 
     // LDS-DMA sources (6 pieces of 1 KB per wave per K-step).  Weights: the K-step's
-    // 16 KB block is contiguous; wave w moves pieces 2w, 2w+1.  Activations: wave w
-    // moves the hi and lo fragments of n-tiles 2w, 2w+1; lane (g = lane >> 4,
-    // n = lane & 15) fetches channels 8g .. 8g+7 of pixel 16 nt + n (16 B), so the
-    // LDS image is lane-linear = the fragment layout.
-    const uint32_t xbytes = a.B * a.Hin * a.Win * a.Cin * 2;
+    // 16 KB block is contiguous; wave w moves pieces 2w, 2w+1.  Activations: the 32
+    // channels of one pixel are one 128-B line of the split-NHWC input
+    // ([g 4][hi 8, lo 8] halves); a piece is 8 pixels = 8 whole lines, region
+    // (nt, half) of n-tile nt = pixels 16 nt + 8 half .. +7.  Lane l fetches pixel
+    // l & 7, channel group g = (l >> 3) & 3, plane h = l >> 5 to LDS unit l, so a
+    // region holds [h][g][pixel] and the fragment read below is conflict-free.
+    // Wave w moves regions (2w, 0..1) and (2w+1, 0..1).
+    const uint32_t xbytes = a.B * a.Hin * a.Win * a.Cin * 4;
     const v4i rw = make_rsrc(a.wpk, 9u * nC * nB * kStepF4 * 16u);
-    const v4i rh = make_rsrc(a.xh, xbytes);
-    const v4i rl = make_rsrc(a.xl, xbytes);
-    const uint32_t g8 = 8 * (lane >> 4);
-    int pb[2], pa[2], pc[2];
-    bool pv[2];
+    const v4i rx = make_rsrc(a.xs, xbytes);
+    const uint32_t loff = ((lane >> 3) & 3u) * 32u + (lane >> 5) * 16u;
+    int pb[4], pa[4], pc[4];
+    bool pv[4];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint32_t P = pix0 + (2 * wave + k) * 16 + (lane & 15u);
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t P = pix0 + (2 * wave + (k >> 1)) * 16 + (k & 1) * 8 + (lane & 7u);
         pv[k] = P < npix;
         const uint32_t Pc = pv[k] ? P : 0;
         const uint32_t hw = Hc * Wc;
@@ -237,20 +240,18 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
         }
         const int dy = a.dy[t], dx = a.dx[t];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < 4; ++k) {
             const int iy = pa[k] + dy, ix = pc[k] + dx;
             const bool ok = pv[k] && iy >= 0 && iy < (int)a.Hin && ix >= 0 && ix < (int)a.Win;
 #if CONV_ABL == 1   // ablation: activations from a tiny L2-resident window
-            const uint32_t off = ((lane & 15u) * a.Cin + c * 32 + g8) * 2u + 0 * (ok ? 1u : 0u);
+            const uint32_t off = ((lane & 7u) * a.Cin * 4u + c * 128u + loff) + 0 * (ok ? 1u : 0u);
 #else
             const uint32_t off =
-                ok ? ((((uint32_t)pb[k] * a.Hin + (uint32_t)iy) * a.Win + (uint32_t)ix) * a.Cin +
-                      c * 32 + g8) * 2u
+                ok ? (((uint32_t)pb[k] * a.Hin + (uint32_t)iy) * a.Win + (uint32_t)ix) * a.Cin * 4u +
+                         c * 128u + loff
                    : 0x7FFFFFF0u;                      // past num_records: zero fill
 #endif
-            const uint32_t nt = 2 * wave + k;
-            dma16(rh, off, 0u, lds_addr(&Bs[buf][(nt * 2) * 64]));
-            dma16(rl, off, 0u, lds_addr(&Bs[buf][(nt * 2 + 1) * 64]));
+            dma16(rx, off, 0u, lds_addr(&Bs[buf][(4 * wave + k) * 64]));
         }
     };
 
@@ -261,13 +262,15 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
         for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
     // Fragments of one K-step: [0..3] A hi, [4..7] A lo, [8..11] B hi, [12..15] B lo.
+    // B lane (g = lane >> 4, n = lane & 15): region (nt, n >> 3), unit h 32 + 8 g + (n & 7).
+    const uint32_t boff = ((lane >> 3) & 1u) * 64u + (lane >> 4) * 8u + (lane & 7u);
     auto read_frags = [&](f4 (&R)[16], uint32_t st) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             R[i] = As[st][((4 * wm + i) * 2) * 64 + lane];
             R[4 + i] = As[st][((4 * wm + i) * 2 + 1) * 64 + lane];
-            R[8 + i] = Bs[st][((4 * wn + i) * 2) * 64 + lane];
-            R[12 + i] = Bs[st][((4 * wn + i) * 2 + 1) * 64 + lane];
+            R[8 + i] = Bs[st][((4 * wn + i) * 2) * 64 + boff];
+            R[12 + i] = Bs[st][((4 * wn + i) * 2) * 64 + boff + 32];
         }
     };
     // rows i0 .. i0+nr-1 of the wave's 4 x 4 tiles; per A fragment the three split
@@ -293,11 +296,19 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     // fragments are read while rows 2-3 of step ks compute.
     auto step = [&](uint32_t ks, const f4 (&R)[16], f4 (&Rn)[16]) {
         mfma_rows(R, 0, 2);
+#if CONV_ABL == 4      // ablation: never wait for the DMA
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
         if (ks + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+#if CONV_ABL != 5      // 5: ablation without the barrier
         __builtin_amdgcn_s_barrier();
+#endif
         const uint32_t st = ks % 3u;
+#if CONV_ABL != 6      // 6: ablation without in-loop staging
         if (ks + 3 < nk) issue_step(ks + 3, st);
+#endif
         if (ks + 1 < nk) read_frags(Rn, st == 2 ? 0u : st + 1);
         mfma_rows(R, 2, 2);
     };
@@ -316,6 +327,9 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
         step(ks + 1, R1, R0);
     }
     if (ks < nk) step(ks, R0, R1);
+#if CONV_ABL == 4
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 #else
     // Ring: step ks in stage ks % 3; steps ks+1, ks+2 in flight while ks computes.
     // Stage (ks+2) % 3 last held step ks-1, whose reads every wave completed before
@@ -390,18 +404,17 @@ int sdfr_conv_pack_weights(const float *w, float scale, uint32_t Cout, uint32_t 
     return check_launch("conv_pack_weights: pack");
 }
 
-int sdfr_conv3x3_f16x3(float *out, const void *x_hi, const void *x_lo, const void *packed,
+int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
                        uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
                        int transposed, void *stream) {
-    if (!out || !x_hi || !x_lo || !packed) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
+    if (!out || !x_split || !packed) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
     if (B == 0 || H == 0 || W == 0 || Cout % kCT || Cin % 32 || Cin == 0 || Cout == 0)
         return fail(SDFR_EINVAL, "conv3x3_f16x3: bad shape (Cout % 128, Cin % 32)");
-    if ((uint64_t)B * H * W * Cin * 2 >= (1ull << 31) || 9ull * Cin * Cout * 4 >= (1ull << 31))
+    if ((uint64_t)B * H * W * Cin * 4 >= (1ull << 31) || 9ull * Cin * Cout * 4 >= (1ull << 31))
         return fail(SDFR_EINVAL, "conv3x3_f16x3: tensor too large for 32-bit offsets (split B)");
     hipStream_t st = (hipStream_t)stream;
     ConvArgs a{};
-    a.xh = reinterpret_cast<const _Float16 *>(x_hi);
-    a.xl = reinterpret_cast<const _Float16 *>(x_lo);
+    a.xs = reinterpret_cast<const _Float16 *>(x_split);
     a.wpk = reinterpret_cast<const f4 *>(packed);
     a.out = out;
     a.B = B;

@@ -120,26 +120,31 @@ struct EpiArgs {
     float *y;
     const float *rgb_w, *rgb_b, *skip;
     float *rgb;
-    _Float16 *yh, *yl;     // split fp16 output planes (instead of y) or null
+    _Float16 *ys;          // split-NHWC fp16 output (instead of y) or null
 };
 
 typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 
-// y (pre-multiplied by the next modulation) as fp32, or as the round-to-nearest
-// hi/lo fp16 split the split-fp16 convolution consumes (conv_f16x3.hip)
+// Round-to-nearest hi/lo fp16 split of 4 channels c .. c+3 (c % 4 == 0, C % 8 == 0)
+// at NHWC element index idx = pix C + c, stored split-NHWC ([pix][C/8][hi 8, lo 8]):
+// hi at 2 idx - (c & 7), lo 8 halves further.
+__device__ __forceinline__ void store_split4(_Float16 *ys, size_t idx, float4 v) {
+    h4v h, l;
+    h[0] = (_Float16)v.x; h[1] = (_Float16)v.y; h[2] = (_Float16)v.z; h[3] = (_Float16)v.w;
+    l[0] = (_Float16)(v.x - (float)h[0]);
+    l[1] = (_Float16)(v.y - (float)h[1]);
+    l[2] = (_Float16)(v.z - (float)h[2]);
+    l[3] = (_Float16)(v.w - (float)h[3]);
+    const size_t o = 2 * idx - (idx & 7u);
+    *reinterpret_cast<h4v *>(ys + o) = h;
+    *reinterpret_cast<h4v *>(ys + o + 8) = l;
+}
+
+// y (pre-multiplied by the next modulation) as fp32, or as the split-NHWC fp16
+// the split-fp16 convolution consumes (conv_f16x3.hip)
 __device__ __forceinline__ void store_y(const EpiArgs &a, size_t idx, float4 v) {
-    if (a.yh) {
-        h4v h, l;
-        h[0] = (_Float16)v.x; h[1] = (_Float16)v.y; h[2] = (_Float16)v.z; h[3] = (_Float16)v.w;
-        l[0] = (_Float16)(v.x - (float)h[0]);
-        l[1] = (_Float16)(v.y - (float)h[1]);
-        l[2] = (_Float16)(v.z - (float)h[2]);
-        l[3] = (_Float16)(v.w - (float)h[3]);
-        *reinterpret_cast<h4v *>(a.yh + idx) = h;
-        *reinterpret_cast<h4v *>(a.yl + idx) = l;
-    } else {
-        *reinterpret_cast<float4 *>(a.y + idx) = v;
-    }
+    if (a.ys) store_split4(a.ys, idx, v);
+    else *reinterpret_cast<float4 *>(a.y + idx) = v;
 }
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -181,11 +186,15 @@ __device__ float skip_up(const float *__restrict__ img, uint32_t h2, uint32_t w2
 
 constexpr uint32_t kEpiPixPerBlock = 64;
 
-// Plain epilogue: lanes of a wave split the C channels of PPW = 64/TPP pixels
-// (TPP threads x NQ float4 per pixel, TPP <= 16 so a wave works on >= 4 pixels
-// at once); the 1x1 ToRGB is a TPP-lane reduction (log2 TPP shuffle steps).
+// Plain epilogue: TPP lanes per pixel (C/4 up to 16, 16 up to C = 256, 64 above),
+// NQ = C/(4 TPP) float4 each,
+// PPW = 64/TPP pixels per wave at a time; the 1x1 ToRGB is a TPP-lane reduction
+// (log2 TPP shuffle steps).  Few channels per lane keep the per-channel constants
+// small (high occupancy), and CH pixel rounds are loaded before any is used so
+// ~8 float4 per lane are in flight (the pass is HBM-bound).
 template <int NQ, bool RGB>
 __global__ __launch_bounds__(256) void epi_plain_kernel(EpiArgs a, uint32_t tpp_log2) {
+    constexpr int CH = NQ >= 8 ? 1 : 8 / NQ;
     const uint32_t TPP = 1u << tpp_log2;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t q = lane & (TPP - 1), g = lane >> tpp_log2;
@@ -207,19 +216,32 @@ __global__ __launch_bounds__(256) void epi_plain_kernel(EpiArgs a, uint32_t tpp_
     }
     const float nw = a.noise ? *a.noise_weight : 0.0f;
     const uint32_t p0 = blockIdx.x * kEpiPixPerBlock;
-    for (uint32_t pp = wave * ppw + g; pp < kEpiPixPerBlock; pp += 4 * ppw) {
-        const uint32_t p = p0 + pp;
-        const bool live = p < HW;
-        float acc[3] = {0.f, 0.f, 0.f};
-        if (live) {
-            const float nz = a.noise ? nw * a.noise[(size_t)b * HW + p] : 0.0f;
+    const uint32_t step = 4 * ppw;                       // pixels between a lane's rounds
+    for (uint32_t pp0 = wave * ppw + g; pp0 < kEpiPixPerBlock; pp0 += CH * step) {
+        float4 cv[CH][NQ];
+        float nz[CH];
+#pragma unroll
+        for (int r = 0; r < CH; ++r) {
+            const uint32_t pp = pp0 + r * step, p = p0 + pp;
+            const bool live = pp < kEpiPixPerBlock && p < HW;
+            const size_t base = ((size_t)b * HW + (live ? p : 0)) * C;
+            nz[r] = (a.noise && live) ? nw * a.noise[(size_t)b * HW + p] : 0.0f;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k)
+                cv[r][k] = live ? ld4(a.conv + base + 4 * (q + k * TPP)) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int r = 0; r < CH; ++r) {
+            const uint32_t pp = pp0 + r * step, p = p0 + pp;
+            const bool live = pp < kEpiPixPerBlock && p < HW;
+            if (!RGB && !live) continue;
             const size_t base = ((size_t)b * HW + p) * C;
+            float acc[3] = {0.f, 0.f, 0.f};
 #pragma unroll
             for (int k = 0; k < NQ; ++k) {
                 const uint32_t c = 4 * (q + k * TPP);
-                const float4 v = act4(ld4(a.conv + base + c), dm[k], nz, bs[k], a.slope,
-                                      a.act_scale);
-                if (a.y || a.yh)
+                const float4 v = act4(cv[r][k], dm[k], nz[r], bs[k], a.slope, a.act_scale);
+                if (live && (a.y || a.ys))
                     store_y(a, base + c,
                             make_float4(v.x * sn[k].x, v.y * sn[k].y, v.z * sn[k].z, v.w * sn[k].w));
                 if (RGB) {
@@ -232,21 +254,19 @@ __global__ __launch_bounds__(256) void epi_plain_kernel(EpiArgs a, uint32_t tpp_
                     }
                 }
             }
-        }
-        if (RGB) {
-            for (uint32_t off = TPP >> 1; off; off >>= 1) {
+            if (RGB) {
+                for (uint32_t off = TPP >> 1; off; off >>= 1) {
 #pragma unroll
-                for (int o = 0; o < 3; ++o) acc[o] += __shfl_xor(acc[o], off, 64);
-            }
-            if (live && q == 0) {
-                const int yy = (int)(p / a.W), xx = (int)(p % a.W);
-#pragma unroll
-                for (int o = 0; o < 3; ++o) {
-                    float v = acc[o] + a.rgb_b[o];
+                    for (int o = 0; o < 3; ++o) acc[o] += __shfl_xor(acc[o], off, 64);
+                }
+                // the butterfly left the sums in every lane: lane q < 3 finishes channel q
+                if (live && q < 3) {
+                    const int yy = (int)(p / a.W), xx = (int)(p % a.W);
+                    float v = (q == 0 ? acc[0] : q == 1 ? acc[1] : acc[2]) + a.rgb_b[q];
                     if (a.skip)
-                        v = v + skip_up(a.skip + ((size_t)b * 3 + o) * (HW / 4), a.H / 2, a.W / 2,
+                        v = v + skip_up(a.skip + ((size_t)b * 3 + q) * (HW / 4), a.H / 2, a.W / 2,
                                         yy, xx, a.fir);
-                    a.rgb[((size_t)b * 3 + o) * HW + p] = v;
+                    a.rgb[((size_t)b * 3 + q) * HW + p] = v;
                 }
             }
         }
@@ -314,8 +334,7 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg)
 // NCHW -> NHWC with modulation, 64 x 64 LDS tiles
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void modulate_nhwc_kernel(float *__restrict__ y,
-                                                            _Float16 *__restrict__ yh,
-                                                            _Float16 *__restrict__ yl,
+                                                            _Float16 *__restrict__ ys,
                                                             const float *__restrict__ x,
                                                             const float *__restrict__ s,
                                                             uint32_t C, uint32_t HW) {
@@ -343,18 +362,8 @@ __global__ __launch_bounds__(256) void modulate_nhwc_kernel(float *__restrict__ 
             const float4 v =
                 make_float4(tile[cl][pl], tile[cl + 1][pl], tile[cl + 2][pl], tile[cl + 3][pl]);
             const size_t idx = ((size_t)b * HW + p) * C + c;
-            if (yh) {
-                h4v h, l;
-                h[0] = (_Float16)v.x; h[1] = (_Float16)v.y; h[2] = (_Float16)v.z; h[3] = (_Float16)v.w;
-                l[0] = (_Float16)(v.x - (float)h[0]);
-                l[1] = (_Float16)(v.y - (float)h[1]);
-                l[2] = (_Float16)(v.z - (float)h[2]);
-                l[3] = (_Float16)(v.w - (float)h[3]);
-                *reinterpret_cast<h4v *>(yh + idx) = h;
-                *reinterpret_cast<h4v *>(yl + idx) = l;
-            } else {
-                *reinterpret_cast<float4 *>(y + idx) = v;
-            }
+            if (ys) store_split4(ys, idx, v);
+            else *reinterpret_cast<float4 *>(y + idx) = v;
         }
     }
 }
@@ -428,17 +437,18 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
     const bool rgb = s.rgb_w != nullptr;
     if (rgb && (!s.rgb || !s.rgb_b)) return fail(SDFR_EINVAL, "styled_epilogue: rgb output missing");
     if (rgb && s.blur_up) return fail(SDFR_EINVAL, "styled_epilogue: ToRGB after a blur is not fused");
-    if (!rgb && !s.y && !s.y_hi) return fail(SDFR_EINVAL, "styled_epilogue: nothing to write");
-    if (s.y && s.y_hi) return fail(SDFR_EINVAL, "styled_epilogue: y and y_hi/y_lo are exclusive");
-    if (!s.y_hi != !s.y_lo) return fail(SDFR_EINVAL, "styled_epilogue: y_hi and y_lo go together");
+    if (!rgb && !s.y && !s.y_split) return fail(SDFR_EINVAL, "styled_epilogue: nothing to write");
+    if (s.y && s.y_split) return fail(SDFR_EINVAL, "styled_epilogue: y and y_split are exclusive");
+    if (s.y_split && s.C % 8) return fail(SDFR_EINVAL, "styled_epilogue: y_split needs C % 8 == 0");
     if (s.skip && (s.H % 2 || s.W % 2)) return fail(SDFR_EINVAL, "styled_epilogue: odd size with skip");
     for (const void *q : {(const void *)s.conv, (const void *)s.demod, (const void *)s.bias,
-                          (const void *)s.s_next, (const void *)s.y, (const void *)s.rgb_w})
+                          (const void *)s.s_next, (const void *)s.y, (const void *)s.rgb_w,
+                          (const void *)s.y_split})
         if (q && !aligned16(q)) return fail(SDFR_EINVAL, "styled_epilogue: pointers must be 16-B aligned");
     EpiArgs a{s.B, s.C, s.H, s.W, s.conv, {s.fir[0], s.fir[1], s.fir[2], s.fir[3]},
               s.demod, s.noise, s.noise_weight, s.bias, s.negative_slope, s.act_scale,
               s.s_next, s.y, s.rgb_w, s.rgb_b, s.skip, s.rgb,
-              reinterpret_cast<_Float16 *>(s.y_hi), reinterpret_cast<_Float16 *>(s.y_lo)};
+              reinterpret_cast<_Float16 *>(s.y_split)};
     hipStream_t st = (hipStream_t)stream;
     if (s.blur_up) {
         const uint32_t nseg = (s.H + kBlurRows - 1) / kBlurRows;
@@ -451,12 +461,12 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
     if (Q <= 64 ? !pow2 : (Q % 64 != 0))
         return fail(SDFR_EUNSUPPORTED,
                     "styled_epilogue: C/4 must be a power of two <= 64 or a multiple of 64");
-    // TPP = min(Q, 16) lanes per pixel, NQ = Q / TPP float4 each (<= 8: C <= 512);
-    // wider channels (Q a multiple of 64) use a whole wave per pixel, NQ = Q / 64
+    // TPP lanes per pixel, NQ = Q / TPP float4 each: a 16-lane ToRGB reduction up to
+    // C = 256 (NQ <= 4), whole waves above
     uint32_t tpp_log2 = 0, nq = 1;
     if (Q <= 16) {
         while ((1u << tpp_log2) < Q) ++tpp_log2;
-    } else if (Q <= 128) {
+    } else if (Q <= 64) {
         tpp_log2 = 4;
         nq = Q / 16;
     } else {
@@ -481,31 +491,31 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
     return check_launch("styled_epilogue");
 }
 
-static int modulate_common(float *y, void *yh, void *yl, const float *x, const float *s,
-                           uint32_t B, uint32_t C, uint32_t HW, void *stream) {
+static int modulate_common(float *y, void *ys, const float *x, const float *s, uint32_t B,
+                           uint32_t C, uint32_t HW, void *stream) {
     if (B == 0 || C == 0 || HW == 0) return SDFR_OK;
-    if ((!y && !yh) || !x || !s || (yh && !yl))
-        return fail(SDFR_EINVAL, "modulate_to_nhwc: null tensor pointer");
+    if ((!y && !ys) || !x || !s) return fail(SDFR_EINVAL, "modulate_to_nhwc: null tensor pointer");
     if (C % 4 || HW % 4) return fail(SDFR_EINVAL, "modulate_to_nhwc: C and H*W must be multiples of 4");
-    if (!aligned16(x) || (y && !aligned16(y)))
+    if (ys && C % 8) return fail(SDFR_EINVAL, "modulate_to_nhwc_split: C must be a multiple of 8");
+    if (!aligned16(x) || (y && !aligned16(y)) || (ys && !aligned16(ys)))
         return fail(SDFR_EINVAL, "modulate_to_nhwc: pointers must be 16-B aligned");
     dim3 grid((HW + 63) / 64, (C + 63) / 64, B);
     modulate_nhwc_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(
-        y, reinterpret_cast<_Float16 *>(yh), reinterpret_cast<_Float16 *>(yl), x, s, C, HW);
+        y, reinterpret_cast<_Float16 *>(ys), x, s, C, HW);
     return check_launch("modulate_to_nhwc");
 }
 
 int sdfr_modulate_to_nhwc(float *y, const float *x, const float *s, uint32_t B, uint32_t C,
                           uint32_t HW, void *stream) {
     if (!y && B && C && HW) return fail(SDFR_EINVAL, "modulate_to_nhwc: null tensor pointer");
-    return modulate_common(y, nullptr, nullptr, x, s, B, C, HW, stream);
+    return modulate_common(y, nullptr, x, s, B, C, HW, stream);
 }
 
-int sdfr_modulate_to_nhwc_split(void *y_hi, void *y_lo, const float *x, const float *s,
-                                uint32_t B, uint32_t C, uint32_t HW, void *stream) {
-    if ((!y_hi || !y_lo) && B && C && HW)
+int sdfr_modulate_to_nhwc_split(void *y_split, const float *x, const float *s, uint32_t B,
+                                uint32_t C, uint32_t HW, void *stream) {
+    if (!y_split && B && C && HW)
         return fail(SDFR_EINVAL, "modulate_to_nhwc_split: null tensor pointer");
-    return modulate_common(nullptr, y_hi, y_lo, x, s, B, C, HW, stream);
+    return modulate_common(nullptr, y_split, x, s, B, C, HW, stream);
 }
 
 }  // extern "C"

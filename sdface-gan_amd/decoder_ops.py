@@ -256,17 +256,16 @@ def styled_epilogue(conv, *, fir, bias, noise_weight, noise=None, demod=None, bl
 
     conv: channels_last [B,C,Hc,Wc] (Hc = 2H+1 when blur_up).  Returns
     (y, rgb [B,3,H,W] or None) with y channels_last [B,C,H,W], or with split_y the
-    pair of fp16 NHWC planes (hi, lo) [B,H,W,C] that conv3x3_f16x3 reads, or None."""
+    split-NHWC fp16 tensor [B,H,W,C/8,2,8] that conv3x3_f16x3 reads, or None."""
     _require_cuda(conv)
     B, C, Hc, Wc = conv.shape
     H, W = (Hc - 1, Wc - 1) if blur_up else (Hc, Wc)
     conv = conv.contiguous(memory_format=torch.channels_last)
     y = (torch.empty(B, C, H, W, device=conv.device, memory_format=torch.channels_last)
          if store_y and not split_y else None)
-    yh = yl = None
+    ys = None
     if store_y and split_y:
-        yh = torch.empty(B, H, W, C, device=conv.device, dtype=torch.float16)
-        yl = torch.empty_like(yh)
+        ys = torch.empty(B, H, W, C // 8, 2, 8, device=conv.device, dtype=torch.float16)
     rgb = torch.empty(B, 3, H, W, device=conv.device) if rgb_w is not None else None
     if noise is not None:
         noise = noise.expand(B, 1, H, W).contiguous()
@@ -297,9 +296,9 @@ def styled_epilogue(conv, *, fir, bias, noise_weight, noise=None, demod=None, bl
     a.rgb_b = cptr(None if rgb_b is None else rgb_b.reshape(-1))
     a.skip = cptr(skip)
     a.rgb = _lib.ptr(rgb)
-    a.y_hi, a.y_lo = _lib.ptr(yh), _lib.ptr(yl)
+    a.y_split = _lib.ptr(ys)
     _lib.check(_lib.lib().sdfr_styled_epilogue(a, _lib.stream_of(conv)), "styled_epilogue")
-    return ((yh, yl) if split_y and store_y else y), rgb
+    return (ys if split_y and store_y else y), rgb
 
 
 # ---------------------------------------------------------------------------
@@ -321,42 +320,50 @@ def conv_pack_weights(weight, scale):
 
 
 def split_nhwc(x):
-    """fp32 tensor (any layout, logically [B,C,H,W]) -> the round-to-nearest fp16 split
-    (hi, lo) as contiguous NHWC planes (x = hi + lo to ~2^-22)."""
-    xh = x.permute(0, 2, 3, 1).contiguous()
+    """fp32 tensor (any layout, logically [B,C,H,W], C % 8 == 0) -> the round-to-nearest
+    fp16 split x = hi + lo (to ~2^-22) in the split-NHWC layout [B,H,W,C/8,2,8]: per
+    pixel and group of 8 channels, 8 hi then 8 lo halves (include/sdfr.h)."""
+    B, C, H, W = x.shape
+    xh = x.permute(0, 2, 3, 1).reshape(B, H, W, C // 8, 1, 8)
     hi = xh.half()
     lo = (xh - hi.float()).half()
-    return hi, lo
+    return torch.cat([hi, lo], dim=4).contiguous()
+
+
+def unsplit_nhwc(xs):
+    """split-NHWC [B,H,W,C/8,2,8] fp16 -> (hi, lo) NHWC fp16 planes [B,H,W,C]."""
+    B, H, W = xs.shape[:3]
+    return xs[:, :, :, :, 0].reshape(B, H, W, -1), xs[:, :, :, :, 1].reshape(B, H, W, -1)
 
 
 def conv3x3_f16x3(x_split, packed, Cout, transposed=False):
-    """x_split = (hi, lo) fp16 NHWC planes [B, H, W, Cin] -> channels_last fp32
-    [B, Cout, H, W] (conv2d, pad 1) or [B, Cout, 2H+1, 2W+1] (conv_transpose2d stride 2),
-    scaled by su (conv_pack_weights)."""
-    xh, xl = x_split
-    _require_cuda(xh, xl)
-    B, H, W, Cin = xh.shape
-    if xh.dtype != torch.float16 or xl.dtype != torch.float16 or xh.shape != xl.shape \
-            or not xh.is_contiguous() or not xl.is_contiguous():
-        raise RuntimeError("conv3x3_f16x3: x_split must be two contiguous fp16 NHWC planes")
+    """x_split = split-NHWC fp16 [B, H, W, Cin/8, 2, 8] (split_nhwc) -> channels_last
+    fp32 [B, Cout, H, W] (conv2d, pad 1) or [B, Cout, 2H+1, 2W+1] (conv_transpose2d
+    stride 2), scaled by su (conv_pack_weights)."""
+    _require_cuda(x_split)
+    if x_split.dtype != torch.float16 or x_split.dim() != 6 or x_split.shape[4:] != (2, 8) \
+            or not x_split.is_contiguous():
+        raise RuntimeError("conv3x3_f16x3: x_split must be a contiguous split-NHWC fp16 "
+                           "tensor [B,H,W,Cin/8,2,8]")
+    B, H, W, Cin = x_split.shape[0], x_split.shape[1], x_split.shape[2], 8 * x_split.shape[3]
     Ho, Wo = (2 * H + 1, 2 * W + 1) if transposed else (H, W)
-    out = torch.empty(B, Cout, Ho, Wo, device=xh.device, memory_format=torch.channels_last)
-    _lib.check(_lib.lib().sdfr_conv3x3_f16x3(_lib.ptr(out), _lib.ptr(xh), _lib.ptr(xl),
+    out = torch.empty(B, Cout, Ho, Wo, device=x_split.device, memory_format=torch.channels_last)
+    _lib.check(_lib.lib().sdfr_conv3x3_f16x3(_lib.ptr(out), _lib.ptr(x_split),
                                              _lib.ptr(packed), B, H, W, Cin, Cout,
-                                             int(bool(transposed)), _lib.stream_of(xh)),
+                                             int(bool(transposed)), _lib.stream_of(x_split)),
                "conv3x3_f16x3")
     return out
 
 
 def modulate_to_nhwc_split(x, s):
-    """(x * s[:, :, None, None]) as the (hi, lo) fp16 NHWC planes, from NCHW fp32 x."""
+    """(x * s[:, :, None, None]) in the split-NHWC fp16 layout [B,H,W,C/8,2,8], from
+    NCHW fp32 x."""
     _require_cuda(x, s)
     B, C, H, W = x.shape
     x = x.contiguous()
     s = s.contiguous()
-    hi = torch.empty(B, H, W, C, device=x.device, dtype=torch.float16)
-    lo = torch.empty_like(hi)
-    _lib.check(_lib.lib().sdfr_modulate_to_nhwc_split(_lib.ptr(hi), _lib.ptr(lo), _lib.ptr(x),
-                                                      _lib.ptr(s), B, C, H * W,
-                                                      _lib.stream_of(x)), "modulate_to_nhwc_split")
-    return hi, lo
+    ys = torch.empty(B, H, W, C // 8, 2, 8, device=x.device, dtype=torch.float16)
+    _lib.check(_lib.lib().sdfr_modulate_to_nhwc_split(_lib.ptr(ys), _lib.ptr(x), _lib.ptr(s),
+                                                      B, C, H * W, _lib.stream_of(x)),
+               "modulate_to_nhwc_split")
+    return ys

@@ -169,11 +169,16 @@ def test_styled_epilogue_rejects_bad_channels(ops):
 
 def test_split_planes_bit_exact(ops):
     """modulate_to_nhwc_split and the epilogue's split y write exactly the
-    round-to-nearest (hi, lo) fp16 split of their fp32 result."""
+    round-to-nearest (hi, lo) fp16 split of their fp32 result, in the split-NHWC
+    layout [B,H,W,C/8,2,8] (also split_nhwc's, which the conv tests feed)."""
     g = torch.Generator().manual_seed(3)
     x = torch.randn(2, 64, 8, 12, generator=g)
     s = torch.rand(2, 64, generator=g) + 0.5
-    hi, lo = ops.modulate_to_nhwc_split(x.to(DEV), s.to(DEV))
+    xs = ops.modulate_to_nhwc_split(x.to(DEV), s.to(DEV))
+    assert xs.shape == (2, 8, 12, 8, 2, 8) and xs.dtype == torch.float16
+    np.testing.assert_array_equal(xs.cpu().numpy(),
+                                  ops.split_nhwc(x * s[:, :, None, None]).numpy())
+    hi, lo = ops.unsplit_nhwc(xs)
     ref = (x * s[:, :, None, None]).permute(0, 2, 3, 1).contiguous()
     rh = ref.half()
     np.testing.assert_array_equal(hi.cpu().numpy(), rh.numpy())
@@ -185,7 +190,8 @@ def test_split_planes_bit_exact(ops):
               noise=torch.randn(2, 1, 8, 12, device=DEV), demod=torch.rand(2, 64, device=DEV),
               s_next=torch.rand(2, 64, device=DEV))
     y, _ = ops.styled_epilogue(conv, **kw)
-    (yh, yl), _ = ops.styled_epilogue(conv, split_y=True, **kw)
+    ys, _ = ops.styled_epilogue(conv, split_y=True, **kw)
+    yh, yl = ops.unsplit_nhwc(ys)
     ref = y.permute(0, 2, 3, 1).contiguous().cpu()
     np.testing.assert_array_equal(yh.cpu().numpy(), ref.half().numpy())
     np.testing.assert_array_equal(yl.cpu().numpy(), (ref - ref.half().float()).half().numpy())
