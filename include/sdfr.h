@@ -310,6 +310,38 @@ int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
                        uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
                        int transposed, void *stream);
 
+/* The regular (transposed = 0) convolution with the plain styled epilogue fused
+ * into it (the conv output never goes to memory): per pixel and channel
+ *   v = lrelu((conv * demod[b,c] + noise_weight * noise[b,h,w]) + bias[c],
+ *             negative_slope) * act_scale         (demod already divided by su)
+ *   y_split = v * s_next[b,c] in split-NHWC (s_next NULL -> v), when y_split
+ *   rgb_partial[k,b,o,h,w] = sum_{c in [128k, 128k+128)} v * rgb_w[b,o,c], when
+ *   rgb_w (k < Cout/128; sdfr_rgb_finish adds the parts, bias and skip).
+ * Same operation order as sdfr_styled_epilogue for v and y.  H*W % 256 == 0. */
+typedef struct sdfr_conv_act_args {
+    const void *x_split;          /* [B,H,W,Cin/8,2,8] fp16                         */
+    const void *packed;           /* sdfr_conv_pack_weights                         */
+    uint32_t B, H, W, Cin, Cout;
+    const float *demod;           /* [B,Cout]                                       */
+    const float *noise;           /* [B,H,W] or NULL                                */
+    const float *noise_weight;    /* [1] (device)                                   */
+    const float *bias;            /* [Cout]                                         */
+    float negative_slope, act_scale;
+    const float *s_next;          /* [B,Cout] or NULL                               */
+    void *y_split;                /* [B,H,W,Cout/8,2,8] fp16 or NULL                */
+    const float *rgb_w;           /* [B,3,Cout] modulated ToRGB weight or NULL      */
+    float *rgb_partial;           /* [Cout/128,B,3,H,W] fp32 (with rgb_w)           */
+} sdfr_conv_act_args;
+
+int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *a, void *stream);
+
+/* ToRGB finish: rgb [B,3,H,W] = sum_k partial[k] + rgb_b[o]
+ *   + upfirdn2d(skip, outer(fir,fir), up 2, pad (2,1)) when skip != NULL
+ * (partial [nparts,B,3,H,W], skip [B,3,H/2,W/2], fir: 4 host floats). */
+int sdfr_rgb_finish(float *rgb, const float *partial, uint32_t nparts, const float *rgb_b,
+                    const float *skip, const float *fir, uint32_t B, uint32_t H, uint32_t W,
+                    void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -38,6 +38,7 @@ EXPORTS = (
     "sdfr_fused_bias_act", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
     "sdfr_modulate_to_nhwc_split",
     "sdfr_conv_pack_bytes", "sdfr_conv_pack_weights", "sdfr_conv3x3_f16x3",
+    "sdfr_conv3x3_f16x3_act", "sdfr_rgb_finish",
 )
 
 
@@ -95,6 +96,17 @@ class StyledEpilogueArgs(ctypes.Structure):
     ]
 
 
+class ConvActArgs(ctypes.Structure):
+    """sdfr_conv_act_args (include/sdfr.h)."""
+    _fields_ = [
+        ("x_split", _vp), ("packed", _vp),
+        ("B", _u32), ("H", _u32), ("W", _u32), ("Cin", _u32), ("Cout", _u32),
+        ("demod", _vp), ("noise", _vp), ("noise_weight", _vp), ("bias", _vp),
+        ("negative_slope", _f32), ("act_scale", _f32),
+        ("s_next", _vp), ("y_split", _vp), ("rgb_w", _vp), ("rgb_partial", _vp),
+    ]
+
+
 _lib = None
 
 
@@ -138,6 +150,9 @@ def lib():
     L.sdfr_conv_pack_bytes.argtypes = [_u32, _u32]
     L.sdfr_conv_pack_weights.argtypes = [_vp, _f32, _u32, _u32, _vp, _vp, _vp]
     L.sdfr_conv3x3_f16x3.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _int, _vp]
+    L.sdfr_conv3x3_f16x3_act.argtypes = [ctypes.POINTER(ConvActArgs), _vp]
+    L.sdfr_rgb_finish.argtypes = [_vp, _vp, _u32, _vp, _vp, ctypes.POINTER(_f32), _u32, _u32,
+                                  _u32, _vp]
     v = L.sdfr_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"libsdfr ABI {v} != expected {ABI_VERSION}; rebuild the library")

@@ -129,6 +129,16 @@ struct ConvClass {
     uint32_t tile0, ntiles;        // workgroups [tile0, tile0 + pad8(ntiles)) of the grid
 };
 
+// Styled epilogue fused into a regular conv (sdfr_conv3x3_f16x3_act).
+struct ActEpi {
+    const float *demod, *noise, *noise_weight, *bias;   // [B,Cout], [B,H,W], [1], [Cout]
+    float slope, scale;
+    const float *s_next;           // [B,Cout] or null
+    _Float16 *ys;                  // split-NHWC [B,H,W,Cout] or null
+    const float *rgb_w;            // [B,3,Cout] or null
+    float *rgbp;                   // [Cout/128, B, 3, H*W] ToRGB partial sums
+};
+
 struct ConvArgs {
     const _Float16 *xs;            // split-NHWC [B, Hin, Win, Cin/8, 2, 8]
     const f4 *wpk;                 // packed fragments (above)
@@ -139,6 +149,7 @@ struct ConvArgs {
     ConvClass cls[4];
     int dy[9], dx[9];              // input pixel = (a + dy, c + dx)
     uint32_t tap[9];               // packed weight tap (3 ky + kx)
+    ActEpi e;                      // conv_x_kernel<true> only
 };
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -173,6 +184,30 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)reinterpret_cast<uintptr_t>(p);
 }
 
+__device__ __forceinline__ float act1(float c, float dm, float nz, float b, float slope,
+                                      float scale) {
+    float v = c * dm;                  // same operation order as decoder.hip's epilogue
+    v = v + nz;
+    v = v + b;
+    v = v > 0.0f ? v : v * slope;
+    return v * scale;
+}
+
+// Round-to-nearest hi/lo split of 4 channels at NHWC element index idx (C % 8 == 0)
+// into split-NHWC (decoder.hip store_split4).
+__device__ __forceinline__ void store_split4(_Float16 *ys, size_t idx, f4 v) {
+    h4 h, l;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        h[r] = (_Float16)v[r];
+        l[r] = (_Float16)(v[r] - (float)h[r]);
+    }
+    const size_t o = 2 * idx - (idx & 7u);
+    *reinterpret_cast<h4 *>(ys + o) = h;
+    *reinterpret_cast<h4 *>(ys + o + 8) = l;
+}
+
+template <bool ACT>
 __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     __shared__ f4 As[kStages][kStepF4];       // [mt 8][hi,lo][64]
     __shared__ f4 Bs[kStages][2 * kStepF4];   // [nt 16][hi,lo][64]
@@ -365,6 +400,70 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
 
     // epilogue: lane (n, g) of tile (i, j) holds channels 16 mt + 4 g .. +3 of pixel 16 nt + n
     const uint32_t n = lane & 15u, g = lane >> 4;
+    if constexpr (ACT) {
+        // Styled epilogue on the accumulators (regular conv, H W % 256 == 0: one face
+        // per workgroup): v = lrelu(acc demod + nw noise + bias) scale; y = v s_next
+        // as split-NHWC; ToRGB partial over this workgroup's 128 channels -> rgbp.
+        __shared__ float red[4][4][16][3];          // [wn][j][n][o] from the wm = 1 waves
+        const ActEpi &e = a.e;
+        const uint32_t HW = Hc * Wc, b = pix0 / HW;
+        const float nw = e.noise ? *e.noise_weight : 0.0f;
+        float part[4][3];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) part[j][0] = part[j][1] = part[j][2] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t ch = cb * kCT + (4 * wm + i) * 16 + 4 * g;
+            const f4 dm = *reinterpret_cast<const f4 *>(e.demod + (size_t)b * a.Cout + ch);
+            const f4 bs = *reinterpret_cast<const f4 *>(e.bias + ch);
+            const f4 sn = e.s_next ? *reinterpret_cast<const f4 *>(e.s_next + (size_t)b * a.Cout + ch)
+                                   : f4{1.0f, 1.0f, 1.0f, 1.0f};
+            f4 rw[3];
+#pragma unroll
+            for (int o = 0; o < 3; ++o)
+                rw[o] = e.rgb_w ? *reinterpret_cast<const f4 *>(e.rgb_w + ((size_t)b * 3 + o) * a.Cout + ch)
+                                : f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t P = pix0 + (4 * wn + j) * 16 + n;
+                const float nz = e.noise ? nw * e.noise[P] : 0.0f;
+                f4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = act1(acc[i][j][r], dm[r], nz, bs[r], e.slope, e.scale);
+                if (e.ys) store_split4(e.ys, (size_t)P * a.Cout + ch, v * sn);
+#pragma unroll
+                for (int o = 0; o < 3; ++o)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) part[j][o] = fmaf(v[r], rw[o][r], part[j][o]);
+            }
+        }
+        if (e.rgb_w) {
+            // sum over the 4 channel groups g (lanes n + 16 g), then over wm (LDS)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int o = 0; o < 3; ++o) {
+                    part[j][o] += __shfl_xor(part[j][o], 16, 64);
+                    part[j][o] += __shfl_xor(part[j][o], 32, 64);
+                }
+            if (wm == 1 && g == 0)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int o = 0; o < 3; ++o) red[wn][j][n][o] = part[j][o];
+            __syncthreads();
+            if (wm == 0 && g < 3) {                 // lane (n, g = o) stores channel o
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t P = pix0 + (4 * wn + j) * 16 + n;
+                    const float s = (g == 0 ? part[j][0] : g == 1 ? part[j][1] : part[j][2]) +
+                                    red[wn][j][n][g];
+                    e.rgbp[(((size_t)cb * a.B + b) * 3 + g) * HW + (P - b * HW)] = s;
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t P = pix0 + (4 * wn + j) * 16 + n;
@@ -404,19 +503,23 @@ int sdfr_conv_pack_weights(const float *w, float scale, uint32_t Cout, uint32_t 
     return check_launch("conv_pack_weights: pack");
 }
 
-int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
-                       uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
-                       int transposed, void *stream) {
-    if (!out || !x_split || !packed) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
+}  // extern "C"
+
+namespace {
+
+// Shared setup of both entry points: shape checks, tap tables, classes; launches
+// conv_x_kernel<ACT>.
+int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B, uint32_t H,
+                uint32_t W, uint32_t Cin, uint32_t Cout, int transposed, bool act,
+                hipStream_t st, const char *what) {
+    if (!x_split || !packed) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
     if (B == 0 || H == 0 || W == 0 || Cout % kCT || Cin % 32 || Cin == 0 || Cout == 0)
         return fail(SDFR_EINVAL, "conv3x3_f16x3: bad shape (Cout % 128, Cin % 32)");
-    if ((uint64_t)B * H * W * Cin * 4 >= (1ull << 31) || 9ull * Cin * Cout * 4 >= (1ull << 31))
+    if ((uint64_t)B * H * W * Cin * 4 >= (1ull << 31) || 9ull * Cin * Cout * 4 >= (1ull << 31) ||
+        (uint64_t)B * H * W * Cout * 4 >= (1ull << 31))
         return fail(SDFR_EINVAL, "conv3x3_f16x3: tensor too large for 32-bit offsets (split B)");
-    hipStream_t st = (hipStream_t)stream;
-    ConvArgs a{};
     a.xs = reinterpret_cast<const _Float16 *>(x_split);
     a.wpk = reinterpret_cast<const f4 *>(packed);
-    a.out = out;
     a.B = B;
     a.Hin = H;
     a.Win = W;
@@ -468,8 +571,51 @@ int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
                 add_class(py ? H : H + 1, px ? W : W + 1, py, px, nt);
             }
     }
-    hipLaunchKernelGGL(conv_x_kernel, dim3(grid), dim3(512), 0, st, a);
-    return check_launch("conv3x3_f16x3");
+    if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid), dim3(512), 0, st, a);
+    return check_launch(what);
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
+                       uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
+                       int transposed, void *stream) {
+    if (!out) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
+    ConvArgs a{};
+    a.out = out;
+    return conv_launch(a, x_split, packed, B, H, W, Cin, Cout, transposed, false,
+                       (hipStream_t)stream, "conv3x3_f16x3");
+}
+
+int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *p, void *stream) {
+    if (!p) return fail(SDFR_EINVAL, "conv3x3_f16x3_act: null args");
+    const sdfr_conv_act_args &s = *p;
+    if (!s.demod || !s.bias || (s.noise && !s.noise_weight))
+        return fail(SDFR_EINVAL, "conv3x3_f16x3_act: null tensor pointer");
+    if (!s.y_split && !s.rgb_w) return fail(SDFR_EINVAL, "conv3x3_f16x3_act: nothing to write");
+    if (s.rgb_w && !s.rgb_partial) return fail(SDFR_EINVAL, "conv3x3_f16x3_act: rgb_partial missing");
+    if (((uint64_t)s.H * s.W) % kPT)
+        return fail(SDFR_EUNSUPPORTED, "conv3x3_f16x3_act: H*W must be a multiple of 256");
+    for (const void *q : {(const void *)s.demod, (const void *)s.bias, (const void *)s.s_next,
+                          (const void *)s.rgb_w, (const void *)s.y_split})
+        if (q && reinterpret_cast<uintptr_t>(q) % 16)
+            return fail(SDFR_EINVAL, "conv3x3_f16x3_act: pointers must be 16-B aligned");
+    ConvArgs a{};
+    a.e.demod = s.demod;
+    a.e.noise = s.noise;
+    a.e.noise_weight = s.noise_weight;
+    a.e.bias = s.bias;
+    a.e.slope = s.negative_slope;
+    a.e.scale = s.act_scale;
+    a.e.s_next = s.s_next;
+    a.e.ys = reinterpret_cast<_Float16 *>(s.y_split);
+    a.e.rgb_w = s.rgb_w;
+    a.e.rgbp = s.rgb_partial;
+    return conv_launch(a, s.x_split, s.packed, s.B, s.H, s.W, s.Cin, s.Cout, 0, true,
+                       (hipStream_t)stream, "conv3x3_f16x3_act");
 }
 
 }  // extern "C"

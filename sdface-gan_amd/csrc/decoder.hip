@@ -330,6 +330,28 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg)
     }
 }
 
+// ToRGB finish after the conv-fused epilogue: one thread per (b, o, pixel).
+__global__ __launch_bounds__(256) void rgb_finish_kernel(float *__restrict__ rgb,
+                                                         const float *__restrict__ part,
+                                                         uint32_t nparts, const float *rgb_b,
+                                                         const float *__restrict__ skip,
+                                                         float f0, float f1, float f2, float f3,
+                                                         uint32_t B, uint32_t H, uint32_t W) {
+    const uint32_t HW = H * W;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n = (uint64_t)B * 3 * HW;
+    if (t >= n) return;
+    const uint32_t p = (uint32_t)(t % HW), bo = (uint32_t)(t / HW), o = bo % 3;
+    float v = part[t];
+    for (uint32_t k = 1; k < nparts; ++k) v += part[k * n + t];
+    v = v + rgb_b[o];
+    if (skip) {
+        const float fir[4] = {f0, f1, f2, f3};
+        v = v + skip_up(skip + (size_t)bo * (HW / 4), H / 2, W / 2, (int)(p / W), (int)(p % W), fir);
+    }
+    rgb[t] = v;
+}
+
 // ----------------------------------------------------------------------------
 // NCHW -> NHWC with modulation, 64 x 64 LDS tiles
 // ----------------------------------------------------------------------------
@@ -503,6 +525,21 @@ static int modulate_common(float *y, void *ys, const float *x, const float *s, u
     modulate_nhwc_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(
         y, reinterpret_cast<_Float16 *>(ys), x, s, C, HW);
     return check_launch("modulate_to_nhwc");
+}
+
+int sdfr_rgb_finish(float *rgb, const float *partial, uint32_t nparts, const float *rgb_b,
+                    const float *skip, const float *fir, uint32_t B, uint32_t H, uint32_t W,
+                    void *stream) {
+    if (B == 0 || H == 0 || W == 0) return SDFR_OK;
+    if (!rgb || !partial || !rgb_b || nparts == 0 || (skip && !fir))
+        return fail(SDFR_EINVAL, "rgb_finish: null pointer");
+    if (skip && (H % 2 || W % 2)) return fail(SDFR_EINVAL, "rgb_finish: odd size with skip");
+    const uint64_t n = (uint64_t)B * 3 * H * W;
+    const float f[4] = {skip ? fir[0] : 0.f, skip ? fir[1] : 0.f, skip ? fir[2] : 0.f,
+                        skip ? fir[3] : 0.f};
+    rgb_finish_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        rgb, partial, nparts, rgb_b, skip, f[0], f[1], f[2], f[3], B, H, W);
+    return check_launch("rgb_finish");
 }
 
 int sdfr_modulate_to_nhwc(float *y, const float *x, const float *s, uint32_t B, uint32_t C,

@@ -355,6 +355,64 @@ def conv3x3_f16x3(x_split, packed, Cout, transposed=False):
     return out
 
 
+def conv3x3_f16x3_act(x_split, packed, Cout, *, demod, bias, noise_weight, noise=None,
+                      s_next=None, store_y=True, rgb_w=None, negative_slope=0.2,
+                      act_scale=math.sqrt(2)):
+    """Regular conv with the plain styled epilogue fused (sdfr_conv3x3_f16x3_act):
+    returns (y split-NHWC [B,H,W,Cout/8,2,8] or None, ToRGB partial sums
+    [Cout/128,B,3,H,W] or None).  demod must already carry 1/su."""
+    _require_cuda(x_split)
+    if x_split.dtype != torch.float16 or x_split.dim() != 6 or x_split.shape[4:] != (2, 8) \
+            or not x_split.is_contiguous():
+        raise RuntimeError("conv3x3_f16x3_act: x_split must be a contiguous split-NHWC fp16 "
+                           "tensor [B,H,W,Cin/8,2,8]")
+    B, H, W, Cin = x_split.shape[0], x_split.shape[1], x_split.shape[2], 8 * x_split.shape[3]
+    dev = x_split.device
+    ys = (torch.empty(B, H, W, Cout // 8, 2, 8, device=dev, dtype=torch.float16)
+          if store_y else None)
+    part = (torch.empty(Cout // 128, B, 3, H, W, device=dev) if rgb_w is not None else None)
+    if noise is not None:
+        noise = noise.expand(B, 1, H, W).contiguous()
+    keep = []
+
+    def cptr(t):
+        if t is None:
+            return None
+        t = t.contiguous()
+        keep.append(t)
+        return _lib.ptr(t)
+
+    a = _lib.ConvActArgs()
+    a.x_split, a.packed = _lib.ptr(x_split), _lib.ptr(packed)
+    a.B, a.H, a.W, a.Cin, a.Cout = B, H, W, Cin, Cout
+    a.demod = cptr(demod)
+    a.noise = cptr(noise)
+    a.noise_weight = cptr(noise_weight)
+    a.bias = cptr(bias.reshape(-1))
+    a.negative_slope, a.act_scale = negative_slope, act_scale
+    a.s_next = cptr(s_next)
+    a.y_split = _lib.ptr(ys)
+    a.rgb_w = cptr(rgb_w)
+    a.rgb_partial = _lib.ptr(part)
+    _lib.check(_lib.lib().sdfr_conv3x3_f16x3_act(a, _lib.stream_of(x_split)), "conv3x3_f16x3_act")
+    return ys, part
+
+
+def rgb_finish(partial, rgb_b, skip=None, fir=None):
+    """ToRGB output [B,3,H,W] = partial.sum(0) + rgb_b + upsampled skip (sdfr_rgb_finish)."""
+    _require_cuda(partial)
+    n, B, _, H, W = partial.shape
+    partial = partial.contiguous()
+    rgb = torch.empty(B, 3, H, W, device=partial.device)
+    rgb_b = rgb_b.reshape(-1).contiguous()
+    skip = skip.contiguous() if skip is not None else None
+    f = (_lib._f32 * 4)(*(fir if fir is not None else [0.0] * 4))
+    _lib.check(_lib.lib().sdfr_rgb_finish(_lib.ptr(rgb), _lib.ptr(partial), n, _lib.ptr(rgb_b),
+                                          _lib.ptr(skip), f, B, H, W,
+                                          _lib.stream_of(partial)), "rgb_finish")
+    return rgb
+
+
 def modulate_to_nhwc_split(x, s):
     """(x * s[:, :, None, None]) in the split-NHWC fp16 layout [B,H,W,C/8,2,8], from
     NCHW fp32 x."""

@@ -24,7 +24,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .decoder_ops import conv3x3_f16x3, conv_pack_weights, modulate_to_nhwc_split  # noqa: E402
+from .decoder_ops import (conv3x3_f16x3, conv3x3_f16x3_act, conv_pack_weights,  # noqa: E402
+                          modulate_to_nhwc_split, rgb_finish)
 from .decoder_ops import (FusedLeakyReLU, fused_leaky_relu, modulate_to_nhwc,  # noqa: F401
                           separable_taps, styled_epilogue, upfirdn2d)
 from .renderer import VolumeFeatureRenderer
@@ -260,6 +261,9 @@ class Decoder(nn.Module):
         # convolutions of the fused path: "f16x3" (split-fp16 MFMA implicit GEMM,
         # csrc/conv_f16x3.hip) or "miopen" (F.conv2d / conv_transpose2d, fp32)
         self.conv_impl = "f16x3"
+        # regular f16x3 convs with the styled epilogue fused into the conv kernel
+        # (sdfr_conv3x3_f16x3_act + sdfr_rgb_finish) instead of a separate pass
+        self.fuse_conv_act = True
         self._fir = None
         self._packs = {}
 
@@ -343,10 +347,12 @@ class Decoder(nn.Module):
         return hit[1], hit[2]
 
     def _fused_forward(self, features, latent, noise):
-        """Same computation as the module path, one MIOpen convolution plus one
-        sdfr_styled_epilogue per layer on channels_last activations; each
-        activation is pre-multiplied by the next layer's modulation and the
-        ToRGB layers are folded into the preceding epilogue."""
+        """Same computation as the module path: per layer one split-fp16 convolution
+        (or MIOpen's) plus one sdfr_styled_epilogue on NHWC activations -- for the
+        regular convolutions the epilogue runs inside the conv kernel
+        (sdfr_conv3x3_f16x3_act); each activation is pre-multiplied by the next
+        layer's modulation and the ToRGB layers are folded into the preceding
+        epilogue."""
         cl = torch.channels_last
         B = features.shape[0]
         seq = [self.conv1] + list(self.convs)
@@ -359,6 +365,26 @@ class Decoder(nn.Module):
             w = mc.scale * mc.weight[0]
             demod = (torch.rsqrt((mods[i] * mods[i]) @ (w * w).sum([2, 3]).t() + 1e-8)
                      if mc.demodulate else None)
+            last = i == len(seq) - 1
+            if (self.fuse_conv_act and split[i] and not mc.upsample and (last or split[i + 1])
+                    and (x.shape[1] * x.shape[2]) % 256 == 0):
+                # regular conv with the epilogue fused: the conv output stays on chip
+                packed, su = self._pack(i, mc)
+                H, W = x.shape[1], x.shape[2]
+                n = noise[i] if noise[i] is not None else features.new_empty(B, 1, H, W).normal_()
+                rgb_w = None
+                if i % 2 == 0:
+                    to_rgb = self.to_rgb1 if i == 0 else self.to_rgbs[i // 2 - 1]
+                    tc = to_rgb.conv
+                    s_rgb = tc.modulation(latent[:, i + 1])
+                    rgb_w = (tc.scale * tc.weight[0, :, :, 0, 0])[None] * s_rgb[:, None, :]
+                x, part = conv3x3_f16x3_act(
+                    x, packed, w.shape[0], demod=demod / su, bias=sc.activate.bias,
+                    noise_weight=sc.noise.weight, noise=n,
+                    s_next=None if last else mods[i + 1], store_y=not last, rgb_w=rgb_w)
+                if part is not None:
+                    rgb = rgb_finish(part, to_rgb.bias, skip=rgb if i else None, fir=self._fir)
+                continue
             if split[i]:
                 packed, su = self._pack(i, mc)
                 out = conv3x3_f16x3(x, packed, w.shape[0], transposed=mc.upsample)
@@ -373,7 +399,6 @@ class Decoder(nn.Module):
             else:
                 H, W = out.shape[2], out.shape[3]
             n = noise[i] if noise[i] is not None else features.new_empty(B, 1, H, W).normal_()
-            last = i == len(seq) - 1
             rgb_w = rgb_b = None
             if i % 2 == 0:
                 to_rgb = self.to_rgb1 if i == 0 else self.to_rgbs[i // 2 - 1]

@@ -240,14 +240,59 @@ def test_conv3x3_f16x3_vs_fp64(ops, B, Cin, Cout, H, W, transposed):
     assert e16 <= 4 * e32 + 1e-6, (e16, e32)
 
 
-@pytest.mark.parametrize("conv_impl", ["f16x3", "miopen"])
-def test_decoder_fused_equals_module_path(sdfr, conv_impl):
+@pytest.mark.parametrize("B,Cin,Cout,H,W,rgb,skip,store_y", [
+    (2, 64, 128, 16, 16, True, True, True),     # one Cout block, ToRGB with skip
+    (1, 256, 512, 16, 32, True, False, True),   # four Cout blocks (partials), no skip
+    (2, 128, 256, 32, 8, True, True, False),    # last layer: rgb only
+    (1, 32, 256, 16, 16, False, False, True),   # y only
+])
+def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, store_y):
+    """sdfr_conv3x3_f16x3_act (+ sdfr_rgb_finish) against sdfr_conv3x3_f16x3 followed by
+    sdfr_styled_epilogue on the same inputs: y (split-NHWC) bit-exact -- same fp32
+    operations in the same order -- and rgb to fp32 summation-order rounding."""
+    g = torch.Generator().manual_seed(B + Cin + Cout + H)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g)
+    packed, su = ops.conv_pack_weights(w.to(DEV), 1 / math.sqrt(Cin * 9))
+    xs = ops.split_nhwc(x.to(DEV))
+    fir = [0.125, 0.375, 0.375, 0.125]
+    demod = (torch.rand(B, Cout, generator=g) + 0.5).to(DEV) / su
+    kw = dict(bias=torch.randn(Cout, generator=g).to(DEV),
+              noise_weight=torch.full((1,), 0.1, device=DEV),
+              noise=torch.randn(B, 1, H, W, generator=g).to(DEV),
+              s_next=(torch.rand(B, Cout, generator=g) + 0.5).to(DEV) if store_y else None,
+              store_y=store_y)
+    rgb_w = torch.randn(B, 3, Cout, generator=g).to(DEV) if rgb else None
+    rgb_b = torch.randn(3, generator=g).to(DEV)
+    sk = torch.randn(B, 3, H // 2, W // 2, generator=g).to(DEV) if skip else None
+    ys, part = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_w=rgb_w, **kw)
+    out = ops.conv3x3_f16x3(xs, packed, Cout)
+    y_ref, rgb_ref = ops.styled_epilogue(out, fir=fir, demod=demod, rgb_w=rgb_w,
+                                         rgb_b=rgb_b if rgb else None, skip=sk,
+                                         split_y=store_y, **kw)
+    if store_y:
+        np.testing.assert_array_equal(ys.cpu().numpy(), y_ref.cpu().numpy())
+    else:
+        assert ys is None
+    if rgb:
+        assert part.shape == (Cout // 128, B, 3, H, W)
+        got = ops.rgb_finish(part, rgb_b, skip=sk, fir=fir)
+        scale = float(rgb_ref.abs().max())
+        _close(f"conv_act_rgb_{Cin}x{Cout}_{H}x{W}", got.cpu(), rgb_ref.cpu(), 1e-5 * scale,
+               1e-6 * scale)
+    else:
+        assert part is None
+
+
+@pytest.mark.parametrize("conv_impl,fuse", [("f16x3", True), ("f16x3", False), ("miopen", False)])
+def test_decoder_fused_equals_module_path(sdfr, conv_impl, fuse):
     """Same weights, latents and noise: HIP-epilogue decoder == op-by-op decoder."""
     opt = sdfr.vol_render_opt()
     opt.model.feature_encoder_in_channels = opt.rendering.width   # as Generator.__init__ sets it
     torch.manual_seed(0)
     dec = sdfr.Decoder(opt.model).to(DEV).eval()
     dec.conv_impl = conv_impl
+    dec.fuse_conv_act = fuse
     with torch.no_grad():
         for m in dec.modules():
             if isinstance(m, sdfr.NoiseInjection):
@@ -266,6 +311,7 @@ def test_decoder_fused_equals_module_path(sdfr, conv_impl):
         dec.use_fused = True
     assert fused.shape == mod.shape == (B, 3, 256, 256)
     scale = float(mod.abs().max())
-    _record[f"decoder_fused_vs_module_scale_{conv_impl}"] = scale
-    _close(f"decoder_fused_vs_module_{conv_impl}", fused.cpu(), mod.cpu(), 1e-4 * max(1.0, scale),
+    tag = conv_impl + ("_act" if fuse else "")
+    _record[f"decoder_fused_vs_module_scale_{tag}"] = scale
+    _close(f"decoder_fused_vs_module_{tag}", fused.cpu(), mod.cpu(), 1e-4 * max(1.0, scale),
            1e-5 * max(1.0, scale))
