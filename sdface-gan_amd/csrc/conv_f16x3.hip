@@ -40,7 +40,10 @@ typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 constexpr int kCT = 128;        // output channels per workgroup
 constexpr int kPT = 256;        // output pixels per workgroup
 constexpr int kStepF4 = 1024;   // f4 of weight fragments per K-step (16 KB)
-constexpr int kStages = 3;      // LDS-DMA ring depth (two K-steps in flight)
+#ifndef CONV_STAGES
+#define CONV_STAGES 3
+#endif
+constexpr int kStages = CONV_STAGES;   // LDS-DMA ring depth (kStages - 1 K-steps in flight)
 
 __device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a),
@@ -112,6 +115,7 @@ __global__ void __launch_bounds__(256) conv_pack_kernel(const float *__restrict_
 #ifndef CONV_REGDB
 #define CONV_REGDB 1      // fragments of step ks+1 read into a second register set mid-step
 #endif
+static_assert(CONV_REGDB || kStages == 3, "the single-register-set ring assumes 3 stages");
 #ifndef CONV_XCD
 #define CONV_XCD 1
 #endif
@@ -334,23 +338,23 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
 #if CONV_ABL == 4      // ablation: never wait for the DMA
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
-        if (ks + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        if (kStages == 3 && ks + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #endif
 #if CONV_ABL != 5      // 5: ablation without the barrier
         __builtin_amdgcn_s_barrier();
 #endif
-        const uint32_t st = ks % 3u;
+        const uint32_t st = ks % kStages;
 #if CONV_ABL != 6      // 6: ablation without in-loop staging
-        if (ks + 3 < nk) issue_step(ks + 3, st);
+        if (ks + kStages < nk) issue_step(ks + kStages, st);
 #endif
-        if (ks + 1 < nk) read_frags(Rn, st == 2 ? 0u : st + 1);
+        if (ks + 1 < nk) read_frags(Rn, st == kStages - 1 ? 0u : st + 1);
         mfma_rows(R, 2, 2);
     };
     issue_step(0, 0);
     if (nk > 1) issue_step(1, 1);
-    if (nk > 2) issue_step(2, 2);
-    if (nk > 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    if (kStages == 3 && nk > 2) issue_step(2, 2);
+    if (kStages == 3 && nk > 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
