@@ -276,7 +276,14 @@ __global__ __launch_bounds__(256) void epi_plain_kernel(EpiArgs a, uint32_t tpp_
 // Blur epilogue: thread = (face, row segment, column, channel quad); a sliding
 // window of 4 horizontally filtered input rows gives the 4x4 separable blur
 // with one new 16-B load per tap column per output row.
-constexpr uint32_t kBlurRows = 16;
+#ifndef BLUR_ROWS
+#define BLUR_ROWS 16
+#endif
+#ifndef BLUR_GROUP
+#define BLUR_GROUP 4
+#endif
+constexpr uint32_t kBlurRows = BLUR_ROWS;
+constexpr int kBlurGroup = BLUR_GROUP;   // input rows loaded together (kBlurRows % it == 0)
 
 __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg) {
     const uint32_t Q = a.C >> 2;
@@ -292,18 +299,25 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg)
     const float *src = a.conv + (size_t)b * Hi * Wi * C + c;
     const float f0 = a.fir[3], f1 = a.fir[2], f2 = a.fir[1], f3 = a.fir[0];   // flipped taps
 
-    auto hrow = [&](int r) -> float4 {
-        float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < 0 || r >= (int)Hi) return h;
-        const float *row = src + (size_t)r * Wi * C;
-        const float fj[4] = {f0, f1, f2, f3};
+    // the 4 horizontal taps of input row r: loads and filter split so that a group
+    // of rows can be loaded before any is filtered (4 rows = 16 loads in flight)
+    auto hload = [&](int r, float4 (&v)[4]) {
+        const bool rok = r >= 0 && r < (int)Hi;
+        const float *row = src + (size_t)(rok ? r : 0) * Wi * C;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int cc = (int)ox + j - 1;
-            if (cc < 0 || cc >= (int)Wi) continue;
-            const float4 v = ld4(row + (size_t)cc * C);
-            h.x = fmaf(v.x, fj[j], h.x); h.y = fmaf(v.y, fj[j], h.y);
-            h.z = fmaf(v.z, fj[j], h.z); h.w = fmaf(v.w, fj[j], h.w);
+            v[j] = (rok && cc >= 0 && cc < (int)Wi) ? ld4(row + (size_t)cc * C)
+                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto hfilt = [&](const float4 (&v)[4]) -> float4 {
+        const float fj[4] = {f0, f1, f2, f3};
+        float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            h.x = fmaf(v[j].x, fj[j], h.x); h.y = fmaf(v[j].y, fj[j], h.y);
+            h.z = fmaf(v[j].z, fj[j], h.z); h.w = fmaf(v[j].w, fj[j], h.w);
         }
         return h;
     };
@@ -314,19 +328,41 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg)
     const float nw = a.noise ? *a.noise_weight : 0.0f;
     const uint32_t y0 = seg * kBlurRows;
     const uint32_t y1 = min(a.H, y0 + kBlurRows);
-    float4 h0 = hrow((int)y0 - 1), h1 = hrow((int)y0), h2 = hrow((int)y0 + 1);
-    for (uint32_t oy = y0; oy < y1; ++oy) {
-        const float4 h3 = hrow((int)oy + 2);
-        float4 s;
-        s.x = fmaf(h3.x, f3, fmaf(h2.x, f2, fmaf(h1.x, f1, h0.x * f0)));
-        s.y = fmaf(h3.y, f3, fmaf(h2.y, f2, fmaf(h1.y, f1, h0.y * f0)));
-        s.z = fmaf(h3.z, f3, fmaf(h2.z, f2, fmaf(h1.z, f1, h0.z * f0)));
-        s.w = fmaf(h3.w, f3, fmaf(h2.w, f2, fmaf(h1.w, f1, h0.w * f0)));
-        const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
-        const float nz = a.noise ? nw * a.noise[pix] : 0.0f;
-        const float4 v = act4(s, dm, nz, bs, a.slope, a.act_scale);
-        store_y(a, pix * C + c, make_float4(v.x * sn.x, v.y * sn.y, v.z * sn.z, v.w * sn.w));
-        h0 = h1; h1 = h2; h2 = h3;
+    float4 h0, h1, h2;
+    {
+        float4 v0[4], v1[4], v2[4];
+        hload((int)y0 - 1, v0);
+        hload((int)y0, v1);
+        hload((int)y0 + 1, v2);
+        h0 = hfilt(v0);
+        h1 = hfilt(v1);
+        h2 = hfilt(v2);
+    }
+    for (uint32_t oy0 = y0; oy0 < y1; oy0 += kBlurGroup) {
+        float4 v[kBlurGroup][4];
+        float nz[kBlurGroup];
+#pragma unroll
+        for (int k = 0; k < kBlurGroup; ++k) {
+            hload((int)(oy0 + k) + 2, v[k]);
+            const size_t pix = ((size_t)b * a.H + min(oy0 + k, a.H - 1)) * a.W + ox;
+            nz[k] = a.noise ? nw * a.noise[pix] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < kBlurGroup; ++k) {
+            const uint32_t oy = oy0 + k;
+            const float4 h3 = hfilt(v[k]);
+            if (oy < y1) {
+                float4 s;
+                s.x = fmaf(h3.x, f3, fmaf(h2.x, f2, fmaf(h1.x, f1, h0.x * f0)));
+                s.y = fmaf(h3.y, f3, fmaf(h2.y, f2, fmaf(h1.y, f1, h0.y * f0)));
+                s.z = fmaf(h3.z, f3, fmaf(h2.z, f2, fmaf(h1.z, f1, h0.z * f0)));
+                s.w = fmaf(h3.w, f3, fmaf(h2.w, f2, fmaf(h1.w, f1, h0.w * f0)));
+                const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
+                const float4 vv = act4(s, dm, nz[k], bs, a.slope, a.act_scale);
+                store_y(a, pix * C + c, make_float4(vv.x * sn.x, vv.y * sn.y, vv.z * sn.z, vv.w * sn.w));
+            }
+            h0 = h1; h1 = h2; h2 = h3;
+        }
     }
 }
 
