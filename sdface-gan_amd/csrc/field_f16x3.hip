@@ -43,7 +43,7 @@ namespace sdfr {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 t_out][hi,lo][64 lanes] x 16 B
-constexpr int kXStage = kXSliceF4 / kThreads;    // float4 staged per thread per slice
+[[maybe_unused]] constexpr int kXStage = kXSliceF4 / kThreads;   // float4 staged per thread per slice
 
 // Schedule options (compile-time; DESIGN.md section 5 records the measured choice):
 //   SDFR_X_PREFETCH  ring staged two slices ahead + next slice's first fragment
@@ -55,6 +55,12 @@ constexpr int kXStage = kXSliceF4 / kThreads;    // float4 staged per thread per
 #endif
 #ifndef SDFR_X_BUFLOAD
 #define SDFR_X_BUFLOAD 1
+#endif
+//   SDFR_X_DMA       ring filled by LDS-DMA two slices ahead, counted vmcnt, raw
+//                    barrier (1) / staged through registers + __syncthreads (0);
+//                    measured 7 % slower than the register ring (6.14 vs 5.71 ms)
+#ifndef SDFR_X_DMA
+#define SDFR_X_DMA 0
 #endif
 
 // ----------------------------------------------------------------------------
@@ -242,15 +248,46 @@ struct XFieldArgs {
 // registers, and reads the first fragment pair of slice it+1 (already visible:
 // written during it-1), so the next slice's first MFMAs do not wait on LDS
 // latency after the barrier.
+//
+// With SDFR_X_DMA the ring is filled by LDS-DMA instead: during slice `it` every
+// wave issues its pieces of slice it+2 into slot (it+2)%3 (free since the barrier
+// that closed it-1), and before the barrier closing `it` waits (counted vmcnt)
+// for its pieces of it+1.  A slice is 16 pieces of 1 KB; every wave also moves
+// pieces 0-1 (the first hi/lo fragment) itself -- identical bytes to the same
+// place -- so it can pre-read them before the barrier from its own completed
+// DMA.  Waves 0/1 move 4 further pieces, waves 2/3 three plus a repeat of 0/1:
+// six per wave per slice.
+constexpr int kXDmaPieces = 6;
+
+__device__ __forceinline__ uint32_t xdma_piece(uint32_t w, int k) {
+    if (k < 2) return (uint32_t)k;
+    if (w < 2) return 2 + 4 * w + (uint32_t)(k - 2);
+    return k < 5 ? 10 + 3 * (w - 2) + (uint32_t)(k - 2) : w - 2;
+}
+
 struct XRing {
     f4 *lds;              // [3][kXSliceF4]
     const f4 *packed;
+#if !SDFR_X_DMA
     f4 st[kXStage];       // the slice staged through registers
+#endif
     f4 pre_h, pre_l;      // first (hi, lo) A fragment of the current slice
     __amdgpu_buffer_rsrc_t rsrc;   // the packed fragments (SDFR_X_BUFLOAD)
+    v4i drsrc;            // the same for the LDS-DMA (SDFR_X_DMA)
     uint32_t it;          // slice iteration (runs across passes)
-    uint32_t tid;
+    uint32_t tid, wave;
 };
+
+// LDS-DMA of slice pf into ring slot `slot` (this wave's pieces)
+template <class Net>
+__device__ __forceinline__ void xdma_issue(XRing &R, uint32_t pf, uint32_t slot) {
+#pragma unroll
+    for (int k = 0; k < kXDmaPieces; ++k) {
+        const uint32_t pc = xdma_piece(R.wave, k);
+        dma16(R.drsrc, (R.tid & 63u) * 16u, (pf * kXSliceF4 + pc * 64u) * 16u,
+              lds_addr(R.lds + slot * kXSliceF4 + pc * 64u));
+    }
+}
 
 __device__ __forceinline__ void xpin(f4 &x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void xpin(float &x) { asm volatile("" : "+v"(x)); }
@@ -266,6 +303,9 @@ template <int V, class Net, int H, class Side>
 __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], const f4 b0h,
                                       const f4 b0l, const f4 b1h, const f4 b1l, Side &&side) {
     const uint32_t cur = R.it % 3u;
+#if SDFR_X_DMA
+    if constexpr ((V & 4) == 0) xdma_issue<Net>(R, (R.it + 2u) % Net::kSlices, (R.it + 2u) % 3u);
+#endif
     const f4 *A = R.lds + cur * kXSliceF4 + (R.tid & 63u);
     f4 ah[8], al[8];
 #pragma unroll
@@ -273,7 +313,7 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
         if constexpr ((V & 2) != 0) {
             ah[i] = b0h * (float)(i + 1);
             al[i] = b1l * (float)(i + 1);
-        } else if (SDFR_X_PREFETCH && i == 0) {
+        } else if ((SDFR_X_PREFETCH || SDFR_X_DMA) && i == 0) {
             ah[0] = R.pre_h;
             al[0] = R.pre_l;
         } else {
@@ -292,6 +332,15 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
         acc1[t] = mfma16(ah[i], b1h, acc1[t]);
     }
     side();
+#if SDFR_X_DMA
+    if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // own pieces of it+1
+    if constexpr ((V & 2) == 0) {
+        const f4 *An = R.lds + ((R.it + 1u) % 3u) * kXSliceF4 + (R.tid & 63u);
+        R.pre_h = An[0];
+        R.pre_l = An[64];
+    }
+    if constexpr ((V & 1) == 0) __builtin_amdgcn_s_barrier();
+#else
     if constexpr ((V & 4) == 0) {
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t wslot = (R.it + 1u + SDFR_X_PREFETCH) % 3u;
@@ -317,6 +366,7 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
         R.pre_l = An[64];
     }
     if constexpr ((V & 1) == 0) __syncthreads();
+#endif
     ++R.it;
 }
 
@@ -470,6 +520,8 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
                                                (int)(Net::kSlices * kXSliceF4 * sizeof(f4)),
                                                0x00020000);
     R.tid = tid;
+    R.wave = __builtin_amdgcn_readfirstlane(wave);
+    R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
     R.it = 0;
     for (uint32_t i = tid; i < (NL + 5) * kW; i += kThreads) {
         float v;
@@ -479,6 +531,13 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
         else v = a.rgb_w[i - (NL + 2) * kW];
         cst[i] = v;
     }
+#if SDFR_X_DMA
+    // prologue: slices 0, 1 -> slots 0, 1 (slice 2 is issued by the first step)
+    xdma_issue<Net>(R, 0, 0);
+    xdma_issue<Net>(R, 1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#else
     // prologue: slices 0 (.. 1) -> slots; the next slice -> registers
     constexpr int kPro = 1 + SDFR_X_PREFETCH;
 #pragma unroll
@@ -486,6 +545,7 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
 #pragma unroll
     for (int i = 0; i < kXStage; ++i) R.st[i] = a.packed[kPro * kXSliceF4 + tid + i * kThreads];
     __syncthreads();
+#endif
     R.pre_h = R.lds[lane];
     R.pre_l = R.lds[64 + lane];
 
@@ -703,6 +763,10 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
             if (a.sdf && ray_ok && g == 0) a.sdf[(size_t)ray_index * G.N + s] = sdf;
         }
     }
+#if SDFR_X_DMA
+    // the ring runs ahead across passes: no LDS-DMA may land after the workgroup ends
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 
     if (!ray_ok) return;
     const size_t HW = (size_t)G.H * G.W;

@@ -125,4 +125,35 @@ int launch_xfield_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
 void fill_geom_args(const sdfr_ngp_render_args *a, float bound, GeomArgs &g);
 void record_event(void *ev, hipStream_t st);
 
+// LDS-DMA: buffer resource over [base, base + bytes) (range-checked: offsets past
+// it read zeros) and one 64-lane x 16-B piece from (voff + soff) to the LDS byte
+// address lds (wave-uniform base + 16 lane).  Inline asm, so the compiler neither
+// drains vmcnt in front of every LDS read nor holds M0; completion is counted by
+// the caller (s_waitcnt vmcnt) and published to the other waves by a barrier.
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4i make_rsrc(const void *base, uint32_t bytes) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    v4i r;
+    r.x = (int)(uint32_t)b;
+    r.y = (int)(uint32_t)(b >> 32);
+    r.z = (int)bytes;
+    r.w = 0x00020000;
+    return r;
+}
+
+__device__ __forceinline__ void dma16(v4i rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
+        : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)reinterpret_cast<uintptr_t>(p);
+}
+
 }  // namespace sdfr
