@@ -120,7 +120,7 @@ static_assert(CONV_REGDB || kStages == 3, "the single-register-set ring assumes 
 #define CONV_XCD 1
 #endif
 #ifndef CONV_ABL
-#define CONV_ABL 0        // timing ablations (wrong results): 1 L2-resident x, 2 no staging, 3 + no barrier
+#define CONV_ABL 0        // timing ablations (wrong results), see the #if CONV_ABL sites
 #endif
 
 // One output-pixel class: the plain convolution has one (every pixel, 9 taps); the
@@ -285,10 +285,15 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
 #if CONV_ABL == 1   // ablation: activations from a tiny L2-resident window
             const uint32_t off = ((lane & 7u) * a.Cin * 4u + c * 128u + loff) + 0 * (ok ? 1u : 0u);
 #else
-            const uint32_t off =
+            uint32_t off =
                 ok ? (((uint32_t)pb[k] * a.Hin + (uint32_t)iy) * a.Win + (uint32_t)ix) * a.Cin * 4u +
                          c * 128u + loff
                    : 0x7FFFFFF0u;                      // past num_records: zero fill
+#if CONV_ABL == 7      // ablation: same pattern folded into a 2 MB (L2-resident) window
+            off &= 0x1FFFFFu;
+#elif CONV_ABL == 8    // ... into a 64 MB window (Infinity-Cache resident)
+            off &= 0x3FFFFFFu;
+#endif
 #endif
             dma16(rx, off, 0u, lds_addr(&Bs[buf][(4 * wave + k) * 64]));
         }
