@@ -131,6 +131,7 @@ struct ConvClass {
     uint32_t py, px;               // output pixel (a, c) -> (sy a + py, sy c + px)
     uint32_t ntaps, t0;            // its taps: dy/dx/tap[t0 .. t0 + ntaps)
     uint32_t tile0, ntiles;        // workgroups [tile0, tile0 + pad8(ntiles)) of the grid
+    uint32_t td[3];                // tap descriptors, 8 bits per tap (tap | dy+1 << 4 | dx+1 << 6)
 };
 
 // Styled epilogue fused into a regular conv (sdfr_conv3x3_f16x3_act).
@@ -174,14 +175,19 @@ __device__ __forceinline__ v4i make_rsrc(const void *base, uint32_t bytes) {
 // tracks it in its own s_waitcnt bookkeeping (no vmcnt(0) drain in front of
 // every ds_read of the ring) nor reserves M0 across it; completion is counted
 // explicitly by the ring below.  Offsets past num_records read zeros.
-__device__ __forceinline__ void dma16(v4i rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
-        : "memory");
+// M0 = LDS destination base of the following DMAs (kernel code here never uses M0
+// otherwise -- checked in the ISA; the register is reserved, so it cannot be
+// declared clobbered).  A DMA's instruction offset moves both its global address
+// and its LDS destination, so one M0 write serves several pieces.
+__device__ __forceinline__ void set_m0(uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(lds) : "memory");
+}
+template <int IOFF>
+__device__ __forceinline__ void dma16(v4i rsrc, uint32_t voff, uint32_t soff) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds"
+                 :
+                 : "v"(voff), "s"(rsrc), "s"(soff), "i"(IOFF)
+                 : "memory");
 }
 
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
@@ -211,202 +217,13 @@ __device__ __forceinline__ void store_split4(_Float16 *ys, size_t idx, f4 v) {
     *reinterpret_cast<h4 *>(ys + o + 8) = l;
 }
 
+// Epilogue of one workgroup tile: raw fp32 output (NHWC, class pixel placement) or,
+// with ACT, the fused styled epilogue (sdfr_conv3x3_f16x3_act).
 template <bool ACT>
-__global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
-    __shared__ f4 As[kStages][kStepF4];       // [mt 8][hi,lo][64]
-    __shared__ f4 Bs[kStages][2 * kStepF4];   // [nt 16][hi,lo][64]
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
-    const uint32_t wm = wave & 1u, wn = wave >> 1;
-    // this workgroup's class (ranges start at multiples of 8: blockIdx.x % 8 is the XCD)
-    uint32_t ci = 0;
-    for (uint32_t i = 1; i < a.ncls; ++i)
-        if (blockIdx.x >= a.cls[i].tile0) ci = i;
-    const ConvClass &cl = a.cls[ci];
-    const uint32_t Hc = cl.Hc, Wc = cl.Wc, py = cl.py, px = cl.px;
-    const uint32_t ntaps = cl.ntaps, t0 = cl.t0, ntiles = cl.ntiles;
-    const uint32_t npix = a.B * Hc * Wc;
-    const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT;
-    const uint32_t loc = blockIdx.x - cl.tile0;
-#if CONV_XCD
-    // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs; give
-    // each XCD one contiguous run of the class's tiles, with the Cout block fastest,
-    // so the tiles that re-read an activation row (the other Cout blocks of the same
-    // pixels, the rows above and below through the taps) run on the same XCD at
-    // about the same time and hit its L2.
-    const uint32_t tile = (loc & 7u) * ((ntiles + 7) >> 3) + (loc >> 3);
-#else
-    const uint32_t tile = loc;
-#endif
-    if (tile >= ntiles) return;                       // padding slot (whole workgroup)
-    const uint32_t cb = tile % nB;
-    const uint32_t pix0 = (tile / nB) * kPT;
-    const uint32_t nk = nC * ntaps;
-
-    // LDS-DMA sources (6 pieces of 1 KB per wave per K-step).  Weights: the K-step's
-    // 16 KB block is contiguous; wave w moves pieces 2w, 2w+1.  Activations: the 32
-    // channels of one pixel are one 128-B line of the split-NHWC input
-    // ([g 4][hi 8, lo 8] halves); a piece is 8 pixels = 8 whole lines, region
-    // (nt, half) of n-tile nt = pixels 16 nt + 8 half .. +7.  Lane l fetches pixel
-    // l & 7, channel group g = (l >> 3) & 3, plane h = l >> 5 to LDS unit l, so a
-    // region holds [h][g][pixel] and the fragment read below is conflict-free.
-    // Wave w moves regions (2w, 0..1) and (2w+1, 0..1).
-    const uint32_t xbytes = a.B * a.Hin * a.Win * a.Cin * 4;
-    const v4i rw = make_rsrc(a.wpk, 9u * nC * nB * kStepF4 * 16u);
-    const v4i rx = make_rsrc(a.xs, xbytes);
-    const uint32_t loff = ((lane >> 3) & 3u) * 32u + (lane >> 5) * 16u;
-    int pb[4], pa[4], pc[4];
-    bool pv[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t P = pix0 + (2 * wave + (k >> 1)) * 16 + (k & 1) * 8 + (lane & 7u);
-        pv[k] = P < npix;
-        const uint32_t Pc = pv[k] ? P : 0;
-        const uint32_t hw = Hc * Wc;
-        pb[k] = (int)(Pc / hw);
-        const uint32_t rem = Pc % hw;
-        pa[k] = (int)(rem / Wc);
-        pc[k] = (int)(rem % Wc);
-    }
-
-    auto issue_step = [&](uint32_t ks, uint32_t buf) {
-        const uint32_t c = ks / ntaps, t = t0 + ks % ntaps;
-        const uint32_t wbase = ((a.tap[t] * nC + c) * nB + cb) * kStepF4 * 16u;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t piece = 2 * wave + k;
-            dma16(rw, lane * 16u, wbase + piece * 1024u, lds_addr(&As[buf][piece * 64]));
-        }
-        const int dy = a.dy[t], dx = a.dx[t];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int iy = pa[k] + dy, ix = pc[k] + dx;
-            const bool ok = pv[k] && iy >= 0 && iy < (int)a.Hin && ix >= 0 && ix < (int)a.Win;
-#if CONV_ABL == 1   // ablation: activations from a tiny L2-resident window
-            const uint32_t off = ((lane & 7u) * a.Cin * 4u + c * 128u + loff) + 0 * (ok ? 1u : 0u);
-#else
-            uint32_t off =
-                ok ? (((uint32_t)pb[k] * a.Hin + (uint32_t)iy) * a.Win + (uint32_t)ix) * a.Cin * 4u +
-                         c * 128u + loff
-                   : 0x7FFFFFF0u;                      // past num_records: zero fill
-#if CONV_ABL == 7      // ablation: same pattern folded into a 2 MB (L2-resident) window
-            off &= 0x1FFFFFu;
-#elif CONV_ABL == 8    // ... into a 64 MB window (Infinity-Cache resident)
-            off &= 0x3FFFFFFu;
-#endif
-#endif
-            dma16(rx, off, 0u, lds_addr(&Bs[buf][(4 * wave + k) * 64]));
-        }
-    };
-
-    f4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-
-    // Fragments of one K-step: [0..3] A hi, [4..7] A lo, [8..11] B hi, [12..15] B lo.
-    // B lane (g = lane >> 4, n = lane & 15): region (nt, n >> 3), unit h 32 + 8 g + (n & 7).
-    const uint32_t boff = ((lane >> 3) & 1u) * 64u + (lane >> 4) * 8u + (lane & 7u);
-    auto read_frags = [&](f4 (&R)[16], uint32_t st) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            R[i] = As[st][((4 * wm + i) * 2) * 64 + lane];
-            R[4 + i] = As[st][((4 * wm + i) * 2 + 1) * 64 + lane];
-            R[8 + i] = Bs[st][((4 * wn + i) * 2) * 64 + boff];
-            R[12 + i] = Bs[st][((4 * wn + i) * 2) * 64 + boff + 32];
-        }
-    };
-    // rows i0 .. i0+nr-1 of the wave's 4 x 4 tiles; per A fragment the three split
-    // terms sweep the 4 B fragments (consecutive MFMAs never share an accumulator)
-    auto mfma_rows = [&](const f4 (&R)[16], int i0, int nr) {
-#pragma unroll
-        for (int i = i0; i < i0 + nr; ++i) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[4 + i], R[8 + j], acc[i][j]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[i], R[12 + j], acc[i][j]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[i], R[8 + j], acc[i][j]);
-        }
-    };
-
-#if CONV_REGDB
-    // Ring: step ks lives in stage ks % 3 and is read into registers half a step
-    // early.  Half-way through step ks (rows 0-1 done) the wave waits for its pieces
-    // of step ks+1 (ks+2's 6 may stay in flight), drains its LDS reads and meets the
-    // others at a raw barrier: after it step ks+1 is in LDS everywhere and nobody
-    // reads stage ks % 3 any more, so step ks+3 is issued into it and step ks+1's
-    // fragments are read while rows 2-3 of step ks compute.
-    auto step = [&](uint32_t ks, const f4 (&R)[16], f4 (&Rn)[16]) {
-        mfma_rows(R, 0, 2);
-#if CONV_ABL == 4      // ablation: never wait for the DMA
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-        if (kStages == 3 && ks + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#endif
-#if CONV_ABL != 5      // 5: ablation without the barrier
-        __builtin_amdgcn_s_barrier();
-#endif
-        const uint32_t st = ks % kStages;
-#if CONV_ABL != 6      // 6: ablation without in-loop staging
-        if (ks + kStages < nk) issue_step(ks + kStages, st);
-#endif
-        if (ks + 1 < nk) read_frags(Rn, st == kStages - 1 ? 0u : st + 1);
-        mfma_rows(R, 2, 2);
-    };
-    issue_step(0, 0);
-    if (nk > 1) issue_step(1, 1);
-    if (kStages == 3 && nk > 2) issue_step(2, 2);
-    if (kStages == 3 && nk > 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    f4 R0[16], R1[16];
-    read_frags(R0, 0);
-    uint32_t ks = 0;
-    for (; ks + 1 < nk; ks += 2) {
-        step(ks, R0, R1);
-        step(ks + 1, R1, R0);
-    }
-    if (ks < nk) step(ks, R0, R1);
-#if CONV_ABL == 4
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-#else
-    // Ring: step ks in stage ks % 3; steps ks+1, ks+2 in flight while ks computes.
-    // Stage (ks+2) % 3 last held step ks-1, whose reads every wave completed before
-    // the barrier that closed step ks-1.
-    issue_step(0, 0);
-    if (nk > 1) issue_step(1, 1);
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    uint32_t cur = 0;
-    for (uint32_t ks = 0; ks < nk; ++ks) {
-        const bool more = ks + 2 < nk;
-#if CONV_ABL == 2 || CONV_ABL == 3   // ablation: no staging in the loop (stale LDS)
-        (void)more;
-#else
-        if (more) issue_step(ks + 2, cur == 0 ? 2u : cur - 1);
-#endif
-        f4 R[16];
-        read_frags(R, cur);
-        mfma_rows(R, 0, 4);
-        // step ks+1 must have landed (only ks+2's 6 pieces may stay in flight), and
-        // this wave's fragment reads of stage `cur` must be done, before the barrier
-#if CONV_ABL == 3   // ablation: no staging, no barrier
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-        if (more) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-#endif
-        cur = cur == 2 ? 0 : cur + 1;
-    }
-#endif
-
+__device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4], uint32_t lane,
+                                              uint32_t wm, uint32_t wn, uint32_t cb, uint32_t pix0,
+                                              uint32_t npix, uint32_t Hc, uint32_t Wc, uint32_t py,
+                                              uint32_t px) {
     // epilogue: lane (n, g) of tile (i, j) holds channels 16 mt + 4 g .. +3 of pixel 16 nt + n
     const uint32_t n = lane & 15u, g = lane >> 4;
     if constexpr (ACT) {
@@ -486,6 +303,253 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     }
 }
 
+template <bool ACT>
+__global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
+    __shared__ f4 As[kStages][kStepF4];       // [mt 8][hi,lo][64]
+    __shared__ f4 Bs[kStages][2 * kStepF4];   // [nt 16][hi,lo][64]
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
+    const uint32_t wm = wave & 1u, wn = wave >> 1;
+    // this workgroup's class (ranges start at multiples of 8: blockIdx.x % 8 is the XCD)
+    uint32_t ci = 0;
+    for (uint32_t i = 1; i < a.ncls; ++i)
+        if (blockIdx.x >= a.cls[i].tile0) ci = i;
+    const ConvClass &cl = a.cls[ci];
+    const uint32_t Hc = cl.Hc, Wc = cl.Wc, py = cl.py, px = cl.px;
+    const uint32_t ntaps = cl.ntaps, ntiles = cl.ntiles;
+    const uint32_t npix = a.B * Hc * Wc;
+    const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT;
+    const uint32_t loc = blockIdx.x - cl.tile0;
+#if CONV_XCD
+    // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs; give
+    // each XCD one contiguous run of the class's tiles, with the Cout block fastest,
+    // so the tiles that re-read an activation row (the other Cout blocks of the same
+    // pixels, the rows above and below through the taps) run on the same XCD at
+    // about the same time and hit its L2.
+    const uint32_t tile = (loc & 7u) * ((ntiles + 7) >> 3) + (loc >> 3);
+#else
+    const uint32_t tile = loc;
+#endif
+    if (tile >= ntiles) return;                       // padding slot (whole workgroup)
+    const uint32_t cb = tile % nB;
+    const uint32_t pix0 = (tile / nB) * kPT;
+    const uint32_t nk = nC * ntaps;
+
+    // LDS-DMA sources (6 pieces of 1 KB per wave per K-step).  Weights: the K-step's
+    // 16 KB block is contiguous; wave w moves pieces 2w, 2w+1.  Activations: the 32
+    // channels of one pixel are one 128-B line of the split-NHWC input
+    // ([g 4][hi 8, lo 8] halves); a piece is 8 pixels = 8 whole lines, region
+    // (nt, half) of n-tile nt = pixels 16 nt + 8 half .. +7.  Lane l fetches pixel
+    // l & 7, channel group g = (l >> 3) & 3, plane h = l >> 5 to LDS unit l, so a
+    // region holds [h][g][pixel] and the fragment read below is conflict-free.
+    // Wave w moves regions (2w, 0..1) and (2w+1, 0..1).
+    const uint32_t xbytes = a.B * a.Hin * a.Win * a.Cin * 4;
+    const v4i rw = make_rsrc(a.wpk, 9u * nC * nB * kStepF4 * 16u);
+    const v4i rx = make_rsrc(a.xs, xbytes);
+    const uint32_t loff = ((lane >> 3) & 3u) * 32u + (lane >> 5) * 16u;
+    // per tap (8-bit descriptors, SGPRs): packed weight tap, dy, dx
+    const uint32_t td0 = cl.td[0], td1 = cl.td[1], td2 = cl.td[2];
+    auto tapdesc = [&](uint32_t t) -> uint32_t {
+        const uint32_t w = t < 4 ? td0 : (t < 8 ? td1 : td2);
+        return (w >> (8 * (t & 3u))) & 0xFFu;
+    };
+    // Per activation piece: the lane's own input offset (its output pixel at dy = dx
+    // = 0, + channel group / plane) and a bit per tap telling whether the tap's
+    // input pixel exists (zero padding otherwise): the K loop then needs one add
+    // and one select per piece, all tap arithmetic being uniform (SALU).
+    uint32_t xoff[4], tmask[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t P = pix0 + (2 * wave + (k >> 1)) * 16 + (k & 1) * 8 + (lane & 7u);
+        const bool pv = P < npix;
+        const uint32_t Pc = pv ? P : 0;
+        const uint32_t hw = Hc * Wc;
+        const uint32_t pb = Pc / hw, rem = Pc % hw, pa = rem / Wc, pc = rem % Wc;
+        xoff[k] = ((pb * a.Hin + pa) * a.Win + pc) * a.Cin * 4u + loff;
+        uint32_t m = 0;
+        for (uint32_t t = 0; t < ntaps; ++t) {
+            const uint32_t d = tapdesc(t);
+            const int iy = (int)pa + (int)((d >> 4) & 3u) - 1, ix = (int)pc + (int)(d >> 6) - 1;
+            if (pv && iy >= 0 && iy < (int)a.Hin && ix >= 0 && ix < (int)a.Win) m |= 1u << t;
+        }
+        tmask[k] = m;
+    }
+
+    // K-step issue order is sequential (0, 1, 2 in the prologue, then ks + 3 at
+    // step ks): (channel group, tap) advance incrementally
+    // The address work (SALU tap decode, VALU offsets) is done in prep_step, ahead
+    // of the barrier and overlapped with MFMAs; fire_step after the barrier only
+    // moves M0 and issues the six DMAs.
+    uint32_t nx_c = 0, nx_t = 0;
+    struct StepDma {
+        uint32_t wsoff;           // weight pieces: global offset of this wave's first
+        uint32_t offs[4];         // activation pieces: per-lane global offsets
+    };
+    auto prep_step = [&]() -> StepDma {
+        StepDma r;
+        const uint32_t c = nx_c, tl = nx_t;
+        const bool wrap = nx_t + 1 == ntaps;
+        nx_t = wrap ? 0u : nx_t + 1;
+        nx_c = wrap ? nx_c + 1 : nx_c;
+        const uint32_t d = tapdesc(tl);
+        const uint32_t wbase = (((d & 15u) * nC + c) * nB + cb) * kStepF4 * 16u;
+        r.wsoff = wbase + 2 * wave * 1024u;
+        const int dy = (int)((d >> 4) & 3u) - 1, dx = (int)(d >> 6) - 1;
+        const uint32_t toff = (uint32_t)((dy * (int)a.Win + dx) * (int)a.Cin * 4) + c * 128u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool ok = (tmask[k] >> tl) & 1u;
+#if CONV_ABL == 1   // ablation: activations from a tiny L2-resident window
+            const uint32_t off = ((lane & 7u) * a.Cin * 4u + c * 128u + loff) + 0 * (ok ? 1u : 0u);
+#else
+            uint32_t off = ok ? xoff[k] + toff : 0x7FFFFFF0u;   // past num_records: zero fill
+#if CONV_ABL == 7      // ablation: same pattern folded into a 2 MB (L2-resident) window
+            off &= 0x1FFFFFu;
+#elif CONV_ABL == 8    // ... into a 64 MB window (Infinity-Cache resident)
+            off &= 0x3FFFFFFu;
+#endif
+#endif
+            r.offs[k] = off;
+        }
+        return r;
+    };
+    auto fire_step = [&](const StepDma &r, uint32_t buf) {
+        set_m0(lds_addr(&As[buf][2 * wave * 64]));
+        dma16<0>(rw, lane * 16u, r.wsoff);
+        dma16<1024>(rw, lane * 16u, r.wsoff);
+        // (one M0 per piece: an instruction offset would move the -- per-lane, possibly
+        // small -- global offsets too)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            set_m0(lds_addr(&Bs[buf][(4 * wave + k) * 64]));
+            dma16<0>(rx, r.offs[k], 0u);
+        }
+    };
+    auto issue_step = [&](uint32_t ks, uint32_t buf) {
+        (void)ks;
+        fire_step(prep_step(), buf);
+    };
+
+    f4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    // Fragments of one K-step: [0..3] A hi, [4..7] A lo, [8..11] B hi, [12..15] B lo.
+    // B lane (g = lane >> 4, n = lane & 15): region (nt, n >> 3), unit h 32 + 8 g + (n & 7).
+    const uint32_t boff = ((lane >> 3) & 1u) * 64u + (lane >> 4) * 8u + (lane & 7u);
+    auto read_frags = [&](f4 (&R)[16], uint32_t st) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            R[i] = As[st][((4 * wm + i) * 2) * 64 + lane];
+            R[4 + i] = As[st][((4 * wm + i) * 2 + 1) * 64 + lane];
+            R[8 + i] = Bs[st][((4 * wn + i) * 2) * 64 + boff];
+            R[12 + i] = Bs[st][((4 * wn + i) * 2) * 64 + boff + 32];
+        }
+    };
+    // rows i0 .. i0+nr-1 of the wave's 4 x 4 tiles; per A fragment the three split
+    // terms sweep the 4 B fragments (consecutive MFMAs never share an accumulator)
+    auto mfma_rows = [&](const f4 (&R)[16], int i0, int nr) {
+#pragma unroll
+        for (int i = i0; i < i0 + nr; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[4 + i], R[8 + j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[i], R[12 + j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[i], R[8 + j], acc[i][j]);
+        }
+    };
+
+#if CONV_REGDB
+    // Ring: step ks lives in stage ks % 3 and is read into registers half a step
+    // early.  Half-way through step ks (rows 0-1 done) the wave waits for its pieces
+    // of step ks+1 (ks+2's 6 may stay in flight), drains its LDS reads and meets the
+    // others at a raw barrier: after it step ks+1 is in LDS everywhere and nobody
+    // reads stage ks % 3 any more, so step ks+3 is issued into it and step ks+1's
+    // fragments are read while rows 2-3 of step ks compute.
+    auto step = [&](uint32_t ks, const f4 (&R)[16], f4 (&Rn)[16]) {
+        const bool fire = ks + kStages < nk;
+        const bool more = kStages == 3 && ks + 2 < nk;
+        StepDma pr = prep_step();                   // (counters advance past nk harmlessly)
+        // materialise the DMA addresses here, in the MFMA shadow (the compiler would
+        // otherwise sink them past the barrier into the issue block)
+        asm volatile("" : "+s"(pr.wsoff));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(pr.offs[k]));
+        mfma_rows(R, 0, 2);
+#if CONV_ABL == 4      // ablation: never wait for the DMA
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+        if (more) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+#if CONV_ABL != 5      // 5: ablation without the barrier
+        __builtin_amdgcn_s_barrier();
+#endif
+        const uint32_t st = ks % kStages;
+#if CONV_ABL != 6      // 6: ablation without in-loop staging
+        if (fire) fire_step(pr, st);
+#endif
+        if (ks + 1 < nk) read_frags(Rn, st == kStages - 1 ? 0u : st + 1);
+        mfma_rows(R, 2, 2);
+    };
+    issue_step(0, 0);
+    if (nk > 1) issue_step(1, 1);
+    if (kStages == 3 && nk > 2) issue_step(2, 2);
+    if (kStages == 3 && nk > 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    f4 R0[16], R1[16];
+    read_frags(R0, 0);
+    uint32_t ks = 0;
+    for (; ks + 1 < nk; ks += 2) {
+        step(ks, R0, R1);
+        step(ks + 1, R1, R0);
+    }
+    if (ks < nk) step(ks, R0, R1);
+#if CONV_ABL == 4
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#else
+    // Ring: step ks in stage ks % 3; steps ks+1, ks+2 in flight while ks computes.
+    // Stage (ks+2) % 3 last held step ks-1, whose reads every wave completed before
+    // the barrier that closed step ks-1.
+    issue_step(0, 0);
+    if (nk > 1) issue_step(1, 1);
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    uint32_t cur = 0;
+    for (uint32_t ks = 0; ks < nk; ++ks) {
+        const bool more = ks + 2 < nk;
+#if CONV_ABL == 2 || CONV_ABL == 3   // ablation: no staging in the loop (stale LDS)
+        (void)more;
+#else
+        if (more) issue_step(ks + 2, cur == 0 ? 2u : cur - 1);
+#endif
+        f4 R[16];
+        read_frags(R, cur);
+        mfma_rows(R, 0, 4);
+        // step ks+1 must have landed (only ks+2's 6 pieces may stay in flight), and
+        // this wave's fragment reads of stage `cur` must be done, before the barrier
+#if CONV_ABL == 3   // ablation: no staging, no barrier
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+        if (more) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#endif
+        cur = cur == 2 ? 0 : cur + 1;
+    }
+#endif
+
+    conv_epilogue<ACT>(a, acc, lane, wm, wn, cb, pix0, npix, Hc, Wc, py, px);
+}
+
+
 }  // namespace
 }  // namespace sdfr
 
@@ -547,6 +611,11 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
         c.tile0 = grid;
         c.ntiles = (B * Hc * Wc + kPT - 1) / kPT * (Cout / kCT);
         grid += (c.ntiles + 7) & ~7u;
+        for (uint32_t t = 0; t < nt; ++t) {
+            const uint32_t d = a.tap[c.t0 + t] | (uint32_t)(a.dy[c.t0 + t] + 1) << 4 |
+                               (uint32_t)(a.dx[c.t0 + t] + 1) << 6;
+            c.td[t >> 2] |= d << (8 * (t & 3u));
+        }
     };
     if (!transposed) {
         a.Hf = H;
