@@ -469,6 +469,7 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     // others at a raw barrier: after it step ks+1 is in LDS everywhere and nobody
     // reads stage ks % 3 any more, so step ks+3 is issued into it and step ks+1's
     // fragments are read while rows 2-3 of step ks compute.
+    uint32_t st_ks = 0;
     auto step = [&](uint32_t ks, const f4 (&R)[16], f4 (&Rn)[16]) {
         const bool fire = ks + kStages < nk;
         const bool more = kStages == 3 && ks + 2 < nk;
@@ -488,11 +489,12 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
 #if CONV_ABL != 5      // 5: ablation without the barrier
         __builtin_amdgcn_s_barrier();
 #endif
-        const uint32_t st = ks % kStages;
+        const uint32_t st = st_ks, st1 = st_ks == kStages - 1 ? 0u : st_ks + 1;
+        st_ks = st1;                                   // ks % kStages, carried
 #if CONV_ABL != 6      // 6: ablation without in-loop staging
         if (fire) fire_step(pr, st);
 #endif
-        if (ks + 1 < nk) read_frags(Rn, st == kStages - 1 ? 0u : st + 1);
+        if (ks + 1 < nk) read_frags(Rn, st1);
         mfma_rows(R, 2, 2);
     };
     issue_step(0, 0);
