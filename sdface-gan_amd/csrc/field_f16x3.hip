@@ -56,6 +56,11 @@ constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 t_out][hi,lo][64 l
 #ifndef SDFR_X_BUFLOAD
 #define SDFR_X_BUFLOAD 1
 #endif
+//   SDFR_X_RAWBAR    slice barrier as lgkmcnt(2) + s_barrier, leaving the next
+//                    slice's first-fragment reads in flight (1) / __syncthreads (0)
+#ifndef SDFR_X_RAWBAR
+#define SDFR_X_RAWBAR 1
+#endif
 //   SDFR_X_DMA       ring filled by LDS-DMA two slices ahead, counted vmcnt, raw
 //                    barrier (1) / staged through registers + __syncthreads (0);
 //                    measured 7 % slower than the register ring (6.14 vs 5.71 ms)
@@ -365,7 +370,17 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
         R.pre_h = An[0];
         R.pre_l = An[64];
     }
+#if SDFR_X_RAWBAR
+    // raw barrier: the slot writes must have landed, the next slice's first-fragment
+    // reads (the two youngest LDS ops, in order behind them) may stay in flight
+    if constexpr ((V & 1) == 0) {
+        if constexpr ((V & 2) == 0 && SDFR_X_PREFETCH) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+#else
     if constexpr ((V & 1) == 0) __syncthreads();
+#endif
 #endif
     ++R.it;
 }
