@@ -338,13 +338,22 @@ class Decoder(nn.Module):
                 and cout % 128 == 0 and cin % 32 == 0)
 
     def _pack(self, i, mc):
-        """Packed split-fp16 weights of layer i, rebuilt when the weight changes."""
+        """Per weight version of layer i: the packed split-fp16 weights, their row
+        scales su and, for the demodulation, su^2 * sum_{ky,kx} w^2 as [Cin, Cout]
+        plus su^2 * 1e-8: rsqrt(s^2 @ that + that) is demod / su exactly (powers
+        of two commute with rounding), in one GEMM + one rsqrt per call."""
         key = (mc.weight.data_ptr(), mc.weight._version, mc.weight.device)
         hit = self._packs.get(i)
         if hit is None or hit[0] != key:
-            hit = (key,) + conv_pack_weights(mc.weight[0], mc.scale)
+            packed, su = conv_pack_weights(mc.weight[0], mc.scale)
+            with torch.no_grad():
+                w = mc.scale * mc.weight[0]
+                s2 = su * su
+                wsq = ((w * w).sum([2, 3]) * s2[:, None]).t().contiguous()
+                eps = s2 * 1e-8
+            hit = (key, packed, su, wsq, eps)
             self._packs[i] = hit
-        return hit[1], hit[2]
+        return hit[1:]
 
     def _fused_forward(self, features, latent, noise):
         """Same computation as the module path: per layer one split-fp16 convolution
@@ -362,14 +371,15 @@ class Decoder(nn.Module):
         rgb = None
         for i, sc in enumerate(seq):
             mc = sc.conv
-            w = mc.scale * mc.weight[0]
-            demod = (torch.rsqrt((mods[i] * mods[i]) @ (w * w).sum([2, 3]).t() + 1e-8)
-                     if mc.demodulate else None)
             last = i == len(seq) - 1
+            cout = mc.weight.shape[1]
+            if split[i]:
+                packed, su, wsq, eps = self._pack(i, mc)
+                demod_su = (torch.rsqrt(torch.addmm(eps, mods[i] * mods[i], wsq))
+                            if mc.demodulate else 1.0 / su.expand(B, -1))
             if (self.fuse_conv_act and split[i] and not mc.upsample and (last or split[i + 1])
                     and (x.shape[1] * x.shape[2]) % 256 == 0):
                 # regular conv with the epilogue fused: the conv output stays on chip
-                packed, su = self._pack(i, mc)
                 H, W = x.shape[1], x.shape[2]
                 n = noise[i] if noise[i] is not None else features.new_empty(B, 1, H, W).normal_()
                 rgb_w = None
@@ -379,21 +389,24 @@ class Decoder(nn.Module):
                     s_rgb = tc.modulation(latent[:, i + 1])
                     rgb_w = (tc.scale * tc.weight[0, :, :, 0, 0])[None] * s_rgb[:, None, :]
                 x, part = conv3x3_f16x3_act(
-                    x, packed, w.shape[0], demod=demod / su, bias=sc.activate.bias,
+                    x, packed, cout, demod=demod_su, bias=sc.activate.bias,
                     noise_weight=sc.noise.weight, noise=n,
                     s_next=None if last else mods[i + 1], store_y=not last, rgb_w=rgb_w)
                 if part is not None:
                     rgb = rgb_finish(part, to_rgb.bias, skip=rgb if i else None, fir=self._fir)
                 continue
             if split[i]:
-                packed, su = self._pack(i, mc)
-                out = conv3x3_f16x3(x, packed, w.shape[0], transposed=mc.upsample)
-                demod = demod / su            # result carries su (power of two): exact
-            elif mc.upsample:
-                out = F.conv_transpose2d(x, w.transpose(0, 1).contiguous(memory_format=cl),
-                                         stride=2)
+                out = conv3x3_f16x3(x, packed, cout, transposed=mc.upsample)
+                demod = demod_su              # result carries su (power of two): exact
             else:
-                out = F.conv2d(x, w.contiguous(memory_format=cl), padding=mc.padding)
+                w = mc.scale * mc.weight[0]
+                demod = (torch.rsqrt((mods[i] * mods[i]) @ (w * w).sum([2, 3]).t() + 1e-8)
+                         if mc.demodulate else None)
+                if mc.upsample:
+                    out = F.conv_transpose2d(x, w.transpose(0, 1).contiguous(memory_format=cl),
+                                             stride=2)
+                else:
+                    out = F.conv2d(x, w.contiguous(memory_format=cl), padding=mc.padding)
             if mc.upsample:
                 H, W = out.shape[2] - 1, out.shape[3] - 1
             else:
