@@ -61,6 +61,15 @@ constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 t_out][hi,lo][64 l
 #ifndef SDFR_X_RAWBAR
 #define SDFR_X_RAWBAR 1
 #endif
+//   SDFR_X_SLICE2    ring of 2 x 32 KB slots holding whole K-steps (both halves):
+//                    one barrier per K-step instead of per half (1) / 3 x 16 KB (0)
+//                    (NgpNet only: SirenNet would spill and exceed 160 KB of LDS)
+#ifndef SDFR_X_SLICE2
+#define SDFR_X_SLICE2 1
+#endif
+#if SDFR_X_SLICE2 && (SDFR_X_DMA || !SDFR_X_PREFETCH || !SDFR_X_BUFLOAD)
+#error "SDFR_X_SLICE2 builds on the prefetching buffer_load register ring"
+#endif
 //   SDFR_X_DMA       ring filled by LDS-DMA two slices ahead, counted vmcnt, raw
 //                    barrier (1) / staged through registers + __syncthreads (0);
 //                    measured 7 % slower than the register ring (6.14 vs 5.71 ms)
@@ -75,6 +84,7 @@ constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 t_out][hi,lo][64 l
 // ----------------------------------------------------------------------------
 struct NgpNet {
     static constexpr bool kSiren = false;
+    static constexpr bool kSlice2 = SDFR_X_SLICE2;   // whole-K-step ring
     static constexpr int kLayers = 5;          // input_linear, pts_linears.0-2, views
     static constexpr int kFilmN = 4;           // FiLM: pts_linears.0-2, views
     static constexpr int kHidden = 3;          // dense layers after layer 0
@@ -86,6 +96,7 @@ struct NgpNet {
 };
 struct SirenNet {
     static constexpr bool kSiren = true;
+    static constexpr bool kSlice2 = false;
     static constexpr int kLayers = 9;          // pts_linears.0-7, views
     static constexpr int kFilmN = 9;
     static constexpr int kHidden = 7;
@@ -273,7 +284,9 @@ __device__ __forceinline__ uint32_t xdma_piece(uint32_t w, int k) {
 struct XRing {
     f4 *lds;              // [3][kXSliceF4]
     const f4 *packed;
-#if !SDFR_X_DMA
+#if SDFR_X_SLICE2
+    f4 st[2 * kXStage];   // the next K-step (both halves) staged through registers (NgpNet)
+#elif !SDFR_X_DMA
     f4 st[kXStage];       // the slice staged through registers
 #endif
     f4 pre_h, pre_l;      // first (hi, lo) A fragment of the current slice
@@ -307,18 +320,21 @@ __device__ __forceinline__ void xpin(float &x) { asm volatile("" : "+v"(x)); }
 template <int V, class Net, int H, class Side>
 __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], const f4 b0h,
                                       const f4 b0l, const f4 b1h, const f4 b1l, Side &&side) {
+    constexpr bool kS2 = Net::kSlice2;
+    // with kS2, K-step fs = it / 2 lives in slot fs % 2 (halves H = 0, 1 at +0 / +16 KB)
     const uint32_t cur = R.it % 3u;
 #if SDFR_X_DMA
     if constexpr ((V & 4) == 0) xdma_issue<Net>(R, (R.it + 2u) % Net::kSlices, (R.it + 2u) % 3u);
 #endif
-    const f4 *A = R.lds + cur * kXSliceF4 + (R.tid & 63u);
+    const f4 *A = kS2 ? R.lds + ((R.it >> 1) & 1u) * (2 * kXSliceF4) + H * kXSliceF4 + (R.tid & 63u)
+                      : R.lds + cur * kXSliceF4 + (R.tid & 63u);
     f4 ah[8], al[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         if constexpr ((V & 2) != 0) {
             ah[i] = b0h * (float)(i + 1);
             al[i] = b1l * (float)(i + 1);
-        } else if ((SDFR_X_PREFETCH || SDFR_X_DMA) && i == 0) {
+        } else if ((kS2 ? H == 1 : (SDFR_X_PREFETCH || SDFR_X_DMA)) && i == 0) {
             ah[0] = R.pre_h;
             al[0] = R.pre_l;
         } else {
@@ -337,6 +353,38 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
         acc1[t] = mfma16(ah[i], b1h, acc1[t]);
     }
     side();
+#if SDFR_X_SLICE2
+    if constexpr (kS2) {
+        // During K-step fs: its register-held successor fs+1 goes to slot (fs+1) % 2
+        // (free since the barrier that closed fs-1), half per half-step, each half's
+        // registers refilled from K-step fs+2; one barrier closes the K-step.
+        if constexpr ((V & 4) == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t fs = R.it >> 1;
+            f4 *wl = R.lds + ((fs + 1u) & 1u) * (2 * kXSliceF4) + H * kXSliceF4;
+#pragma unroll
+            for (int i = 0; i < kXStage; ++i) wl[R.tid + i * kThreads] = R.st[H * kXStage + i];
+            const uint32_t pf = (2u * fs + 4u + H) % Net::kSlices;
+#pragma unroll
+            for (int i = 0; i < kXStage; ++i)
+                R.st[H * kXStage + i] = __builtin_bit_cast(
+                    f4, __builtin_amdgcn_raw_buffer_load_b128(
+                            R.rsrc, (int)((R.tid + i * kThreads) * sizeof(f4)),
+                            (int)(pf * kXSliceF4 * sizeof(f4)), 0));
+        }
+        if constexpr (H == 0) {
+            if constexpr ((V & 2) == 0) {           // first fragment of the second half (same slot)
+                R.pre_h = A[kXSliceF4];
+                R.pre_l = A[kXSliceF4 + 64];
+            }
+        } else if constexpr ((V & 1) == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        ++R.it;
+        return;
+    }
+#endif
 #if SDFR_X_DMA
     if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // own pieces of it+1
     if constexpr ((V & 2) == 0) {
@@ -465,7 +513,7 @@ struct NoAct {
 template <int V, class Net>
 __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a) {
     constexpr int NL = Net::kLayers, NF = Net::kFilmN;
-    __shared__ f4 ring_lds[3 * kXSliceF4];                 // 48 KB weight ring
+    __shared__ f4 ring_lds[(Net::kSlice2 ? 4 : 3) * kXSliceF4];   // 64 / 48 KB weight ring
     __shared__ float cst[(NL + 5) * kW];                   // bias_s[NL], 1/su0, sigma_w, rgb_w[3]
     __shared__ float film_lds[NF * 2 * kW];                // the workgroup's face
     __shared__ f4 facc_lds[kWaves][16 * 64];               // 64 KB: feature accumulators
@@ -546,6 +594,16 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
         else v = a.rgb_w[i - (NL + 2) * kW];
         cst[i] = v;
     }
+    if constexpr (Net::kSlice2) {
+#if SDFR_X_SLICE2
+    // prologue: K-step 0 (half-slices 0, 1) -> slot 0; K-step 1 -> registers
+#pragma unroll
+    for (int i = 0; i < 2 * kXStage; ++i) R.lds[tid + i * kThreads] = a.packed[tid + i * kThreads];
+#pragma unroll
+    for (int i = 0; i < 2 * kXStage; ++i) R.st[i] = a.packed[2 * kXSliceF4 + tid + i * kThreads];
+    __syncthreads();
+#endif
+    } else {
 #if SDFR_X_DMA
     // prologue: slices 0, 1 -> slots 0, 1 (slice 2 is issued by the first step)
     xdma_issue<Net>(R, 0, 0);
@@ -561,6 +619,7 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
     for (int i = 0; i < kXStage; ++i) R.st[i] = a.packed[kPro * kXSliceF4 + tid + i * kThreads];
     __syncthreads();
 #endif
+    }
     R.pre_h = R.lds[lane];
     R.pre_l = R.lds[64 + lane];
 
