@@ -284,40 +284,47 @@ __global__ __launch_bounds__(256) void epi_plain_kernel(EpiArgs a, uint32_t tpp_
 #endif
 constexpr uint32_t kBlurRows = BLUR_ROWS;
 constexpr int kBlurGroup = BLUR_GROUP;   // input rows loaded together (kBlurRows % it == 0)
+#ifndef BLUR_COLS
+#define BLUR_COLS 4
+#endif
+constexpr int kBlurCols = BLUR_COLS;     // adjacent output columns per thread
 
 __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg) {
+    constexpr int NC = kBlurCols;                     // output columns per thread
     const uint32_t Q = a.C >> 2;
+    const uint32_t WG = (a.W + NC - 1) / NC;           // column groups
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t total = (uint64_t)a.B * nseg * a.W * Q;
+    const uint64_t total = (uint64_t)a.B * nseg * WG * Q;
     if (t >= total) return;
     const uint32_t q = (uint32_t)(t % Q);
-    const uint32_t ox = (uint32_t)((t / Q) % a.W);
-    const uint32_t seg = (uint32_t)((t / ((uint64_t)Q * a.W)) % nseg);
-    const uint32_t b = (uint32_t)(t / ((uint64_t)Q * a.W * nseg));
+    const uint32_t ox0 = (uint32_t)((t / Q) % WG) * NC;
+    const uint32_t seg = (uint32_t)((t / ((uint64_t)Q * WG)) % nseg);
+    const uint32_t b = (uint32_t)(t / ((uint64_t)Q * WG * nseg));
     const uint32_t c = 4 * q;
     const uint32_t Hi = a.H + 1, Wi = a.W + 1, C = a.C;
     const float *src = a.conv + (size_t)b * Hi * Wi * C + c;
     const float f0 = a.fir[3], f1 = a.fir[2], f2 = a.fir[1], f3 = a.fir[0];   // flipped taps
 
-    // the 4 horizontal taps of input row r: loads and filter split so that a group
-    // of rows can be loaded before any is filtered (4 rows = 16 loads in flight)
-    auto hload = [&](int r, float4 (&v)[4]) {
+    // input columns ox0 - 1 .. ox0 + NC + 1 of row r (shared by the NC outputs);
+    // loads and filter split so that a group of rows is loaded before any is
+    // filtered (4 rows x (NC + 3) loads in flight)
+    auto hload = [&](int r, float4 (&v)[NC + 3]) {
         const bool rok = r >= 0 && r < (int)Hi;
         const float *row = src + (size_t)(rok ? r : 0) * Wi * C;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int cc = (int)ox + j - 1;
+        for (int j = 0; j < NC + 3; ++j) {
+            const int cc = (int)ox0 + j - 1;
             v[j] = (rok && cc >= 0 && cc < (int)Wi) ? ld4(row + (size_t)cc * C)
                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    auto hfilt = [&](const float4 (&v)[4]) -> float4 {
+    auto hfilt = [&](const float4 (&v)[NC + 3], int k) -> float4 {   // output column ox0 + k
         const float fj[4] = {f0, f1, f2, f3};
         float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            h.x = fmaf(v[j].x, fj[j], h.x); h.y = fmaf(v[j].y, fj[j], h.y);
-            h.z = fmaf(v[j].z, fj[j], h.z); h.w = fmaf(v[j].w, fj[j], h.w);
+            h.x = fmaf(v[k + j].x, fj[j], h.x); h.y = fmaf(v[k + j].y, fj[j], h.y);
+            h.z = fmaf(v[k + j].z, fj[j], h.z); h.w = fmaf(v[k + j].w, fj[j], h.w);
         }
         return h;
     };
@@ -328,40 +335,51 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg)
     const float nw = a.noise ? *a.noise_weight : 0.0f;
     const uint32_t y0 = seg * kBlurRows;
     const uint32_t y1 = min(a.H, y0 + kBlurRows);
-    float4 h0, h1, h2;
+    float4 h0[NC], h1[NC], h2[NC];
     {
-        float4 v0[4], v1[4], v2[4];
+        float4 v0[NC + 3], v1[NC + 3], v2[NC + 3];
         hload((int)y0 - 1, v0);
         hload((int)y0, v1);
         hload((int)y0 + 1, v2);
-        h0 = hfilt(v0);
-        h1 = hfilt(v1);
-        h2 = hfilt(v2);
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            h0[k] = hfilt(v0, k);
+            h1[k] = hfilt(v1, k);
+            h2[k] = hfilt(v2, k);
+        }
     }
     for (uint32_t oy0 = y0; oy0 < y1; oy0 += kBlurGroup) {
-        float4 v[kBlurGroup][4];
-        float nz[kBlurGroup];
+        float4 v[kBlurGroup][NC + 3];
+        float nz[kBlurGroup][NC];
 #pragma unroll
-        for (int k = 0; k < kBlurGroup; ++k) {
-            hload((int)(oy0 + k) + 2, v[k]);
-            const size_t pix = ((size_t)b * a.H + min(oy0 + k, a.H - 1)) * a.W + ox;
-            nz[k] = a.noise ? nw * a.noise[pix] : 0.0f;
+        for (int g = 0; g < kBlurGroup; ++g) {
+            hload((int)(oy0 + g) + 2, v[g]);
+            const size_t prow = ((size_t)b * a.H + min(oy0 + g, a.H - 1)) * a.W;
+#pragma unroll
+            for (int k = 0; k < NC; ++k)
+                nz[g][k] = a.noise ? nw * a.noise[prow + min(ox0 + k, a.W - 1)] : 0.0f;
         }
 #pragma unroll
-        for (int k = 0; k < kBlurGroup; ++k) {
-            const uint32_t oy = oy0 + k;
-            const float4 h3 = hfilt(v[k]);
-            if (oy < y1) {
-                float4 s;
-                s.x = fmaf(h3.x, f3, fmaf(h2.x, f2, fmaf(h1.x, f1, h0.x * f0)));
-                s.y = fmaf(h3.y, f3, fmaf(h2.y, f2, fmaf(h1.y, f1, h0.y * f0)));
-                s.z = fmaf(h3.z, f3, fmaf(h2.z, f2, fmaf(h1.z, f1, h0.z * f0)));
-                s.w = fmaf(h3.w, f3, fmaf(h2.w, f2, fmaf(h1.w, f1, h0.w * f0)));
-                const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
-                const float4 vv = act4(s, dm, nz[k], bs, a.slope, a.act_scale);
-                store_y(a, pix * C + c, make_float4(vv.x * sn.x, vv.y * sn.y, vv.z * sn.z, vv.w * sn.w));
+        for (int g = 0; g < kBlurGroup; ++g) {
+            const uint32_t oy = oy0 + g;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                const float4 h3 = hfilt(v[g], k);
+                if (oy < y1 && ox0 + k < a.W) {
+                    float4 s;
+                    s.x = fmaf(h3.x, f3, fmaf(h2[k].x, f2, fmaf(h1[k].x, f1, h0[k].x * f0)));
+                    s.y = fmaf(h3.y, f3, fmaf(h2[k].y, f2, fmaf(h1[k].y, f1, h0[k].y * f0)));
+                    s.z = fmaf(h3.z, f3, fmaf(h2[k].z, f2, fmaf(h1[k].z, f1, h0[k].z * f0)));
+                    s.w = fmaf(h3.w, f3, fmaf(h2[k].w, f2, fmaf(h1[k].w, f1, h0[k].w * f0)));
+                    const size_t pix = ((size_t)b * a.H + oy) * a.W + ox0 + k;
+                    const float4 vv = act4(s, dm, nz[g][k], bs, a.slope, a.act_scale);
+                    store_y(a, pix * C + c,
+                            make_float4(vv.x * sn.x, vv.y * sn.y, vv.z * sn.z, vv.w * sn.w));
+                }
+                h0[k] = h1[k];
+                h1[k] = h2[k];
+                h2[k] = h3;
             }
-            h0 = h1; h1 = h2; h2 = h3;
         }
     }
 }
@@ -510,7 +528,7 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     if (s.blur_up) {
         const uint32_t nseg = (s.H + kBlurRows - 1) / kBlurRows;
-        const uint64_t total = (uint64_t)s.B * nseg * s.W * (s.C / 4);
+        const uint64_t total = (uint64_t)s.B * nseg * ((s.W + kBlurCols - 1) / kBlurCols) * (s.C / 4);
         epi_blur_kernel<<<(uint32_t)((total + 255) / 256), 256, 0, st>>>(a, nseg);
         return check_launch("styled_epilogue(blur)");
     }
