@@ -190,6 +190,24 @@ def reduce_loss_dict(loss_dict):
     return dict(zip(keys, vals))
 
 
+def allreduce_grads(params):
+    """Mean of the gradients over ranks as ONE flat all-reduce: for a backward
+    that bypasses the DDP wrapper (the stage-1 sphere init calls
+    ``g_module.init_forward``, training_utils.py:309, so under DDP the
+    reference's replicas drift apart there)."""
+    world = _world()
+    grads = [p.grad for p in params if p.grad is not None]
+    if world == 1 or not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat)
+    flat /= world
+    off = 0
+    for g in grads:
+        g.copy_(flat[off:off + g.numel()].view_as(g))
+        off += g.numel()
+
+
 # ---------------------------------------------------------------------------
 # the data-parallel stage-2 trainer
 # ---------------------------------------------------------------------------
@@ -332,5 +350,283 @@ class FullPipelineTrainer:
 
     def state_dict(self):
         """{g, d, g_ema} as the reference's checkpoints (training_utils.py:857-880)."""
+        return {"g": self.g_module.state_dict(), "d": self.d_module.state_dict(),
+                "g_ema": self.generator_test.state_dict()}
+
+
+# ---------------------------------------------------------------------------
+# stage 1: the volume renderer on its own (training_utils.py:197-551)
+# ---------------------------------------------------------------------------
+class VolumeRenderDiscConv2d(nn.Module):
+    """sdf_model.py:1224-1249."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True,
+                 activate=False):
+        super().__init__()
+        self.conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride, padding,
+                              bias=bias and not activate)
+        self.activate = activate
+        if self.activate:
+            self.activation = FusedLeakyReLU(out_channels, bias=bias, scale=1)
+            coef = math.sqrt(1 / (in_channels * kernel_size * kernel_size))
+            nn.init.uniform_(self.activation.bias, a=-coef, b=coef)
+
+    def forward(self, input):
+        out = self.conv(input)
+        return self.activation(out) if self.activate else out
+
+
+class AddCoords(nn.Module):
+    """sdf_model.py:1252-1275: append the y, x pixel coordinates in [-1, 1]."""
+
+    def forward(self, input_tensor):
+        b, _, dim_y, dim_x = input_tensor.shape
+        dev = input_tensor.device
+        xx = torch.arange(dim_x, dtype=torch.float32, device=dev).repeat(1, 1, dim_y, 1)
+        yy = torch.arange(dim_y, dtype=torch.float32, device=dev).repeat(1, 1, dim_x, 1)
+        yy = yy.transpose(2, 3)
+        xx = (xx / (dim_x - 1)) * 2 - 1
+        yy = (yy / (dim_y - 1)) * 2 - 1
+        return torch.cat([input_tensor, yy.repeat(b, 1, 1, 1), xx.repeat(b, 1, 1, 1)], dim=1)
+
+
+class CoordConv2d(nn.Module):
+    """sdf_model.py:1278-1296."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True):
+        super().__init__()
+        self.addcoords = AddCoords()
+        self.conv = nn.Conv2d(in_channels + 2, out_channels, kernel_size, stride=stride,
+                              padding=padding, bias=bias)
+
+    def forward(self, input_tensor):
+        return self.conv(self.addcoords(input_tensor))
+
+
+class CoordConvLayer(nn.Module):
+    """sdf_model.py:1299-1322."""
+
+    def __init__(self, in_channel, out_channel, kernel_size, bias=True, activate=True):
+        super().__init__()
+        self.activate = activate
+        self.padding = kernel_size // 2 if kernel_size > 2 else 0
+        self.conv = CoordConv2d(in_channel, out_channel, kernel_size, padding=self.padding,
+                                stride=1, bias=bias and not activate)
+        if activate:
+            self.activation = FusedLeakyReLU(out_channel, bias=bias, scale=1)
+        coef = math.sqrt(1 / (in_channel * kernel_size * kernel_size))
+        nn.init.uniform_(self.activation.bias, a=-coef, b=coef)
+
+    def forward(self, input):
+        out = self.conv(input)
+        return self.activation(out) if self.activate else out
+
+
+class VolumeRenderResBlock(nn.Module):
+    """sdf_model.py:1325-1351."""
+
+    def __init__(self, in_channel, out_channel):
+        super().__init__()
+        self.conv1 = CoordConvLayer(in_channel, out_channel, 3)
+        self.conv2 = CoordConvLayer(out_channel, out_channel, 3)
+        self.pooling = nn.AvgPool2d(2)
+        self.downsample = nn.AvgPool2d(2)
+        self.skip = (VolumeRenderDiscConv2d(in_channel, out_channel, 1)
+                     if out_channel != in_channel else None)
+
+    def forward(self, input):
+        out = self.pooling(self.conv2(self.conv1(input)))
+        skip_in = self.downsample(input)
+        if self.skip is not None:
+            skip_in = self.skip(skip_in)
+        return (out + skip_in) / math.sqrt(2)
+
+
+class VolumeRenderDiscriminator(nn.Module):
+    """sdf_model.py:1354-1398: judges the renderer's 64^2 thumbnails, with a
+    viewpoint (azimuth, elevation) regression head unless no_viewpoint_loss."""
+
+    def __init__(self, opt):
+        super().__init__()
+        init_size = opt.renderer_spatial_output_dim
+        self.viewpoint_loss = not opt.no_viewpoint_loss
+        final_out_channel = 3 if self.viewpoint_loss else 1
+        channels = {2: 400, 4: 400, 8: 400, 16: 400, 32: 256, 64: 128, 128: 64}
+        convs = [VolumeRenderDiscConv2d(3, channels[init_size], 1, activate=True)]
+        log_size = int(math.log(init_size, 2))
+        in_channel = channels[init_size]
+        for i in range(log_size - 1, 0, -1):
+            out_channel = channels[2 ** i]
+            convs.append(VolumeRenderResBlock(in_channel, out_channel))
+            in_channel = out_channel
+        self.convs = nn.Sequential(*convs)
+        self.final_conv = VolumeRenderDiscConv2d(in_channel, final_out_channel, 2)
+
+    def forward(self, input):
+        out = self.final_conv(self.convs(input))
+        gan_preds = out[:, 0:1].view(-1, 1)
+        viewpoints_preds = out[:, 1:].view(-1, 2) if self.viewpoint_loss else None
+        return gan_preds, viewpoints_preds
+
+
+def viewpoints_loss(viewpoint_pred, viewpoint_target):
+    """sdf_losses.py:7-10."""
+    return F.smooth_l1_loss(viewpoint_pred, viewpoint_target)
+
+
+def eikonal_loss(eikonal_term, sdf=None, beta=100):
+    """sdf_losses.py:13-24: (|grad sdf| - 1)^2 and the minimal-surface term."""
+    eik = 0 if eikonal_term is None else ((eikonal_term.norm(dim=-1) - 1) ** 2).mean()
+    if sdf is None:
+        surf = torch.tensor(0.0, device=eikonal_term.device)
+    else:
+        surf = torch.exp(-beta * torch.abs(sdf)).mean()
+    return eik, surf
+
+
+def _coordinates(n, device):
+    r = torch.arange(0, n, dtype=torch.long, device=device)
+    x, y, z = torch.meshgrid(r, r, r, indexing="ij")
+    return torch.stack([x, y, z], dim=-1)
+
+
+def smoothness(generator, bounding_box, styles, device, sample_points=32, voxel_size=0.1,
+               margin=0.05):
+    """smoothLoss.py:5-27: total variation of the hash-grid features over a random
+    32^3 voxel block inside the bounding box ([3, 2] min / max per axis)."""
+    offset_max = bounding_box[:, 1] - bounding_box[:, 0] - (sample_points - 1) * voxel_size \
+        - 2 * margin
+    offset = torch.rand(3).to(offset_max) * offset_max + margin
+    coords = _coordinates(sample_points - 1, "cpu").float().to(bounding_box)
+    pts = (coords + torch.rand((1, 1, 1, 3)).to(bounding_box)) * voxel_size \
+        + bounding_box[:, 0] + offset
+    pts = ((pts - bounding_box[:, 0]) / (bounding_box[:, 1] - bounding_box[:, 0])).to(device)
+    sdf = generator.renderer.network.query_sdf(pts, styles)
+    tv_x = torch.pow(sdf[1:, ...] - sdf[:-1, ...], 2).sum()
+    tv_y = torch.pow(sdf[:, 1:, ...] - sdf[:, :-1, ...], 2).sum()
+    tv_z = torch.pow(sdf[:, :, 1:, ...] - sdf[:, :, :-1, ...], 2).sum()
+    return (tv_x + tv_y + tv_z) / (sample_points ** 3)
+
+
+class RendererTrainer:
+    """Stage 1: Generator(full_pipeline=False) + EMA copy + VolumeRenderDiscriminator
+    with the reference's optimizers (config.py:196-200: Adam, G lr 2e-5, D lr 2e-4,
+    betas (0, 0.9)).  The renderer trains through the op-by-op path: every
+    hash-grid / SH evaluation is the HIP encoder op with its HIP backward (table
+    gradients by fp32 atomics, dy_dx for the eikonal term), so it needs the GPU.
+    ``sphere_init_step()`` is one iteration of the SDF-to-sphere initialisation,
+    ``step(real_thumbs)`` one D + G iteration (training_utils.py:287-451)."""
+
+    def __init__(self, opt, device, seed=0):
+        self.opt, self.t, self.device = opt, opt.training, device
+        self.world = _world()
+        torch.manual_seed(seed)
+        random.seed(seed)
+        self.generator = Generator(opt.model, opt.rendering, full_pipeline=False).to(device)
+        self.generator_test = Generator(opt.model, opt.rendering, ema=True,
+                                        full_pipeline=False).to(device).eval()
+        self.discriminator = VolumeRenderDiscriminator(opt.model).to(device)
+        accumulate(self.generator_test, self.generator, 0)
+        self.optimizer = torch.optim.Adam(self.generator.parameters(), lr=2e-5, betas=(0.0, 0.9))
+        self.optimizer_d = torch.optim.Adam(self.discriminator.parameters(), lr=2e-4,
+                                            betas=(0.0, 0.9))
+        self.g_module, self.d_module = self.generator, self.discriminator
+        if self.world > 1:
+            from torch.nn.parallel import DistributedDataParallel as DDP
+            kw = dict(broadcast_buffers=False)
+            if device.type == "cuda":
+                kw.update(device_ids=[device.index], output_device=device.index)
+            self.generator = DDP(self.generator, **kw)
+            self.discriminator = DDP(self.discriminator, **kw)
+        self.accum = 0.5 ** (32 / (10 * 1000))
+        self.iteration = 0
+
+    def _cams(self, n):
+        c = self.opt.camera
+        return generate_camera_params(self.t.renderer_output_size, self.device, batch=n,
+                                      uniform=c.uniform, azim_range=c.azim, elev_range=c.elev,
+                                      fov_ang=c.fov, dist_radius=c.dist_radius)
+
+    def sphere_init_step(self, batch=3):
+        """MLP init to a sphere SDF (training_utils.py:287-317): L1(sdf, |x| - r)."""
+        noise = mixing_noise(batch, self.t.style_dim, self.t.mixing, self.device)
+        cam, focal, near, far, _ = self._cams(batch)
+        sdf, target = self.g_module.init_forward(noise, cam, focal, near, far)
+        loss = F.l1_loss(sdf, target)
+        loss.backward()
+        allreduce_grads(list(self.g_module.parameters()))
+        self.optimizer.step()
+        self.g_module.zero_grad(set_to_none=True)
+        return loss.detach()
+
+    def step(self, real_imgs):
+        t, dev = self.t, self.device
+        batch, chunk = real_imgs.shape[0], t.chunk
+        view = t.view_lambda > 0
+        with_sdf = getattr(t, "with_sdf", True)
+        zero = torch.zeros((), device=dev)
+        loss = {}
+
+        # --- discriminator (training_utils.py:336-394)
+        requires_grad(self.g_module.parameters(), False)
+        requires_grad(self.d_module.parameters(), True)
+        self.d_module.zero_grad(set_to_none=True)
+        noise = mixing_noise(batch, t.style_dim, t.mixing, dev)
+        cam, focal, near, far, gt_view = self._cams(batch)
+        gen = []
+        for j in range(0, batch, chunk):
+            _, fake = self.g_module([n[j:j + chunk] for n in noise], cam[j:j + chunk],
+                                    focal[j:j + chunk], near[j:j + chunk], far[j:j + chunk])
+            gen.append(fake)
+        gen = torch.cat(gen, 0)
+        fake_pred, fake_view_pred = self.discriminator(gen.detach())
+        d_view = t.view_lambda * viewpoints_loss(fake_view_pred, gt_view) if view else zero
+        real = real_imgs.detach().requires_grad_(True)
+        real_pred, _ = self.discriminator(real)
+        d_gan = d_logistic_loss(real_pred, fake_pred)
+        r1 = t.r1 * 0.5 * d_r1_loss(real_pred, real)
+        (d_gan + r1 + d_view).backward()
+        self.optimizer_d.step()
+        loss.update(d=d_gan, r1=r1, d_view=d_view, real_score=real_pred.mean(),
+                    fake_score=fake_pred.mean())
+
+        # --- generator (training_utils.py:396-451)
+        requires_grad(self.g_module.parameters(), True)
+        requires_grad(self.d_module.parameters(), False)
+        eik_on, surf_on = with_sdf and t.eikonal_lambda > 0, t.min_surf_lambda > 0
+        g_view = g_eik = g_surf = g_smooth = zero
+        for j in range(0, batch, chunk):
+            noise = mixing_noise(chunk, t.style_dim, t.mixing, dev)
+            cam, focal, near, far, gt_view = self._cams(chunk)
+            out = self.generator(noise, cam, focal, near, far, return_sdf=surf_on,
+                                 return_eikonal=eik_on)
+            fake = out[1]
+            sdf = out[2] if surf_on else None
+            eik_term = out[2 + int(surf_on)] if eik_on else None
+            fake_pred, fake_view_pred = self.discriminator(fake)
+            if view:
+                g_view = t.view_lambda * viewpoints_loss(fake_view_pred, gt_view)
+            if eik_on:
+                g_eik, g_surf = eikonal_loss(eik_term, sdf=sdf, beta=t.min_surf_beta)
+                g_eik = t.eikonal_lambda * g_eik
+                if surf_on:
+                    g_surf = t.min_surf_lambda * g_surf
+                # fixed box of the reference (training_utils.py:433-436); only the
+                # hash-grid network has query_sdf (the reference raises for SIREN)
+                if hasattr(self.g_module.renderer.network, "query_sdf"):
+                    box = torch.tensor([[-1.0, 7.0], [-1.3, 3.7], [-1.7, 1.4]], device=dev)
+                    g_smooth = 1000 * smoothness(self.g_module, box, noise, dev)
+            g_gan = g_nonsaturating_loss(fake_pred)
+            (g_gan + g_view + g_eik + g_surf + g_smooth).backward()
+        self.optimizer.step()
+        self.g_module.zero_grad(set_to_none=True)
+        loss.update(g=g_gan, g_view=g_view, g_eikonal=g_eik, g_minimal_surface=g_surf,
+                    g_smooth=g_smooth)
+        accumulate(self.generator_test, self.g_module, self.accum)
+        self.iteration += 1
+        return reduce_loss_dict(loss)
+
+    def state_dict(self):
+        """{g, d, g_ema} as the reference's volume_renderer checkpoints."""
         return {"g": self.g_module.state_dict(), "d": self.d_module.state_dict(),
                 "g_ema": self.generator_test.state_dict()}
