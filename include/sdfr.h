@@ -205,6 +205,14 @@ int sdfr_render_ngp_encode_only(const sdfr_ngp_weights *w,
  * the product build accepts 0 only (SDFR_EINVAL otherwise). */
 int sdfr_debug_set_field_variant(int variant);
 
+/* Selects the hash-grid gather variant of the ngp encode stage for later calls
+ * (process-global; default 2, overridable at load by SDFR_ENC_MODE): the low
+ * bits are the levels handled per thread (1, 2 or 4), +8 disables the paired
+ * 16-B x-corner loads (only with 1 level per thread: mode 9).  Every mode
+ * produces bit-identical features; modes exist to measure the gather
+ * (scripts/encode_time.py).  SDFR_EINVAL for any other value. */
+int sdfr_debug_set_encode_mode(int mode);
+
 /* Accuracy probe for the two device sin implementations the field kernel can
  * use (software Cody-Waite + polynomial, hardware v_sin_f32 after reduction):
  * out_cw[i] = sin_cw(x[i]), out_hw[i] = sin_hw(x[i]), n elements. */

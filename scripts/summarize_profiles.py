@@ -37,8 +37,15 @@ def counters(path):
     return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
 
 
-def pick(d, key):
-    hits = [k for k in d if key in k]
+def pick(d, name):
+    """Duration of kernel `name`: exact name, else the same name up to its argument
+    list (the counter and trace CSVs may differ in the 'void ' prefix)."""
+    if name in d:
+        return d[name]
+    def base(k):
+        k = k[5:] if k.startswith("void ") else k
+        return k[:k.rfind("(")] if k.endswith(")") else k
+    hits = [k for k in d if base(k) == base(name)]
     return d[hits[0]] if hits else None
 
 
@@ -75,7 +82,7 @@ def main():
             "fetch_bytes_corrected": None if f is None else f * 1024 * 2,
             "write_bytes": None if w is None else w * 1024,
             "dispatches": {"fetch": nf.get(name), "write": nw.get(name)},
-            "avg_duration_ns": pick(durations, name.split("(")[0]),
+            "avg_duration_ns": pick(durations, name),
         }
     (dst / f"{a.tag}_traffic.json").write_text(json.dumps(out, indent=1))
 

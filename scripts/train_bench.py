@@ -1,13 +1,21 @@
-"""BASELINE configs[2] / configs[4]: stage-2 training throughput, DDP over RCCL.
+"""BASELINE configs[2] / configs[4]: training throughput, DDP over RCCL.
 
-    python scripts/train_bench.py [--net ngp|siren] [--steps K] [--warmup W]
+    python scripts/train_bench.py [--stage 1|2] [--net ngp|siren] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 scripts/train_bench.py ...
 
 Random-init G/D (no checkpoints offline), synthetic real images; per GPU batch 8 in
 chunks of 2 (train.py defaults), R1 every 16, path regularisation every 4 steps.
 One JSON line: training steps/s and faces/s (all ranks; each step renders
 batch D-fakes + batch G-fakes, + batch/2 every 4th step), timed between barriers,
-max over ranks."""
+max over ranks.
+
+--stage 1 measures renderer training (training_utils.py:287-451; SURVEY §8(d) "stage 1
+reported separately as 64^2 thumbs/s"): the renderer trains through the op-by-op path
+with the HIP hash-grid / SH encoder forward and backward (table gradients by fp32
+atomics, dy_dx for the eikonal term), VolumeRenderDiscriminator on 64^2 thumbs, the
+eikonal + minimal-surface + smoothness losses; one step = one D and one G iteration
+over `batch` thumbs (D-fakes + G-fakes).  Stage 1 uses batch 8 in chunks of 2 too
+unless --batch/--chunk say otherwise."""
 import argparse
 import json
 import os
@@ -24,6 +32,7 @@ from sdfr_loader import load  # noqa: E402
 
 def main():
     p = argparse.ArgumentParser()
+    p.add_argument("--stage", type=int, default=2, choices=[1, 2])
     p.add_argument("--net", default="ngp", choices=["ngp", "siren"])
     p.add_argument("--steps", type=int, default=8)
     p.add_argument("--warmup", type=int, default=4)
@@ -38,13 +47,18 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     sdfr = load()
-    from sdface_gan_amd.training import FullPipelineTrainer
-    opt = sdfr.vol_render_opt(ngp=a.net == "ngp", batch=a.batch, chunk=a.chunk)
-    tr = FullPipelineTrainer(opt, dev, seed=0)
+    from sdface_gan_amd.training import FullPipelineTrainer, RendererTrainer
+    opt = sdfr.vol_render_opt(ngp=a.net == "ngp", batch=a.batch, chunk=a.chunk,
+                              train_renderer=a.stage == 1)
+    if a.stage == 1:
+        tr = RendererTrainer(opt, dev, seed=0)
+        size = opt.training.renderer_output_size
+    else:
+        tr = FullPipelineTrainer(opt, dev, seed=0)
+        size = opt.model.size
     tr.g_module.renderer.rng_device = "device"
     tr.generator_test.renderer.rng_device = "device"
     torch.manual_seed(1000 + rank)
-    size = opt.model.size
     real = [torch.rand(a.batch, 3, size, size, device=dev) * 2 - 1 for _ in range(4)]
     for k in range(a.warmup):
         tr.step(real[k % 4])
@@ -63,14 +77,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     if rank == 0:
+        metric = ("stage-1 renderer training throughput (HIP encoder forward + backward)"
+                  if a.stage == 1 else
+                  "stage-2 training throughput (renderer frozen, fused HIP forward)")
+        unit = "64^2 thumbs/s (real-batch thumbs)" if a.stage == 1 else \
+            "faces/s (real-batch faces)"
         print(json.dumps({
-            "metric": "stage-2 training throughput (renderer frozen, fused HIP forward)",
-            "value": world * a.batch * a.steps / el, "unit": "faces/s (real-batch faces)",
+            "metric": metric, "value": world * a.batch * a.steps / el, "unit": unit,
             "steps_per_s": a.steps / el, "ms_per_step": el / a.steps * 1e3, "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "scaling": "weak",
-            "config": {"workload": f"train.py stage 2, {a.net} renderer, random-init G/D",
+            "config": {"workload": f"train.py stage {a.stage}, {a.net} renderer, random-init G/D",
                        "batch_per_gpu": a.batch, "chunk": a.chunk, "size": size,
-                       "parallelism": f"ddp{world} (RCCL all-reduce of decoder + D grads)"},
+                       "parallelism": f"ddp{world} (RCCL all-reduce of "
+                                      f"{'G' if a.stage == 1 else 'decoder'} + D grads)"},
             "losses": {k: float(v) for k, v in losses.items()}}), flush=True)
     if world > 1:
         dist.destroy_process_group()

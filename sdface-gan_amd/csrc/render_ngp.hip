@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "render_ngp.h"
@@ -116,48 +117,114 @@ struct EncodeArgs {
     const int32_t *offsets;
     float *enc;                    // [L][S_total][2]
     LevelTable lt;
+    int pair_ok;                   // table 16-B aligned (paired corner loads)
 };
 
+// Encode launch options (SDFR_ENC_MODE = LPT | 8*!PAIR overrides, ablations only):
+//  PAIR  the x-neighbour corners (g0, g0+1) come from one aligned 16-B load
+//        whenever their rows are {i, i^1} (hash prime 1 on x: always for even
+//        g0; dense rows: for even i); a second 8-B load only for the lanes
+//        where they are not (-14% encode time, scripts/encode_time.py).
+//  LPT   levels per thread {y, y+16/LPT, ...}: the ray/sample/normalisation
+//        chain is computed once for LPT levels and LPT gathers are in flight.
+constexpr uint32_t kEncDefault = 2;
+
+// level_interp<3,2> with paired x-corner loads: the same corner weights
+// (x factor first, then y, z) and the same fma order over corners 0..7, so the
+// result is bit-identical to level_interp.
+__device__ __forceinline__ void level_interp_pair(const float *__restrict__ grid,
+                                                  const LevelParam &q,
+                                                  const LevelCoord<3, 2> &lc, float (&out)[2]) {
+    float v[8][2];
+    float wts[8];
+#pragma unroll
+    for (uint32_t idx = 0; idx < 8; idx += 2) {
+        uint32_t pl[3];
+        float w0 = __fsub_rn(1.0f, lc.pos[0]), w1 = lc.pos[0];
+#pragma unroll
+        for (uint32_t d = 1; d < 3; ++d) {
+            const bool hi = idx & (1u << d);
+            pl[d] = hi ? lc.pg[d] + 1 : lc.pg[d];
+            const float f = hi ? lc.pos[d] : __fsub_rn(1.0f, lc.pos[d]);
+            w0 = __fmul_rn(w0, f);
+            w1 = __fmul_rn(w1, f);
+        }
+        wts[idx] = w0;
+        wts[idx + 1] = w1;
+        pl[0] = lc.pg[0];
+        const uint32_t i0 = grid_index<3>(q, 0, pl);
+        pl[0] = lc.pg[0] + 1;
+        const uint32_t i1 = grid_index<3>(q, 0, pl);
+        const float4 t = *reinterpret_cast<const float4 *>(grid + (size_t)(i0 & ~1u) * 2);
+        const bool odd = i0 & 1u;
+        v[idx][0] = odd ? t.z : t.x;
+        v[idx][1] = odd ? t.w : t.y;
+        if (i1 == (i0 ^ 1u)) {
+            v[idx + 1][0] = odd ? t.x : t.z;
+            v[idx + 1][1] = odd ? t.y : t.w;
+        } else {
+            const float2 u = *reinterpret_cast<const float2 *>(grid + (size_t)i1 * 2);
+            v[idx + 1][0] = u.x;
+            v[idx + 1][1] = u.y;
+        }
+    }
+    out[0] = out[1] = 0.0f;
+#pragma unroll
+    for (uint32_t idx = 0; idx < 8; ++idx)
+#pragma unroll
+        for (uint32_t c = 0; c < 2; ++c) out[c] = __fmaf_rn(wts[idx], v[idx][c], out[c]);
+}
+
+template <bool PAIR, uint32_t LPT>
 __global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
     const uint32_t sid = blockIdx.x * 256 + threadIdx.x;
     if (sid >= a.g.S_total) return;
-    const uint32_t level = blockIdx.y;
-    LevelParam q = a.lt.p[level];
-    finish_level(q, a.offsets, level, 3, 0, 0);
-    float2 *out = reinterpret_cast<float2 *>(a.enc) + (size_t)level * a.g.S_total + sid;
+    float2 *out = reinterpret_cast<float2 *>(a.enc) + sid;
+    constexpr uint32_t kStep = 16 / LPT;
 
     const SampleId id = decode_sid(a.g, sid);
-    if (!id.valid) {
-        *out = make_float2(0.0f, 0.0f);
-        return;
-    }
-    const uint32_t y = id.ray_local / a.g.W, x = id.ray_local % a.g.W;
-    const uint32_t ray_index = (id.b * a.g.H + y) * a.g.W + x;
-    Ray ray;
-    make_ray(a.g.cam + (size_t)id.b * 12, a.g.focal[id.b], a.g.pix_x[x], a.g.pix_y[y],
-             a.g.half_res, ray);
-    const float nr = a.g.near_[id.b], fr = a.g.far_[id.b];
-    const float z = sample_z(a.g.sc, nr, fr, ray_index, id.s);
-    const float span = __fsub_rn(fr, nr);
+    bool zero = !id.valid;
     float u[3];
-    bool oob = false;
+    if (!zero) {
+        const uint32_t y = id.ray_local / a.g.W, x = id.ray_local % a.g.W;
+        const uint32_t ray_index = (id.b * a.g.H + y) * a.g.W + x;
+        Ray ray;
+        make_ray(a.g.cam + (size_t)id.b * 12, a.g.focal[id.b], a.g.pix_x[x], a.g.pix_y[y],
+                 a.g.half_res, ray);
+        const float nr = a.g.near_[id.b], fr = a.g.far_[id.b];
+        const float z = sample_z(a.g.sc, nr, fr, ray_index, id.s);
+        const float span = __fsub_rn(fr, nr);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));            // :343
-        const float np_ = a.g.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;  // :349
-        u[k] = __fdiv_rn(__fadd_rn(np_, a.g.bound), __fmul_rn(2.0f, a.g.bound));   // grid.py:149
-        if (u[k] < 0 || u[k] > 1) oob = true;
+        for (int k = 0; k < 3; ++k) {
+            const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));            // :343
+            const float np_ = a.g.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;  // :349
+            u[k] = __fdiv_rn(__fadd_rn(np_, a.g.bound), __fmul_rn(2.0f, a.g.bound));   // grid.py:149
+            if (u[k] < 0 || u[k] > 1) zero = true;                                 // OOB -> 0
+        }
     }
-    if (oob) {
-        *out = make_float2(0.0f, 0.0f);
+    if (zero) {
+#pragma unroll
+        for (uint32_t j = 0; j < LPT; ++j)
+            out[(size_t)(blockIdx.y + j * kStep) * a.g.S_total] = make_float2(0.0f, 0.0f);
         return;
     }
-    const float *grid = a.emb + (size_t)q.offset * 2;
-    LevelCoord<3, 2> lc;
-    level_coord<3, 2>(u, q, 0, 0, lc);
-    float res[2];
-    level_interp<3, 2>(grid, q, 0, lc, res);
-    *out = make_float2(res[0], res[1]);
+#pragma unroll
+    for (uint32_t j = 0; j < LPT; ++j) {
+        const uint32_t level = blockIdx.y + j * kStep;
+        LevelParam q = a.lt.p[level];
+        finish_level(q, a.offsets, level, 3, 0, 0);
+        const float *grid = a.emb + (size_t)q.offset * 2;
+        LevelCoord<3, 2> lc;
+        level_coord<3, 2>(u, q, 0, 0, lc);
+        float res[2];
+        // pairs are 16-B aligned when the level base (offset) is even and the
+        // table itself is 16-B aligned (host check, a.pair_ok)
+        if (PAIR && a.pair_ok && !(q.offset & 1u))
+            level_interp_pair(grid, q, lc, res);
+        else
+            level_interp<3, 2>(grid, q, 0, lc, res);
+        out[(size_t)level * a.g.S_total] = make_float2(res[0], res[1]);
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -690,6 +757,17 @@ static int launch_prep(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
     return check_launch("render_ngp: prep");
 }
 
+static uint32_t g_encode_mode = [] {
+    const char *e = std::getenv("SDFR_ENC_MODE");   // ablations only
+    return e ? (uint32_t)std::atoi(e) : kEncDefault;
+}();
+
+template <bool PAIR, uint32_t LPT>
+static void launch_encode_mode(uint32_t nchunks, hipStream_t st, const EncodeArgs &e) {
+    hipLaunchKernelGGL((ngp_encode_kernel<PAIR, LPT>), dim3(nchunks, 16 / LPT), dim3(256), 0, st,
+                       e);
+}
+
 static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
                          const GeomArgs &g, float *enc, hipStream_t st) {
     EncodeArgs e;
@@ -697,8 +775,15 @@ static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *
     e.emb = w->embeddings;
     e.offsets = w->offsets;
     e.enc = enc;
+    e.pair_ok = (reinterpret_cast<uintptr_t>(w->embeddings) & 15u) == 0;
     make_level_table(16, w->log2_per_level_scale, w->base_resolution, e.lt);
-    hipLaunchKernelGGL(ngp_encode_kernel, dim3((g.S_total + 255) / 256, 16), dim3(256), 0, st, e);
+    const uint32_t nchunks = (g.S_total + 255) / 256;
+    switch (g_encode_mode) {
+        case 8 | 1: launch_encode_mode<false, 1>(nchunks, st, e); break;
+        case 2: launch_encode_mode<true, 2>(nchunks, st, e); break;
+        case 4: launch_encode_mode<true, 4>(nchunks, st, e); break;
+        default: launch_encode_mode<true, 1>(nchunks, st, e); break;
+    }
     return check_launch("render_ngp: encode");
 }
 
@@ -714,6 +799,13 @@ int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t 
     hipLaunchKernelGGL(sin_probe_kernel, dim3((n + 255) / 256), dim3(256), 0,
                        (hipStream_t)stream, x, out_cw, out_hw, n);
     return check_launch("sin_probe");
+}
+
+int sdfr_debug_set_encode_mode(int mode) {
+    if (mode != 1 && mode != 2 && mode != 4 && mode != 9)
+        return fail(SDFR_EINVAL, "sdfr_debug_set_encode_mode: mode must be 1, 2, 4 or 9");
+    g_encode_mode = (uint32_t)mode;
+    return SDFR_OK;
 }
 
 int sdfr_debug_set_field_variant(int variant) {

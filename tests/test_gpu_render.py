@@ -111,18 +111,25 @@ def _tile_order_to_samples(enc, B, H, W, N):
     return e.reshape(B * H * W * N, L * 2)
 
 
+@pytest.mark.parametrize("mode", [2, 1, 4, 9])
 @pytest.mark.parametrize("name", ["render_small", "render_face64"])
-def test_encode_stage_bit_exact(sdfr, oracle_mod, golden_dir, renderer_sd, name):
+def test_encode_stage_bit_exact(sdfr, oracle_mod, golden_dir, renderer_sd, name, mode):
     """Every sample's 32 hash-grid features equal the oracle's, bit for bit: this
-    pins ray generation, sampling, normalisation and the grid index math."""
+    pins ray generation, sampling, normalisation and the grid index math, for
+    every gather variant (levels per thread 1/2/4, paired or single corner loads)."""
     g = np.load(golden_dir / f"{name}.npz")
     res, N = int(g["res"]), int(g["n_samples"])
     ren = make_renderer(sdfr, renderer_sd, res, N)
     cam, focal, near, far, lat, tr = _inputs(g)
     B = cam.shape[0]
-    with torch.no_grad():
-        ws = ren.fused_forward(cam, focal, near, far, lat, t_rand=tr, encode_only=True)
-    torch.cuda.synchronize()
+    L = sdfr._lib
+    L.check(L.lib().sdfr_debug_set_encode_mode(mode), "sdfr_debug_set_encode_mode")
+    try:
+        with torch.no_grad():
+            ws = ren.fused_forward(cam, focal, near, far, lat, t_rand=tr, encode_only=True)
+        torch.cuda.synchronize()
+    finally:
+        L.check(L.lib().sdfr_debug_set_encode_mode(2), "sdfr_debug_set_encode_mode")
     tiles = (res * res + 15) // 16
     S = B * tiles * N * 16
     enc = ws[: S * 16 * 2 * 4].view(torch.float32).cpu().numpy()
