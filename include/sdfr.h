@@ -206,11 +206,12 @@ int sdfr_render_ngp_encode_only(const sdfr_ngp_weights *w,
 int sdfr_debug_set_field_variant(int variant);
 
 /* Selects the hash-grid gather variant of the ngp encode stage for later calls
- * (process-global; default 2, overridable at load by SDFR_ENC_MODE): the low
- * bits are the levels handled per thread (1, 2 or 4), +8 disables the paired
- * 16-B x-corner loads (only with 1 level per thread: mode 9).  Every mode
- * produces bit-identical features; modes exist to measure the gather
- * (scripts/encode_time.py).  SDFR_EINVAL for any other value. */
+ * (process-global; default 289, overridable at load by SDFR_ENC_MODE): the low
+ * bits are the levels handled per thread (1 or 2), +8 disables the paired
+ * x-corner loads (mode 9), +32 gives each thread two samples, +256 pairs any
+ * consecutive rows with dword-aligned 16-B loads.  Accepted: 1, 2, 9, 33, 257,
+ * 289, 290.  Every mode produces bit-identical features; modes exist to measure
+ * the gather (scripts/encode_time.py).  SDFR_EINVAL for any other value. */
 int sdfr_debug_set_encode_mode(int mode);
 
 /* Accuracy probe for the two device sin implementations the field kernel can

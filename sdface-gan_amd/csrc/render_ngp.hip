@@ -120,14 +120,26 @@ struct EncodeArgs {
     int pair_ok;                   // table 16-B aligned (paired corner loads)
 };
 
-// Encode launch options (SDFR_ENC_MODE = LPT | 8*!PAIR overrides, ablations only):
-//  PAIR  the x-neighbour corners (g0, g0+1) come from one aligned 16-B load
-//        whenever their rows are {i, i^1} (hash prime 1 on x: always for even
-//        g0; dense rows: for even i); a second 8-B load only for the lanes
-//        where they are not (-14% encode time, scripts/encode_time.py).
-//  LPT   levels per thread {y, y+16/LPT, ...}: the ray/sample/normalisation
-//        chain is computed once for LPT levels and LPT gathers are in flight.
-constexpr uint32_t kEncDefault = 2;
+// Encode launch options (sdfr_debug_set_encode_mode / SDFR_ENC_MODE, ablations
+// only; all bit-identical; times per 32 faces from scripts/encode_time.py):
+//  +8 off   PAIR: the x-neighbour corners (g0, g0+1) from one aligned 16-B load
+//           whenever their rows are {i, i^1} (hash prime 1 on x: always for
+//           even g0; dense rows: for even i), an 8-B load of the second row
+//           only for the other lanes.                      mode 9 0.94 -> 1 0.84 ms
+//  +256     A8: the same with dword-aligned 16-B loads, so ANY consecutive rows
+//           i, i+-1 come from one load (every dense row, 2/3 of the hashed
+//           g0 parities).                                       -> 257 0.80 ms
+//  low bits LPT levels per thread {y, y+16/LPT} (2: mode 2 0.83 ms; 4 was
+//           slower, 1.17 ms, with four levels' tables live in each L2).
+//  +32      SPT = 2 samples per thread, 256 apart: twice the corner loads in
+//           flight per wave.                                    -> 289 0.77 ms
+// The gather is bound by L1 tag lookups (one 128-B line per lane per load
+// instruction, ~54 cycles per wave-load measured): the wins above all cut
+// load instructions per sample-level (6 -> ~4.9).  Measured and dropped:
+// XCD-owned levels (each XCD's blocks on two levels only: 1.22 vs 1.08 ms),
+// sc1 (L2-dropping) output stores (+-1%), adjacent level pairs {2y, 2y+1}
+// (1.09 ms), whole image rows per wave (0.86 ms), 4 samples per thread (0.78 ms).
+constexpr uint32_t kEncDefault = 256 | 32 | 1;
 
 // level_interp<3,2> with paired x-corner loads: the same corner weights
 // (x factor first, then y, z) and the same fma order over corners 0..7, so the
@@ -175,55 +187,129 @@ __device__ __forceinline__ void level_interp_pair(const float *__restrict__ grid
         for (uint32_t c = 0; c < 2; ++c) out[c] = __fmaf_rn(wts[idx], v[idx][c], out[c]);
 }
 
-template <bool PAIR, uint32_t LPT>
-__global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
-    const uint32_t sid = blockIdx.x * 256 + threadIdx.x;
-    if (sid >= a.g.S_total) return;
-    float2 *out = reinterpret_cast<float2 *>(a.enc) + sid;
-    constexpr uint32_t kStep = 16 / LPT;
-
-    const SampleId id = decode_sid(a.g, sid);
-    bool zero = !id.valid;
-    float u[3];
-    if (!zero) {
-        const uint32_t y = id.ray_local / a.g.W, x = id.ray_local % a.g.W;
-        const uint32_t ray_index = (id.b * a.g.H + y) * a.g.W + x;
-        Ray ray;
-        make_ray(a.g.cam + (size_t)id.b * 12, a.g.focal[id.b], a.g.pix_x[x], a.g.pix_y[y],
-                 a.g.half_res, ray);
-        const float nr = a.g.near_[id.b], fr = a.g.far_[id.b];
-        const float z = sample_z(a.g.sc, nr, fr, ray_index, id.s);
-        const float span = __fsub_rn(fr, nr);
+// Normalised grid coordinate u of sample `sid` (grid.py:149 on the reference's
+// pts/normalisation chain, sdf_model.py:343-349); false for tile padding and for
+// samples outside [0,1]^3, whose features are 0 (gridencoder.cu:104-111).
+__device__ __forceinline__ bool sample_u(const GeomArgs &g, uint32_t sid, float (&u)[3]) {
+    const SampleId id = decode_sid(g, sid);
+    if (!id.valid) return false;
+    const uint32_t y = id.ray_local / g.W, x = id.ray_local % g.W;
+    const uint32_t ray_index = (id.b * g.H + y) * g.W + x;
+    Ray ray;
+    make_ray(g.cam + (size_t)id.b * 12, g.focal[id.b], g.pix_x[x], g.pix_y[y], g.half_res, ray);
+    const float nr = g.near_[id.b], fr = g.far_[id.b];
+    const float z = sample_z(g.sc, nr, fr, ray_index, id.s);
+    const float span = __fsub_rn(fr, nr);
+    bool in = true;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));            // :343
-            const float np_ = a.g.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;  // :349
-            u[k] = __fdiv_rn(__fadd_rn(np_, a.g.bound), __fmul_rn(2.0f, a.g.bound));   // grid.py:149
-            if (u[k] < 0 || u[k] > 1) zero = true;                                 // OOB -> 0
+    for (int k = 0; k < 3; ++k) {
+        const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));            // :343
+        const float np_ = g.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;  // :349
+        u[k] = __fdiv_rn(__fadd_rn(np_, g.bound), __fmul_rn(2.0f, g.bound));     // grid.py:149
+        if (u[k] < 0 || u[k] > 1) in = false;
+    }
+    return in;
+}
+
+// One thread: SPT samples (256 apart) x LPT levels ({y, y+16/LPT, ...}, or
+// {LPT y, LPT y + 1, ...} with ADJ).  Branch-free: padding / out-of-box samples
+// gather at u = 0.5 and store 0, so every corner load of the thread can be in
+// flight at once.
+// 8-B-aligned 16-B row pair (global_load_dwordx4 at dword alignment)
+typedef float f4_a8 __attribute__((ext_vector_type(4), aligned(8)));
+
+// level_interp_pair with dword-aligned (not 16-B aligned) pair loads: the two
+// x-corners come from ONE 16-B load whenever their rows are consecutive,
+// i1 = i0 +- 1 (every dense row; hashed rows for 2/3 of the g0 parities), else
+// from the aligned pair holding i0 plus an 8-B load of i1.  Same weights and
+// fma order as level_interp: bit-identical.
+__device__ __forceinline__ void level_interp_adj(const float *__restrict__ grid,
+                                                 const LevelParam &q,
+                                                 const LevelCoord<3, 2> &lc, float (&out)[2]) {
+    float v[8][2];
+    float wts[8];
+#pragma unroll
+    for (uint32_t idx = 0; idx < 8; idx += 2) {
+        uint32_t pl[3];
+        float w0 = __fsub_rn(1.0f, lc.pos[0]), w1 = lc.pos[0];
+#pragma unroll
+        for (uint32_t d = 1; d < 3; ++d) {
+            const bool hi = idx & (1u << d);
+            pl[d] = hi ? lc.pg[d] + 1 : lc.pg[d];
+            const float f = hi ? lc.pos[d] : __fsub_rn(1.0f, lc.pos[d]);
+            w0 = __fmul_rn(w0, f);
+            w1 = __fmul_rn(w1, f);
+        }
+        wts[idx] = w0;
+        wts[idx + 1] = w1;
+        pl[0] = lc.pg[0];
+        const uint32_t i0 = grid_index<3>(q, 0, pl);
+        pl[0] = lc.pg[0] + 1;
+        const uint32_t i1 = grid_index<3>(q, 0, pl);
+        const bool up = i1 == i0 + 1u, down = i1 + 1u == i0;
+        // rows loaded: {base, base+1}, all inside the level (hsize is even)
+        const uint32_t base = up ? i0 : (down ? i1 : (i0 & ~1u));
+        const f4_a8 t = *reinterpret_cast<const f4_a8 *>(grid + (size_t)base * 2);
+        const bool lo0 = base == i0;
+        v[idx][0] = lo0 ? t.x : t.z;
+        v[idx][1] = lo0 ? t.y : t.w;
+        if (up || down) {
+            v[idx + 1][0] = up ? t.z : t.x;
+            v[idx + 1][1] = up ? t.w : t.y;
+        } else {
+            const float2 u = *reinterpret_cast<const float2 *>(grid + (size_t)i1 * 2);
+            v[idx + 1][0] = u.x;
+            v[idx + 1][1] = u.y;
         }
     }
-    if (zero) {
+    out[0] = out[1] = 0.0f;
 #pragma unroll
-        for (uint32_t j = 0; j < LPT; ++j)
-            out[(size_t)(blockIdx.y + j * kStep) * a.g.S_total] = make_float2(0.0f, 0.0f);
-        return;
+    for (uint32_t idx = 0; idx < 8; ++idx)
+#pragma unroll
+        for (uint32_t c = 0; c < 2; ++c) out[c] = __fmaf_rn(wts[idx], v[idx][c], out[c]);
+}
+
+// One thread: SPT samples (256 apart) x LPT levels {y, y + 16/LPT, ...}.
+// Branch-free: padding / out-of-box samples gather at u = 0.5 and store 0, so
+// every corner load of the thread can be in flight at once.
+template <bool PAIR, bool A8, uint32_t LPT, uint32_t SPT>
+__global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
+    float2 *out = reinterpret_cast<float2 *>(a.enc);
+    uint32_t sid[SPT];
+    bool live[SPT], in[SPT];
+    float u[SPT][3];
+#pragma unroll
+    for (uint32_t k = 0; k < SPT; ++k) {
+        sid[k] = (blockIdx.x * SPT + k) * 256 + threadIdx.x;
+        live[k] = sid[k] < a.g.S_total;
+        in[k] = live[k] && sample_u(a.g, sid[k], u[k]);
+        if (!in[k]) u[k][0] = u[k][1] = u[k][2] = 0.5f;
     }
 #pragma unroll
     for (uint32_t j = 0; j < LPT; ++j) {
-        const uint32_t level = blockIdx.y + j * kStep;
+        const uint32_t level = blockIdx.y + j * (16 / LPT);
         LevelParam q = a.lt.p[level];
         finish_level(q, a.offsets, level, 3, 0, 0);
         const float *grid = a.emb + (size_t)q.offset * 2;
-        LevelCoord<3, 2> lc;
-        level_coord<3, 2>(u, q, 0, 0, lc);
-        float res[2];
         // pairs are 16-B aligned when the level base (offset) is even and the
-        // table itself is 16-B aligned (host check, a.pair_ok)
-        if (PAIR && a.pair_ok && !(q.offset & 1u))
-            level_interp_pair(grid, q, lc, res);
-        else
-            level_interp<3, 2>(grid, q, 0, lc, res);
-        out[(size_t)level * a.g.S_total] = make_float2(res[0], res[1]);
+        // table itself is 16-B aligned (host check, a.pair_ok); an even level
+        // size keeps every aligned pair inside the level
+        const bool pair = PAIR && a.pair_ok && !((q.offset | q.hsize) & 1u);
+#pragma unroll
+        for (uint32_t k = 0; k < SPT; ++k) {
+            LevelCoord<3, 2> lc;
+            level_coord<3, 2>(u[k], q, 0, 0, lc);
+            float res[2];
+            if (pair && A8)
+                level_interp_adj(grid, q, lc, res);
+            else if (pair)
+                level_interp_pair(grid, q, lc, res);
+            else
+                level_interp<3, 2>(grid, q, 0, lc, res);
+            if (live[k])
+                out[(size_t)level * a.g.S_total + sid[k]] =
+                    in[k] ? make_float2(res[0], res[1]) : make_float2(0.0f, 0.0f);
+        }
     }
 }
 
@@ -762,10 +848,11 @@ static uint32_t g_encode_mode = [] {
     return e ? (uint32_t)std::atoi(e) : kEncDefault;
 }();
 
-template <bool PAIR, uint32_t LPT>
-static void launch_encode_mode(uint32_t nchunks, hipStream_t st, const EncodeArgs &e) {
-    hipLaunchKernelGGL((ngp_encode_kernel<PAIR, LPT>), dim3(nchunks, 16 / LPT), dim3(256), 0, st,
-                       e);
+template <bool PAIR, bool A8, uint32_t LPT, uint32_t SPT>
+static void launch_encode_mode(hipStream_t st, const EncodeArgs &e) {
+    const uint32_t blocks = (e.g.S_total + 256 * SPT - 1) / (256 * SPT);
+    hipLaunchKernelGGL((ngp_encode_kernel<PAIR, A8, LPT, SPT>), dim3(blocks, 16 / LPT),
+                       dim3(256), 0, st, e);
 }
 
 static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
@@ -777,12 +864,14 @@ static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *
     e.enc = enc;
     e.pair_ok = (reinterpret_cast<uintptr_t>(w->embeddings) & 15u) == 0;
     make_level_table(16, w->log2_per_level_scale, w->base_resolution, e.lt);
-    const uint32_t nchunks = (g.S_total + 255) / 256;
     switch (g_encode_mode) {
-        case 8 | 1: launch_encode_mode<false, 1>(nchunks, st, e); break;
-        case 2: launch_encode_mode<true, 2>(nchunks, st, e); break;
-        case 4: launch_encode_mode<true, 4>(nchunks, st, e); break;
-        default: launch_encode_mode<true, 1>(nchunks, st, e); break;
+        case 8 | 1: launch_encode_mode<false, false, 1, 1>(st, e); break;
+        case 1: launch_encode_mode<true, false, 1, 1>(st, e); break;
+        case 2: launch_encode_mode<true, false, 2, 1>(st, e); break;
+        case 32 | 1: launch_encode_mode<true, false, 1, 2>(st, e); break;
+        case 256 | 1: launch_encode_mode<true, true, 1, 1>(st, e); break;
+        case 256 | 32 | 2: launch_encode_mode<true, true, 2, 2>(st, e); break;
+        default: launch_encode_mode<true, true, 1, 2>(st, e); break;   // 289
     }
     return check_launch("render_ngp: encode");
 }
@@ -802,8 +891,12 @@ int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t 
 }
 
 int sdfr_debug_set_encode_mode(int mode) {
-    if (mode != 1 && mode != 2 && mode != 4 && mode != 9)
-        return fail(SDFR_EINVAL, "sdfr_debug_set_encode_mode: mode must be 1, 2, 4 or 9");
+    const int ok[] = {1, 2, 9, 33, 257, 289, 290};
+    bool found = false;
+    for (int m : ok) found |= m == mode;
+    if (!found)
+        return fail(SDFR_EINVAL,
+                    "sdfr_debug_set_encode_mode: unknown mode");
     g_encode_mode = (uint32_t)mode;
     return SDFR_OK;
 }

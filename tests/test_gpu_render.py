@@ -111,7 +111,7 @@ def _tile_order_to_samples(enc, B, H, W, N):
     return e.reshape(B * H * W * N, L * 2)
 
 
-@pytest.mark.parametrize("mode", [2, 1, 4, 9])
+@pytest.mark.parametrize("mode", [289, 1, 2, 9, 33, 257, 290])
 @pytest.mark.parametrize("name", ["render_small", "render_face64"])
 def test_encode_stage_bit_exact(sdfr, oracle_mod, golden_dir, renderer_sd, name, mode):
     """Every sample's 32 hash-grid features equal the oracle's, bit for bit: this
@@ -129,7 +129,7 @@ def test_encode_stage_bit_exact(sdfr, oracle_mod, golden_dir, renderer_sd, name,
             ws = ren.fused_forward(cam, focal, near, far, lat, t_rand=tr, encode_only=True)
         torch.cuda.synchronize()
     finally:
-        L.check(L.lib().sdfr_debug_set_encode_mode(2), "sdfr_debug_set_encode_mode")
+        L.check(L.lib().sdfr_debug_set_encode_mode(289), "sdfr_debug_set_encode_mode")
     tiles = (res * res + 15) // 16
     S = B * tiles * N * 16
     enc = ws[: S * 16 * 2 * 4].view(torch.float32).cpu().numpy()

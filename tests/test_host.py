@@ -42,9 +42,9 @@ def test_argument_errors_mirror_reference(sdfr):
     assert rc == sdfr._lib.SDFR_EINVAL
     rc = lib.sdfr_sh_encode_forward(nul, nul, 4, 3, 6, nul, nul)
     assert rc == sdfr._lib.SDFR_EUNSUPPORTED
-    for bad in (0, 3, 8, 10):
+    for bad in (0, 3, 4, 8, 10, 18):
         assert lib.sdfr_debug_set_encode_mode(bad) == sdfr._lib.SDFR_EINVAL
-    assert lib.sdfr_debug_set_encode_mode(2) == sdfr._lib.SDFR_OK
+    assert lib.sdfr_debug_set_encode_mode(289) == sdfr._lib.SDFR_OK
     w, a = sdfr._lib.NgpWeights(), sdfr._lib.NgpRenderArgs()
     rc = lib.sdfr_render_ngp_forward(ctypes.byref(w), ctypes.byref(a), nul)
     assert rc in (sdfr._lib.SDFR_EINVAL, sdfr._lib.SDFR_EUNSUPPORTED)
