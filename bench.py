@@ -169,14 +169,16 @@ def main():
     f16x3 = args.field_precision == "f16x3"
     field_kernel = ("field_x_kernel<0, sdfr::SirenNet>" if siren else
                     "field_x_kernel<0, sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
-    traffic = None
-    tj = Path(args.traffic_json)
-    if tj.exists():
+    def traffic_of(kernel):
+        """HBM bytes per launch of `kernel` at this batch, from the committed
+        rocprofv3 PMC passes (profiles/, scripts/summarize_profiles.py), or None."""
+        tj = Path(args.traffic_json)
         try:
-            per = json.loads(tj.read_text())["kernels"][field_kernel]
-            traffic = per["bytes_per_launch_per_face"] * B
-        except (KeyError, ValueError, TypeError):
-            traffic = None
+            return json.loads(tj.read_text())["kernels"][kernel]["bytes_per_launch_per_face"] * B
+        except (OSError, KeyError, ValueError, TypeError):
+            return None
+
+    traffic = traffic_of(field_kernel)
     if f16x3:
         # fp32-accurate GEMMs as 3 fp16 MFMA terms: the attainable fp32-equivalent
         # peak is the dense fp16 MFMA peak / 3 (DESIGN.md section 5)
@@ -216,7 +218,8 @@ def main():
         "roofline_gather": None if siren else {
             "kernel": "ngp_encode_kernel (sampling + 16-level hash-grid gather)",
             "bound": "hbm", "achieved": gather_gbps, "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": gather_gbps / HBM_PEAK_GBPS},
+            "unit": "GB/s", "frac": gather_gbps / HBM_PEAK_GBPS,
+            "traffic": traffic_of("ngp_encode_kernel")},
         "stage_ms_per_step": {"renderer_total": render_ms, "hash_grid": enc_ms,
                               "field": field_ms},
         "cpu_baseline": None,

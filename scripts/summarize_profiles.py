@@ -97,7 +97,19 @@ def main():
                           "bytes_per_launch_per_face": total / a.batch,
                           "fetch_bytes_per_face": fk["fetch_bytes_corrected"] / a.batch,
                           "write_bytes_per_face": fk["write_bytes"] / a.batch}
-    tj.write_text(json.dumps({"unit": "HBM bytes per face per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+    ek = next((v for k, v in out["kernels"].items() if f"::{ENCODE}" in k), None)
+    if ek and ek["fetch_bytes_raw"] is not None and ek["write_bytes"] is not None:
+        # gathers: FETCH_SIZE's gfx950 undercount is calibrated for wide streams
+        # only, so the raw count is the reported traffic, the doubled one a bound
+        per[ENCODE] = {"source": f"profiles/{a.tag}_traffic.json",
+                       "bytes_per_launch_per_face":
+                           (ek["fetch_bytes_raw"] + ek["write_bytes"]) / a.batch,
+                       "bytes_per_launch_per_face_fetch_doubled":
+                           (ek["fetch_bytes_corrected"] + ek["write_bytes"]) / a.batch,
+                       "fetch_bytes_raw_per_face": ek["fetch_bytes_raw"] / a.batch,
+                       "write_bytes_per_face": ek["write_bytes"] / a.batch}
+    tj.write_text(json.dumps({"unit": "HBM bytes per face per launch (FETCH_SIZE x2 + WRITE_SIZE; "
+                                      "ngp_encode_kernel: FETCH_SIZE raw + WRITE_SIZE)",
                               "kernels": per}, indent=1))
     print(json.dumps(out, indent=1))
 

@@ -38,7 +38,11 @@ def main():
     p.add_argument("--warmup", type=int, default=4)
     p.add_argument("--batch", type=int, default=8)
     p.add_argument("--chunk", type=int, default=2)
+    p.add_argument("--miopen-find", action="store_true",
+                   help="torch.backends.cudnn.benchmark = True (MIOpen find per conv shape "
+                        "during warmup instead of its heuristics)")
     a = p.parse_args()
+    torch.backends.cudnn.benchmark = a.miopen_find
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -88,6 +92,7 @@ def main():
             "steps": a.steps, "warmup": a.warmup, "scaling": "weak",
             "config": {"workload": f"train.py stage {a.stage}, {a.net} renderer, random-init G/D",
                        "batch_per_gpu": a.batch, "chunk": a.chunk, "size": size,
+                       "miopen_find": a.miopen_find,
                        "parallelism": f"ddp{world} (RCCL all-reduce of "
                                       f"{'G' if a.stage == 1 else 'decoder'} + D grads)"},
             "losses": {k: float(v) for k, v in losses.items()}}), flush=True)
