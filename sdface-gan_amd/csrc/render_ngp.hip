@@ -138,7 +138,8 @@ struct EncodeArgs {
 // load instructions per sample-level (6 -> ~4.9).  Measured and dropped:
 // XCD-owned levels (each XCD's blocks on two levels only: 1.22 vs 1.08 ms),
 // sc1 (L2-dropping) output stores (+-1%), adjacent level pairs {2y, 2y+1}
-// (1.09 ms), whole image rows per wave (0.86 ms), 4 samples per thread (0.78 ms).
+// (1.09 ms), whole image rows per wave (0.86 ms), 4 samples per thread (0.78 ms),
+// nontemporal table loads (2.1 ms: the table no longer stays in L2).
 constexpr uint32_t kEncDefault = 256 | 32 | 1;
 
 // level_interp<3,2> with paired x-corner loads: the same corner weights
