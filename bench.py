@@ -2,18 +2,21 @@
 
 Workload (BASELINE.json configs[1], eval.py's 5000-image generation): per step
 one Generator forward -- mapping MLP -> fused HIP renderer (64^2 rays x 24
-samples, hash grid, FiLM-SIREN on fp32 MFMA, compositing) -> StyleGAN2
-decoder to 256^2 (PyTorch-ROCm, fp32) -- on a batch of B random latents with
+samples, hash grid, FiLM-SIREN on split-fp16 MFMA at fp32 accuracy, compositing)
+-> StyleGAN2 decoder to 256^2 (HIP implicit-GEMM convolutions with fused
+epilogues) -- on a batch of B random latents with
 random cameras, random-init weights (pretrained weights are not available
 offline), decoder noise drawn per step as in eval.py.  PNG encoding is not
 timed.  One process per GPU (torchrun); faces shard across ranks with no
 data-path collective (weak scaling): value = all faces / max-over-ranks time.
 
-Also reported: the dominant kernel's roofline (the fused field kernel, fp32
-MFMA bound) from HIP events recorded on the renderer's stream around that
-kernel during the timed steps, the hash-grid gather kernel's HBM-roofline
-fraction, and a CPU baseline (the oracle renderer + PyTorch-CPU decoder) on
-the host cores for a bounded sample.
+Also reported: the dominant kernel's roofline (the fused field kernel, MFMA
+bound) from HIP events recorded on the renderer's stream around that kernel
+during the timed steps, the hash-grid gather kernel's HBM-roofline fraction,
+a CPU baseline (the oracle renderer + PyTorch-CPU decoder) on the host cores
+for a bounded sample, and after the timed region, outside
+`value`: faces/s at B = 1 (eval.py's own batch) and 8, and at B with every
+image copied to pinned host memory ("with host copy").
 """
 from __future__ import annotations
 
@@ -53,6 +56,8 @@ def parse():
                    help="renderer network: ngp (headline, configs[1]) or siren "
                         "(rendering.type 'sdf', configs[4]'s generator)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the B=1/8 and host-copy measurements")
     p.add_argument("--traffic-json", default=str(REPO / "profiles" / "field_traffic.json"))
     return p.parse_args()
 
@@ -108,6 +113,28 @@ def cpu_baseline(seconds, siren=False):
                       f"1 face per call, {el:.1f}s"}
 
 
+def extras(step, B, graphed_step, steps=10, warm=3):
+    """Outside the timed region (this rank only): faces/s at B = 1 and 8 (eager,
+    and at B = 1 also replayed from a HIP graph, GraphedGenerator), and at B with
+    each step's images copied to pinned host memory as eval.py's PNG writer needs
+    them (the copy of step k overlaps step k+1's kernels)."""
+    def rate(nb, host=False, fn=step):
+        buf = torch.empty(nb, 3, 256, 256, pin_memory=True) if host else None
+        for _ in range(warm):
+            fn(nb)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            img = fn(nb)
+            if host:
+                buf.copy_(img, non_blocking=True)
+        torch.cuda.synchronize()
+        return nb * steps / (time.perf_counter() - t0)
+    return {"faces_per_s_b1": rate(1), "faces_per_s_b1_graph": rate(1, fn=graphed_step),
+            "faces_per_s_b8": rate(8),
+            f"faces_per_s_b{B}_with_host_copy": rate(B, host=True), "unit": "faces/s (one GPU)"}
+
+
 def main():
     args = parse()
     world, rank, device = setup_dist(args)
@@ -122,10 +149,10 @@ def main():
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)
 
-    def step():
-        z = torch.randn(B, opt.model.style_dim, device=device, generator=gen)
+    def step(nb=B):
+        z = torch.randn(nb, opt.model.style_dim, device=device, generator=gen)
         cam, focal, near, far, _ = sdfr.generate_camera_params(
-            res, device, batch=B, azim_range=opt.camera.azim, elev_range=opt.camera.elev,
+            res, device, batch=nb, azim_range=opt.camera.azim, elev_range=opt.camera.elev,
             fov_ang=opt.camera.fov, dist_radius=opt.camera.dist_radius)
         with torch.no_grad():
             rgb, thumb = g([z], cam, focal, near, far, truncation=1, truncation_latent=None)
@@ -224,6 +251,16 @@ def main():
                               "field": field_ms},
         "cpu_baseline": None,
     }
+    if not args.no_extras:
+        gg = sdfr.GraphedGenerator(g)
+
+        def graphed_step(nb):
+            z = torch.randn(nb, opt.model.style_dim, device=device, generator=gen)
+            cam, focal, near, far, _ = sdfr.generate_camera_params(
+                res, device, batch=nb, azim_range=opt.camera.azim, elev_range=opt.camera.elev,
+                fov_ang=opt.camera.fov, dist_radius=opt.camera.dist_radius)
+            return gg(z, cam, focal, near, far)[0]
+        line["extras"] = extras(step, B, graphed_step)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, siren)
     if rank == 0:

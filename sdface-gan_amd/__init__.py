@@ -12,6 +12,7 @@ Drop-in surface (reference: im2scene/sdf/models/):
   align_volume, extract_mesh_with_marching_cubes,
   xyz2mesh                                              (sdf_utils.py:164-223)
   SDFOptions, vol_render_opt                            (sdf_utils.py:447, training_utils.py:144)
+Beyond the reference: GraphedGenerator (HIP-graph replay of the inference forward).
 """
 from . import _lib  # noqa: F401
 from .camera import generate_camera_params  # noqa: F401
@@ -20,6 +21,7 @@ from . import decoder_ops  # noqa: F401
 from .generator import (Blur, Decoder, EqualLinear, FusedLeakyReLU, Generator,  # noqa: F401
                         MappingLinear, ModulatedConv2d, NoiseInjection, PixelNorm, StyledConv,
                         ToRGB, Upsample, fused_leaky_relu, make_kernel, upfirdn2d)
+from .graphs import GraphedGenerator  # noqa: F401
 from .mesh import align_volume, extract_mesh_with_marching_cubes, xyz2mesh  # noqa: F401
 from .options import AttrDict, SDFOptions, vol_render_opt  # noqa: F401
 from . import training  # noqa: F401  (stage-2 DDP trainer, Discriminator, losses)

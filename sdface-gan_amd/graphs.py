@@ -1,0 +1,87 @@
+"""HIP-graph replay of the whole inference forward (no reference counterpart).
+
+eval.py generates one face per ``Generator.forward`` call (``eval.py:92-113``,
+batch 1).  At that size the GPU work is ~1.5 ms and the host's per-call launch
+cost (mapping MLP, camera-free renderer launch, decoder layers) is comparable,
+so ``GraphedGenerator`` captures the complete forward -- mapping, fused renderer,
+fused decoder, decoder noise and the per-ray sampling offsets drawn from the
+device RNG -- once per batch size into a ``torch.cuda.CUDAGraph`` and replays it
+with the caller's latents and cameras copied into static input buffers.
+Replays produce bit-identical images to the eager forward on the same inputs
+(``tests/test_gpu_render.py::test_graphed_generator_matches_eager``); random
+draws inside the graph (noise, sampling offsets) advance the device generator
+on every replay as they do eagerly.
+
+Requirements: the generator is on a CUDA device in eval mode, takes the fused
+paths (no autograd), and its renderer draws sampling offsets on the device
+(``renderer.rng_device = "device"``; the reference-compatible host draw would be
+a pageable copy inside the graph).
+"""
+from __future__ import annotations
+
+import torch
+
+
+class GraphedGenerator:
+    """``GraphedGenerator(g)(z, cam, focal, near, far) -> (rgb, thumb)``.
+
+    Same arguments as ``Generator.forward`` for the eval use (one style tensor,
+    truncation / truncation_latent fixed at construction); one graph per batch
+    size, captured on first use.  Outputs live in the graph's static buffers and
+    are overwritten by the next replay of the same batch size: copy them to keep
+    them (eval.py moves each image to the host right away)."""
+
+    def __init__(self, generator, truncation=1, truncation_latent=None, randomize_noise=True):
+        p = next(generator.parameters())
+        if not p.is_cuda:
+            raise RuntimeError("GraphedGenerator needs the generator on a GPU")
+        if generator.training:
+            raise RuntimeError("GraphedGenerator needs generator.eval()")
+        if generator.renderer.rng_device != "device":
+            raise RuntimeError("GraphedGenerator needs renderer.rng_device = 'device' "
+                               "(sampling offsets drawn inside the graph)")
+        self.g = generator
+        self.device = p.device
+        self.kw = dict(truncation=truncation, truncation_latent=truncation_latent,
+                       randomize_noise=randomize_noise)
+        self._graphs = {}
+
+    def _capture(self, B):
+        dev = self.device
+        static = {"z": torch.zeros(B, self.g.style_dim, device=dev),
+                  "cam": torch.zeros(B, 3, 4, device=dev),
+                  "focal": torch.ones(B, 1, 1, device=dev),
+                  "near": torch.full((B, 1, 1), 0.88, device=dev),
+                  "far": torch.full((B, 1, 1), 1.12, device=dev)}
+        static["cam"][:, :, :3] = torch.eye(3, device=dev)
+        static["cam"][:, 2, 3] = 1.0
+
+        def fwd():
+            with torch.no_grad():
+                return self.g([static["z"]], static["cam"], static["focal"], static["near"],
+                              static["far"], **self.kw)
+
+        # warm up on a side stream: first calls pack decoder weights, pick paths
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                fwd()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = fwd()
+        return graph, static, out
+
+    def __call__(self, z, cam_poses, focals, near, far):
+        B = z.shape[0]
+        if B not in self._graphs:
+            self._graphs[B] = self._capture(B)
+        graph, static, out = self._graphs[B]
+        static["z"].copy_(z)
+        static["cam"].copy_(cam_poses)
+        for k, v in (("focal", focals), ("near", near), ("far", far)):
+            v = torch.as_tensor(v, dtype=torch.float32, device=self.device)
+            static[k].copy_(v.reshape(-1, 1, 1).expand(B, 1, 1))
+        graph.replay()
+        return out

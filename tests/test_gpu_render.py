@@ -347,3 +347,38 @@ def test_siren_fused_equals_module_path(sdfr, siren_sd):
         u = ren(ext, focal, near, far, styles=lat, t_rand=tr)
     _cmp("siren_module", "rgb", f[0].cpu().numpy(), u[0].cpu().numpy(), "module_rgb")
     _cmp("siren_module", "features", f[1].cpu().numpy(), u[1].cpu().numpy(), "module_features")
+
+
+def test_graphed_generator_matches_eager(sdfr):
+    """HIP-graph replay of the whole inference forward (sdface-gan_amd/graphs.py):
+    the same images as the eager forward, bit for bit, from the same device-RNG
+    state (decoder noise and sampling offsets are drawn inside the graph), a fresh
+    draw on every replay, and new latents/cameras picked up from the inputs."""
+    dev = torch.device("cuda", 0)
+    opt = sdfr.vol_render_opt()
+    torch.manual_seed(3)
+    g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
+    g.renderer.rng_device = "device"
+    gg = sdfr.GraphedGenerator(g)
+    for B in (1, 3):
+        z = torch.randn(B, 256, device=dev)
+        cam, focal, near, far, _ = sdfr.generate_camera_params(64, dev, batch=B)
+        torch.cuda.manual_seed(11)
+        with torch.no_grad():
+            ref_rgb, ref_thumb = g([z], cam, focal, near, far)
+        gg(z, cam, focal, near, far)                  # capture (+ warmup draws)
+        torch.cuda.manual_seed(11)
+        rgb, thumb = gg(z, cam, focal, near, far)
+        torch.cuda.synchronize()
+        assert rgb.shape == (B, 3, 256, 256) and thumb.shape == (B, 3, 64, 64)
+        assert torch.equal(rgb, ref_rgb) and torch.equal(thumb, ref_thumb)
+        first = rgb.clone()
+        rgb2, _ = gg(z, cam, focal, near, far)        # next draw of noise / offsets
+        assert not torch.equal(rgb2, first)
+        z2 = torch.randn(B, 256, device=dev)
+        torch.cuda.manual_seed(12)
+        with torch.no_grad():
+            ref2, _ = g([z2], cam, focal, near, far)
+        torch.cuda.manual_seed(12)
+        got2, _ = gg(z2, cam, focal, near, far)
+        assert torch.equal(got2, ref2)

@@ -173,3 +173,10 @@ def test_xyz2mesh_faces(sdfr):
     res = sdfr.xyz2mesh(xyz)
     verts, faces = res if isinstance(res, tuple) else (res.vertices, res.faces)
     assert verts.shape == (20, 3) and faces.shape[1] == 3 and faces.max() < 20
+
+
+def test_graphed_generator_rejects_cpu(sdfr):
+    opt = sdfr.vol_render_opt()
+    g = sdfr.Generator(opt.model, opt.rendering).eval()
+    with pytest.raises(RuntimeError, match="on a GPU"):
+        sdfr.GraphedGenerator(g)
