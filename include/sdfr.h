@@ -214,6 +214,15 @@ int sdfr_debug_set_field_variant(int variant);
  * the gather (scripts/encode_time.py).  SDFR_EINVAL for any other value. */
 int sdfr_debug_set_encode_mode(int mode);
 
+/* Upper bound on the sample segments per ray of the f16x3 ngp field stage
+ * (process-global, default 4): batches too small to give every CU a workgroup
+ * split each ray's samples over up to this many workgroups and chain the
+ * segments in a merge kernel (sdf_model.py:273-289's cumprod re-associated:
+ * fp32-rounding-level differences).  1 disables the split.  The workspace size
+ * (sdfr_render_ngp_workspace_bytes) already covers the default bound.
+ * SDFR_EINVAL unless 1, 2 or 4. */
+int sdfr_debug_set_field_split(int max_segments);
+
 /* Accuracy probe for the two device sin implementations the field kernel can
  * use (software Cody-Waite + polynomial, hardware v_sin_f32 after reduction):
  * out_cw[i] = sin_cw(x[i]), out_hw[i] = sin_hw(x[i]), n elements. */

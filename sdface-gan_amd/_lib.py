@@ -34,7 +34,7 @@ EXPORTS = (
     "sdfr_sh_encode_forward", "sdfr_sh_encode_backward",
     "sdfr_render_ngp_workspace_bytes", "sdfr_render_ngp_forward",
     "sdfr_render_ngp_encode_only", "sdfr_debug_set_field_variant", "sdfr_debug_sin_probe",
-    "sdfr_debug_set_encode_mode",
+    "sdfr_debug_set_encode_mode", "sdfr_debug_set_field_split",
     "sdfr_render_siren_workspace_bytes", "sdfr_render_siren_forward",
     "sdfr_fused_bias_act", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
     "sdfr_modulate_to_nhwc_split",
@@ -137,6 +137,7 @@ def lib():
                                               ctypes.POINTER(NgpRenderArgs), _vp]
     L.sdfr_debug_set_field_variant.argtypes = [_int]
     L.sdfr_debug_set_encode_mode.argtypes = [_int]
+    L.sdfr_debug_set_field_split.argtypes = [_int]
     L.sdfr_render_siren_workspace_bytes.restype = ctypes.c_size_t
     L.sdfr_render_siren_workspace_bytes.argtypes = [_u32]
     L.sdfr_render_siren_forward.argtypes = [ctypes.POINTER(SirenWeights),

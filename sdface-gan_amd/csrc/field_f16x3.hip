@@ -255,7 +255,19 @@ struct XFieldArgs {
     const float *sigma_noise;      // [B,H,W,N] or null (no_sdf only)
     int force_background, with_sdf;
     float *rgb, *features, *sdf, *xyz, *mask;
+    uint32_t nseg;                 // sample segments per ray (1: whole rays, no merge)
+    float *part;                   // nseg > 1: [nseg][kPartQ][rays] segment partials
 };
+
+// Small batches (eval.py renders one face per call) fill a fraction of the chip
+// with one workgroup per 4 tiles: the 24 samples of a ray are then split into
+// nseg segments marched by different workgroups, each compositing its samples
+// front to back from T = 1, and field_merge_kernel chains the segments
+// (acc = acc_1 + T_1 acc_2 + T_1 T_2 acc_3 ..., T = prod T_k), which is the
+// same sum with the transmittance product re-associated (fp32-rounding-level
+// differences; tests/test_gpu_render.py compares split and unsplit renders).
+// Partials per (segment, ray): 256 features, rgb[3], xyz[3], T, w_last.
+constexpr uint32_t kPartQ = kW + 8;
 
 // Weight ring: 3 LDS slots.  With SDFR_X_PREFETCH, during slice `it` the wave
 // computes from slot it%3, writes slice it+2 (held in registers since slice
@@ -524,8 +536,9 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
     // a workgroup's 4 waves own 4 consecutive tiles of ONE face (grid = faces x
     // ceil(tiles_per_face / 4)), so the face's FiLM vectors are shared in LDS
     const uint32_t wg_per_face = (G.tiles_per_face + kWaves - 1) / kWaves;
-    const uint32_t b = blockIdx.x / wg_per_face;
-    uint32_t tile_local = (blockIdx.x % wg_per_face) * kWaves + wave;
+    const uint32_t seg = blockIdx.x % a.nseg, blk = blockIdx.x / a.nseg;
+    const uint32_t b = blk / wg_per_face;
+    uint32_t tile_local = (blk % wg_per_face) * kWaves + wave;
     const bool tile_ok = tile_local < G.tiles_per_face;
     if (!tile_ok) tile_local = G.tiles_per_face - 1;
     const uint32_t tile = b * G.tiles_per_face + tile_local;
@@ -669,10 +682,13 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
             }
         }
     };
-    load_inputs(0);
-
+    // this workgroup's passes (all of them unless the rays are split)
     const uint32_t npass = (G.N + 1) / 2;
-    for (uint32_t p = 0; p < npass; ++p) {
+    const uint32_t pps = (npass + a.nseg - 1) / a.nseg;
+    const uint32_t p_begin = seg * pps, p_end = min(npass, p_begin + pps);
+    load_inputs(2 * p_begin);
+
+    for (uint32_t p = p_begin; p < p_end; ++p) {
         f4 X0[16], X1[16], Y0[16], Y1[16];
         f4 e0h, e0l, e1h, e1l;
         {
@@ -758,7 +774,7 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
         xstep<V, Net, 0>(R, X0, X1, vxh, vxl, vxh, vxl, [] {});
         xstep<V, Net, 1>(R, X0, X1, vxh, vxl, vxh, vxl, [] {});
 
-        if (p + 1 < npass) load_inputs(2 * p + 2);
+        if (p + 1 < p_end) load_inputs(2 * p + 2);
         const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
         // compositing of the pass's two samples, front to back
 #pragma unroll
@@ -843,6 +859,27 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
 #endif
 
     if (!ray_ok) return;
+    if (a.nseg > 1) {
+        const size_t R = (size_t)G.total_tiles * kTileRays;
+        float *pp = a.part + (size_t)seg * kPartQ * R + (size_t)tile * kTileRays + n;
+        if (a.features) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const uint32_t jf = 16 * t + 4 * g;
+                const f4 v = facc[t * 64 + lane];
+                pp[(size_t)(jf + 0) * R] = v.x;
+                pp[(size_t)(jf + 1) * R] = v.y;
+                pp[(size_t)(jf + 2) * R] = v.z;
+                pp[(size_t)(jf + 3) * R] = v.w;
+            }
+        }
+        if (g == 0) {
+            const float q[8] = {racc0, racc1, racc2, xacc0, xacc1, xacc2, T, w_last};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pp[(size_t)(kW + k) * R] = q[k];
+        }
+        return;
+    }
     const size_t HW = (size_t)G.H * G.W;
     const size_t pix = (size_t)py * G.W + px;
     if (g < 3) {
@@ -869,9 +906,63 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
     }
 }
 
+// Chains the nseg segment partials of every ray (see kPartQ): one thread per
+// (ray, quantity), quantities on grid.y.
+__global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
+    const GeomArgs &G = a.g;
+    const uint32_t rid = blockIdx.x * 256 + threadIdx.x, q = blockIdx.y;
+    const size_t R = (size_t)G.total_tiles * kTileRays;
+    if (rid >= R) return;
+    const uint32_t tile = rid / kTileRays, b = tile / G.tiles_per_face;
+    const uint32_t ray_local = (tile % G.tiles_per_face) * kTileRays + rid % kTileRays;
+    const size_t HW = (size_t)G.H * G.W;
+    if (ray_local >= HW) return;
+    float *dst;
+    if (q < kW) dst = a.features ? a.features + ((size_t)b * kW + q) * HW + ray_local : nullptr;
+    else if (q < kW + 3) dst = a.rgb + ((size_t)b * 3 + (q - kW)) * HW + ray_local;
+    else if (q < kW + 6) dst = a.xyz ? a.xyz + ((size_t)b * 3 + (q - kW - 3)) * HW + ray_local
+                                     : nullptr;
+    else if (q == kW + 7) dst = a.mask ? a.mask + (size_t)b * HW + ray_local : nullptr;
+    else dst = nullptr;                                  // T itself is not an output
+    if (!dst) return;
+    const float *pp = a.part + rid;
+    const size_t segq = (size_t)kPartQ * R;
+    float acc = pp[(size_t)q * R], Tp = pp[(size_t)(kW + 6) * R];
+    for (uint32_t k = 1; k < a.nseg; ++k) {
+        const float v = pp[k * segq + (size_t)q * R];
+        acc = q == kW + 7 ? __fmul_rn(Tp, v) : __fmaf_rn(Tp, v, acc);   // w_last: last segment's
+        Tp = __fmul_rn(Tp, pp[k * segq + (size_t)(kW + 6) * R]);
+    }
+    if (q >= kW && q < kW + 3) acc = __fadd_rn(-1.0f, __fmul_rn(2.0f, acc));
+    *dst = acc;
+}
+
 // ----------------------------------------------------------------------------
 // host
 // ----------------------------------------------------------------------------
+static uint32_t g_field_split_max = 4;
+void set_field_split_max(uint32_t m) { g_field_split_max = m; }
+
+// Segments per ray: enough workgroups for every CU (>= 256), at most
+// g_field_split_max, at least one pass (two samples) in every segment, and never
+// with force_background (its last weight needs the whole ray's sum).
+uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background) {
+    const uint32_t wgs = B * ((tiles_per_face + kWaves - 1) / kWaves);
+    const uint32_t npass = (N + 1) / 2;
+    uint32_t nseg = 1;
+    while (!force_background && wgs * nseg < 256 && 2 * nseg <= g_field_split_max) {
+        const uint32_t c = 2 * nseg, pps = (npass + c - 1) / c;
+        if ((c - 1) * pps >= npass) break;            // no empty last segment
+        nseg = c;
+    }
+    return nseg;
+}
+
+size_t field_part_bytes(uint32_t B, uint32_t tiles_per_face, uint32_t N) {
+    const uint32_t nseg = field_nseg(B, tiles_per_face, N, 0);
+    return nseg > 1 ? (size_t)nseg * kPartQ * B * tiles_per_face * kTileRays * sizeof(float) : 0;
+}
+
 template <class Net>
 static size_t xws_bytes() {
     return (size_t)Net::kSlices * kXSliceF4 * sizeof(f4) + 2 * Net::kLayers * kW * sizeof(float);
@@ -924,7 +1015,8 @@ static int launch_xprep(const NetPtrs &P, const sdfr_ngp_render_args *a, char *x
 
 template <class Net>
 static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const GeomArgs &g,
-                         const float *enc, char *xws, const float *film, hipStream_t st) {
+                         const float *enc, char *xws, const float *film, hipStream_t st,
+                         float *part = nullptr) {
     XFieldArgs f;
     f.g = g;
     f.enc = enc;
@@ -945,7 +1037,9 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     f.sdf = a->sdf;
     f.xyz = a->xyz;
     f.mask = a->mask;
-    const uint32_t blocks = g.B * ((g.tiles_per_face + kWaves - 1) / kWaves);
+    f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background) : 1;
+    f.part = part;
+    const uint32_t blocks = g.B * ((g.tiles_per_face + kWaves - 1) / kWaves) * f.nseg;
     switch (field_variant()) {
 #ifdef SDFR_ABLATION
 #define SDFR_XFIELD_CASE(V)                                                                  \
@@ -963,7 +1057,11 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
         default:
             hipLaunchKernelGGL((field_x_kernel<0, Net>), dim3(blocks), dim3(kThreads), 0, st, f);
     }
-    return check_launch("render: field (f16x3)");
+    int rc = check_launch("render: field (f16x3)");
+    if (rc || f.nseg == 1) return rc;
+    const uint32_t rays = g.total_tiles * kTileRays;
+    hipLaunchKernelGGL(field_merge_kernel, dim3((rays + 255) / 256, kPartQ), dim3(256), 0, st, f);
+    return check_launch("render: field segment merge");
 }
 
 static NetPtrs ngp_ptrs(const sdfr_ngp_weights *w) {
@@ -999,8 +1097,8 @@ int launch_xprep_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, c
 
 int launch_xfield_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
                       const GeomArgs &g, const float *enc, char *xws, const float *film,
-                      hipStream_t st) {
-    return launch_xfield<NgpNet>(ngp_ptrs(w), a, g, enc, xws, film, st);
+                      hipStream_t st, float *part) {
+    return launch_xfield<NgpNet>(ngp_ptrs(w), a, g, enc, xws, film, st, part);
 }
 
 // ----------------------------------------------------------------------------

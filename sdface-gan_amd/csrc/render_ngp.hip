@@ -714,7 +714,8 @@ static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 // enc [L][S][2] | packed fp32 fragments | film | split-fp16 region (field_f16x3.hip)
 static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t L,
-                        size_t *o_packed, size_t *o_film, size_t *o_x = nullptr) {
+                        size_t *o_packed, size_t *o_film, size_t *o_x = nullptr,
+                        size_t *o_part = nullptr) {
     const size_t tiles = (size_t)B * ((H * W + kTileRays - 1) / kTileRays);
     const size_t S = tiles * N * kTileRays;
     size_t off = align256(S * L * 2 * sizeof(float));
@@ -724,6 +725,8 @@ static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t
     off += align256((size_t)B * kFilm * 2 * kW * sizeof(float));
     if (o_x) *o_x = off;
     off += align256(f16x3_ws_bytes(0));
+    if (o_part) *o_part = off;
+    off += align256(field_part_bytes(B, (H * W + kTileRays - 1) / kTileRays, N));
     return off;
 }
 
@@ -891,6 +894,13 @@ int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t 
     return check_launch("sin_probe");
 }
 
+int sdfr_debug_set_field_split(int max_segments) {
+    if (max_segments != 1 && max_segments != 2 && max_segments != 4)
+        return fail(SDFR_EINVAL, "sdfr_debug_set_field_split: max_segments must be 1, 2 or 4");
+    set_field_split_max((uint32_t)max_segments);
+    return SDFR_OK;
+}
+
 int sdfr_debug_set_encode_mode(int mode) {
     const int ok[] = {1, 2, 9, 33, 257, 289, 290};
     bool found = false;
@@ -937,8 +947,8 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     int rc = validate(w, a);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    size_t o_packed, o_film, o_x;
-    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film, &o_x);
+    size_t o_packed, o_film, o_x, o_part;
+    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film, &o_x, &o_part);
     char *ws = reinterpret_cast<char *>(a->workspace);
     float *enc = reinterpret_cast<float *>(ws);
     f4 *packed = reinterpret_cast<f4 *>(ws + o_packed);
@@ -952,7 +962,8 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
         record_event(a->stage_events[1], st);
         if ((rc = launch_encode(w, a, g, enc, st))) return rc;
         record_event(a->stage_events[2], st);
-        if ((rc = launch_xfield_ngp(w, a, g, enc, ws + o_x, film, st))) return rc;
+        float *part = reinterpret_cast<float *>(ws + o_part);
+        if ((rc = launch_xfield_ngp(w, a, g, enc, ws + o_x, film, st, part))) return rc;
         record_event(a->stage_events[3], st);
         return SDFR_OK;
     }

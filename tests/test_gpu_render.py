@@ -382,3 +382,31 @@ def test_graphed_generator_matches_eager(sdfr):
         torch.cuda.manual_seed(12)
         got2, _ = gg(z2, cam, focal, near, far)
         assert torch.equal(got2, ref2)
+
+
+@pytest.mark.parametrize("B,res,N", [(1, 64, 24), (2, 64, 24), (1, 32, 18), (3, 10, 7)])
+def test_field_sample_split_matches_whole_rays(sdfr, renderer_sd, B, res, N):
+    """Small batches split each ray's samples over up to 4 workgroups and chain the
+    segments (sdfr_debug_set_field_split); the result equals the whole-ray march
+    up to the re-associated transmittance product (fp32 rounding)."""
+    ren = make_renderer(sdfr, renderer_sd, res, N, return_sdf=True, return_xyz=True)
+    torch.manual_seed(B * 100 + res + N)
+    cam, focal, near, far, _ = sdfr.generate_camera_params(res, DEV, batch=B)
+    lat = torch.randn(B, 256, device=DEV)
+    tr = torch.rand(B, res, res)
+    L = sdfr._lib
+    outs = []
+    try:
+        for m in (1, 4):
+            L.check(L.lib().sdfr_debug_set_field_split(m), "sdfr_debug_set_field_split")
+            with torch.no_grad():
+                outs.append([t.clone() for t in ren(cam, focal, near, far, styles=lat,
+                                                    t_rand=tr)[:5]])
+    finally:
+        L.check(L.lib().sdfr_debug_set_field_split(4), "sdfr_debug_set_field_split")
+    (rgb1, f1, sdf1, m1, x1), (rgb4, f4, sdf4, m4, x4) = outs
+    assert torch.equal(sdf1, sdf4)                      # per-sample heads: unchanged
+    torch.testing.assert_close(rgb4, rgb1, rtol=0, atol=2e-6)
+    torch.testing.assert_close(f4, f1, rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(x4, x1, rtol=0, atol=2e-6)
+    torch.testing.assert_close(m4, m1, rtol=1e-5, atol=1e-7)

@@ -58,7 +58,13 @@ def test_workspace_size(sdfr):
     enc = 2 * 4096 * 24 * 16 * 2 * 4
     fixed = 67 * 1024 * 16 + 2 * 8 * 256 * 4          # fp32 fragments + FiLM vectors
     xfixed = 68 * 1024 * 16 + 2 * 5 * 256 * 4         # split-fp16 fragments, su, bias_s
-    assert enc + fixed + xfixed <= n <= enc + fixed + xfixed + 1024
+    # 2 faces = 128 workgroups: rays split in 2 sample segments, partials of
+    # (256 features + rgb, xyz, T, w_last) per segment and ray
+    part = 2 * (256 + 8) * 2 * 4096 * 4
+    assert enc + fixed + xfixed + part <= n <= enc + fixed + xfixed + part + 1280
+    n32 = lib.sdfr_render_ngp_workspace_bytes(32, 64, 64, 24, 16)   # >= 256 workgroups: no split
+    assert n32 <= 16 * enc + fixed + 32 * 8 * 256 * 4 + xfixed + 1280
+    assert lib.sdfr_debug_set_field_split(3) == sdfr._lib.SDFR_EINVAL
 
 
 def test_state_dict_matches_reference(sdfr, golden_dir):
