@@ -145,7 +145,7 @@ __device__ __forceinline__ void split8(const float (&v)[8], f4 &hi, f4 &lo) {
 }
 
 // ----------------------------------------------------------------------------
-// prep 1: per-row power-of-two scales and scaled biases (one block per layer)
+// prep 1: per-row power-of-two scales and scaled biases (one wave per row)
 // ----------------------------------------------------------------------------
 struct XScaleArgs {
     const float *w[kMaxLayers];
@@ -156,11 +156,15 @@ struct XScaleArgs {
 };
 
 __global__ void __launch_bounds__(256) xscale_kernel(const XScaleArgs a) {
-    const uint32_t layer = blockIdx.x, row = threadIdx.x;
+    const uint32_t layer = blockIdx.x, lane = threadIdx.x & 63u;
+    const uint32_t row = blockIdx.y * 4 + (threadIdx.x >> 6);
     const uint32_t K = a.K[layer];
     const float *wr = a.w[layer] + (size_t)row * K;
-    float m = 0.0f;
-    for (uint32_t k = 0; k < K; ++k) m = fmaxf(m, fabsf(wr[k]));
+    float m = 0.0f;                        // max is order-independent: exact
+    for (uint32_t k = lane; k < K; k += 64) m = fmaxf(m, fabsf(wr[k]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane != 0) return;
     float su = 1.0f;
     if (m > 0.0f && m < 3.0e38f) {
         int ex;
@@ -992,7 +996,7 @@ static int launch_xprep(const NetPtrs &P, const sdfr_ngp_render_args *a, char *x
     }
     sa.su = su;
     sa.bias_s = bias_s;
-    hipLaunchKernelGGL(xscale_kernel, dim3(Net::kLayers), dim3(256), 0, st, sa);
+    hipLaunchKernelGGL(xscale_kernel, dim3(Net::kLayers, kW / 4), dim3(256), 0, st, sa);
     int rc = check_launch("render: xscale");
     if (rc) return rc;
     XPrepArgs p;
