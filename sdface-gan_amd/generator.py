@@ -266,6 +266,7 @@ class Decoder(nn.Module):
         self.fuse_conv_act = True
         self._fir = None
         self._packs = {}
+        self._mod_stack = None
 
     def mean_latent(self, renderer_latent):
         return self.style(renderer_latent).mean(0, keepdim=True)
@@ -355,6 +356,35 @@ class Decoder(nn.Module):
             self._packs[i] = hit
         return hit[1:]
 
+    def _modulations(self, latent):
+        """Every conv and ToRGB modulation of the fused path (EqualLinear,
+        sdf_model.py:676-699) as ONE batched GEMM: the 11 weight matrices
+        (x scale, zero-padded to the widest) and biases (x lr_mul) are stacked once
+        per weight version, latent rows gathered per layer; one baddbmm instead of
+        three small kernels per layer.  fp32, summation order of the batched GEMM."""
+        seq = [self.conv1] + list(self.convs)
+        rgbs = [self.to_rgb1] + list(self.to_rgbs)
+        lins = [sc.conv.modulation for sc in seq] + [t.conv.modulation for t in rgbs]
+        key = tuple((m.weight.data_ptr(), m.weight._version, m.bias._version) for m in lins)
+        if self._mod_stack is None or self._mod_stack[0] != key:
+            cmax = max(m.weight.shape[0] for m in lins)
+            w0 = lins[0].weight
+            wt = w0.new_zeros(len(lins), w0.shape[1], cmax)
+            bs = w0.new_zeros(len(lins), 1, cmax)
+            with torch.no_grad():
+                for k, m in enumerate(lins):
+                    c = m.weight.shape[0]
+                    wt[k, :, :c] = (m.weight * m.scale).t()
+                    bs[k, 0, :c] = m.bias * m.lr_mul
+            # latent index per stacked layer: conv i -> i, ToRGB k -> 2k + 1
+            idx = torch.tensor(list(range(len(seq))) + [2 * k + 1 for k in range(len(rgbs))],
+                               device=w0.device)
+            self._mod_stack = (key, wt, bs, idx, [m.weight.shape[0] for m in lins], len(seq))
+        _, wt, bs, idx, cins, nconv = self._mod_stack
+        out = torch.baddbmm(bs, latent.index_select(1, idx).transpose(0, 1), wt)
+        mods = [out[k, :, :c].contiguous() for k, c in enumerate(cins)]
+        return mods[:nconv], mods[nconv:]
+
     def _fused_forward(self, features, latent, noise):
         """Same computation as the module path: per layer one split-fp16 convolution
         (or MIOpen's) plus one sdfr_styled_epilogue on NHWC activations -- for the
@@ -365,7 +395,7 @@ class Decoder(nn.Module):
         cl = torch.channels_last
         B = features.shape[0]
         seq = [self.conv1] + list(self.convs)
-        mods = [sc.conv.modulation(latent[:, i]) for i, sc in enumerate(seq)]
+        mods, rgb_mods = self._modulations(latent)
         split = [self._conv_x(sc.conv) for sc in seq]     # layer i's input as hi/lo planes
         x = (modulate_to_nhwc_split if split[0] else modulate_to_nhwc)(features, mods[0])
         rgb = None
@@ -386,7 +416,7 @@ class Decoder(nn.Module):
                 if i % 2 == 0:
                     to_rgb = self.to_rgb1 if i == 0 else self.to_rgbs[i // 2 - 1]
                     tc = to_rgb.conv
-                    s_rgb = tc.modulation(latent[:, i + 1])
+                    s_rgb = rgb_mods[i // 2]
                     rgb_w = (tc.scale * tc.weight[0, :, :, 0, 0])[None] * s_rgb[:, None, :]
                 x, part = conv3x3_f16x3_act(
                     x, packed, cout, demod=demod_su, bias=sc.activate.bias,
@@ -416,7 +446,7 @@ class Decoder(nn.Module):
             if i % 2 == 0:
                 to_rgb = self.to_rgb1 if i == 0 else self.to_rgbs[i // 2 - 1]
                 tc = to_rgb.conv
-                s_rgb = tc.modulation(latent[:, i + 1])
+                s_rgb = rgb_mods[i // 2]
                 rgb_w = (tc.scale * tc.weight[0, :, :, 0, 0])[None] * s_rgb[:, None, :]
                 rgb_b = to_rgb.bias
             x, rgb_new = styled_epilogue(
