@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(256)
 grid_fwd_kernel(const float *__restrict__ inputs, const float *__restrict__ emb,
                 const int32_t *__restrict__ offsets, float *__restrict__ outputs,
                 float *__restrict__ dy_dx, uint32_t B, uint32_t L, const LevelTable lt,
-                uint32_t gridtype, int align_corners, uint32_t interp) {
+                uint32_t gridtype, int align_corners, uint32_t interp, int pair_ok) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const uint32_t level = blockIdx.y;
@@ -69,8 +69,31 @@ grid_fwd_kernel(const float *__restrict__ inputs, const float *__restrict__ emb,
     }
     LevelCoord<D, C> lc;
     level_coord<D, C>(x, q, align_corners, interp, lc);
+    // the 2^D corner rows, read once for the value AND every dy_dx term (which
+    // are differences of the same corners, gridencoder.cu:201-244); paired
+    // 16-B x-neighbour loads for D = 3, C = 2 on even-sized, even-based levels
+    float v[1u << D][C];
+    if constexpr (D == 3 && C == 2) {
+        if (pair_ok && !((q.offset | q.hsize) & 1u))
+            level_corners<D, C, true>(grid, q, align_corners, lc, v);
+        else
+            level_corners<D, C, false>(grid, q, align_corners, lc, v);
+    } else {
+        level_corners<D, C, false>(grid, q, align_corners, lc, v);
+    }
+    // value: corner weights and fma order of gridencoder.cu:160-192 (level_interp)
     float res[C];
-    level_interp<D, C>(grid, q, align_corners, lc, res);
+#pragma unroll
+    for (uint32_t c = 0; c < C; ++c) res[c] = 0.0f;
+#pragma unroll
+    for (uint32_t idx = 0; idx < (1u << D); ++idx) {
+        float w = 1.0f;
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d)
+            w = __fmul_rn(w, (idx & (1u << d)) ? lc.pos[d] : __fsub_rn(1.0f, lc.pos[d]));
+#pragma unroll
+        for (uint32_t c = 0; c < C; ++c) res[c] = __fmaf_rn(w, v[idx][c], res[c]);
+    }
 #pragma unroll
     for (uint32_t c = 0; c < C; ++c) out[c] = res[c];
 
@@ -83,28 +106,22 @@ grid_fwd_kernel(const float *__restrict__ inputs, const float *__restrict__ emb,
 #pragma unroll
         for (uint32_t idx = 0; idx < (1u << (D - 1)); ++idx) {
             float w = q.scale;
-            uint32_t pl[D];
+            uint32_t cl = 0;                       // corner with bit gd = 0
 #pragma unroll
             for (uint32_t nd = 0; nd < D - 1; ++nd) {
                 const uint32_t d = (nd >= gd) ? (nd + 1) : nd;
                 if ((idx & (1u << nd)) == 0) {
                     w = __fmul_rn(w, __fsub_rn(1.0f, lc.pos[d]));
-                    pl[d] = lc.pg[d];
                 } else {
                     w = __fmul_rn(w, lc.pos[d]);
-                    pl[d] = lc.pg[d] + 1;
+                    cl |= 1u << d;
                 }
             }
-            pl[gd] = lc.pg[gd];
-            const uint32_t il = grid_index<D>(q, align_corners, pl) * C;
-            pl[gd] = lc.pg[gd] + 1;
-            const uint32_t ir = grid_index<D>(q, align_corners, pl) * C;
-            float vl[C], vr[C];
-            load_row<C>(grid, il, vl);
-            load_row<C>(grid, ir, vr);
+            const uint32_t cr = cl | (1u << gd);
 #pragma unroll
             for (uint32_t c = 0; c < C; ++c)
-                rg[c] = __fmaf_rn(__fmul_rn(w, __fsub_rn(vr[c], vl[c])), lc.pos_d[gd], rg[c]);
+                rg[c] = __fmaf_rn(__fmul_rn(w, __fsub_rn(v[cr][c], v[cl][c])), lc.pos_d[gd],
+                                  rg[c]);
         }
 #pragma unroll
         for (uint32_t c = 0; c < C; ++c) dd[gd * C + c] = rg[c];
@@ -177,8 +194,9 @@ static int grid_fwd_launch(const float *in, const float *emb, const int32_t *off
                            float *dydx, uint32_t B, uint32_t L, const LevelTable &lt,
                            uint32_t gt, int ac, uint32_t interp, hipStream_t st) {
     dim3 grid((B + 255) / 256, L);
+    const int pair_ok = (reinterpret_cast<uintptr_t>(emb) & 7u) == 0;
     hipLaunchKernelGGL((grid_fwd_kernel<D, C>), grid, dim3(256), 0, st, in, emb, off, out, dydx,
-                       B, L, lt, gt, ac, interp);
+                       B, L, lt, gt, ac, interp, pair_ok);
     return check_launch("grid_encode_forward");
 }
 

@@ -216,14 +216,10 @@ __device__ __forceinline__ bool sample_u(const GeomArgs &g, uint32_t sid, float 
 // {LPT y, LPT y + 1, ...} with ADJ).  Branch-free: padding / out-of-box samples
 // gather at u = 0.5 and store 0, so every corner load of the thread can be in
 // flight at once.
-// 8-B-aligned 16-B row pair (global_load_dwordx4 at dword alignment)
-typedef float f4_a8 __attribute__((ext_vector_type(4), aligned(8)));
-
-// level_interp_pair with dword-aligned (not 16-B aligned) pair loads: the two
-// x-corners come from ONE 16-B load whenever their rows are consecutive,
-// i1 = i0 +- 1 (every dense row; hashed rows for 2/3 of the g0 parities), else
-// from the aligned pair holding i0 plus an 8-B load of i1.  Same weights and
-// fma order as level_interp: bit-identical.
+// level_interp_pair with dword-aligned (not 16-B aligned) pair loads
+// (load_xpair, sdfr_common.h): the two x-corners come from ONE 16-B load
+// whenever their rows are consecutive.  Same weights and fma order as
+// level_interp: bit-identical.
 __device__ __forceinline__ void level_interp_adj(const float *__restrict__ grid,
                                                  const LevelParam &q,
                                                  const LevelCoord<3, 2> &lc, float (&out)[2]) {
@@ -247,21 +243,7 @@ __device__ __forceinline__ void level_interp_adj(const float *__restrict__ grid,
         const uint32_t i0 = grid_index<3>(q, 0, pl);
         pl[0] = lc.pg[0] + 1;
         const uint32_t i1 = grid_index<3>(q, 0, pl);
-        const bool up = i1 == i0 + 1u, down = i1 + 1u == i0;
-        // rows loaded: {base, base+1}, all inside the level (hsize is even)
-        const uint32_t base = up ? i0 : (down ? i1 : (i0 & ~1u));
-        const f4_a8 t = *reinterpret_cast<const f4_a8 *>(grid + (size_t)base * 2);
-        const bool lo0 = base == i0;
-        v[idx][0] = lo0 ? t.x : t.z;
-        v[idx][1] = lo0 ? t.y : t.w;
-        if (up || down) {
-            v[idx + 1][0] = up ? t.z : t.x;
-            v[idx + 1][1] = up ? t.w : t.y;
-        } else {
-            const float2 u = *reinterpret_cast<const float2 *>(grid + (size_t)i1 * 2);
-            v[idx + 1][0] = u.x;
-            v[idx + 1][1] = u.y;
-        }
+        load_xpair(grid, i0, i1, v[idx], v[idx + 1]);
     }
     out[0] = out[1] = 0.0f;
 #pragma unroll

@@ -200,6 +200,55 @@ __device__ __forceinline__ void level_interp(const float *__restrict__ grid,
         for (uint32_t c = 0; c < C; ++c) out[c] = __fmaf_rn(wts[idx], v[idx][c], out[c]);
 }
 
+// 8-B-aligned 16-B row pair (global_load_dwordx4 at dword alignment)
+typedef float f4_a8 __attribute__((ext_vector_type(4), aligned(8)));
+
+// Rows i0 (x-corner g0) and i1 (g0+1) of a C = 2 level whose size is even:
+// ONE 16-B load when the rows are consecutive, i1 = i0 +- 1 (every dense row;
+// hashed rows -- prime 1 on x -- for 2/3 of the g0 parities), else the aligned
+// pair holding i0 plus an 8-B load of i1 (for those lanes only).  Every row
+// read lies inside the level.
+__device__ __forceinline__ void load_xpair(const float *__restrict__ grid, uint32_t i0,
+                                           uint32_t i1, float (&v0)[2], float (&v1)[2]) {
+    const bool up = i1 == i0 + 1u, down = i1 + 1u == i0;
+    const uint32_t base = up ? i0 : (down ? i1 : (i0 & ~1u));
+    const f4_a8 t = *reinterpret_cast<const f4_a8 *>(grid + (size_t)base * 2);
+    const bool lo0 = base == i0;
+    v0[0] = lo0 ? t.x : t.z;
+    v0[1] = lo0 ? t.y : t.w;
+    if (up || down) {
+        v1[0] = up ? t.z : t.x;
+        v1[1] = up ? t.w : t.y;
+    } else {
+        const float2 u = *reinterpret_cast<const float2 *>(grid + (size_t)i1 * 2);
+        v1[0] = u.x;
+        v1[1] = u.y;
+    }
+}
+
+// All 2^D corner rows of one level, corner idx bit d = (g_d or g_d + 1); with
+// PAIR (D = 3, C = 2 only) the x-neighbours through load_xpair.
+template <uint32_t D, uint32_t C, bool PAIR>
+__device__ __forceinline__ void level_corners(const float *__restrict__ grid,
+                                              const LevelParam &q, int align_corners,
+                                              const LevelCoord<D, C> &lc,
+                                              float (&v)[1u << D][C]) {
+#pragma unroll
+    for (uint32_t idx = 0; idx < (1u << D); idx += (PAIR ? 2u : 1u)) {
+        uint32_t pl[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) pl[d] = (idx & (1u << d)) ? lc.pg[d] + 1 : lc.pg[d];
+        const uint32_t i0 = grid_index<D>(q, align_corners, pl);
+        if constexpr (PAIR) {
+            static_assert(C == 2, "paired corner loads need C = 2");
+            pl[0] = lc.pg[0] + 1;
+            load_xpair(grid, i0, grid_index<D>(q, align_corners, pl), v[idx], v[idx + 1]);
+        } else {
+            load_row<C>(grid, i0 * C, v[idx]);
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------
 // device: ray generation + sampling (sdf_model.py:207-222, 310-351, 363-378)
 // ----------------------------------------------------------------------------
