@@ -143,3 +143,27 @@ def test_device_sin_accuracy(sdfr):
     ref = torch.sin(xs.double())
     assert (cw.cpu().double() - ref).abs().max() < 2e-7
     assert (hw.cpu().double() - ref).abs().max() < 1e-6
+
+
+def test_grid_backward_large_privatised_levels(sdfr, oracle_mod, table):
+    """200 k samples in the renderer's coordinate range: the coarse levels'
+    gradients go through the LDS-privatised kernel (one global add per row and
+    workgroup), the rest through direct atomics; both are order-dependent fp32
+    sums of the same per-sample products."""
+    offsets, pls, emb = table
+    rng = np.random.default_rng(9)
+    n = 200_000
+    x = rng.uniform(0.23, 0.78, size=(n, 3)).astype(np.float32)
+    x[:7] = [[-0.1, 0.5, 0.5], [1.2, 0.5, 0.5], [0, 0, 0], [1, 1, 1], [0.5, 0.5, 0.5],
+             [0.999, 0.001, 0.5], [0.25, 0.75, 1.0]]                 # OOB and edges
+    xt = torch.from_numpy(x).to(DEV)
+    et = torch.nn.Parameter(torch.from_numpy(emb).to(DEV))
+    ot = torch.from_numpy(offsets).to(DEV)
+    out = sdfr.grid_encode(xt, et, ot, pls, 16, True, 0, False, 0)
+    grad = torch.from_numpy(rng.normal(size=out.shape).astype(np.float32)).to(DEV)
+    out.backward(grad)
+    g_lbc = grad.view(n, 16, 2).permute(1, 0, 2).contiguous().cpu().numpy()
+    ge, _ = oracle_mod.grid_encode_backward(g_lbc, x, emb, offsets, pls, 16)
+    got = et.grad.cpu().numpy()
+    np.testing.assert_allclose(got, ge, rtol=1e-4, atol=2e-5 * float(np.abs(ge).max()))
+    assert np.count_nonzero(got) == np.count_nonzero(ge)
