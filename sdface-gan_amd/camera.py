@@ -56,7 +56,9 @@ def generate_camera_params(resolution, device, batch=1, locations=None, sweep=Fa
     x_axis = F.normalize(torch.cross(up, z_axis, dim=1), eps=1e-5)
     y_axis = F.normalize(torch.cross(z_axis, x_axis, dim=1), eps=1e-5)
     is_close = torch.isclose(x_axis, torch.tensor(0.0), atol=5e-3).all(dim=1, keepdim=True)
-    if is_close.any():
+    # sdf_utils.py:151-154 branches on is_close.any(), a host sync per call; on the
+    # GPU the replacement is always formed and selected per row (same result)
+    if x_axis.is_cuda or is_close.any():
         repl = F.normalize(torch.cross(y_axis, z_axis, dim=1), eps=1e-5)
         x_axis = torch.where(is_close, repl, x_axis)
     R = torch.cat((x_axis[:, None, :], y_axis[:, None, :], z_axis[:, None, :]), dim=1)
