@@ -72,3 +72,14 @@ def test_sdf_volume_256_properties(sdfr):
     assert sdf.shape == (1, 256, 256, 256, 1)
     assert torch.isfinite(sdf).all() and torch.isfinite(a[2]).all()
     assert torch.equal(sdf, b[3]) and torch.equal(a[2], b[2])
+
+
+def test_align_volume_on_gpu_matches_reference(sdfr, golden_dir):
+    """align_volume with the sampling grid formed on the device: the reference's
+    golden (sdf_utils.align_volume on CPU) up to the GPU grid_sample's rounding,
+    and exactly 1 in every cell whose scaled coordinate leaves the cube."""
+    g = np.load(golden_dir / "mesh128.npz")
+    out = sdfr.align_volume(torch.from_numpy(g["vol"]).to("cuda:0")).cpu().numpy()
+    ref = g["vol_aligned"]
+    np.testing.assert_allclose(out, ref, rtol=0, atol=2e-6)
+    assert np.array_equal(out == 1.0, ref == 1.0)
