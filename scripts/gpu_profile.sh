@@ -14,7 +14,7 @@ rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
 [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_trace" -o trace \
-    -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-extras > gpurun_out/prof_trace.log 2>&1
+    -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-extras > gpurun_out/prof_trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/prof_fetch" -o fetch \
     -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/prof_fetch.log 2>&1
