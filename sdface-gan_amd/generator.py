@@ -267,6 +267,7 @@ class Decoder(nn.Module):
         self._fir = None
         self._packs = {}
         self._mod_stack = None
+        self._demod_stack = None
 
     def mean_latent(self, renderer_latent):
         return self.style(renderer_latent).mean(0, keepdim=True)
@@ -383,7 +384,34 @@ class Decoder(nn.Module):
         _, wt, bs, idx, cins, nconv = self._mod_stack
         out = torch.baddbmm(bs, latent.index_select(1, idx).transpose(0, 1), wt)
         mods = [out[k, :, :c].contiguous() for k, c in enumerate(cins)]
-        return mods[:nconv], mods[nconv:]
+        return mods[:nconv], mods[nconv:], out[:nconv]
+
+    def _demods(self, seq, split, mods_raw):
+        """demod / su of every split-fp16 layer (see _pack) in one batched GEMM +
+        one rsqrt: the layers' [Cin, Cout] weight sums and eps rows are stacked
+        (zero-padded) once per weight version; mods_raw is _modulations' padded
+        [layers, B, Cmax] output (its padding is exactly 0)."""
+        layers = [i for i, sc in enumerate(seq) if split[i] and sc.conv.demodulate]
+        if not layers:
+            return {}
+        packs = {i: self._pack(i, seq[i].conv) for i in layers}
+        key = tuple(self._packs[i][0] for i in layers)
+        if getattr(self, "_demod_stack", None) is None or self._demod_stack[0] != key:
+            cmax = mods_raw.shape[-1]
+            omax = max(packs[i][2].shape[1] for i in layers)
+            w0 = packs[layers[0]][2]
+            wsq = w0.new_zeros(len(layers), cmax, omax)
+            eps = w0.new_zeros(len(layers), 1, omax)
+            for j, i in enumerate(layers):
+                cin, cout = packs[i][2].shape
+                wsq[j, :cin, :cout] = packs[i][2]
+                eps[j, 0, :cout] = packs[i][3]
+            sel = torch.tensor(layers, device=w0.device)
+            self._demod_stack = (key, wsq, eps, sel)
+        _, wsq, eps, sel = self._demod_stack
+        m = mods_raw.index_select(0, sel)
+        d = torch.rsqrt(torch.baddbmm(eps, m * m, wsq))
+        return {i: d[j, :, :packs[i][2].shape[1]].contiguous() for j, i in enumerate(layers)}
 
     def _fused_forward(self, features, latent, noise):
         """Same computation as the module path: per layer one split-fp16 convolution
@@ -395,8 +423,9 @@ class Decoder(nn.Module):
         cl = torch.channels_last
         B = features.shape[0]
         seq = [self.conv1] + list(self.convs)
-        mods, rgb_mods = self._modulations(latent)
+        mods, rgb_mods, mods_raw = self._modulations(latent)
         split = [self._conv_x(sc.conv) for sc in seq]     # layer i's input as hi/lo planes
+        demods = self._demods(seq, split, mods_raw)
         x = (modulate_to_nhwc_split if split[0] else modulate_to_nhwc)(features, mods[0])
         rgb = None
         for i, sc in enumerate(seq):
@@ -405,8 +434,7 @@ class Decoder(nn.Module):
             cout = mc.weight.shape[1]
             if split[i]:
                 packed, su, wsq, eps = self._pack(i, mc)
-                demod_su = (torch.rsqrt(torch.addmm(eps, mods[i] * mods[i], wsq))
-                            if mc.demodulate else 1.0 / su.expand(B, -1))
+                demod_su = demods[i] if mc.demodulate else 1.0 / su.expand(B, -1)
             if (self.fuse_conv_act and split[i] and not mc.upsample and (last or split[i + 1])
                     and (x.shape[1] * x.shape[2]) % 256 == 0):
                 # regular conv with the epilogue fused: the conv output stays on chip
