@@ -255,11 +255,10 @@ def main():
         gg = sdfr.GraphedGenerator(g)
 
         def graphed_step(nb):
-            z = torch.randn(nb, opt.model.style_dim, device=device, generator=gen)
-            cam, focal, near, far, _ = sdfr.generate_camera_params(
-                res, device, batch=nb, azim_range=opt.camera.azim, elev_range=opt.camera.elev,
-                fov_ang=opt.camera.fov, dist_radius=opt.camera.dist_radius)
-            return gg(z, cam, focal, near, far)[0]
+            # latents, cameras, sampling offsets and noise drawn inside the graph
+            return gg.random_faces(nb, res, azim_range=opt.camera.azim,
+                                   elev_range=opt.camera.elev, fov_ang=opt.camera.fov,
+                                   dist_radius=opt.camera.dist_radius)[0]
         line["extras"] = extras(step, B, graphed_step)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, siren)

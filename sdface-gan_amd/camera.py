@@ -51,7 +51,11 @@ def generate_camera_params(resolution, device, batch=1, locations=None, sweep=Fa
     camera_dir = torch.stack([x, y, z], dim=1).view(-1, 3)
     camera_loc = dist * camera_dir
 
-    up = torch.tensor([[0, 1, 0]]).float().to(device) * torch.ones_like(dist)
+    if dist.is_cuda:      # same (0, 1, 0) rows without a host->device copy (graph-capturable)
+        up = torch.zeros_like(camera_dir)
+        up[:, 1] = 1.0
+    else:
+        up = torch.tensor([[0, 1, 0]]).float().to(device) * torch.ones_like(dist)
     z_axis = F.normalize(camera_dir, eps=1e-5)
     x_axis = F.normalize(torch.cross(up, z_axis, dim=1), eps=1e-5)
     y_axis = F.normalize(torch.cross(z_axis, x_axis, dim=1), eps=1e-5)

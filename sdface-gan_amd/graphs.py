@@ -23,7 +23,9 @@ import torch
 
 
 class GraphedGenerator:
-    """``GraphedGenerator(g)(z, cam, focal, near, far) -> (rgb, thumb)``.
+    """``GraphedGenerator(g)(z, cam, focal, near, far) -> (rgb, thumb)``, or
+    ``GraphedGenerator(g).random_faces(B) -> (rgb, thumb)`` with the latents and
+    cameras drawn inside the graph too.
 
     Same arguments as ``Generator.forward`` for the eval use (one style tensor,
     truncation / truncation_latent fixed at construction); one graph per batch
@@ -61,7 +63,33 @@ class GraphedGenerator:
                 return self.g([static["z"]], static["cam"], static["focal"], static["near"],
                               static["far"], **self.kw)
 
-        # warm up on a side stream: first calls pack decoder weights, pick paths
+        graph, out = self._record(fwd)
+        return graph, static, out
+
+    def random_faces(self, B, resolution=64, **camera_kw):
+        """B faces from fresh latents z ~ N(0, 1) and cameras drawn by
+        generate_camera_params(resolution, **camera_kw) -- eval.py's whole
+        per-image loop body -- with the draws inside the graph as well."""
+        key = ("random", B, resolution, tuple(sorted(camera_kw.items())))
+        if key not in self._graphs:
+            from .camera import generate_camera_params
+
+            def fwd():
+                z = torch.randn(B, self.g.style_dim, device=self.device)
+                cam, focal, near, far, _ = generate_camera_params(resolution, self.device,
+                                                                  batch=B, **camera_kw)
+                with torch.no_grad():
+                    return self.g([z], cam, focal, near, far, **self.kw)
+
+            self._graphs[key] = self._record(fwd)
+        graph, out = self._graphs[key]
+        graph.replay()
+        return out
+
+    def _record(self, fwd):
+        """Warm up on a side stream (first calls pack decoder weights and pick
+        paths), then capture one call of fwd."""
+        dev = self.device
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
@@ -71,7 +99,7 @@ class GraphedGenerator:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             out = fwd()
-        return graph, static, out
+        return graph, out
 
     def __call__(self, z, cam_poses, focals, near, far):
         B = z.shape[0]

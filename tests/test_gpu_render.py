@@ -410,3 +410,25 @@ def test_field_sample_split_matches_whole_rays(sdfr, renderer_sd, B, res, N):
     torch.testing.assert_close(f4, f1, rtol=1e-5, atol=2e-5)
     torch.testing.assert_close(x4, x1, rtol=0, atol=2e-6)
     torch.testing.assert_close(m4, m1, rtol=1e-5, atol=1e-7)
+
+
+def test_graphed_random_faces_matches_eager(sdfr):
+    """GraphedGenerator.random_faces: latents and cameras drawn inside the graph,
+    the same images as eval.py's eager loop body from the same RNG state."""
+    dev = torch.device("cuda", 0)
+    opt = sdfr.vol_render_opt()
+    torch.manual_seed(4)
+    g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
+    g.renderer.rng_device = "device"
+    gg = sdfr.GraphedGenerator(g)
+    gg.random_faces(2, 64)                               # capture
+    torch.cuda.manual_seed(21)
+    rgb, thumb = gg.random_faces(2, 64)
+    torch.cuda.manual_seed(21)
+    with torch.no_grad():
+        z = torch.randn(2, 256, device=dev)
+        cam, focal, near, far, _ = sdfr.generate_camera_params(64, dev, batch=2)
+        ref_rgb, ref_thumb = g([z], cam, focal, near, far)
+    assert torch.equal(rgb, ref_rgb) and torch.equal(thumb, ref_thumb)
+    first = rgb.clone()
+    assert not torch.equal(gg.random_faces(2, 64)[0], first)
