@@ -229,6 +229,11 @@ int sdfr_debug_set_field_split(int max_segments);
 int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t n,
                          void *stream);
 
+/* Accuracy probe for the split-fp16 field kernel's FiLM sin, whose argument is in
+ * revolutions (1/(2 pi) folded into the FiLM vectors): out[i] = sin(2 pi u[i]) by
+ * v_fract_f32 + v_sin_f32, n elements. */
+int sdfr_debug_sin_rev_probe(const float *u, float *out, uint32_t n, void *stream);
+
 /* ---------------------------------------------------------------------------
  * StyleGAN2 decoder ops (im2scene/sdf/models/sdf_op.py).
  *

@@ -34,6 +34,7 @@ EXPORTS = (
     "sdfr_sh_encode_forward", "sdfr_sh_encode_backward",
     "sdfr_render_ngp_workspace_bytes", "sdfr_render_ngp_forward",
     "sdfr_render_ngp_encode_only", "sdfr_debug_set_field_variant", "sdfr_debug_sin_probe",
+    "sdfr_debug_sin_rev_probe",
     "sdfr_debug_set_encode_mode", "sdfr_debug_set_field_split",
     "sdfr_render_siren_workspace_bytes", "sdfr_render_siren_forward",
     "sdfr_fused_bias_act", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
@@ -143,6 +144,7 @@ def lib():
     L.sdfr_render_siren_forward.argtypes = [ctypes.POINTER(SirenWeights),
                                             ctypes.POINTER(NgpRenderArgs), _vp]
     L.sdfr_debug_sin_probe.argtypes = [_vp, _vp, _vp, _u32, _vp]
+    L.sdfr_debug_sin_rev_probe.argtypes = [_vp, _vp, _u32, _vp]
     L.sdfr_fused_bias_act.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_uint64, _u32, _u32, _int, _int,
                                       _f32, _f32, _vp]
     L.sdfr_upfirdn2d.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32] + [_int] * 8 + [_vp]

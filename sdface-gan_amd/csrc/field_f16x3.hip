@@ -153,6 +153,7 @@ struct XScaleArgs {
     uint32_t K[kMaxLayers];
     float *su;       // [layers][256]
     float *bias_s;   // [layers][256]
+    int raw_bias0;   // layer 0's bias stays unscaled (ngp: added after the GEMM)
 };
 
 __global__ void __launch_bounds__(256) xscale_kernel(const XScaleArgs a) {
@@ -173,7 +174,8 @@ __global__ void __launch_bounds__(256) xscale_kernel(const XScaleArgs a) {
         su = ldexpf(1.0f, -ex);
     }
     a.su[layer * kW + row] = su;
-    a.bias_s[layer * kW + row] = __fmul_rn(a.b[layer][row], su);
+    a.bias_s[layer * kW + row] =
+        (layer == 0 && a.raw_bias0) ? a.b[0][row] : __fmul_rn(a.b[layer][row], su);
 }
 
 // ----------------------------------------------------------------------------
@@ -212,11 +214,16 @@ __global__ void __launch_bounds__(256) xprep_kernel(const XPrepArgs a) {
             acc = __fmaf_rn(s4.w, w4.w, acc);
         }
         const float lin = __fadd_rn(acc, bias[j]);
-        // LinearLayer: std_init * linear + bias_init (sdf_model.py:39, 58-59); the
-        // gamma absorbs the row scale of the layer it modulates, exactly
-        const float v = which ? __fadd_rn(__fmul_rn(0.25f, lin), 0.0f)
-                              : __fdiv_rn(__fadd_rn(__fmul_rn(15.0f, lin), 30.0f),
-                                          a.su[Net::film_layer(f) * kW + j]);
+        // LinearLayer: std_init * linear + bias_init (sdf_model.py:39, 58-59).  The
+        // activation sin(gamma x + beta) runs as sin_rev(fma(gamma'', x_s, beta''))
+        // with the argument in revolutions: gamma'' = gamma / (su 2pi) also absorbs
+        // the row scale su of the layer it modulates, beta'' = beta / 2pi; each is
+        // one correctly rounded division (in double) of the reference's fp32 value
+        constexpr double k2pi = 6.283185307179586476925;
+        const float v = which
+            ? (float)((double)__fadd_rn(__fmul_rn(0.25f, lin), 0.0f) / k2pi)
+            : (float)((double)__fadd_rn(__fmul_rn(15.0f, lin), 30.0f) /
+                      ((double)a.su[Net::film_layer(f) * kW + j] * k2pi));
         a.film[(((size_t)b * NF + f) * 2 + which) * kW + j] = v;
         return;
     }
@@ -451,13 +458,15 @@ __device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], 
 
 // Activate tile pair (2q, 2q+1) of one sample column in place and split it
 // into the (hi, lo) B fragment of k-step q.
-//   MODE 0: identity layer, x * (1/su)            (ngp input_linear)
-//   MODE 1: FiLM sin(gamma' x + beta)              (sdf_model.py:67, two roundings)
+//   MODE 0: identity layer, fma(x 2^-es, 1/su, b)  (ngp input_linear: the GEMM ran
+//           on features scaled by 2^es and accumulated from zero, see feat_scale)
+//   MODE 1: FiLM sin(gamma x + beta) = sin_rev(fma(gamma'', x_s, beta''))  (sdf_model.py:67;
+//           revolutions, see xprep_kernel)
 //   MODE 2: FiLM + partial sigma_linear dot product (the sdf head)
 template <int MODE, int V>
 __device__ __forceinline__ void act_pair(f4 &za, f4 &zb, int q, const float *gam,
                                          const float *bet, const float *sw, float &sdfp,
-                                         uint32_t g) {
+                                         uint32_t g, int es = 0) {
     if constexpr ((V & 8) != 0) {
         xpin(za);
         xpin(zb);
@@ -469,13 +478,12 @@ __device__ __forceinline__ void act_pair(f4 &za, f4 &zb, int q, const float *gam
         const f4 z = half ? zb : za;
         const int f0 = 16 * (2 * q + half) + 4 * (int)g;
         const f4 gm = *reinterpret_cast<const f4 *>(gam + f0);
-        f4 bt = {0.0f, 0.0f, 0.0f, 0.0f};
-        if constexpr (MODE != 0) bt = *reinterpret_cast<const f4 *>(bet + f0);
+        const f4 bt = *reinterpret_cast<const f4 *>(bet + f0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float x;
-            if constexpr (MODE == 0) x = __fmul_rn(z[r], gm[r]);
-            else x = sin_hw(__fadd_rn(__fmul_rn(gm[r], z[r]), bt[r]));
+            if constexpr (MODE == 0) x = __fmaf_rn(__builtin_ldexpf(z[r], -es), gm[r], bt[r]);
+            else x = sin_rev(__fmaf_rn(gm[r], z[r], bt[r]));
             v[4 * half + r] = x;
         }
         if constexpr (MODE == 2) {
@@ -488,6 +496,31 @@ __device__ __forceinline__ void act_pair(f4 &za, f4 &zb, int q, const float *gam
     xpin(za);
     xpin(zb);
     if constexpr (MODE == 2) xpin(sdfp);
+}
+
+// ngp layer-0 inputs: the 32 hash-grid features of a sample span the 4 lane
+// groups of its column.  They are scaled by the power of two 2^es that brings the
+// sample's max |x| into [0.5, 1) before the hi/lo split, so neither fp16 part
+// goes subnormal at any table scale (the reference initialises the table to
+// U(-1e-4, 1e-4), grid.py:138-140, where unscaled features would lose their lo
+// parts); the scaling is exact and undone exactly in act_pair<0>.
+__device__ __forceinline__ int feat_scale(float (&v)[8]) {
+    float m = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    if (!(m > 0.0f && m < 3.0e38f)) return 0;          // zeros (out of bounds) / non-finite
+    int ex = __builtin_amdgcn_frexp_expf(m);          // m = f 2^ex, f in [0.5, 1)
+    const int es = ex < -100 ? 100 : -ex;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = __builtin_ldexpf(v[j], es);
+    return es;
+}
+
+__device__ __forceinline__ void zero_acc(f4 (&acc)[16]) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 }
 
 __device__ __forceinline__ void init_acc(f4 (&acc)[16], const float *bias, uint32_t g) {
@@ -530,7 +563,7 @@ template <int V, class Net>
 __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a) {
     constexpr int NL = Net::kLayers, NF = Net::kFilmN;
     __shared__ f4 ring_lds[(Net::kSlice2 ? 4 : 3) * kXSliceF4];   // 64 / 48 KB weight ring
-    __shared__ float cst[(NL + 5) * kW];                   // bias_s[NL], 1/su0, sigma_w, rgb_w[3]
+    __shared__ float cst[(NL + 5) * kW];                   // bias_s[NL] (ngp layer 0 unscaled), 1/su0, sigma_w, rgb_w[3]
     __shared__ float film_lds[NF * 2 * kW];                // the workgroup's face
     __shared__ f4 facc_lds[kWaves][16 * 64];               // 64 KB: feature accumulators
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -695,6 +728,7 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
     for (uint32_t p = p_begin; p < p_end; ++p) {
         f4 X0[16], X1[16], Y0[16], Y1[16];
         f4 e0h, e0l, e1h, e1l;
+        int es0 = 0, es1 = 0;
         {
             float v0[8], v1[8];
 #pragma unroll
@@ -703,6 +737,10 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
                 v0[2 * c + 1] = en[0][c].y;
                 v1[2 * c] = en[1][c].x;
                 v1[2 * c + 1] = en[1][c].y;
+            }
+            if constexpr (!Net::kSiren) {
+                es0 = feat_scale(v0);
+                es1 = feat_scale(v1);
             }
             split8(v0, e0h, e0l);
             split8(v1, e1h, e1l);
@@ -728,13 +766,19 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
                 act_film(0)(za, zb, q, j);
             } else {
                 float dummy = 0.0f;
-                act_pair<0, V>(za, zb, q, inv_su0, nullptr, nullptr, dummy, g);
+                act_pair<0, V>(za, zb, q, inv_su0, bias_l, nullptr, dummy, g, j ? es1 : es0);
             }
         };
 
-        // layer 0 (32 -> 256 ngp / 3 -> 256 siren) -> X
-        init_acc(X0, bias_l, g);
-        init_acc(X1, bias_l, g);
+        // layer 0 (32 -> 256 ngp / 3 -> 256 siren) -> X; ngp accumulates from zero
+        // (scaled features) and adds its bias in act_pair<0>
+        if constexpr (Net::kSiren) {
+            init_acc(X0, bias_l, g);
+            init_acc(X1, bias_l, g);
+        } else {
+            zero_acc(X0);
+            zero_acc(X1);
+        }
         xstep<V, Net, 0>(R, X0, X1, e0h, e0l, e1h, e1l, [] {});
         xstep<V, Net, 1>(R, X0, X1, e0h, e0l, e1h, e1l, [&] {
             act_l0(X0[0], X0[1], 0, 0);
@@ -824,7 +868,7 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
                 f4 fv;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    fv[r] = sin_hw(__fadd_rn(__fmul_rn(gm[r], Xj[t][r]), bt[r]));
+                    fv[r] = sin_rev(__fmaf_rn(gm[r], Xj[t][r], bt[r]));
                     p0 = __fmaf_rn(fv[r], w0[r], p0);
                     p1 = __fmaf_rn(fv[r], w1[r], p1);
                     p2 = __fmaf_rn(fv[r], w2[r], p2);
@@ -996,6 +1040,7 @@ static int launch_xprep(const NetPtrs &P, const sdfr_ngp_render_args *a, char *x
     }
     sa.su = su;
     sa.bias_s = bias_s;
+    sa.raw_bias0 = !Net::kSiren;
     hipLaunchKernelGGL(xscale_kernel, dim3(Net::kLayers, kW / 4), dim3(256), 0, st, sa);
     int rc = check_launch("render: xscale");
     if (rc) return rc;

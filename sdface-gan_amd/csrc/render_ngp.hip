@@ -340,6 +340,12 @@ __global__ void sin_probe_kernel(const float *__restrict__ x, float *__restrict_
     hw[i] = sin_hw(x[i]);
 }
 
+__global__ void sin_rev_probe_kernel(const float *__restrict__ u, float *__restrict__ out,
+                                     uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = sin_rev(u[i]);
+}
+
 // Streaming state for the weight ring: slot s of `lds` holds one K-slice.
 struct Ring {
     f4 *lds;              // [3][kSliceF4]
@@ -874,6 +880,13 @@ int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t 
     hipLaunchKernelGGL(sin_probe_kernel, dim3((n + 255) / 256), dim3(256), 0,
                        (hipStream_t)stream, x, out_cw, out_hw, n);
     return check_launch("sin_probe");
+}
+
+int sdfr_debug_sin_rev_probe(const float *u, float *out, uint32_t n, void *stream) {
+    if (n == 0) return SDFR_OK;
+    hipLaunchKernelGGL(sin_rev_probe_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                       (hipStream_t)stream, u, out, n);
+    return check_launch("sin_rev_probe");
 }
 
 int sdfr_debug_set_field_split(int max_segments) {

@@ -533,9 +533,10 @@ class Generator(nn.Module):
                       for s in styles]
         return styles
 
-    def init_forward(self, styles, cam_poses, focals, near=0.88, far=1.12):
+    def init_forward(self, styles, cam_poses, focals, near=0.88, far=1.12, t_rand=None):
         latent = self.styles_and_noise_forward(styles)
-        return self.renderer.mlp_init_pass(cam_poses, focals, near, far, styles=latent[0])
+        return self.renderer.mlp_init_pass(cam_poses, focals, near, far, styles=latent[0],
+                                           t_rand=t_rand)
 
     def forward(self, styles, cam_poses, focals, near=0.88, far=1.12, return_latents=False,
                 inject_index=None, truncation=1, truncation_latent=None, input_is_latent=False,

@@ -16,6 +16,12 @@ Requirements: the generator is on a CUDA device in eval mode, takes the fused
 paths (no autograd), and its renderer draws sampling offsets on the device
 (``renderer.rng_device = "device"``; the reference-compatible host draw would be
 a pageable copy inside the graph).
+
+Weight updates: a graph freezes the kernels' pointer arguments and the decoder's
+packed / stacked weight caches.  Every call compares each parameter's and
+buffer's (data_ptr, version) with the values at capture -- an EMA step,
+``load_state_dict`` or a moved tensor changes them -- and re-captures when they
+differ, so a replay never mixes a new renderer with a stale decoder.
 """
 from __future__ import annotations
 
@@ -47,6 +53,19 @@ class GraphedGenerator:
         self.kw = dict(truncation=truncation, truncation_latent=truncation_latent,
                        randomize_noise=randomize_noise)
         self._graphs = {}
+        self._tensors = list(generator.parameters()) + list(generator.buffers())
+        self._wkey = None
+
+    def _weights_key(self):
+        return tuple((t.data_ptr(), t._version) for t in self._tensors)
+
+    def _check_weights(self):
+        """Drop every captured graph when a parameter or buffer changed since capture."""
+        key = self._weights_key()
+        if key != self._wkey:
+            self._graphs.clear()
+            self._tensors = list(self.g.parameters()) + list(self.g.buffers())
+            self._wkey = self._weights_key()
 
     def _capture(self, B):
         dev = self.device
@@ -70,6 +89,12 @@ class GraphedGenerator:
         """B faces from fresh latents z ~ N(0, 1) and cameras drawn by
         generate_camera_params(resolution, **camera_kw) -- eval.py's whole
         per-image loop body -- with the draws inside the graph as well."""
+        for k, v in camera_kw.items():
+            if isinstance(v, torch.Tensor):
+                raise TypeError(f"random_faces: camera_kw[{k!r}] is a tensor; a graph freezes "
+                                "it -- pass plain numbers (or call the graphed forward with "
+                                "explicit cameras)")
+        self._check_weights()
         key = ("random", B, resolution, tuple(sorted(camera_kw.items())))
         if key not in self._graphs:
             from .camera import generate_camera_params
@@ -99,10 +124,12 @@ class GraphedGenerator:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             out = fwd()
+        self._wkey = self._weights_key()          # caches as packed by the warm-up calls
         return graph, out
 
     def __call__(self, z, cam_poses, focals, near, far):
         B = z.shape[0]
+        self._check_weights()
         if B not in self._graphs:
             self._graphs[B] = self._capture(B)
         graph, static, out = self._graphs[B]

@@ -315,7 +315,12 @@ class VolumeFeatureRenderer(nn.Module):
                             -(self.j - self.out_im_res * .5) / focal,
                             -torch.ones_like(self.i).expand(focal.shape[0], self.out_im_res,
                                                             self.out_im_res)], -1)
-        rays_d = torch.sum(dirs[..., None, :] * c2w[:, None, None, :3, :3], -1)
+        # torch.sum over the 3-wide last dim (sdf_model.py:213) as its explicit
+        # left-to-right form: what torch-CPU computes, and the same on every device
+        # (a GPU reduction may round differently, which the 4096-resolution hash
+        # level turns into different cells; tests pin it against the golden rays)
+        prod = dirs[..., None, :] * c2w[:, None, None, :3, :3]
+        rays_d = prod[..., 0] + prod[..., 1] + prod[..., 2]
         rays_o = c2w[:, None, None, :3, -1].expand(rays_d.shape)
         viewdirs = dirs if self.static_viewdirs else rays_d
         return rays_o, rays_d, viewdirs
@@ -416,7 +421,7 @@ class VolumeFeatureRenderer(nn.Module):
         return self.render_rays(rays, styles=styles, return_eikonal=return_eikonal,
                                 t_rand=t_rand)
 
-    def mlp_init_pass(self, cam_poses, focal, near, far, styles=None):
+    def mlp_init_pass(self, cam_poses, focal, near, far, styles=None, t_rand=None):
         rays_o, rays_d, viewdirs = self.get_rays(focal, cam_poses)
         viewdirs = viewdirs / torch.norm(viewdirs, dim=-1, keepdim=True)
         near = near.unsqueeze(-1) * torch.ones_like(rays_d[..., :1])
@@ -425,7 +430,9 @@ class VolumeFeatureRenderer(nn.Module):
         mids = .5 * (z_vals[..., 1:] + z_vals[..., :-1])
         upper = torch.cat([mids, z_vals[..., -1:]], -1)
         lower = torch.cat([z_vals[..., :1], mids], -1)
-        t_rand = self._draw_t_rand(z_vals.shape, z_vals.device)
+        if t_rand is None:
+            t_rand = self._draw_t_rand(z_vals.shape, z_vals.device)
+        t_rand = t_rand.to(z_vals.device).reshape(z_vals.shape)
         z_vals = lower + (upper - lower) * t_rand
         pts = rays_o.unsqueeze(3) + rays_d.unsqueeze(3) * z_vals.unsqueeze(-1)
         normalized_pts = pts * 2 / ((far - near).unsqueeze(3)) if self.z_normalize else pts

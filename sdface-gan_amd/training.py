@@ -156,10 +156,14 @@ def requires_grad(params, flag=True):
 
 @torch.no_grad()
 def accumulate(model1, model2, decay=0.999):
+    """EMA of model2's parameters into model1 (sdf_utils.py:64-69).  The update runs
+    on the parameters themselves (not ``.data``), so it bumps their version
+    counters: the fused decoder's packed-weight caches and GraphedGenerator key on
+    (data_ptr, version) and must see every EMA step."""
     par1 = dict(model1.named_parameters())
     par2 = dict(model2.named_parameters())
     for k in par1.keys():
-        par1[k].data.mul_(decay).add_(par2[k].data, alpha=1 - decay)
+        par1[k].mul_(decay).add_(par2[k].detach(), alpha=1 - decay)
 
 
 def make_noise(batch, latent_dim, n_noise, device):
@@ -316,7 +320,11 @@ class FullPipelineTrainer:
         self.g_module.zero_grad(set_to_none=True)
         loss["g"] = g_gan_loss
 
-        # --- path length regularisation (training_utils.py:744-776)
+        # --- path length regularisation (training_utils.py:744-776).  As the reference,
+        # every pass of the chunk loop runs the WHOLE path batch (its loop index is
+        # unused, :760-763): path_batch / chunk passes on the same latents and
+        # cameras (fresh decoder noise each), gradients and the path-length EMA
+        # accumulated over them.
         path_loss = torch.zeros((), device=dev)
         path_lengths = torch.zeros((), device=dev)
         if t.g_reg_every > 0 and i % t.g_reg_every == 0:
@@ -326,9 +334,7 @@ class FullPipelineTrainer:
             for j in range(0, pbs, chunk):
                 last = j + chunk >= pbs
                 with self._sync(self.generator, last):
-                    img, latents = self.generator([n[j:j + chunk] for n in noise],
-                                                  cam[j:j + chunk], focal[j:j + chunk],
-                                                  near[j:j + chunk], far[j:j + chunk],
+                    img, latents = self.generator(noise, cam, focal, near, far,
                                                   return_latents=True)
                     path_loss, self.mean_path_length, path_lengths = g_path_regularize(
                         img, latents, self.mean_path_length)

@@ -136,9 +136,14 @@ def _install_encoders():
         if dy_dx is not None:
             dy_dx.copy_(torch.from_numpy(dd))
 
+    def sh_encode_backward(grad, inputs, B, D, C, dy_dx, grad_inputs):
+        gi = oracle.sh_encode_backward(_t2n(grad), _t2n(inputs), C, _t2n(dy_dx))
+        grad_inputs.copy_(torch.from_numpy(gi))
+
     _stub("_gridencoder", grid_encode_forward=grid_encode_forward,
           grid_encode_backward=grid_encode_backward)
-    _stub("_shencoder", sh_encode_forward=sh_encode_forward)
+    _stub("_shencoder", sh_encode_forward=sh_encode_forward,
+          sh_encode_backward=sh_encode_backward)
 
 
 def import_reference():
@@ -227,8 +232,10 @@ def case_camera(sdf_utils):
         ext, focal, near, far, vp = sdf_utils.generate_camera_params(64, "cpu", batch=5, **kw)
         for k, v in zip(["ext", "focal", "near", "far", "vp"], [ext, focal, near, far, vp]):
             res[f"{name}_{k}"] = _t2n(v)
-    locs = torch.tensor([[0., 0.], [0.3, -0.1], [-0.45, 0.2]])
-    ext, focal, near, far, vp = sdf_utils.generate_camera_params(128, "cpu", batch=3, locations=locs)
+    # the last two rows look straight down / up: the degenerate-axis fix (:151-154)
+    locs = torch.tensor([[0., 0.], [0.3, -0.1], [-0.45, 0.2], [0.2, np.pi / 2],
+                         [-0.1, -np.pi / 2]])
+    ext, focal, near, far, vp = sdf_utils.generate_camera_params(128, "cpu", batch=5, locations=locs)
     for k, v in zip(["ext", "focal", "near", "far", "vp"], [ext, focal, near, far, vp]):
         res[f"loc_{k}"] = _t2n(v)
     res["loc_locations"] = _t2n(locs)
@@ -236,10 +243,12 @@ def case_camera(sdf_utils):
     print("camera.npz")
 
 
-def _generator(sdf_model, sdf_utils, size=256, res=64, n_samples=24, full_pipeline=True, **rk):
+def _generator(sdf_model, sdf_utils, size=256, res=64, n_samples=24, full_pipeline=True,
+               table_amp=1.0, train_renderer=False, **rk):
     opt = make_opts(sdf_utils, size=size, n_samples=n_samples, res=res, **rk)
+    opt.model.freeze_renderer = not train_renderer
     g = sdf_model.Generator(opt.model, opt.rendering, full_pipeline=full_pipeline)
-    W.det_init_(g)
+    W.det_init_(g, table_amp=table_amp)
     g.eval()
     return g, opt
 
@@ -249,9 +258,10 @@ def _cams(sdf_utils, B, res, seed):
     return sdf_utils.generate_camera_params(res, "cpu", batch=B)
 
 
-def case_render(sdf_model, sdf_utils, name, B, res, n_samples, intermediates, seed, **rk):
+def case_render(sdf_model, sdf_utils, name, B, res, n_samples, intermediates, seed, table_amp=1.0,
+                **rk):
     g, opt = _generator(sdf_model, sdf_utils, res=res, n_samples=n_samples, full_pipeline=False,
-                        **rk)
+                        table_amp=table_amp, **rk)
     ext, focal, near, far, vp = _cams(sdf_utils, B, res, seed)
     torch.manual_seed(seed + 1)
     z = torch.randn(B, 256)
@@ -264,7 +274,7 @@ def case_render(sdf_model, sdf_utils, name, B, res, n_samples, intermediates, se
     d = dict(z=_t2n(z), ext=_t2n(ext), focal=_t2n(focal), near=_t2n(near), far=_t2n(far),
              latent=_t2n(latent), t_rand=t_rand, rgb=_t2n(rgb),
              render_opts=np.array(repr(dict(opt.rendering))), res=np.int64(res),
-             n_samples=np.int64(n_samples))
+             n_samples=np.int64(n_samples), table_amp=np.float64(table_amp))
     if feat is not None:
         d["features"] = _t2n(feat)
     if sdf is not None:
@@ -339,6 +349,98 @@ def case_siren(sdf_model, sdf_utils):
     print("state_dict_keys_siren.npz", len(shapes), "keys")
 
 
+def case_table_scales(sdf_model, sdf_utils):
+    """The hash table at the reference's own init scale U(-1e-4, 1e-4) (grid.py:138-140)
+    and at a trained-like U(-0.05, 0.05): the operand scales the split-fp16 field
+    kernel meets in practice (the other fixtures use U(-1, 1) to expose index errors)."""
+    for tag, amp in (("tab1e4", 1e-4), ("tab05", 0.05)):
+        case_render(sdf_model, sdf_utils, f"render_small_{tag}", B=2, res=8, n_samples=24,
+                    intermediates=False, seed=111, table_amp=amp)
+        case_render(sdf_model, sdf_utils, f"render_face64_{tag}", B=1, res=64, n_samples=24,
+                    intermediates=False, seed=141, table_amp=amp)
+
+
+def _stage1_generator(sdf_model, sdf_utils, res, n_samples, table_amp=1.0, **rk):
+    """Stage-1 configuration (training_utils.py:150-161): renderer trained, sdf returned
+    (min_surf_lambda > 0), no feature output, Generator(full_pipeline=False)."""
+    return _generator(sdf_model, sdf_utils, res=res, n_samples=n_samples, full_pipeline=False,
+                      table_amp=table_amp, train_renderer=True, no_features_output=True,
+                      return_sdf=True, **rk)
+
+
+def case_eikonal(sdf_model, sdf_utils):
+    """Stage-1 forward with return_sdf / return_eikonal (training_utils.py:411-413): the
+    eikonal term d sdf / d pts (sdf_model.py:224-229) through the grid encoder's
+    dy_dx (grid.py:44-52), plus the gradients a stage-1 style loss sends into the
+    network.  Reference semantics: the custom backward writes grad_inputs through the
+    CUDA op, outside autograd, so the eikonal term is a constant (requires_grad False)
+    and the eikonal loss reaches no parameter."""
+    res, N, B = 8, 24, 2
+    g, opt = _stage1_generator(sdf_model, sdf_utils, res, N, table_amp=0.05)
+    ext, focal, near, far, vp = _cams(sdf_utils, B, res, 91)
+    torch.manual_seed(92)
+    z = torch.randn(B, 256)
+    torch.manual_seed(93)
+    with _RandRecorder() as rr:
+        _, thumb, sdf, eik = g([z], ext, focal, near, far, return_sdf=True,
+                               return_eikonal=True)
+    eik_loss = ((eik.norm(dim=-1) - 1) ** 2).mean()
+    surf = torch.exp(-100 * torch.abs(sdf)).mean()
+    loss = thumb.mean() + surf + (eik_loss if eik_loss.requires_grad else 0)
+    loss.backward()
+    net = g.renderer.network
+    n_dense = int(net.encoder.offsets[2])                  # levels 0-1: dense rows
+    np.savez_compressed(
+        OUT / "eikonal.npz", z=_t2n(z), ext=_t2n(ext), focal=_t2n(focal), near=_t2n(near),
+        far=_t2n(far), t_rand=_t2n(rr.draws[0]), thumb=_t2n(thumb), sdf=_t2n(sdf),
+        eikonal=_t2n(eik), eik_requires_grad=np.bool_(eik.requires_grad),
+        eik_loss=np.float64(eik_loss.item()),
+        grad_sigma_w=_t2n(net.sigma_linear.weight.grad),
+        grad_input_w=_t2n(net.input_linear.weight.grad),
+        grad_beta=_t2n(g.renderer.sigmoid_beta.grad),
+        grad_table_dense=_t2n(net.encoder.embeddings.grad[:n_dense]),
+        res=np.int64(res), n_samples=np.int64(N), table_amp=np.float64(0.05))
+    print("eikonal.npz", tuple(eik.shape), "eik requires_grad:", eik.requires_grad)
+
+
+def case_init_pass(sdf_model, sdf_utils):
+    """Sphere initialisation (training_utils.py:287-317): Generator.init_forward ->
+    mlp_init_pass (sdf_model.py:380-409, 1156-1161) with its stratified torch.rand
+    draw captured, and the L1 loss's gradients."""
+    res, N, B = 8, 24, 3
+    g, opt = _stage1_generator(sdf_model, sdf_utils, res, N, table_amp=0.05)
+    ext, focal, near, far, vp = _cams(sdf_utils, B, res, 95)
+    torch.manual_seed(96)
+    z = torch.randn(B, 256)
+    torch.manual_seed(97)
+    with _RandRecorder() as rr:
+        sdf, target = g.init_forward([z], ext, focal, near, far)
+    loss = torch.nn.functional.l1_loss(sdf, target)
+    loss.backward()
+    net = g.renderer.network
+    np.savez_compressed(
+        OUT / "init_pass.npz", z=_t2n(z), ext=_t2n(ext), focal=_t2n(focal), near=_t2n(near),
+        far=_t2n(far), t_rand=_t2n(rr.draws[0]), sdf=_t2n(sdf), target=_t2n(target),
+        loss=np.float64(loss.item()), grad_sigma_w=_t2n(net.sigma_linear.weight.grad),
+        grad_input_w=_t2n(net.input_linear.weight.grad),
+        res=np.int64(res), n_samples=np.int64(N), table_amp=np.float64(0.05))
+    print("init_pass.npz", tuple(sdf.shape), f"loss {loss.item():.5f}")
+
+
+def case_fc(sdf_model, sdf_utils):
+    """rendering.fc = 1 with type 'sdf': the positional-encoding ReLU MLP FCGenerator
+    (sdf_model.py:197-200, 1599-1670), 100 % reference code on CPU."""
+    case_render(sdf_model, sdf_utils, "render_fc_small", B=2, res=8, n_samples=24,
+                intermediates=False, seed=151, type="sdf", fc=1, return_sdf=True,
+                return_xyz=True)
+    g, _ = _generator(sdf_model, sdf_utils, res=8, n_samples=24, full_pipeline=False, type="sdf",
+                      fc=1)
+    sd = g.state_dict()
+    shapes = np.array([repr((k, tuple(sd[k].shape))) for k in sorted(sd)])
+    np.savez_compressed(OUT / "state_dict_keys_fc.npz", entries=shapes)
+    print("state_dict_keys_fc.npz", len(shapes), "keys")
+
+
 def case_generator(sdf_model, sdf_utils):
     g, opt = _generator(sdf_model, sdf_utils, size=256, res=64, n_samples=24)
     ext, focal, near, far, vp = _cams(sdf_utils, 1, 64, 31)
@@ -392,8 +494,12 @@ def case_init_stats(sdf_model, sdf_utils):
 def main():
     sdf_model, sdf_utils = import_reference()
     if len(sys.argv) > 1:                       # selected cases only, e.g. `mesh`
+        import inspect
         for name in sys.argv[1:]:
-            globals()[f"case_{name}"](sdf_model, sdf_utils)
+            fn = globals()[f"case_{name}"]
+            args = (sdf_model, sdf_utils)
+            n = len(inspect.signature(fn).parameters)
+            fn(*args[2 - n:] if n else ())
         return
     case_init_stats(sdf_model, sdf_utils)
     case_encoders()
@@ -408,6 +514,10 @@ def main():
     case_generator(sdf_model, sdf_utils)
     case_mesh(sdf_model, sdf_utils)
     case_siren(sdf_model, sdf_utils)
+    case_table_scales(sdf_model, sdf_utils)
+    case_eikonal(sdf_model, sdf_utils)
+    case_init_pass(sdf_model, sdf_utils)
+    case_fc(sdf_model, sdf_utils)
 
 
 if __name__ == "__main__":

@@ -5,7 +5,9 @@ SURVEY.md §8b) gets U[lo,hi) values from ``oracle.det_uniform`` (an integer
 hash of the flat index, so identical on any host) with ranges that follow the
 reference's own init scales (sdf_model.py:23-69, 437-466, 541-701, grid.py:136-140),
 except the hash table, which uses U(-1,1) so index errors cannot hide behind
-the reference's tiny U(-1e-4,1e-4) init.
+the reference's tiny U(-1e-4,1e-4) init.  ``table_amp`` selects another table
+amplitude: the reference's own init scale (1e-4) and a trained-like one (0.05)
+pin the split-fp16 field kernel at the operand scales it meets in practice.
 """
 from __future__ import annotations
 
@@ -24,8 +26,8 @@ def name_seed(name: str) -> int:
     return zlib.crc32(name.encode()) & 0x7FFFFFFF
 
 
-def det_table(rows, cols, seed=7):
-    return det_uniform((rows, cols), -1.0, 1.0, seed)
+def det_table(rows, cols, seed=7, amp=1.0):
+    return det_uniform((rows, cols), -amp, amp, seed)
 
 
 def _u(std):
@@ -79,7 +81,7 @@ def init_range(name: str, shape):
 
 
 @torch.no_grad()
-def det_init_(module: torch.nn.Module):
+def det_init_(module: torch.nn.Module, table_amp=1.0):
     sd = module.state_dict()
     for name in sorted(sd.keys()):
         t = sd[name]
@@ -89,14 +91,14 @@ def det_init_(module: torch.nn.Module):
         if rng is None:
             continue
         if name.endswith("encoder.embeddings"):
-            v = det_table(t.shape[0], t.shape[1], seed=7)
+            v = det_table(t.shape[0], t.shape[1], seed=7, amp=table_amp)
         else:
             v = det_uniform(tuple(t.shape), rng[0], rng[1], name_seed(name))
         t.copy_(torch.from_numpy(v).reshape(t.shape))
     return module
 
 
-def det_state_dict(entries, prefix=""):
+def det_state_dict(entries, prefix="", table_amp=1.0):
     """Build {name: tensor} for (name, shape) entries without any module.
 
     Keys whose value is fixed at construction get it here: the grid offsets
@@ -113,7 +115,7 @@ def det_state_dict(entries, prefix=""):
         elif name.endswith("sigmoid_beta"):
             sd[name] = torch.full(tuple(shape), 0.1)
         elif name.endswith("encoder.embeddings"):
-            sd[name] = torch.from_numpy(det_table(shape[0], shape[1], seed=7))
+            sd[name] = torch.from_numpy(det_table(shape[0], shape[1], seed=7, amp=table_amp))
         else:
             rng = init_range(name, tuple(shape))
             if rng is None:
@@ -123,9 +125,13 @@ def det_state_dict(entries, prefix=""):
     return sd
 
 
-def golden_entries(golden_dir, siren=False):
+def golden_entries(golden_dir, siren=False, kind=None):
     """(name, shape) of the reference Generator's state dict: the ngp one, or with
-    siren=True the SirenGenerator renderer's (full_pipeline=False)."""
+    siren=True / kind="siren" the SirenGenerator renderer's, kind="fc" the
+    FCGenerator renderer's (both full_pipeline=False)."""
     import ast
-    z = np.load(golden_dir / ("state_dict_keys_siren.npz" if siren else "state_dict_keys.npz"))
+    kind = kind or ("siren" if siren else "ngp")
+    fname = {"ngp": "state_dict_keys.npz", "siren": "state_dict_keys_siren.npz",
+             "fc": "state_dict_keys_fc.npz"}[kind]
+    z = np.load(golden_dir / fname)
     return [ast.literal_eval(str(e)) for e in z["entries"]]

@@ -315,3 +315,59 @@ def test_decoder_fused_equals_module_path(sdfr, conv_impl, fuse):
     _record[f"decoder_fused_vs_module_scale_{tag}"] = scale
     _close(f"decoder_fused_vs_module_{tag}", fused.cpu(), mod.cpu(), 1e-4 * max(1.0, scale),
            1e-5 * max(1.0, scale))
+
+
+def test_ema_accumulate_invalidates_fused_caches(sdfr):
+    """training.accumulate (the EMA step, sdf_utils.py:64-69) bumps the parameters'
+    versions, so the fused decoder's packed-weight / modulation / demodulation
+    caches are rebuilt: after an EMA step the fused image equals the module path's
+    on the NEW weights (not the first call's)."""
+    from importlib import import_module
+    training = import_module(sdfr.Generator.__module__.rsplit(".", 1)[0] + ".training")
+    opt = sdfr.vol_render_opt()
+    torch.manual_seed(0)
+    g_ema = sdfr.Generator(opt.model, opt.rendering, ema=True).to(DEV).eval()
+    torch.manual_seed(1)
+    g = sdfr.Generator(opt.model, opt.rendering).to(DEV)
+    B = 2
+    feats = torch.randn(B, 256, 64, 64, device=DEV)
+    z = [torch.randn(B, 256, device=DEV)]
+    noise = [torch.randn(B, 1, 2 ** r, 2 ** r, device=DEV) for r in (6, 7, 7, 8, 8)]
+    dec = g_ema.decoder
+    with torch.no_grad():
+        first, _ = dec(feats, z, noise=noise)                  # fills the caches
+        training.accumulate(g_ema, g, 0.5)
+        fused, _ = dec(feats, z, noise=noise)
+        dec.use_fused = False
+        mod, _ = dec(feats, z, noise=noise)
+        dec.use_fused = True
+    assert not torch.equal(first, fused)
+    scale = float(mod.abs().max())
+    _close("ema_fused_vs_module", fused.cpu(), mod.cpu(), 1e-4 * max(1.0, scale))
+
+
+def test_graphed_generator_recaptures_after_weight_update(sdfr):
+    """GraphedGenerator keys its graphs on every tensor's (data_ptr, version): after an
+    in-place weight update the replay equals the eager forward on the new weights."""
+    dev = torch.device("cuda", 0)
+    opt = sdfr.vol_render_opt()
+    torch.manual_seed(5)
+    g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
+    g.renderer.rng_device = "device"
+    gg = sdfr.GraphedGenerator(g)
+    z = torch.randn(2, 256, device=dev)
+    cam, focal, near, far, _ = sdfr.generate_camera_params(64, dev, batch=2)
+    gg(z, cam, focal, near, far)
+    with torch.no_grad():
+        for p in g.decoder.parameters():
+            p.mul_(0.9)
+        g.renderer.network.views_linears.weight.mul_(1.1)
+    gg(z, cam, focal, near, far)                      # re-captures (warm-up draws)
+    torch.cuda.manual_seed(7)
+    got, _ = gg(z, cam, focal, near, far)
+    torch.cuda.manual_seed(7)
+    with torch.no_grad():
+        ref, _ = g([z], cam, focal, near, far)
+    assert torch.equal(got, ref)
+    with pytest.raises(TypeError, match="tensor"):
+        gg.random_faces(1, 64, locations=torch.zeros(1, 2, device=dev))

@@ -145,6 +145,23 @@ def test_device_sin_accuracy(sdfr):
     assert (hw.cpu().double() - ref).abs().max() < 1e-6
 
 
+def test_device_sin_rev_accuracy(sdfr):
+    """The split-fp16 field kernel's FiLM sin: argument in revolutions (1/(2 pi) folded
+    into gamma / beta), v_fract_f32 + v_sin_f32.  Against float64 sin(2 pi u) over the
+    FiLM range (|gamma x + beta| <= 200 rad, i.e. |u| <= 32) and far beyond it (|u| up
+    to 4096, where the exact fract keeps the hardware sin in its domain)."""
+    lib = sdfr._lib
+    gen = torch.Generator().manual_seed(1)
+    for span, tol in ((64.0, 1e-6), (8192.0, 1e-6)):
+        us = ((torch.rand(1 << 20, dtype=torch.float64, generator=gen) - 0.5) * span).float()
+        ud = us.to(DEV)
+        out = torch.empty_like(ud)
+        lib.check(lib.lib().sdfr_debug_sin_rev_probe(lib.ptr(ud), lib.ptr(out), ud.numel(),
+                                                     lib.stream_of(ud)), "sin_rev probe")
+        ref = torch.sin(2 * np.pi * us.double())
+        assert (out.cpu().double() - ref).abs().max() < tol, span
+
+
 def test_grid_backward_large_privatised_levels(sdfr, oracle_mod, table):
     """200 k samples in the renderer's coordinate range: the coarse levels'
     gradients go through the LDS-privatised kernel (one global add per row and

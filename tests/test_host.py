@@ -1,4 +1,5 @@
 """CPU: the C-ABI library, the drop-in module surface and the PyTorch parts."""
+import ast
 import ctypes
 import re
 from pathlib import Path
@@ -102,8 +103,8 @@ def test_camera_matches_reference(sdfr, golden_dir):
         out = sdfr.generate_camera_params(64, "cpu", batch=5, **kw)
         for k, v in zip(["ext", "focal", "near", "far", "vp"], out):
             np.testing.assert_array_equal(v.numpy(), g[f"{name}_{k}"], err_msg=f"{name}_{k}")
-    out = sdfr.generate_camera_params(128, "cpu", batch=3,
-                                      locations=torch.from_numpy(g["loc_locations"]))
+    locs = torch.from_numpy(g["loc_locations"])
+    out = sdfr.generate_camera_params(128, "cpu", batch=locs.shape[0], locations=locs)
     for k, v in zip(["ext", "focal", "near", "far", "vp"], out):
         np.testing.assert_array_equal(v.numpy(), g[f"loc_{k}"])
 
@@ -186,3 +187,50 @@ def test_graphed_generator_rejects_cpu(sdfr):
     g = sdfr.Generator(opt.model, opt.rendering).eval()
     with pytest.raises(RuntimeError, match="on a GPU"):
         sdfr.GraphedGenerator(g)
+
+
+def test_get_rays_bit_exact_vs_reference(sdfr, golden_dir):
+    """get_rays' rays_d as the explicit left-to-right sum equals the reference's
+    torch.sum (sdf_model.py:213) on CPU, bit for bit (the GPU test repeats it on cuda)."""
+    g = np.load(golden_dir / "render_small.npz")
+    opt = sdfr.vol_render_opt()
+    ren = sdfr.VolumeFeatureRenderer(opt.rendering, style_dim=256, out_im_res=int(g["res"]))
+    _, rays_d, viewdirs = ren.get_rays(torch.from_numpy(g["focal"]), torch.from_numpy(g["ext"]))
+    np.testing.assert_array_equal(rays_d.numpy(), g["rays_d"])
+    vd = viewdirs / torch.norm(viewdirs, dim=-1, keepdim=True)
+    np.testing.assert_array_equal(vd.numpy(), g["viewdirs"])
+
+
+def _golden_renderer(sdfr, golden_dir, name, kind):
+    g = np.load(golden_dir / f"{name}.npz")
+    opt = sdfr.vol_render_opt(ngp=kind == "ngp", fc=kind == "fc")
+    r = opt.rendering
+    r.N_samples = int(g["n_samples"])
+    for k, v in ast.literal_eval(str(g["render_opts"])).items():   # the fixture's options
+        if k in ("return_sdf", "return_xyz", "static_viewdirs", "force_background", "perturb"):
+            r[k] = v
+    ren = sdfr.VolumeFeatureRenderer(r, style_dim=256, out_im_res=int(g["res"]))
+    amp = float(g["table_amp"]) if "table_amp" in g.files else 1.0
+    sd = W.det_state_dict(W.golden_entries(golden_dir, kind=kind), "renderer.", table_amp=amp)
+    ren.load_state_dict({k[len("renderer."):]: v for k, v in sd.items()}, strict=True)
+    return g, ren.eval()
+
+
+def test_fc_state_dict_matches_reference(sdfr, golden_dir):
+    opt = sdfr.vol_render_opt(ngp=False, fc=True)
+    g = sdfr.Generator(opt.model, opt.rendering, full_pipeline=False)
+    mine = {k: tuple(v.shape) for k, v in g.state_dict().items()}
+    assert mine == dict(W.golden_entries(golden_dir, kind="fc"))
+
+
+def test_fc_renderer_matches_reference_cpu(sdfr, golden_dir):
+    """rendering.fc = 1 (FCGenerator, sdf_model.py:1599-1670): the drop-in renderer on
+    CPU runs the reference's torch ops in the reference's order."""
+    g, ren = _golden_renderer(sdfr, golden_dir, "render_fc_small", "fc")
+    assert isinstance(ren.network, sdfr.FCGenerator)
+    t = lambda k: torch.from_numpy(g[k])  # noqa: E731
+    with torch.no_grad():
+        rgb, feat, sdf, mask, xyz, _ = ren(t("ext"), t("focal"), t("near"), t("far"),
+                                           styles=t("latent"), t_rand=t("t_rand"))
+    for k, v in dict(rgb=rgb, features=feat, sdf=sdf, xyz=xyz, mask=mask).items():
+        np.testing.assert_allclose(v.numpy(), g[k], rtol=0, atol=1e-6, err_msg=k)

@@ -138,7 +138,8 @@ def test_ray_sampling_bit_exact(oracle_mod, golden_dir, name):
 
 def _render(oracle_mod, golden_dir, name, **kw):
     g = np.load(golden_dir / f"{name}.npz")
-    sd = W.det_state_dict(W.golden_entries(golden_dir), "renderer.")
+    amp = float(g["table_amp"]) if "table_amp" in g.files else 1.0
+    sd = W.det_state_dict(W.golden_entries(golden_dir), "renderer.", table_amp=amp)
     tr = g["t_rand"] if g["t_rand"].size else None
     out = oracle_mod.render_ngp(sd, g["ext"], g["focal"], g["near"], g["far"], g["latent"],
                                 N=int(g["n_samples"]), res=int(g["res"]), t_rand=tr,
@@ -150,6 +151,9 @@ def _render(oracle_mod, golden_dir, name, **kw):
     ("render_small", {}),
     ("render_mesh_opts", dict(static_viewdirs=True, force_background=True)),
     ("render_face64", {}),
+    # the reference's table init scale U(-1e-4, 1e-4) and a trained-like U(-0.05, 0.05)
+    ("render_small_tab1e4", {}), ("render_small_tab05", {}),
+    ("render_face64_tab1e4", {}), ("render_face64_tab05", {}),
 ])
 def test_renderer_restatement_matches_reference(oracle_mod, golden_dir, name, kw):
     g, out = _render(oracle_mod, golden_dir, name, **kw)
