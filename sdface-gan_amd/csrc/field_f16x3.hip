@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "render_ngp.h"
 
@@ -954,6 +955,505 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
     }
 }
 
+// ----------------------------------------------------------------------------
+// field_x2_kernel: two waves per SIMD.
+//
+// field_x_kernel runs ONE wave per SIMD (472 VGPR+AGPR: two 16-ray sample
+// columns of accumulators in and out of a layer), so every LDS / barrier /
+// dependency latency of the wave is exposed and its VALU issues at the
+// single-wave rate (4 cycles per instruction).  Here a workgroup is 8 waves, two
+// per SIMD, each with ONE sample column of MFMA N = 16 = 8 rays x 2 samples
+// (lanes n < 8: sample 2p of ray n, lanes n >= 8: sample 2p+1 of ray n-8), half
+// the accumulators (<= 256 registers), so one wave's MFMAs run while its partner
+// waits or issues VALU.  Each A fragment now feeds 3 MFMAs instead of 6 (twice
+// the LDS read traffic per MFMA, 2 ds_read_b128 per 48 MFMA cycles per SIMD).
+// The two samples of a ray meet in the compositing through one DPP row rotation
+// (ror 8) per exchanged value; the transmittance chain, weights and sums are
+// formed in the same order in both lanes (sample 2p, then 2p+1), the feature
+// accumulator of a ray (8 KB per wave in LDS) is updated by the sample-2p lane.
+// The workgroup still covers 4 tiles of 16 rays of ONE face (wave w: tile w & 3,
+// rays 8 (w >> 2) .. +7), so the grid, the sample-segment split and the partial
+// layout are those of field_x_kernel.
+// ----------------------------------------------------------------------------
+constexpr int kWaves2 = 8;
+constexpr int kThreads2 = kWaves2 * 64;
+constexpr int kXStage2 = kXSliceF4 / kThreads2;     // float4 staged per thread per half-slice
+
+__device__ __forceinline__ float ror8(float v) {   // lane n <- lane (n + 8) mod 16 of its row
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+}
+
+struct XRing2 {
+    f4 *lds;
+    f4 st[2 * kXStage2];  // ngp: the next K-step (both halves); siren: st[0..kXStage2)
+    f4 pre_h, pre_l;      // first (hi, lo) A fragment of the current slice
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t it, tid;
+};
+
+// One half k-step of one sample column: 8 output tiles x 3 split terms = 24
+// MFMAs, term-major so each accumulator is touched every 8th MFMA; then `side`,
+// the ring staging and the slice barrier (as xstep).
+template <int V, class Net, int H, class Side>
+__device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, const f4 bl,
+                                       Side &&side) {
+    constexpr bool kS2 = Net::kSlice2;
+    const uint32_t lane = R.tid & 63u;
+    const f4 *A = kS2 ? R.lds + ((R.it >> 1) & 1u) * (2 * kXSliceF4) + H * kXSliceF4 + lane
+                      : R.lds + (R.it % 3u) * kXSliceF4 + lane;
+    // A fragments in groups of two tiles, the next group's LDS reads issued ahead of
+    // the current group's 6 MFMAs (32 registers of fragments, not 64)
+    f4 ah[8], al[8];
+    auto load = [&](int i) {
+        if constexpr ((V & 2) != 0) {
+            ah[i] = bh * (float)(i + 1);
+            al[i] = bl * (float)(i + 1);
+        } else if ((kS2 ? H == 1 : true) && i == 0) {
+            ah[0] = R.pre_h;
+            al[0] = R.pre_l;
+        } else {
+            ah[i] = A[(2 * i) * 64];
+            al[i] = A[(2 * i + 1) * 64];
+        }
+    };
+    load(0);
+    load(1);
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+        if (grp < 3) {
+            load(2 * grp + 2);
+            load(2 * grp + 3);
+        }
+        const int i0 = 2 * grp, i1 = 2 * grp + 1;
+        acc[8 * H + i0] = mfma16(al[i0], bh, acc[8 * H + i0]);
+        acc[8 * H + i1] = mfma16(al[i1], bh, acc[8 * H + i1]);
+        acc[8 * H + i0] = mfma16(ah[i0], bl, acc[8 * H + i0]);
+        acc[8 * H + i1] = mfma16(ah[i1], bl, acc[8 * H + i1]);
+        acc[8 * H + i0] = mfma16(ah[i0], bh, acc[8 * H + i0]);
+        acc[8 * H + i1] = mfma16(ah[i1], bh, acc[8 * H + i1]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    side();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((V & 4) != 0) {
+        if constexpr ((V & 1) == 0) __builtin_amdgcn_s_barrier();
+    } else if constexpr (kS2) {
+        const uint32_t fs = R.it >> 1;
+        f4 *wl = R.lds + ((fs + 1u) & 1u) * (2 * kXSliceF4) + H * kXSliceF4;
+#pragma unroll
+        for (int i = 0; i < kXStage2; ++i) wl[R.tid + i * kThreads2] = R.st[H * kXStage2 + i];
+        const uint32_t pf = (2u * fs + 4u + H) % Net::kSlices;
+#pragma unroll
+        for (int i = 0; i < kXStage2; ++i)
+            R.st[H * kXStage2 + i] = __builtin_bit_cast(
+                f4, __builtin_amdgcn_raw_buffer_load_b128(
+                        R.rsrc, (int)((R.tid + i * kThreads2) * sizeof(f4)),
+                        (int)(pf * kXSliceF4 * sizeof(f4)), 0));
+        if constexpr (H == 0) {
+            if constexpr ((V & 2) == 0) {
+                R.pre_h = A[kXSliceF4];
+                R.pre_l = A[kXSliceF4 + 64];
+            }
+        } else if constexpr ((V & 1) == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+    } else {
+        const uint32_t wslot = (R.it + 2u) % 3u;
+#pragma unroll
+        for (int i = 0; i < kXStage2; ++i) R.lds[wslot * kXSliceF4 + R.tid + i * kThreads2] = R.st[i];
+        const uint32_t pf = (R.it + 3u) % Net::kSlices;
+#pragma unroll
+        for (int i = 0; i < kXStage2; ++i)
+            R.st[i] = __builtin_bit_cast(
+                f4, __builtin_amdgcn_raw_buffer_load_b128(
+                        R.rsrc, (int)((R.tid + i * kThreads2) * sizeof(f4)),
+                        (int)(pf * kXSliceF4 * sizeof(f4)), 0));
+        if constexpr ((V & 2) == 0) {
+            const f4 *An = R.lds + ((R.it + 1u) % 3u) * kXSliceF4 + lane;
+            R.pre_h = An[0];
+            R.pre_l = An[64];
+        }
+        if constexpr ((V & 1) == 0) {
+            asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+    ++R.it;
+}
+
+template <int V, class Net, class ActIn, class ActOut>
+__device__ __forceinline__ void dense_layer2(XRing2 &R, f4 (&in)[16], f4 (&out)[16],
+                                             ActIn &&act_in, ActOut &&act_out) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int qn = q < 7 ? q + 1 : 7;
+        xstep2<V, Net, 0>(R, out, in[2 * q], in[2 * q + 1], [&] {
+            if (q < 7) act_in(in[2 * qn], in[2 * qn + 1], qn);
+        });
+        xstep2<V, Net, 1>(R, out, in[2 * q], in[2 * q + 1], [&] {
+            if (q == 7) act_out(out[0], out[1], 0);
+        });
+    }
+}
+
+struct NoAct2 {
+    __device__ __forceinline__ void operator()(f4 &, f4 &, int) const {}
+};
+
+template <int V, class Net>
+__global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs a) {
+    constexpr int NL = Net::kLayers, NF = Net::kFilmN;
+    __shared__ f4 ring_lds[(Net::kSlice2 ? 4 : 3) * kXSliceF4];   // 64 / 48 KB weight ring
+    __shared__ float cst[(NL + 5) * kW];                   // bias_s[NL] (ngp layer 0 unscaled), 1/su0, sigma_w, rgb_w[3]
+    __shared__ float film_lds[NF * 2 * kW];                // the workgroup's face
+    __shared__ f4 facc_lds[kWaves2][16 * 32];              // 64 KB: [tile][g][ray8] feature sums
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t n = lane & 15u, g = lane >> 4, r8 = n & 7u;
+    const bool colB = n >= 8u;                             // sample 2p+1 of the pair
+    const GeomArgs &G = a.g;
+
+    const uint32_t wg_per_face = (G.tiles_per_face + kWaves - 1) / kWaves;
+    const uint32_t seg = blockIdx.x % a.nseg, blk = blockIdx.x / a.nseg;
+    const uint32_t b = blk / wg_per_face;
+    uint32_t tile_local = (blk % wg_per_face) * kWaves + (wave & 3u);
+    const bool tile_ok = tile_local < G.tiles_per_face;
+    if (!tile_ok) tile_local = G.tiles_per_face - 1;
+    const uint32_t tile = b * G.tiles_per_face + tile_local;
+    const uint32_t ray_in_tile = 8u * (wave >> 2) + r8;
+    uint32_t ray_local = tile_local * kTileRays + ray_in_tile;
+    const bool ray_ok = tile_ok && ray_local < G.H * G.W;
+    if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
+    const uint32_t py = ray_local / G.W, px = ray_local % G.W;
+    const uint32_t ray_index = (b * G.H + py) * G.W + px;
+
+    Ray ray;
+    make_ray(G.cam + (size_t)b * 12, G.focal[b], G.pix_x[px], G.pix_y[py], G.half_res, ray);
+    const float nr = G.near_[b], fr = G.far_[b];
+    const float span = __fsub_rn(fr, nr);
+    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
+    f4 vxh, vxl;
+    {
+        const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
+        const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
+        const float v2 = G.static_viewdirs ? ray.dir[2] : ray.d[2];
+        const float vn = norm3_torch(v0, v1, v2);
+        const float ux = __fdiv_rn(v0, vn), uy = __fdiv_rn(v1, vn), uz = __fdiv_rn(v2, vn);
+        float v[8];
+        if constexpr (Net::kSiren) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = 0.0f;
+            if (g == 0) {
+                v[0] = ux;
+                v[1] = uy;
+                v[2] = uz;
+            }
+        } else {
+            const f4 qa = sh_quad(ux, uy, uz, (2 * g) & 3), qb = sh_quad(ux, uy, uz, (2 * g + 1) & 3);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = g < 2 ? qa[r] : 0.0f;
+                v[4 + r] = g < 2 ? qb[r] : 0.0f;
+            }
+        }
+        split8(v, vxh, vxl);
+    }
+    const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
+    {
+        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * NF * 2 * kW);
+        f4 *dst = reinterpret_cast<f4 *>(film_lds);
+        for (uint32_t i = tid; i < NF * 2 * kW / 4; i += kThreads2) dst[i] = src[i];
+    }
+    XRing2 R;
+    R.lds = ring_lds;
+    R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<f4 *>(a.packed), 0,
+                                               (int)(Net::kSlices * kXSliceF4 * sizeof(f4)),
+                                               0x00020000);
+    R.tid = tid;
+    R.it = 0;
+    for (uint32_t i = tid; i < (NL + 5) * kW; i += kThreads2) {
+        float v;
+        if (i < NL * kW) v = a.bias_s[i];
+        else if (i < (NL + 1) * kW) v = __fdiv_rn(1.0f, a.su[i - NL * kW]);
+        else if (i < (NL + 2) * kW) v = a.sigma_w[i - (NL + 1) * kW];
+        else v = a.rgb_w[i - (NL + 2) * kW];
+        cst[i] = v;
+    }
+    if constexpr (Net::kSlice2) {
+        // prologue: K-step 0 (half-slices 0, 1) -> slot 0; K-step 1 -> registers
+#pragma unroll
+        for (int i = 0; i < 2 * kXStage2; ++i) R.lds[tid + i * kThreads2] = a.packed[tid + i * kThreads2];
+#pragma unroll
+        for (int i = 0; i < 2 * kXStage2; ++i)
+            R.st[i] = a.packed[2 * kXSliceF4 + tid + i * kThreads2];
+    } else {
+        // prologue: slices 0, 1 -> slots 0, 1; slice 2 -> registers
+#pragma unroll
+        for (int i = 0; i < 2 * kXStage2; ++i) R.lds[tid + i * kThreads2] = a.packed[tid + i * kThreads2];
+#pragma unroll
+        for (int i = 0; i < kXStage2; ++i) R.st[i] = a.packed[2 * kXSliceF4 + tid + i * kThreads2];
+    }
+    f4 *facc = facc_lds[wave];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) facc[t * 64 + lane] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    __syncthreads();
+    R.pre_h = R.lds[lane];
+    R.pre_l = R.lds[64 + lane];
+
+    float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
+    float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
+    const float *bias_l = cst;
+    const float *inv_su0 = cst + NL * kW;
+    const float *sig_w = cst + (NL + 1) * kW, *rgb_w = cst + (NL + 2) * kW;
+    auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
+    auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
+    const float sig_b = a.sigma_b[0];
+    const float rgb_b0 = a.rgb_b[0], rgb_b1 = a.rgb_b[1], rgb_b2 = a.rgb_b[2];
+
+    const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
+    const size_t tile_sid = (size_t)(tile * G.N) * kTileRays + ray_in_tile;
+    float2 en[4];
+    auto load_inputs = [&](uint32_t s0) {
+        uint32_t s = s0 + (colB ? 1u : 0u);
+        if (s >= G.N) s = G.N - 1;
+        if constexpr (Net::kSiren) {
+            const float z = sample_z(G.sc, nr, fr, ray_index, s);
+            float np_[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));
+                np_[k] = G.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;
+            }
+            const bool g0 = g == 0;
+            en[0] = make_float2(g0 ? np_[0] : 0.0f, g0 ? np_[1] : 0.0f);
+            en[1] = make_float2(g0 ? np_[2] : 0.0f, 0.0f);
+            en[2] = make_float2(0.0f, 0.0f);
+            en[3] = make_float2(0.0f, 0.0f);
+        } else {
+            const size_t sid = tile_sid + (size_t)s * kTileRays;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) en[c] = enc2[(4 * g + c) * (size_t)G.S_total + sid];
+        }
+    };
+    const uint32_t npass = (G.N + 1) / 2;
+    const uint32_t pps = (npass + a.nseg - 1) / a.nseg;
+    const uint32_t p_begin = seg * pps, p_end = min(npass, p_begin + pps);
+    load_inputs(2 * p_begin);
+
+    for (uint32_t p = p_begin; p < p_end; ++p) {
+        f4 X[16], Y[16];
+        f4 eh, el;
+        int es = 0;
+        {
+            float v[8];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                v[2 * c] = en[c].x;
+                v[2 * c + 1] = en[c].y;
+            }
+            if constexpr (!Net::kSiren) es = feat_scale(v);
+            split8(v, eh, el);
+        }
+        float sdfp = 0.0f;
+        auto act_film = [&](int f) {
+            return [&, f](f4 &za, f4 &zb, int q) {
+                float dummy = 0.0f;
+                act_pair<1, V>(za, zb, q, fg(f), fb(f), nullptr, dummy, g);
+            };
+        };
+        auto act_sdf = [&](int f) {
+            return [&, f](f4 &za, f4 &zb, int q) {
+                act_pair<2, V>(za, zb, q, fg(f), fb(f), sig_w, sdfp, g);
+            };
+        };
+        auto act_l0 = [&](f4 &za, f4 &zb, int q) {
+            if constexpr (Net::kSiren) {
+                act_film(0)(za, zb, q);
+            } else {
+                float dummy = 0.0f;
+                act_pair<0, V>(za, zb, q, inv_su0, bias_l, nullptr, dummy, g, es);
+            }
+        };
+
+        if constexpr (Net::kSiren) init_acc(X, bias_l, g);
+        else zero_acc(X);
+        xstep2<V, Net, 0>(R, X, eh, el, [] {});
+        xstep2<V, Net, 1>(R, X, eh, el, [&] { act_l0(X[0], X[1], 0); });
+        if constexpr (Net::kSiren) {
+            init_acc(Y, bias_l + 1 * kW, g);
+            dense_layer2<V, Net>(R, X, Y, act_l0, act_film(1));
+            for (int l = 2; l < 6; l += 2) {
+                init_acc(X, bias_l + l * kW, g);
+                dense_layer2<V, Net>(R, Y, X, act_film(l - 1), act_film(l));
+                init_acc(Y, bias_l + (l + 1) * kW, g);
+                dense_layer2<V, Net>(R, X, Y, act_film(l), act_film(l + 1));
+            }
+            init_acc(X, bias_l + 6 * kW, g);
+            dense_layer2<V, Net>(R, Y, X, act_film(5), act_film(6));
+            init_acc(Y, bias_l + 7 * kW, g);
+            dense_layer2<V, Net>(R, X, Y, act_film(6), act_sdf(7));
+        } else {
+            init_acc(Y, bias_l + kW, g);
+            dense_layer2<V, Net>(R, X, Y, act_l0, act_film(0));
+            init_acc(X, bias_l + 2 * kW, g);
+            dense_layer2<V, Net>(R, Y, X, act_film(0), act_film(1));
+            init_acc(Y, bias_l + 3 * kW, g);
+            dense_layer2<V, Net>(R, X, Y, act_film(1), act_sdf(2));
+        }
+        init_acc(X, bias_l + (NL - 1) * kW, g);
+        dense_layer2<V, Net>(R, Y, X, act_sdf(NF - 2), NoAct2{});
+        xstep2<V, Net, 0>(R, X, vxh, vxl, [] {});
+        xstep2<V, Net, 1>(R, X, vxh, vxl, [] {});
+
+        if (p + 1 < p_end) load_inputs(2 * p + 2);
+        if constexpr ((V & 16) != 0) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) racc0 += (X[t][0] + X[t][1]) + (X[t][2] + X[t][3]);
+            racc0 += sdfp;
+            continue;
+        }
+        // compositing of the pass's two samples (this lane's s = 2p + colB), front to back
+        const uint32_t s = 2 * p + (colB ? 1u : 0u);
+        const bool s_ok = s < G.N;
+        const uint32_t sc_ = s_ok ? s : G.N - 1;
+        const float sdf = __fadd_rn(group_sum(sdfp), sig_b);
+        const float z = sample_z(G.sc, nr, fr, ray_index, sc_);
+        const float dist = (sc_ + 1 < G.N)
+                               ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), z),
+                                           dnorm)
+                               : __fmul_rn(1e10f, dnorm);
+        float alpha;
+        if (a.with_sdf) {
+            const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
+            alpha = 1.0f - expf(-sig * dist);
+        } else {
+            float raw = sdf;
+            if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
+            const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+            alpha = 1.0f - expf(-sp * dist);
+        }
+        if (!s_ok) alpha = 0.0f;
+        // the pair's weights, identically in both lanes (sample 2p, then 2p+1)
+        const float alpha_o = ror8(alpha);
+        const float aA = colB ? alpha_o : alpha, aB = colB ? alpha : alpha_o;
+        const bool lastA = 2 * p + 1 == G.N, lastB = 2 * p + 2 == G.N;
+        float wA = aA * T;
+        if (a.force_background && lastA) wA = 1.0f - wsum;
+        T = T * ((1.0f - aA) + 1e-10f);
+        wsum += wA;
+        float wB = aB * T;
+        if (a.force_background && lastB) wB = 1.0f - wsum;
+        if (2 * p + 1 < G.N) {
+            T = T * ((1.0f - aB) + 1e-10f);
+            wsum += wB;
+        } else {
+            wB = 0.0f;
+        }
+        // colour features f = sin(gamma_v x + beta_v); rgb_linear
+        const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
+        float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int f0 = 16 * t + 4 * (int)g;
+            const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
+            const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
+            const f4 w0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
+            const f4 w1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
+            const f4 w2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
+            f4 fv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                fv[r] = sin_rev(__fmaf_rn(gm[r], X[t][r], bt[r]));
+                p0 = __fmaf_rn(fv[r], w0[r], p0);
+                p1 = __fmaf_rn(fv[r], w1[r], p1);
+                p2 = __fmaf_rn(fv[r], w2[r], p2);
+            }
+            X[t] = fv;
+        }
+        const float q0 = sigmoidf_(__fadd_rn(group_sum(p0), rgb_b0));
+        const float q1 = sigmoidf_(__fadd_rn(group_sum(p1), rgb_b1));
+        const float q2 = sigmoidf_(__fadd_rn(group_sum(p2), rgb_b2));
+        const float o0 = ror8(q0), o1 = ror8(q1), o2 = ror8(q2);
+        racc0 = __fmaf_rn(wB, colB ? q0 : o0, __fmaf_rn(wA, colB ? o0 : q0, racc0));
+        racc1 = __fmaf_rn(wB, colB ? q1 : o1, __fmaf_rn(wA, colB ? o1 : q1, racc1));
+        racc2 = __fmaf_rn(wB, colB ? q2 : o2, __fmaf_rn(wA, colB ? o2 : q2, racc2));
+        w_last = (2 * p + 1 < G.N) ? wB : wA;
+        if (a.xyz) {
+            const float zo = ror8(z);
+            const float zA = colB ? zo : z, zB = colB ? z : zo;
+            xacc0 = __fmaf_rn(wB, __fadd_rn(ray.o[0], __fmul_rn(ray.d[0], zB)),
+                              __fmaf_rn(wA, __fadd_rn(ray.o[0], __fmul_rn(ray.d[0], zA)), xacc0));
+            xacc1 = __fmaf_rn(wB, __fadd_rn(ray.o[1], __fmul_rn(ray.d[1], zB)),
+                              __fmaf_rn(wA, __fadd_rn(ray.o[1], __fmul_rn(ray.d[1], zA)), xacc1));
+            xacc2 = __fmaf_rn(wB, __fadd_rn(ray.o[2], __fmul_rn(ray.d[2], zB)),
+                              __fmaf_rn(wA, __fadd_rn(ray.o[2], __fmul_rn(ray.d[2], zA)), xacc2));
+        }
+        if (a.features) {
+            // facc += wA fA + wB fB (in that order) by the sample-2p lane of the ray
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                f4 ob;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ob[r] = ror8(X[t][r]);
+                if (!colB) {
+                    f4 v = facc[(t * 4 + g) * 8 + r8];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = __fmaf_rn(wB, ob[r], __fmaf_rn(wA, X[t][r], v[r]));
+                    facc[(t * 4 + g) * 8 + r8] = v;
+                }
+            }
+        }
+        if (a.sdf && ray_ok && g == 0 && s_ok) a.sdf[(size_t)ray_index * G.N + s] = sdf;
+    }
+    if (!ray_ok || colB) return;
+    if (a.nseg > 1) {
+        const size_t Rr = (size_t)G.total_tiles * kTileRays;
+        float *pp = a.part + (size_t)seg * kPartQ * Rr + (size_t)tile * kTileRays + ray_in_tile;
+        if (a.features) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const uint32_t jf = 16 * t + 4 * g;
+                const f4 v = facc[(t * 4 + g) * 8 + r8];
+                pp[(size_t)(jf + 0) * Rr] = v.x;
+                pp[(size_t)(jf + 1) * Rr] = v.y;
+                pp[(size_t)(jf + 2) * Rr] = v.z;
+                pp[(size_t)(jf + 3) * Rr] = v.w;
+            }
+        }
+        if (g == 0) {
+            const float q[8] = {racc0, racc1, racc2, xacc0, xacc1, xacc2, T, w_last};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pp[(size_t)(kW + k) * Rr] = q[k];
+        }
+        return;
+    }
+    const size_t HW = (size_t)G.H * G.W;
+    const size_t pix = (size_t)py * G.W + px;
+    if (g < 3) {
+        const float rc = g == 0 ? racc0 : (g == 1 ? racc1 : racc2);
+        a.rgb[((size_t)b * 3 + g) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, rc));
+        if (a.xyz) {
+            const float xc = g == 0 ? xacc0 : (g == 1 ? xacc1 : xacc2);
+            a.xyz[((size_t)b * 3 + g) * HW + pix] = xc;
+        }
+    } else if (a.mask) {
+        a.mask[(size_t)b * HW + pix] = w_last;
+    }
+    if (a.features) {
+        float *fbp = a.features + (size_t)b * kW * HW + pix;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t jf = 16 * t + 4 * g;
+            const f4 v = facc[(t * 4 + g) * 8 + r8];
+            fbp[(size_t)(jf + 0) * HW] = v.x;
+            fbp[(size_t)(jf + 1) * HW] = v.y;
+            fbp[(size_t)(jf + 2) * HW] = v.z;
+            fbp[(size_t)(jf + 3) * HW] = v.w;
+        }
+    }
+}
+
 // Chains the nseg segment partials of every ray (see kPartQ): one thread per
 // (ray, quantity), quantities on grid.y.
 __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
@@ -988,6 +1488,17 @@ __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
 // ----------------------------------------------------------------------------
 // host
 // ----------------------------------------------------------------------------
+// field kernel generation: 2 = field_x2_kernel (two waves per SIMD, default),
+// 1 = field_x_kernel (one wave per SIMD); SDFR_FIELD_KERNEL=1 selects the latter
+// (A/B timing only)
+static int field_kernel_gen() {
+    static const int gen = [] {
+        const char *e = std::getenv("SDFR_FIELD_KERNEL");
+        return (e && e[0] == '1') ? 1 : 2;
+    }();
+    return gen;
+}
+
 static uint32_t g_field_split_max = 4;
 void set_field_split_max(uint32_t m) { g_field_split_max = m; }
 
@@ -1089,7 +1600,26 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background) : 1;
     f.part = part;
     const uint32_t blocks = g.B * ((g.tiles_per_face + kWaves - 1) / kWaves) * f.nseg;
-    switch (field_variant()) {
+    if (field_kernel_gen() == 2) {
+        switch (field_variant()) {
+#ifdef SDFR_ABLATION
+#define SDFR_X2FIELD_CASE(V)                                                                   \
+    case V:                                                                                    \
+        hipLaunchKernelGGL((field_x2_kernel<V, Net>), dim3(blocks), dim3(kThreads2), 0, st, f); \
+        break;
+            SDFR_X2FIELD_CASE(1)
+            SDFR_X2FIELD_CASE(2)
+            SDFR_X2FIELD_CASE(4)
+            SDFR_X2FIELD_CASE(8)
+            SDFR_X2FIELD_CASE(16)
+            SDFR_X2FIELD_CASE(31)
+#undef SDFR_X2FIELD_CASE
+#endif
+            default:
+                hipLaunchKernelGGL((field_x2_kernel<0, Net>), dim3(blocks), dim3(kThreads2), 0, st,
+                                   f);
+        }
+    } else switch (field_variant()) {
 #ifdef SDFR_ABLATION
 #define SDFR_XFIELD_CASE(V)                                                                  \
     case V:                                                                                  \

@@ -257,6 +257,9 @@ class FullPipelineTrainer:
         self.mean_path_length = 0.0
         self.accum = 0.5 ** (32 / (10 * 1000))
         self.iteration = 0
+        # decoder noise drawn per forward as the reference (True), or the decoder's
+        # fixed noise buffers (False: reproducible gradients, tests)
+        self.randomize_noise = True
 
     def _cams(self, n):
         c = self.opt.camera
@@ -269,28 +272,26 @@ class FullPipelineTrainer:
         """no_sync() for every chunk but the last: one all-reduce per optimizer step."""
         return nullcontext() if last or not hasattr(model, "no_sync") else model.no_sync()
 
-    def step(self, real_imgs):
-        t, dev = self.t, self.device
-        i = self.iteration
-        style_dim = self.opt.model.style_dim
+    def d_backward(self, noise, cams, real_imgs, d_regularize):
+        """The discriminator half-step's gradients (training_utils.py:661-712): over
+        the batch in chunks, the fake images from the frozen-path generator, the
+        logistic loss and (every d_reg_every) R1, accumulated locally and
+        all-reduced once, on the last chunk.  Returns the last chunk's terms."""
+        t = self.t
         batch, chunk = real_imgs.shape[0], t.chunk
-        loss = {}
-
-        # --- discriminator (training_utils.py:652-716)
+        cam, focal, near, far = cams[:4]
         requires_grad(self.g_train, False)
         requires_grad(self.d_module.parameters(), True)
         self.d_module.zero_grad(set_to_none=True)
-        d_regularize = i % t.d_reg_every == 0
-        noise = mixing_noise(batch, style_dim, t.mixing, dev)
-        cam, focal, near, far, _ = self._cams(batch)
-        r1_loss = torch.zeros((), device=dev)
+        r1_loss = torch.zeros((), device=real_imgs.device)
         for j in range(0, batch, chunk):
             last = j + chunk >= batch
             with self._sync(self.discriminator, last):
                 with torch.no_grad():
                     gen_imgs, _ = self.g_module([n[j:j + chunk] for n in noise], cam[j:j + chunk],
                                                 focal[j:j + chunk], near[j:j + chunk],
-                                                far[j:j + chunk])
+                                                far[j:j + chunk],
+                                                randomize_noise=self.randomize_noise)
                 real = real_imgs[j:j + chunk].detach().requires_grad_(d_regularize)
                 fake_pred = self.discriminator(gen_imgs)
                 real_pred = self.discriminator(real)
@@ -300,22 +301,47 @@ class FullPipelineTrainer:
                 else:
                     r1_loss = torch.zeros_like(r1_loss)
                 (d_gan_loss + r1_loss).backward()
+        return d_gan_loss, r1_loss, real_pred, fake_pred
+
+    def g_backward(self, chunk_inputs, n_chunks):
+        """The generator half-step's gradients (training_utils.py:717-742): per chunk
+        (noise, cameras) from ``chunk_inputs`` -- drawn lazily by step() so the RNG
+        order is the reference's -- the non-saturating loss plus 0.001 x L1 to the
+        4x nearest-upsampled thumbnail; one all-reduce on the last chunk."""
+        requires_grad(self.g_train, True)
+        requires_grad(self.d_module.parameters(), False)
+        for k, (noise, cams) in enumerate(chunk_inputs):
+            cam, focal, near, far = cams[:4]
+            with self._sync(self.generator, k == n_chunks - 1):
+                fake_img, fake_thumb = self.generator(noise, cam, focal, near, far,
+                                                      randomize_noise=self.randomize_noise)
+                fake_up = F.interpolate(fake_thumb, scale_factor=4)   # nn.Upsample(4), nearest
+                g_gan_loss = g_nonsaturating_loss(self.d_module(fake_img))
+                (g_gan_loss + 0.001 * g_content_loss(fake_img, fake_up)).backward()
+        return g_gan_loss
+
+    def step(self, real_imgs):
+        t, dev = self.t, self.device
+        i = self.iteration
+        style_dim = self.opt.model.style_dim
+        batch, chunk = real_imgs.shape[0], t.chunk
+        loss = {}
+
+        # --- discriminator (training_utils.py:652-716)
+        d_regularize = i % t.d_reg_every == 0
+        noise = mixing_noise(batch, style_dim, t.mixing, dev)
+        cams = self._cams(batch)
+        d_gan_loss, r1_loss, real_pred, fake_pred = self.d_backward(noise, cams, real_imgs,
+                                                                    d_regularize)
         self.optimizer_d.step()
         loss.update(d=d_gan_loss, real_score=real_pred.mean(), fake_score=fake_pred.mean(),
                     r1=r1_loss.mean())
 
         # --- generator (training_utils.py:717-742)
-        requires_grad(self.g_train, True)
-        requires_grad(self.d_module.parameters(), False)
-        for j in range(0, batch, chunk):
-            last = j + chunk >= batch
-            with self._sync(self.generator, last):
-                noise = mixing_noise(chunk, style_dim, t.mixing, dev)
-                cam, focal, near, far, _ = self._cams(chunk)
-                fake_img, fake_thumb = self.generator(noise, cam, focal, near, far)
-                fake_up = F.interpolate(fake_thumb, scale_factor=4)   # nn.Upsample(4), nearest
-                g_gan_loss = g_nonsaturating_loss(self.d_module(fake_img))
-                (g_gan_loss + 0.001 * g_content_loss(fake_img, fake_up)).backward()
+        n_chunks = len(range(0, batch, chunk))
+        inputs = ((mixing_noise(chunk, style_dim, t.mixing, dev), self._cams(chunk))
+                  for _ in range(n_chunks))
+        g_gan_loss = self.g_backward(inputs, n_chunks)
         self.optimizer.step()
         self.g_module.zero_grad(set_to_none=True)
         loss["g"] = g_gan_loss
@@ -335,7 +361,8 @@ class FullPipelineTrainer:
                 last = j + chunk >= pbs
                 with self._sync(self.generator, last):
                     img, latents = self.generator(noise, cam, focal, near, far,
-                                                  return_latents=True)
+                                                  return_latents=True,
+                                                  randomize_noise=self.randomize_noise)
                     path_loss, self.mean_path_length, path_lengths = g_path_regularize(
                         img, latents, self.mean_path_length)
                     w = t.path_regularize * t.g_reg_every * path_loss
@@ -553,6 +580,8 @@ class RendererTrainer:
                                       uniform=c.uniform, azim_range=c.azim, elev_range=c.elev,
                                       fov_ang=c.fov, dist_radius=c.dist_radius)
 
+    _sync = staticmethod(FullPipelineTrainer._sync)
+
     def sphere_init_step(self, batch=3):
         """MLP init to a sphere SDF (training_utils.py:287-317): L1(sdf, |x| - r)."""
         noise = mixing_noise(batch, self.t.style_dim, self.t.mixing, self.device)
@@ -565,20 +594,17 @@ class RendererTrainer:
         self.g_module.zero_grad(set_to_none=True)
         return loss.detach()
 
-    def step(self, real_imgs):
-        t, dev = self.t, self.device
+    def d_backward(self, noise, cams, real_imgs):
+        """The discriminator half-step's gradients (training_utils.py:346-389): fake
+        thumbnails generated in chunks, then ONE discriminator pass over the batch
+        (logistic loss + R1 + viewpoint regression), all-reduced by DDP."""
+        t = self.t
         batch, chunk = real_imgs.shape[0], t.chunk
-        view = t.view_lambda > 0
-        with_sdf = getattr(t, "with_sdf", True)
-        zero = torch.zeros((), device=dev)
-        loss = {}
-
-        # --- discriminator (training_utils.py:336-394)
+        zero = torch.zeros((), device=real_imgs.device)
+        cam, focal, near, far, gt_view = cams
         requires_grad(self.g_module.parameters(), False)
         requires_grad(self.d_module.parameters(), True)
         self.d_module.zero_grad(set_to_none=True)
-        noise = mixing_noise(batch, t.style_dim, t.mixing, dev)
-        cam, focal, near, far, gt_view = self._cams(batch)
         gen = []
         for j in range(0, batch, chunk):
             _, fake = self.g_module([n[j:j + chunk] for n in noise], cam[j:j + chunk],
@@ -586,44 +612,33 @@ class RendererTrainer:
             gen.append(fake)
         gen = torch.cat(gen, 0)
         fake_pred, fake_view_pred = self.discriminator(gen.detach())
+        view = t.view_lambda > 0
         d_view = t.view_lambda * viewpoints_loss(fake_view_pred, gt_view) if view else zero
         real = real_imgs.detach().requires_grad_(True)
         real_pred, _ = self.discriminator(real)
         d_gan = d_logistic_loss(real_pred, fake_pred)
         r1 = t.r1 * 0.5 * d_r1_loss(real_pred, real)
         (d_gan + r1 + d_view).backward()
+        return d_gan, r1, d_view, real_pred, fake_pred
+
+    def step(self, real_imgs):
+        t, dev = self.t, self.device
+        batch, chunk = real_imgs.shape[0], t.chunk
+        loss = {}
+
+        # --- discriminator (training_utils.py:336-394)
+        noise = mixing_noise(batch, t.style_dim, t.mixing, dev)
+        cams = self._cams(batch)
+        d_gan, r1, d_view, real_pred, fake_pred = self.d_backward(noise, cams, real_imgs)
         self.optimizer_d.step()
         loss.update(d=d_gan, r1=r1, d_view=d_view, real_score=real_pred.mean(),
                     fake_score=fake_pred.mean())
 
         # --- generator (training_utils.py:396-451)
-        requires_grad(self.g_module.parameters(), True)
-        requires_grad(self.d_module.parameters(), False)
-        eik_on, surf_on = with_sdf and t.eikonal_lambda > 0, t.min_surf_lambda > 0
-        g_view = g_eik = g_surf = g_smooth = zero
-        for j in range(0, batch, chunk):
-            noise = mixing_noise(chunk, t.style_dim, t.mixing, dev)
-            cam, focal, near, far, gt_view = self._cams(chunk)
-            out = self.generator(noise, cam, focal, near, far, return_sdf=surf_on,
-                                 return_eikonal=eik_on)
-            fake = out[1]
-            sdf = out[2] if surf_on else None
-            eik_term = out[2 + int(surf_on)] if eik_on else None
-            fake_pred, fake_view_pred = self.discriminator(fake)
-            if view:
-                g_view = t.view_lambda * viewpoints_loss(fake_view_pred, gt_view)
-            if eik_on:
-                g_eik, g_surf = eikonal_loss(eik_term, sdf=sdf, beta=t.min_surf_beta)
-                g_eik = t.eikonal_lambda * g_eik
-                if surf_on:
-                    g_surf = t.min_surf_lambda * g_surf
-                # fixed box of the reference (training_utils.py:433-436); only the
-                # hash-grid network has query_sdf (the reference raises for SIREN)
-                if hasattr(self.g_module.renderer.network, "query_sdf"):
-                    box = torch.tensor([[-1.0, 7.0], [-1.3, 3.7], [-1.7, 1.4]], device=dev)
-                    g_smooth = 1000 * smoothness(self.g_module, box, noise, dev)
-            g_gan = g_nonsaturating_loss(fake_pred)
-            (g_gan + g_view + g_eik + g_surf + g_smooth).backward()
+        n_chunks = len(range(0, batch, chunk))
+        inputs = ((mixing_noise(chunk, t.style_dim, t.mixing, dev), self._cams(chunk))
+                  for _ in range(n_chunks))
+        g_gan, g_view, g_eik, g_surf, g_smooth = self.g_backward(inputs, n_chunks)
         self.optimizer.step()
         self.g_module.zero_grad(set_to_none=True)
         loss.update(g=g_gan, g_view=g_view, g_eikonal=g_eik, g_minimal_surface=g_surf,
@@ -631,6 +646,43 @@ class RendererTrainer:
         accumulate(self.generator_test, self.g_module, self.accum)
         self.iteration += 1
         return reduce_loss_dict(loss)
+
+    def g_backward(self, chunk_inputs, n_chunks):
+        """The generator half-step's gradients (training_utils.py:396-440): per chunk
+        the adversarial, viewpoint, eikonal, minimal-surface and smoothness terms,
+        accumulated locally and all-reduced on the last chunk."""
+        t, dev = self.t, self.device
+        view = t.view_lambda > 0
+        with_sdf = getattr(t, "with_sdf", True)
+        zero = torch.zeros((), device=dev)
+        requires_grad(self.g_module.parameters(), True)
+        requires_grad(self.d_module.parameters(), False)
+        eik_on, surf_on = with_sdf and t.eikonal_lambda > 0, t.min_surf_lambda > 0
+        g_view = g_eik = g_surf = g_smooth = zero
+        for k, (noise, cams) in enumerate(chunk_inputs):
+            cam, focal, near, far, gt_view = cams
+            with self._sync(self.generator, k == n_chunks - 1):
+                out = self.generator(noise, cam, focal, near, far, return_sdf=surf_on,
+                                     return_eikonal=eik_on)
+                fake = out[1]
+                sdf = out[2] if surf_on else None
+                eik_term = out[2 + int(surf_on)] if eik_on else None
+                fake_pred, fake_view_pred = self.d_module(fake)
+                if view:
+                    g_view = t.view_lambda * viewpoints_loss(fake_view_pred, gt_view)
+                if eik_on:
+                    g_eik, g_surf = eikonal_loss(eik_term, sdf=sdf, beta=t.min_surf_beta)
+                    g_eik = t.eikonal_lambda * g_eik
+                    if surf_on:
+                        g_surf = t.min_surf_lambda * g_surf
+                    # fixed box of the reference (training_utils.py:433-436); only the
+                    # hash-grid network has query_sdf (the reference raises for SIREN)
+                    if hasattr(self.g_module.renderer.network, "query_sdf"):
+                        box = torch.tensor([[-1.0, 7.0], [-1.3, 3.7], [-1.7, 1.4]], device=dev)
+                        g_smooth = 1000 * smoothness(self.g_module, box, noise, dev)
+                g_gan = g_nonsaturating_loss(fake_pred)
+                (g_gan + g_view + g_eik + g_surf + g_smooth).backward()
+        return g_gan, g_view, g_eik, g_surf, g_smooth
 
     def state_dict(self):
         """{g, d, g_ema} as the reference's volume_renderer checkpoints."""
