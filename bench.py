@@ -62,14 +62,57 @@ def parse():
     return p.parse_args()
 
 
-def setup_dist(args):
+def setup_dist(args=None):
+    """One process per GPU (torchrun's RANK / LOCAL_RANK / WORLD_SIZE): backend "nccl"
+    (RCCL over xGMI).  SDFR_BENCH_BACKEND=gloo with SDFR_BENCH_SAME_DEVICE=1 runs the
+    same multi-rank path with every rank on cuda:0 (the world-2 test on a one-GPU
+    box, tests/test_gpu_train.py)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SDFR_BENCH_SAME_DEVICE") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("SDFR_BENCH_BACKEND", "nccl")
+        kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
     return world, rank, torch.device("cuda", local)
+
+
+def timed_steps(step, steps, world, device, before_step=None):
+    """The timed region: barrier + synchronize on both sides of exactly `steps`
+    steps; returns the MAX over ranks of the wall time (seconds)."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        if before_step is not None:
+            before_step(k)
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def host_info():
+    """Host CPU facts for the CPU baseline line: logical CPUs and the model name."""
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model}
 
 
 def build_generator(sdfr, device, seed, ngp=True):
@@ -108,9 +151,9 @@ def cpu_baseline(seconds, siren=False):
             if el >= seconds and faces >= 2:
                 break
     return {"value": faces / el, "unit": "faces/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "kind": "port", **host_info(),
             "sample": f"{faces} faces (64^2x24 oracle renderer + CPU decoder to 256^2), "
-                      f"1 face per call, {el:.1f}s"}
+                      f"1 face per call, {el:.1f}s; cores = torch intra-op threads used"}
 
 
 def extras(step, B, graphed_step, steps=10, warm=3):
@@ -169,22 +212,10 @@ def main():
             e.record()              # materialise the event handles before the timed loop
     torch.cuda.synchronize()
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
+    def set_events(k):
         g.renderer.stage_events = evs[k]
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_steps(step, args.steps, world, device, before_step=set_events)
     g.renderer.stage_events = None
-    if world > 1:
-        t = torch.tensor([elapsed], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     enc_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     field_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
@@ -194,8 +225,8 @@ def main():
     field_tflops = flop * samples / (field_ms * 1e-3) / 1e12
     gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9 if not siren else 0.0
     f16x3 = args.field_precision == "f16x3"
-    field_kernel = ("field_x_kernel<0, sdfr::SirenNet>" if siren else
-                    "field_x_kernel<0, sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
+    field_kernel = ("field_x2_kernel<0, sdfr::SirenNet>" if siren else
+                    "field_x2_kernel<0, sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
     def traffic_of(kernel):
         """HBM bytes per launch of `kernel` at this batch, from the committed
         rocprofv3 PMC passes (profiles/, scripts/summarize_profiles.py), or None."""

@@ -978,6 +978,28 @@ __global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a
 constexpr int kWaves2 = 8;
 constexpr int kThreads2 = kWaves2 * 64;
 constexpr int kXStage2 = kXSliceF4 / kThreads2;     // float4 staged per thread per half-slice
+// SDFR_X2_DMA: the weight ring is filled by LDS-DMA (buffer_load ... lds) into 4
+// half-slice slots, three half-steps ahead, one barrier per half-step (1), or
+// staged through registers + ds_write (0: ngp 2 whole-K-step slots, siren 3
+// half-slice slots).  The register path moves 32 KB per K-step through VGPRs and
+// the LDS store port (measured 16 % of the kernel by ablation).
+#ifndef SDFR_X2_DMA
+#define SDFR_X2_DMA 1
+#endif
+// SDFR_X2_STAGGER: waves 4-7 issue each half-step's register work (the next input
+// pair's activation) BEFORE their MFMAs, waves 0-3 after, so the two waves of a SIMD
+// enter every barrier interval with complementary work (matrix beside VALU)
+// instead of in lockstep (MI355X_MICROARCH.md, two waves per SIMD, item 9)
+#ifndef SDFR_X2_STAGGER
+#define SDFR_X2_STAGGER 0
+#endif
+// SDFR_X2_SIDE: the MFMA group (of 4, two tiles each) after which the register work
+// is issued when not staggered (4 = after all of them)
+#ifndef SDFR_X2_SIDE
+#define SDFR_X2_SIDE 4
+#endif
+constexpr int kX2DmaSlots = 4;
+constexpr int kX2DmaPieces = 16 / kWaves2;          // 1 KB pieces per wave per half-slice
 
 __device__ __forceinline__ float ror8(float v) {   // lane n <- lane (n + 8) mod 16 of its row
     return __builtin_bit_cast(
@@ -986,11 +1008,39 @@ __device__ __forceinline__ float ror8(float v) {   // lane n <- lane (n + 8) mod
 
 struct XRing2 {
     f4 *lds;
-    f4 st[2 * kXStage2];  // ngp: the next K-step (both halves); siren: st[0..kXStage2)
+    f4 st[2 * kXStage2];  // register path: ngp the next K-step (both halves), siren st[0..kXStage2)
     f4 pre_h, pre_l;      // first (hi, lo) A fragment of the current slice
     __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t it, tid;
+    v4i drsrc;            // the packed fragments for the LDS-DMA
+    uint32_t it, tid, wave;
+    bool late;            // waves 4-7 (SDFR_X2_STAGGER)
 };
+
+// One 1 KB LDS-DMA piece: source byte offset sbase + soff, LDS byte address lbase +
+// loff.  The two additions run inside the asm, so the compiler keeps only the
+// per-wave bases live (the constants are rematerialised at each use): with the
+// sums formed outside, the 68 distinct per-step addresses of an unrolled pass were
+// hoisted into SGPRs and spilled.
+__device__ __forceinline__ void dma16x(v4i rsrc, uint32_t voff, uint32_t sbase, uint32_t soff,
+                                       uint32_t lbase, uint32_t loff) {
+    uint32_t keep, so;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_add_u32 m0, %4, %5\n\ts_add_u32 %1, %6, %7\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %3, %1 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep), "=&s"(so)
+        : "v"(voff), "s"(rsrc), "s"(lbase), "s"(loff), "s"(sbase), "s"(soff)
+        : "memory", "scc");
+}
+
+// LDS-DMA of half-slice `slice` into ring slot `slot` (this wave's pieces)
+__device__ __forceinline__ void x2_dma(XRing2 &R, uint32_t slice, uint32_t slot) {
+    const uint32_t sbase = R.wave * (kX2DmaPieces * 1024u);
+    const uint32_t lbase = lds_addr(R.lds) + sbase;
+#pragma unroll
+    for (int k = 0; k < kX2DmaPieces; ++k)
+        dma16x(R.drsrc, (R.tid & 63u) * 16u, sbase, slice * kXSliceF4 * 16u + k * 1024u, lbase,
+               slot * kXSliceF4 * 16u + k * 1024u);
+}
 
 // One half k-step of one sample column: 8 output tiles x 3 split terms = 24
 // MFMAs, term-major so each accumulator is touched every 8th MFMA; then `side`,
@@ -998,10 +1048,14 @@ struct XRing2 {
 template <int V, class Net, int H, class Side>
 __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, const f4 bl,
                                        Side &&side) {
-    constexpr bool kS2 = Net::kSlice2;
+    constexpr bool kS2 = Net::kSlice2 && !SDFR_X2_DMA;
+    constexpr bool kDma = SDFR_X2_DMA;
     const uint32_t lane = R.tid & 63u;
-    const f4 *A = kS2 ? R.lds + ((R.it >> 1) & 1u) * (2 * kXSliceF4) + H * kXSliceF4 + lane
-                      : R.lds + (R.it % 3u) * kXSliceF4 + lane;
+    if constexpr (kDma && (V & 4) == 0)
+        x2_dma(R, (R.it + 3u) % Net::kSlices, (R.it + 3u) % kX2DmaSlots);
+    const f4 *A = kDma ? R.lds + (R.it % kX2DmaSlots) * kXSliceF4 + lane
+                : kS2  ? R.lds + ((R.it >> 1) & 1u) * (2 * kXSliceF4) + H * kXSliceF4 + lane
+                       : R.lds + (R.it % 3u) * kXSliceF4 + lane;
     // A fragments in groups of two tiles, the next group's LDS reads issued ahead of
     // the current group's 6 MFMAs (32 registers of fragments, not 64)
     f4 ah[8], al[8];
@@ -1009,7 +1063,7 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
         if constexpr ((V & 2) != 0) {
             ah[i] = bh * (float)(i + 1);
             al[i] = bl * (float)(i + 1);
-        } else if ((kS2 ? H == 1 : true) && i == 0) {
+        } else if (!kDma && (kS2 ? H == 1 : true) && i == 0) {
             ah[0] = R.pre_h;
             al[0] = R.pre_l;
         } else {
@@ -1017,6 +1071,9 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
             al[i] = A[(2 * i + 1) * 64];
         }
     };
+#if SDFR_X2_STAGGER
+    if (R.late) side();
+#endif
     load(0);
     load(1);
 #pragma unroll
@@ -1033,10 +1090,25 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
         acc[8 * H + i0] = mfma16(ah[i0], bh, acc[8 * H + i0]);
         acc[8 * H + i1] = mfma16(ah[i1], bh, acc[8 * H + i1]);
         __builtin_amdgcn_sched_barrier(0);
+#if !SDFR_X2_STAGGER && SDFR_X2_SIDE < 4
+        if (grp == SDFR_X2_SIDE) side();
+#endif
     }
+#if SDFR_X2_STAGGER
+    if (!R.late) side();
+#elif SDFR_X2_SIDE >= 4
     side();
+#endif
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr ((V & 4) != 0) {
+    if constexpr (kDma) {
+        // own pieces of half-slice it+1 (issued two half-steps ago) have landed; the
+        // barrier publishes every wave's (and closes this slot for the DMA of it+4)
+        if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kX2DmaPieces) : "memory");
+        if constexpr ((V & 1) == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+    } else if constexpr ((V & 4) != 0) {
         if constexpr ((V & 1) == 0) __builtin_amdgcn_s_barrier();
     } else if constexpr (kS2) {
         const uint32_t fs = R.it >> 1;
@@ -1105,7 +1177,7 @@ struct NoAct2 {
 template <int V, class Net>
 __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs a) {
     constexpr int NL = Net::kLayers, NF = Net::kFilmN;
-    __shared__ f4 ring_lds[(Net::kSlice2 ? 4 : 3) * kXSliceF4];   // 64 / 48 KB weight ring
+    __shared__ f4 ring_lds[(SDFR_X2_DMA ? kX2DmaSlots : (Net::kSlice2 ? 4 : 3)) * kXSliceF4];
     __shared__ float cst[(NL + 5) * kW];                   // bias_s[NL] (ngp layer 0 unscaled), 1/su0, sigma_w, rgb_w[3]
     __shared__ float film_lds[NF * 2 * kW];                // the workgroup's face
     __shared__ f4 facc_lds[kWaves2][16 * 32];              // 64 KB: [tile][g][ray8] feature sums
@@ -1171,6 +1243,9 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
                                                (int)(Net::kSlices * kXSliceF4 * sizeof(f4)),
                                                0x00020000);
     R.tid = tid;
+    R.wave = __builtin_amdgcn_readfirstlane(wave);
+    R.late = R.wave >= 4;
+    R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
     R.it = 0;
     for (uint32_t i = tid; i < (NL + 5) * kW; i += kThreads2) {
         float v;
@@ -1180,7 +1255,11 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
         else v = a.rgb_w[i - (NL + 2) * kW];
         cst[i] = v;
     }
-    if constexpr (Net::kSlice2) {
+    if constexpr (SDFR_X2_DMA) {
+        // prologue: half-slices 0-2 -> slots 0-2 (slice 3 is issued by the first step)
+        for (uint32_t k = 0; k < 3; ++k) x2_dma(R, k % Net::kSlices, k);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (Net::kSlice2) {
         // prologue: K-step 0 (half-slices 0, 1) -> slot 0; K-step 1 -> registers
 #pragma unroll
         for (int i = 0; i < 2 * kXStage2; ++i) R.lds[tid + i * kThreads2] = a.packed[tid + i * kThreads2];
@@ -1242,6 +1321,12 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
     load_inputs(2 * p_begin);
 
     for (uint32_t p = p_begin; p < p_end; ++p) {
+        // a pass consumes exactly Net::kSlices half-slices, a multiple of every ring's
+        // slot count (68 = 17 x 4 ngp, 132 = 44 x 3 siren): restarting the step counter
+        // keeps the slot cycle and makes every slot / slice index a compile-time constant
+        static_assert(Net::kSlices % kX2DmaSlots == 0 && Net::kSlices % 3 == (Net::kSiren ? 0 : 2),
+                      "ring slot cycle");
+        R.it = 0;
         f4 X[16], Y[16];
         f4 eh, el;
         int es = 0;
@@ -1406,6 +1491,10 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
         }
         if (a.sdf && ray_ok && g == 0 && s_ok) a.sdf[(size_t)ray_index * G.N + s] = sdf;
     }
+#if SDFR_X2_DMA
+    // the ring runs ahead across passes: no LDS-DMA may land after the workgroup ends
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     if (!ray_ok || colB) return;
     if (a.nseg > 1) {
         const size_t Rr = (size_t)G.total_tiles * kTileRays;

@@ -1,0 +1,122 @@
+"""Checkpoint layout, resume and stage gating (training_utils.py:197-226, 318-324,
+526-547, 555-606, 858-879; sdf_utils.py:382-401; train.py:69-89; eval.py:73-77),
+on CPU with the SIREN network (configs[4]'s renderer; the ngp encoders need the GPU)."""
+import random
+
+import pytest
+import torch
+
+
+def _stage2_opt(sdfr):
+    opt = sdfr.vol_render_opt(ngp=False, size=32, batch=2, chunk=1)
+    opt.model.renderer_spatial_output_dim = 8
+    opt.training.renderer_output_size = 8
+    opt.rendering.N_samples = 4
+    opt.training.d_reg_every = 2
+    opt.training.g_reg_every = 2
+    return opt
+
+
+def _stage1_opt(sdfr):
+    opt = sdfr.vol_render_opt(ngp=False, train_renderer=True, size=32, batch=2, chunk=1)
+    opt.model.renderer_spatial_output_dim = 8
+    opt.training.renderer_output_size = 8
+    opt.rendering.N_samples = 4
+    return opt
+
+
+def _loader(res, seed):
+    g = torch.Generator().manual_seed(seed)
+    while True:
+        yield torch.rand(2, 3, res, res, generator=g) * 2 - 1
+
+
+def _reseed(s):
+    torch.manual_seed(s)
+    random.seed(s)
+
+
+def test_get_ckpt_nums(sdfr, tmp_path):
+    from sdface_gan_amd import checkpoint as ck
+    assert ck.get_ckpt_nums(tmp_path / "missing") is None
+    assert ck.get_ckpt_nums(tmp_path) is None
+    for n in ("models_0001000.pt", "models_0000500.pt", "models_x.pt", "other_0002000.pt"):
+        (tmp_path / n).write_bytes(b"")
+    assert ck.get_ckpt_nums(tmp_path) == "1000"
+    p = ck.ckpt_path(tmp_path, "exp", 2, 42)
+    assert p == tmp_path / "exp" / "full_pipeline" / "models_0000042.pt"
+
+
+def test_stage2_save_resume_bit_identical(sdfr, tmp_path):
+    """Two uninterrupted iterations after a checkpoint == the same two iterations
+    after resuming from it in a fresh trainer (same RNG seed for the data draws)."""
+    from sdface_gan_amd import checkpoint as ck
+    from sdface_gan_amd.training import FullPipelineTrainer
+    opt = _stage2_opt(sdfr)
+    cpu = torch.device("cpu")
+    a = FullPipelineTrainer(opt, cpu, seed=3)
+    data = _loader(32, 0)
+    for _ in range(2):
+        a.step(next(data))
+    ck.save(ck.ckpt_path(tmp_path, "exp", 2, a.iteration - 1), a)
+    payload = ck.load_file(ck.ckpt_path(tmp_path, "exp", 2, 1))
+    assert {"g", "d", "g_ema", "g_optim", "d_optim"} <= set(payload)
+    tail = [next(data) for _ in range(2)]
+    _reseed(11)
+    for x in tail:
+        a.step(x)
+    b = FullPipelineTrainer(opt, cpu, seed=99)          # different init: the load must matter
+    assert ck.resume(b, tmp_path, "exp", 2) == 2
+    assert b.mean_path_length == payload["mean_path_length"]
+    _reseed(11)
+    for x in tail:
+        b.step(x)
+    for name, sa, sb in (("g", a.g_module, b.g_module), ("d", a.d_module, b.d_module),
+                         ("g_ema", a.generator_test, b.generator_test)):
+        for k, v in sa.state_dict().items():
+            assert torch.equal(v, sb.state_dict()[k]), f"{name}.{k}"
+    assert a.iteration == b.iteration == 4
+
+
+def test_load_size_matched(sdfr):
+    from sdface_gan_amd import checkpoint as ck
+    opt = _stage2_opt(sdfr)
+    g = sdfr.Generator(opt.model, opt.rendering)
+    sd = {k: v.clone() + 1 for k, v in g.state_dict().items()}
+    k0 = "renderer.network.rgb_linear.weight"
+    sd[k0] = torch.zeros(5, 5)                          # wrong shape: skipped
+    copied = ck.load_size_matched(g, sd)
+    assert k0 not in copied and len(copied) == len(sd) - 1
+    assert torch.equal(g.state_dict()["style.0.weight"], sd["style.0.weight"])
+
+
+def test_two_stage_pipeline_gating_and_files(sdfr, tmp_path):
+    """train.py's gating: stage 1 writes the sphere init, a periodic checkpoint and
+    vol_renderer.pt; stage 2 starts from vol_renderer.pt's g_ema (size-matched) and
+    writes full_pipeline.pt; then nothing is left to train."""
+    from sdface_gan_amd import checkpoint as ck
+    from sdface_gan_amd import pipeline
+    cpu = torch.device("cpu")
+    assert ck.stage_plan(tmp_path, "exp") == (True, True)
+    o1 = _stage1_opt(sdfr)
+    t1 = pipeline.train_vol_render(o1, "exp", _loader(8, 1), cpu, tmp_path, iters=2,
+                                   sphere_init_iters=1)
+    d = tmp_path / "exp"
+    assert (d / "sdf_init_models.pt").exists() and (d / "vol_renderer.pt").exists()
+    assert (d / "volume_renderer" / "models_0000000.pt").exists()     # i % 1000 == 0
+    assert ck.stage_plan(tmp_path, "exp") == (False, True)
+    assert ck.stage_plan(tmp_path, "exp", wod=True) == (False, True)
+    o2 = _stage2_opt(sdfr)
+    t2 = pipeline.train_full_pipeline(o2, "exp", _loader(32, 2), cpu, tmp_path, iters=1)
+    assert (d / "full_pipeline.pt").exists()
+    assert ck.stage_plan(tmp_path, "exp") == (False, False)
+    vol = ck.load_file(d / "vol_renderer.pt")["g_ema"]
+    full = t2.g_module.state_dict()
+    for k, v in vol.items():                             # renderer frozen in stage 2
+        if k.startswith("renderer."):
+            assert torch.equal(full[k], v), k
+    assert t1.iteration == 2
+    # a second stage-1 run resumes after the newest periodic checkpoint (iteration 0)
+    t1b = pipeline.train_vol_render(o1, "exp", _loader(8, 1), cpu, tmp_path, iters=1,
+                                    sphere_init_iters=1)
+    assert t1b.iteration == 2

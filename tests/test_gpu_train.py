@@ -1,0 +1,139 @@
+"""GPU: the training configurations on one MI355X.
+
+configs[2] (ffhq_256_sdf_ngp train.py) and configs[4] (the ngp=0 SIREN generator):
+one full-size stage-2 FullPipelineTrainer step (batch 8, chunk 2, 256^2: the frozen
+renderer on the fused HIP forward, the decoder trained on the module path), one
+stage-1 RendererTrainer sphere-init + D/G step at 64^2 (chunk 2: every hash-grid
+evaluation on the HIP encoder forward / backward, dy_dx for the eikonal term), for
+both networks; then the data-parallel paths with two processes sharing the GPU over
+gloo: a DDP stage-2 step (replicas stay identical) and bench.py's own multi-rank
+timing (barrier + MAX over ranks, value = all ranks' faces / time).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _snap(module, prefixes):
+    return {k: v.detach().clone() for k, v in module.state_dict().items()
+            if k.startswith(prefixes)}
+
+
+def _changed(before, module):
+    now = module.state_dict()
+    return [k for k, v in before.items() if not torch.equal(v, now[k])]
+
+
+@pytest.mark.parametrize("ngp", [True, False], ids=["ngp", "siren"])
+def test_stage2_full_size_step(sdfr, ngp):
+    from sdface_gan_amd.training import FullPipelineTrainer
+    opt = sdfr.vol_render_opt(ngp=ngp)                     # size 256, batch 8, chunk 2
+    assert (opt.training.batch, opt.training.chunk, opt.model.size) == (8, 2, 256)
+    tr = FullPipelineTrainer(opt, DEV, seed=0)
+    frozen = _snap(tr.g_module, ("renderer.", "style."))
+    dec = _snap(tr.g_module, ("decoder.",))
+    d0 = _snap(tr.d_module, ("",))
+    cam, focal, near, far, _ = sdfr.generate_camera_params(64, DEV, batch=2)
+    with torch.no_grad():                                  # stage 2: the fused renderer
+        assert tr.g_module.renderer._fused_ok(cam, torch.zeros(2, 256, device=DEV), False)
+    torch.manual_seed(1)
+    for _ in range(2):                                     # i = 0: R1 and path regularisation
+        losses = tr.step(torch.rand(8, 3, 256, 256, device=DEV) * 2 - 1)
+        for k, v in losses.items():
+            assert torch.isfinite(v), (k, v)
+    assert not _changed(frozen, tr.g_module), "frozen renderer / mapping was updated"
+    assert len(_changed(dec, tr.g_module)) > 10
+    assert len(_changed(d0, tr.d_module)) > 10
+    ema = tr.generator_test.state_dict()
+    assert any(not torch.equal(ema[k], v) for k, v in tr.g_module.state_dict().items()
+               if k.startswith("decoder.") and k.endswith("weight"))
+
+
+@pytest.mark.parametrize("ngp", [True, False], ids=["ngp", "siren"])
+def test_stage1_step_64(sdfr, ngp):
+    from sdface_gan_amd.training import RendererTrainer
+    opt = sdfr.vol_render_opt(ngp=ngp, train_renderer=True)    # 64^2 thumbs, batch 8, chunk 2
+    tr = RendererTrainer(opt, DEV, seed=0)
+    g0 = _snap(tr.g_module, ("renderer.",))
+    d0 = _snap(tr.d_module, ("",))
+    torch.manual_seed(2)
+    init = tr.sphere_init_step(batch=3)
+    assert torch.isfinite(init)
+    losses = tr.step(torch.rand(8, 3, 64, 64, device=DEV) * 2 - 1)
+    for k, v in losses.items():
+        assert torch.isfinite(v), (k, v)
+    assert float(losses["g_eikonal"]) > 0
+    changed = _changed(g0, tr.g_module)
+    if ngp:
+        assert "renderer.network.encoder.embeddings" in changed     # HIP table gradients
+    assert "renderer.network.sigma_linear.weight" in changed
+    assert len(_changed(d0, tr.d_module)) > 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _ddp_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, str(REPO))
+    from sdfr_loader import load
+    sdfr = load()
+    from sdface_gan_amd.training import FullPipelineTrainer
+    opt = sdfr.vol_render_opt(batch=2, chunk=1)
+    tr = FullPipelineTrainer(opt, torch.device("cuda", 0), seed=3)
+    torch.manual_seed(50 + rank)
+    losses = tr.step(torch.rand(2, 3, 256, 256, device="cuda") * 2 - 1)
+    torch.save({"losses": {k: float(v) for k, v in losses.items()},
+                "d": {k: v.cpu() for k, v in tr.d_module.state_dict().items()},
+                "dec": {k: v.cpu() for k, v in tr.g_module.state_dict().items()
+                        if k.startswith("decoder.")}},
+               os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ddp_world2_on_one_gpu(tmp_path):
+    """Two ranks on cuda:0 over gloo: one stage-2 DDP step; replicas bit-identical."""
+    mp.spawn(_ddp_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    for part in ("d", "dec"):
+        for k, v in r0[part].items():
+            assert torch.equal(v, r1[part][k]), f"{part} {k} diverged"
+    assert r0["losses"] == r1["losses"]
+
+
+def test_bench_multi_rank_timing_world2():
+    """bench.py's multi-rank path (torchrun, barrier + MAX-over-ranks timing, value =
+    all ranks' faces / time) with two gloo ranks sharing the GPU."""
+    env = dict(os.environ, SDFR_BENCH_BACKEND="gloo", SDFR_BENCH_SAME_DEVICE="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(REPO / "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "4",
+           "--no-cpu-baseline", "--no-extras"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]                # rank 0 prints one line
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["scaling"] == "weak"
+    assert rec["value"] > 0
+    assert abs(rec["value"] - 2 * 4 * 3 / (rec["ms_per_step"] * 3 / 1e3)) < 1e-6 * rec["value"]
