@@ -44,40 +44,6 @@ namespace sdfr {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 t_out][hi,lo][64 lanes] x 16 B
-[[maybe_unused]] constexpr int kXStage = kXSliceF4 / kThreads;   // float4 staged per thread per slice
-
-// Schedule options (compile-time; DESIGN.md section 5 records the measured choice):
-//   SDFR_X_PREFETCH  ring staged two slices ahead + next slice's first fragment
-//                    read before the barrier (1) / one slice ahead (0)
-//   SDFR_X_BUFLOAD   ring staging loads as buffer_load (scalar slice offset, no
-//                    per-load 64-bit address VALU) (1) / global_load (0)
-#ifndef SDFR_X_PREFETCH
-#define SDFR_X_PREFETCH 1
-#endif
-#ifndef SDFR_X_BUFLOAD
-#define SDFR_X_BUFLOAD 1
-#endif
-//   SDFR_X_RAWBAR    slice barrier as lgkmcnt(2) + s_barrier, leaving the next
-//                    slice's first-fragment reads in flight (1) / __syncthreads (0)
-#ifndef SDFR_X_RAWBAR
-#define SDFR_X_RAWBAR 1
-#endif
-//   SDFR_X_SLICE2    ring of 2 x 32 KB slots holding whole K-steps (both halves):
-//                    one barrier per K-step instead of per half (1) / 3 x 16 KB (0)
-//                    (NgpNet only: SirenNet would spill and exceed 160 KB of LDS)
-#ifndef SDFR_X_SLICE2
-#define SDFR_X_SLICE2 1
-#endif
-#if SDFR_X_SLICE2 && (SDFR_X_DMA || !SDFR_X_PREFETCH || !SDFR_X_BUFLOAD)
-#error "SDFR_X_SLICE2 builds on the prefetching buffer_load register ring"
-#endif
-//   SDFR_X_DMA       ring filled by LDS-DMA two slices ahead, counted vmcnt, raw
-//                    barrier (1) / staged through registers + __syncthreads (0);
-//                    measured 7 % slower than the register ring (6.14 vs 5.71 ms)
-#ifndef SDFR_X_DMA
-#define SDFR_X_DMA 0
-#endif
-
 // ----------------------------------------------------------------------------
 // network policies.  Weight matrices ("layers") in order: layer 0, the dense
 // 256x256 layers, the views layer.  Slices: 2 per k-step of 32 input features
@@ -85,7 +51,7 @@ constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 t_out][hi,lo][64 l
 // ----------------------------------------------------------------------------
 struct NgpNet {
     static constexpr bool kSiren = false;
-    static constexpr bool kSlice2 = SDFR_X_SLICE2;   // whole-K-step ring
+    static constexpr bool kSlice2 = true;            // register ring: whole-K-step slots
     static constexpr int kLayers = 5;          // input_linear, pts_linears.0-2, views
     static constexpr int kFilmN = 4;           // FiLM: pts_linears.0-2, views
     static constexpr int kHidden = 3;          // dense layers after layer 0
@@ -129,6 +95,8 @@ __device__ __forceinline__ int xperm_k(int l, uint32_t q, uint32_t g, uint32_t j
 }
 
 __device__ __forceinline__ h8 as_h8(f4 v) { return __builtin_bit_cast(h8, v); }
+__device__ __forceinline__ void xpin(f4 &x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void xpin(float &x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(a), as_h8(b), c, 0, 0, 0);
 }
@@ -186,6 +154,7 @@ struct XPrepArgs {
     const float *styles;           // [B,256]
     const float *gw[kMaxLayers], *gb[kMaxLayers], *bw[kMaxLayers], *bb[kMaxLayers];
     const float *w[kMaxLayers];
+    const float *lb[kMaxLayers];   // layer biases (unscaled)
     const float *su;               // [layers][256]
     float *film;                   // [B][films][2][256]
     f4 *packed;                    // [slices][8][2][64] fp16x8
@@ -216,15 +185,34 @@ __global__ void __launch_bounds__(256) xprep_kernel(const XPrepArgs a) {
         }
         const float lin = __fadd_rn(acc, bias[j]);
         // LinearLayer: std_init * linear + bias_init (sdf_model.py:39, 58-59).  The
-        // activation sin(gamma x + beta) runs as sin_rev(fma(gamma'', x_s, beta''))
-        // with the argument in revolutions: gamma'' = gamma / (su 2pi) also absorbs
-        // the row scale su of the layer it modulates, beta'' = beta / 2pi; each is
-        // one correctly rounded division (in double) of the reference's fp32 value
+        // activation sin(gamma (W x + b) + beta) of the modulated layer runs as
+        // sin_rev(fma(gamma'', z, beta'')) on its bias-free, row-scaled GEMM output
+        // z = su W x, in revolutions: gamma'' = gamma / (su 2pi) and
+        // beta'' = (gamma b + beta) / 2pi, each one correctly rounded division (in
+        // double) of the reference's fp32 gamma, beta and b.  Folding the bias into
+        // beta'' leaves the accumulators starting from zero (no bias rows in LDS).
         constexpr double k2pi = 6.283185307179586476925;
-        const float v = which
-            ? (float)((double)__fadd_rn(__fmul_rn(0.25f, lin), 0.0f) / k2pi)
-            : (float)((double)__fadd_rn(__fmul_rn(15.0f, lin), 30.0f) /
-                      ((double)a.su[Net::film_layer(f) * kW + j] * k2pi));
+        const int l = Net::film_layer(f);
+        const float gam = __fadd_rn(__fmul_rn(15.0f, lin), 30.0f);
+        float v;
+        if (which) {
+            // gamma of the same row: recomputed here (its block is another workgroup)
+            const f4 *gr = reinterpret_cast<const f4 *>(a.gw[f] + (size_t)j * kW);
+            float ga = 0.0f;
+#pragma unroll 8
+            for (uint32_t k = 0; k < kW / 4; ++k) {
+                const f4 w4 = gr[k], s4 = sr[k];
+                ga = __fmaf_rn(s4.x, w4.x, ga);
+                ga = __fmaf_rn(s4.y, w4.y, ga);
+                ga = __fmaf_rn(s4.z, w4.z, ga);
+                ga = __fmaf_rn(s4.w, w4.w, ga);
+            }
+            const float g = __fadd_rn(__fmul_rn(15.0f, __fadd_rn(ga, a.gb[f][j])), 30.0f);
+            const float bet = __fadd_rn(__fmul_rn(0.25f, lin), 0.0f);
+            v = (float)(((double)g * (double)a.lb[l][j] + (double)bet) / k2pi);
+        } else {
+            v = (float)((double)gam / ((double)a.su[l * kW + j] * k2pi));
+        }
         a.film[(((size_t)b * NF + f) * 2 + which) * kW + j] = v;
         return;
     }
@@ -280,182 +268,6 @@ struct XFieldArgs {
 // differences; tests/test_gpu_render.py compares split and unsplit renders).
 // Partials per (segment, ray): 256 features, rgb[3], xyz[3], T, w_last.
 constexpr uint32_t kPartQ = kW + 8;
-
-// Weight ring: 3 LDS slots.  With SDFR_X_PREFETCH, during slice `it` the wave
-// computes from slot it%3, writes slice it+2 (held in registers since slice
-// it-1) into slot (it+2)%3 -- the slot of slice it-1, which every wave finished
-// reading before the barrier that closed slice it-1 -- loads slice it+3 into
-// registers, and reads the first fragment pair of slice it+1 (already visible:
-// written during it-1), so the next slice's first MFMAs do not wait on LDS
-// latency after the barrier.
-//
-// With SDFR_X_DMA the ring is filled by LDS-DMA instead: during slice `it` every
-// wave issues its pieces of slice it+2 into slot (it+2)%3 (free since the barrier
-// that closed it-1), and before the barrier closing `it` waits (counted vmcnt)
-// for its pieces of it+1.  A slice is 16 pieces of 1 KB; every wave also moves
-// pieces 0-1 (the first hi/lo fragment) itself -- identical bytes to the same
-// place -- so it can pre-read them before the barrier from its own completed
-// DMA.  Waves 0/1 move 4 further pieces, waves 2/3 three plus a repeat of 0/1:
-// six per wave per slice.
-constexpr int kXDmaPieces = 6;
-
-__device__ __forceinline__ uint32_t xdma_piece(uint32_t w, int k) {
-    if (k < 2) return (uint32_t)k;
-    if (w < 2) return 2 + 4 * w + (uint32_t)(k - 2);
-    return k < 5 ? 10 + 3 * (w - 2) + (uint32_t)(k - 2) : w - 2;
-}
-
-struct XRing {
-    f4 *lds;              // [3][kXSliceF4]
-    const f4 *packed;
-#if SDFR_X_SLICE2
-    f4 st[2 * kXStage];   // the next K-step (both halves) staged through registers (NgpNet)
-#elif !SDFR_X_DMA
-    f4 st[kXStage];       // the slice staged through registers
-#endif
-    f4 pre_h, pre_l;      // first (hi, lo) A fragment of the current slice
-    __amdgpu_buffer_rsrc_t rsrc;   // the packed fragments (SDFR_X_BUFLOAD)
-    v4i drsrc;            // the same for the LDS-DMA (SDFR_X_DMA)
-    uint32_t it;          // slice iteration (runs across passes)
-    uint32_t tid, wave;
-};
-
-// LDS-DMA of slice pf into ring slot `slot` (this wave's pieces)
-template <class Net>
-__device__ __forceinline__ void xdma_issue(XRing &R, uint32_t pf, uint32_t slot) {
-#pragma unroll
-    for (int k = 0; k < kXDmaPieces; ++k) {
-        const uint32_t pc = xdma_piece(R.wave, k);
-        dma16(R.drsrc, (R.tid & 63u) * 16u, (pf * kXSliceF4 + pc * 64u) * 16u,
-              lds_addr(R.lds + slot * kXSliceF4 + pc * 64u));
-    }
-}
-
-__device__ __forceinline__ void xpin(f4 &x) { asm volatile("" : "+v"(x)); }
-__device__ __forceinline__ void xpin(float &x) { asm volatile("" : "+v"(x)); }
-
-// One half k-step: 8 output tiles (8H .. 8H+7) x 2 sample columns x 3 split
-// terms = 48 MFMAs on one LDS ring slot, then `side` (register work issued in
-// the MFMA shadow), the ring staging (XRing) and the slice barrier.
-// Ablation variants (profiling builds only, sdfr_debug_set_field_variant; V = 0
-// is the product): bit 0 drops the slice barrier, bit 1 the LDS A-fragment reads,
-// bit 2 the ring staging, bit 3 the per-layer activations, bit 4 the per-pass
-// compositing.  Any V != 0 computes wrong results by construction.
-template <int V, class Net, int H, class Side>
-__device__ __forceinline__ void xstep(XRing &R, f4 (&acc0)[16], f4 (&acc1)[16], const f4 b0h,
-                                      const f4 b0l, const f4 b1h, const f4 b1l, Side &&side) {
-    constexpr bool kS2 = Net::kSlice2;
-    // with kS2, K-step fs = it / 2 lives in slot fs % 2 (halves H = 0, 1 at +0 / +16 KB)
-    const uint32_t cur = R.it % 3u;
-#if SDFR_X_DMA
-    if constexpr ((V & 4) == 0) xdma_issue<Net>(R, (R.it + 2u) % Net::kSlices, (R.it + 2u) % 3u);
-#endif
-    const f4 *A = kS2 ? R.lds + ((R.it >> 1) & 1u) * (2 * kXSliceF4) + H * kXSliceF4 + (R.tid & 63u)
-                      : R.lds + cur * kXSliceF4 + (R.tid & 63u);
-    f4 ah[8], al[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        if constexpr ((V & 2) != 0) {
-            ah[i] = b0h * (float)(i + 1);
-            al[i] = b1l * (float)(i + 1);
-        } else if ((kS2 ? H == 1 : (SDFR_X_PREFETCH || SDFR_X_DMA)) && i == 0) {
-            ah[0] = R.pre_h;
-            al[0] = R.pre_l;
-        } else {
-            ah[i] = A[(2 * i) * 64];
-            al[i] = A[(2 * i + 1) * 64];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int t = 8 * H + i;
-        acc0[t] = mfma16(al[i], b0h, acc0[t]);
-        acc1[t] = mfma16(al[i], b1h, acc1[t]);
-        acc0[t] = mfma16(ah[i], b0l, acc0[t]);
-        acc1[t] = mfma16(ah[i], b1l, acc1[t]);
-        acc0[t] = mfma16(ah[i], b0h, acc0[t]);
-        acc1[t] = mfma16(ah[i], b1h, acc1[t]);
-    }
-    side();
-#if SDFR_X_SLICE2
-    if constexpr (kS2) {
-        // During K-step fs: its register-held successor fs+1 goes to slot (fs+1) % 2
-        // (free since the barrier that closed fs-1), half per half-step, each half's
-        // registers refilled from K-step fs+2; one barrier closes the K-step.
-        if constexpr ((V & 4) == 0) {
-            __builtin_amdgcn_sched_barrier(0);
-            const uint32_t fs = R.it >> 1;
-            f4 *wl = R.lds + ((fs + 1u) & 1u) * (2 * kXSliceF4) + H * kXSliceF4;
-#pragma unroll
-            for (int i = 0; i < kXStage; ++i) wl[R.tid + i * kThreads] = R.st[H * kXStage + i];
-            const uint32_t pf = (2u * fs + 4u + H) % Net::kSlices;
-#pragma unroll
-            for (int i = 0; i < kXStage; ++i)
-                R.st[H * kXStage + i] = __builtin_bit_cast(
-                    f4, __builtin_amdgcn_raw_buffer_load_b128(
-                            R.rsrc, (int)((R.tid + i * kThreads) * sizeof(f4)),
-                            (int)(pf * kXSliceF4 * sizeof(f4)), 0));
-        }
-        if constexpr (H == 0) {
-            if constexpr ((V & 2) == 0) {           // first fragment of the second half (same slot)
-                R.pre_h = A[kXSliceF4];
-                R.pre_l = A[kXSliceF4 + 64];
-            }
-        } else if constexpr ((V & 1) == 0) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-        ++R.it;
-        return;
-    }
-#endif
-#if SDFR_X_DMA
-    if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // own pieces of it+1
-    if constexpr ((V & 2) == 0) {
-        const f4 *An = R.lds + ((R.it + 1u) % 3u) * kXSliceF4 + (R.tid & 63u);
-        R.pre_h = An[0];
-        R.pre_l = An[64];
-    }
-    if constexpr ((V & 1) == 0) __builtin_amdgcn_s_barrier();
-#else
-    if constexpr ((V & 4) == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t wslot = (R.it + 1u + SDFR_X_PREFETCH) % 3u;
-#pragma unroll
-        for (int i = 0; i < kXStage; ++i)
-            R.lds[wslot * kXSliceF4 + R.tid + i * kThreads] = R.st[i];
-        const uint32_t pf = (R.it + 2u + SDFR_X_PREFETCH) % Net::kSlices;
-#pragma unroll
-        for (int i = 0; i < kXStage; ++i) {
-#if SDFR_X_BUFLOAD
-            R.st[i] = __builtin_bit_cast(
-                f4, __builtin_amdgcn_raw_buffer_load_b128(
-                        R.rsrc, (int)((R.tid + i * kThreads) * sizeof(f4)),
-                        (int)(pf * kXSliceF4 * sizeof(f4)), 0));
-#else
-            R.st[i] = R.packed[pf * kXSliceF4 + R.tid + i * kThreads];
-#endif
-        }
-    }
-    if constexpr ((V & 2) == 0 && SDFR_X_PREFETCH) {
-        const f4 *An = R.lds + ((R.it + 1u) % 3u) * kXSliceF4 + (R.tid & 63u);
-        R.pre_h = An[0];
-        R.pre_l = An[64];
-    }
-#if SDFR_X_RAWBAR
-    // raw barrier: the slot writes must have landed, the next slice's first-fragment
-    // reads (the two youngest LDS ops, in order behind them) may stay in flight
-    if constexpr ((V & 1) == 0) {
-        if constexpr ((V & 2) == 0 && SDFR_X_PREFETCH) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    }
-#else
-    if constexpr ((V & 1) == 0) __syncthreads();
-#endif
-#endif
-    ++R.it;
-}
 
 // Activate tile pair (2q, 2q+1) of one sample column in place and split it
 // into the (hi, lo) B fragment of k-step q.
@@ -524,436 +336,6 @@ __device__ __forceinline__ void zero_acc(f4 (&acc)[16]) {
     for (int t = 0; t < 16; ++t) acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 }
 
-__device__ __forceinline__ void init_acc(f4 (&acc)[16], const float *bias, uint32_t g) {
-#pragma unroll
-    for (int t = 0; t < 16; ++t) acc[t] = *reinterpret_cast<const f4 *>(bias + 16 * t + 4 * g);
-}
-
-// A 256 -> 256 layer: out = W in + b over 8 k-steps.  In k-step q the next
-// input pair (q+1) of each sample column is activated in the MFMA shadow; the
-// last k-step activates the first pair of this layer's own output (its tiles
-// 0-7 completed in the k-step's first half).
-template <int V, class Net, class ActIn, class ActOut>
-__device__ __forceinline__ void dense_layer(XRing &R, f4 (&in0)[16], f4 (&in1)[16],
-                                            f4 (&out0)[16], f4 (&out1)[16], ActIn &&act_in,
-                                            ActOut &&act_out) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int qn = q < 7 ? q + 1 : 7;
-        xstep<V, Net, 0>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1],
-                         [&] {
-                             if (q < 7) act_in(in0[2 * qn], in0[2 * qn + 1], qn, 0);
-                         });
-        xstep<V, Net, 1>(R, out0, out1, in0[2 * q], in0[2 * q + 1], in1[2 * q], in1[2 * q + 1],
-                         [&] {
-                             if (q < 7) {
-                                 act_in(in1[2 * qn], in1[2 * qn + 1], qn, 1);
-                             } else {
-                                 act_out(out0[0], out0[1], 0, 0);
-                                 act_out(out1[0], out1[1], 0, 1);
-                             }
-                         });
-    }
-}
-
-struct NoAct {
-    __device__ __forceinline__ void operator()(f4 &, f4 &, int, int) const {}
-};
-
-template <int V, class Net>
-__global__ void __launch_bounds__(kThreads, 1) field_x_kernel(const XFieldArgs a) {
-    constexpr int NL = Net::kLayers, NF = Net::kFilmN;
-    __shared__ f4 ring_lds[(Net::kSlice2 ? 4 : 3) * kXSliceF4];   // 64 / 48 KB weight ring
-    __shared__ float cst[(NL + 5) * kW];                   // bias_s[NL] (ngp layer 0 unscaled), 1/su0, sigma_w, rgb_w[3]
-    __shared__ float film_lds[NF * 2 * kW];                // the workgroup's face
-    __shared__ f4 facc_lds[kWaves][16 * 64];               // 64 KB: feature accumulators
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t n = lane & 15u, g = lane >> 4;
-    const GeomArgs &G = a.g;
-
-    // a workgroup's 4 waves own 4 consecutive tiles of ONE face (grid = faces x
-    // ceil(tiles_per_face / 4)), so the face's FiLM vectors are shared in LDS
-    const uint32_t wg_per_face = (G.tiles_per_face + kWaves - 1) / kWaves;
-    const uint32_t seg = blockIdx.x % a.nseg, blk = blockIdx.x / a.nseg;
-    const uint32_t b = blk / wg_per_face;
-    uint32_t tile_local = (blk % wg_per_face) * kWaves + wave;
-    const bool tile_ok = tile_local < G.tiles_per_face;
-    if (!tile_ok) tile_local = G.tiles_per_face - 1;
-    const uint32_t tile = b * G.tiles_per_face + tile_local;
-    uint32_t ray_local = tile_local * kTileRays + n;
-    const bool ray_ok = tile_ok && ray_local < G.H * G.W;
-    if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
-    const uint32_t py = ray_local / G.W, px = ray_local % G.W;
-    const uint32_t ray_index = (b * G.H + py) * G.W + px;
-
-    Ray ray;
-    make_ray(G.cam + (size_t)b * 12, G.focal[b], G.pix_x[px], G.pix_y[py], G.half_res, ray);
-    const float nr = G.near_[b], fr = G.far_[b];
-    const float span = __fsub_rn(fr, nr);
-    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
-    // the views layer's last k-step fragment (identical for both sample columns):
-    // ngp: lanes g = 0, 1 hold SH 0-7 / 8-15 (K 272 -> 288); siren: lane group 0
-    // holds the unit view direction (K 259 -> 288); the rest is zero padding
-    f4 vxh, vxl;
-    {
-        const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
-        const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
-        const float v2 = G.static_viewdirs ? ray.dir[2] : ray.d[2];
-        const float vn = norm3_torch(v0, v1, v2);
-        const float ux = __fdiv_rn(v0, vn), uy = __fdiv_rn(v1, vn), uz = __fdiv_rn(v2, vn);
-        float v[8];
-        if constexpr (Net::kSiren) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = 0.0f;
-            if (g == 0) {
-                v[0] = ux;
-                v[1] = uy;
-                v[2] = uz;
-            }
-        } else {
-            const f4 qa = sh_quad(ux, uy, uz, (2 * g) & 3), qb = sh_quad(ux, uy, uz, (2 * g + 1) & 3);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[r] = g < 2 ? qa[r] : 0.0f;
-                v[4 + r] = g < 2 ? qb[r] : 0.0f;
-            }
-        }
-        split8(v, vxh, vxl);
-    }
-    const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
-    {
-        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * NF * 2 * kW);
-        f4 *dst = reinterpret_cast<f4 *>(film_lds);
-        for (uint32_t i = tid; i < NF * 2 * kW / 4; i += kThreads) dst[i] = src[i];
-    }
-
-    XRing R;
-    R.lds = ring_lds;
-    R.packed = a.packed;
-    R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<f4 *>(a.packed), 0,
-                                               (int)(Net::kSlices * kXSliceF4 * sizeof(f4)),
-                                               0x00020000);
-    R.tid = tid;
-    R.wave = __builtin_amdgcn_readfirstlane(wave);
-    R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
-    R.it = 0;
-    for (uint32_t i = tid; i < (NL + 5) * kW; i += kThreads) {
-        float v;
-        if (i < NL * kW) v = a.bias_s[i];
-        else if (i < (NL + 1) * kW) v = __fdiv_rn(1.0f, a.su[i - NL * kW]);
-        else if (i < (NL + 2) * kW) v = a.sigma_w[i - (NL + 1) * kW];
-        else v = a.rgb_w[i - (NL + 2) * kW];
-        cst[i] = v;
-    }
-    if constexpr (Net::kSlice2) {
-#if SDFR_X_SLICE2
-    // prologue: K-step 0 (half-slices 0, 1) -> slot 0; K-step 1 -> registers
-#pragma unroll
-    for (int i = 0; i < 2 * kXStage; ++i) R.lds[tid + i * kThreads] = a.packed[tid + i * kThreads];
-#pragma unroll
-    for (int i = 0; i < 2 * kXStage; ++i) R.st[i] = a.packed[2 * kXSliceF4 + tid + i * kThreads];
-    __syncthreads();
-#endif
-    } else {
-#if SDFR_X_DMA
-    // prologue: slices 0, 1 -> slots 0, 1 (slice 2 is issued by the first step)
-    xdma_issue<Net>(R, 0, 0);
-    xdma_issue<Net>(R, 1, 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#else
-    // prologue: slices 0 (.. 1) -> slots; the next slice -> registers
-    constexpr int kPro = 1 + SDFR_X_PREFETCH;
-#pragma unroll
-    for (int i = 0; i < kPro * kXStage; ++i) R.lds[tid + i * kThreads] = a.packed[tid + i * kThreads];
-#pragma unroll
-    for (int i = 0; i < kXStage; ++i) R.st[i] = a.packed[kPro * kXSliceF4 + tid + i * kThreads];
-    __syncthreads();
-#endif
-    }
-    R.pre_h = R.lds[lane];
-    R.pre_l = R.lds[64 + lane];
-
-    f4 *facc = facc_lds[wave];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) facc[t * 64 + lane] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
-    float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
-
-    const float *bias_l = cst;                     // [NL][256] (scaled)
-    const float *inv_su0 = cst + NL * kW;
-    const float *sig_w = cst + (NL + 1) * kW, *rgb_w = cst + (NL + 2) * kW;
-    auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
-    auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
-    const float sig_b = a.sigma_b[0];
-    const float rgb_b0 = a.rgb_b[0], rgb_b1 = a.rgb_b[1], rgb_b2 = a.rgb_b[2];
-
-    // layer-0 inputs of the pass's two samples:
-    //   ngp   the hash-grid features, lane group g holds levels 4g..4g+3 (K 8g..8g+7)
-    //   siren the normalised point (sdf_model.py:343-349) in lane group 0
-    const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
-    const size_t tile_sid = (size_t)(tile * G.N) * kTileRays + n;
-    float2 en[2][4];
-    auto load_inputs = [&](uint32_t s0) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            uint32_t s = s0 + j;
-            if (s >= G.N) s = G.N - 1;
-            if constexpr (Net::kSiren) {
-                const float z = sample_z(G.sc, nr, fr, ray_index, s);
-                float np_[3];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));
-                    np_[k] = G.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;
-                }
-                const bool g0 = g == 0;
-                en[j][0] = make_float2(g0 ? np_[0] : 0.0f, g0 ? np_[1] : 0.0f);
-                en[j][1] = make_float2(g0 ? np_[2] : 0.0f, 0.0f);
-                en[j][2] = make_float2(0.0f, 0.0f);
-                en[j][3] = make_float2(0.0f, 0.0f);
-            } else {
-                const size_t sid = tile_sid + (size_t)s * kTileRays;
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    en[j][c] = enc2[(4 * g + c) * (size_t)G.S_total + sid];
-            }
-        }
-    };
-    // this workgroup's passes (all of them unless the rays are split)
-    const uint32_t npass = (G.N + 1) / 2;
-    const uint32_t pps = (npass + a.nseg - 1) / a.nseg;
-    const uint32_t p_begin = seg * pps, p_end = min(npass, p_begin + pps);
-    load_inputs(2 * p_begin);
-
-    for (uint32_t p = p_begin; p < p_end; ++p) {
-        f4 X0[16], X1[16], Y0[16], Y1[16];
-        f4 e0h, e0l, e1h, e1l;
-        int es0 = 0, es1 = 0;
-        {
-            float v0[8], v1[8];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                v0[2 * c] = en[0][c].x;
-                v0[2 * c + 1] = en[0][c].y;
-                v1[2 * c] = en[1][c].x;
-                v1[2 * c + 1] = en[1][c].y;
-            }
-            if constexpr (!Net::kSiren) {
-                es0 = feat_scale(v0);
-                es1 = feat_scale(v1);
-            }
-            split8(v0, e0h, e0l);
-            split8(v1, e1h, e1l);
-        }
-        float sdfp0 = 0.0f, sdfp1 = 0.0f;
-        // activation of layer l's output: ngp layer 0 is the identity input_linear,
-        // every other layer is a FiLM with film index film_layer^-1(l); the last
-        // hidden layer also feeds the sdf head
-        auto act_film = [&](int f) {
-            return [&, f](f4 &za, f4 &zb, int q, int) {
-                float dummy = 0.0f;
-                act_pair<1, V>(za, zb, q, fg(f), fb(f), nullptr, dummy, g);
-            };
-        };
-        auto act_sdf = [&](int f) {
-            return [&, f](f4 &za, f4 &zb, int q, int j) {
-                if (j == 0) act_pair<2, V>(za, zb, q, fg(f), fb(f), sig_w, sdfp0, g);
-                else act_pair<2, V>(za, zb, q, fg(f), fb(f), sig_w, sdfp1, g);
-            };
-        };
-        auto act_l0 = [&](f4 &za, f4 &zb, int q, int j) {
-            if constexpr (Net::kSiren) {
-                act_film(0)(za, zb, q, j);
-            } else {
-                float dummy = 0.0f;
-                act_pair<0, V>(za, zb, q, inv_su0, bias_l, nullptr, dummy, g, j ? es1 : es0);
-            }
-        };
-
-        // layer 0 (32 -> 256 ngp / 3 -> 256 siren) -> X; ngp accumulates from zero
-        // (scaled features) and adds its bias in act_pair<0>
-        if constexpr (Net::kSiren) {
-            init_acc(X0, bias_l, g);
-            init_acc(X1, bias_l, g);
-        } else {
-            zero_acc(X0);
-            zero_acc(X1);
-        }
-        xstep<V, Net, 0>(R, X0, X1, e0h, e0l, e1h, e1l, [] {});
-        xstep<V, Net, 1>(R, X0, X1, e0h, e0l, e1h, e1l, [&] {
-            act_l0(X0[0], X0[1], 0, 0);
-            act_l0(X1[0], X1[1], 0, 1);
-        });
-        if constexpr (Net::kSiren) {
-            // pts_linears.1-7 (X->Y, then (Y->X, X->Y) x 3); film f modulates layer f
-            init_acc(Y0, bias_l + 1 * kW, g);
-            init_acc(Y1, bias_l + 1 * kW, g);
-            dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_l0, act_film(1));
-            for (int l = 2; l < 6; l += 2) {                  // layers 2-5
-                init_acc(X0, bias_l + l * kW, g);
-                init_acc(X1, bias_l + l * kW, g);
-                dense_layer<V, Net>(R, Y0, Y1, X0, X1, act_film(l - 1), act_film(l));
-                init_acc(Y0, bias_l + (l + 1) * kW, g);
-                init_acc(Y1, bias_l + (l + 1) * kW, g);
-                dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_film(l), act_film(l + 1));
-            }
-            init_acc(X0, bias_l + 6 * kW, g);
-            init_acc(X1, bias_l + 6 * kW, g);
-            dense_layer<V, Net>(R, Y0, Y1, X0, X1, act_film(5), act_film(6));
-            init_acc(Y0, bias_l + 7 * kW, g);
-            init_acc(Y1, bias_l + 7 * kW, g);
-            dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_film(6), act_sdf(7));
-        } else {
-            // pts_linears.0-2: film f modulates layer f+1
-            init_acc(Y0, bias_l + kW, g);
-            init_acc(Y1, bias_l + kW, g);
-            dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_l0, act_film(0));
-            init_acc(X0, bias_l + 2 * kW, g);
-            init_acc(X1, bias_l + 2 * kW, g);
-            dense_layer<V, Net>(R, Y0, Y1, X0, X1, act_film(0), act_film(1));
-            init_acc(Y0, bias_l + 3 * kW, g);
-            init_acc(Y1, bias_l + 3 * kW, g);
-            dense_layer<V, Net>(R, X0, X1, Y0, Y1, act_film(1), act_sdf(2));
-        }
-        // views FiLM ([h_last, SH | viewdir] -> 256) -> X; h_last pairs finish the sdf head
-        init_acc(X0, bias_l + (NL - 1) * kW, g);
-        init_acc(X1, bias_l + (NL - 1) * kW, g);
-        dense_layer<V, Net>(R, Y0, Y1, X0, X1, act_sdf(NF - 2), NoAct{});
-        xstep<V, Net, 0>(R, X0, X1, vxh, vxl, vxh, vxl, [] {});
-        xstep<V, Net, 1>(R, X0, X1, vxh, vxl, vxh, vxl, [] {});
-
-        if (p + 1 < p_end) load_inputs(2 * p + 2);
-        const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
-        // compositing of the pass's two samples, front to back
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint32_t s = 2 * p + j;
-            if (s >= G.N) break;
-            f4 (&Xj)[16] = j ? X1 : X0;
-            if constexpr ((V & 16) != 0) {
-#pragma unroll
-                for (int t = 0; t < 16; ++t) racc0 += (Xj[t][0] + Xj[t][1]) + (Xj[t][2] + Xj[t][3]);
-                continue;
-            }
-            const float sdf = __fadd_rn(group_sum(j ? sdfp1 : sdfp0), sig_b);
-            const float z = sample_z(G.sc, nr, fr, ray_index, s);
-            const float dist = (s + 1 < G.N)
-                                   ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, s + 1), z),
-                                               dnorm)
-                                   : __fmul_rn(1e10f, dnorm);
-            float alpha;
-            if (a.with_sdf) {
-                const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
-                alpha = 1.0f - expf(-sig * dist);
-            } else {
-                float raw = sdf;
-                if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + s];
-                const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
-                alpha = 1.0f - expf(-sp * dist);
-            }
-            float w = alpha * T;
-            if (a.force_background && s + 1 == G.N) w = 1.0f - wsum;
-            T = T * ((1.0f - alpha) + 1e-10f);
-            wsum += w;
-            // colour features f = sin(gamma_v' x + beta_v); rgb_linear; compositing
-            float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const int f0 = 16 * t + 4 * (int)g;
-                const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
-                const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
-                const f4 w0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
-                const f4 w1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
-                const f4 w2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
-                f4 fv;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    fv[r] = sin_rev(__fmaf_rn(gm[r], Xj[t][r], bt[r]));
-                    p0 = __fmaf_rn(fv[r], w0[r], p0);
-                    p1 = __fmaf_rn(fv[r], w1[r], p1);
-                    p2 = __fmaf_rn(fv[r], w2[r], p2);
-                }
-                Xj[t] = fv;
-            }
-            const float r0 = __fadd_rn(group_sum(p0), rgb_b0);
-            const float r1 = __fadd_rn(group_sum(p1), rgb_b1);
-            const float r2 = __fadd_rn(group_sum(p2), rgb_b2);
-            w_last = w;
-            racc0 = __fmaf_rn(w, sigmoidf_(r0), racc0);
-            racc1 = __fmaf_rn(w, sigmoidf_(r1), racc1);
-            racc2 = __fmaf_rn(w, sigmoidf_(r2), racc2);
-            if (a.xyz) {
-                xacc0 = __fmaf_rn(w, __fadd_rn(ray.o[0], __fmul_rn(ray.d[0], z)), xacc0);
-                xacc1 = __fmaf_rn(w, __fadd_rn(ray.o[1], __fmul_rn(ray.d[1], z)), xacc1);
-                xacc2 = __fmaf_rn(w, __fadd_rn(ray.o[2], __fmul_rn(ray.d[2], z)), xacc2);
-            }
-            if (a.features) {
-#pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    f4 v = facc[t * 64 + lane];
-                    v.x = __fmaf_rn(w, Xj[t].x, v.x);
-                    v.y = __fmaf_rn(w, Xj[t].y, v.y);
-                    v.z = __fmaf_rn(w, Xj[t].z, v.z);
-                    v.w = __fmaf_rn(w, Xj[t].w, v.w);
-                    facc[t * 64 + lane] = v;
-                }
-            }
-            if (a.sdf && ray_ok && g == 0) a.sdf[(size_t)ray_index * G.N + s] = sdf;
-        }
-    }
-#if SDFR_X_DMA
-    // the ring runs ahead across passes: no LDS-DMA may land after the workgroup ends
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-
-    if (!ray_ok) return;
-    if (a.nseg > 1) {
-        const size_t R = (size_t)G.total_tiles * kTileRays;
-        float *pp = a.part + (size_t)seg * kPartQ * R + (size_t)tile * kTileRays + n;
-        if (a.features) {
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const uint32_t jf = 16 * t + 4 * g;
-                const f4 v = facc[t * 64 + lane];
-                pp[(size_t)(jf + 0) * R] = v.x;
-                pp[(size_t)(jf + 1) * R] = v.y;
-                pp[(size_t)(jf + 2) * R] = v.z;
-                pp[(size_t)(jf + 3) * R] = v.w;
-            }
-        }
-        if (g == 0) {
-            const float q[8] = {racc0, racc1, racc2, xacc0, xacc1, xacc2, T, w_last};
-#pragma unroll
-            for (int k = 0; k < 8; ++k) pp[(size_t)(kW + k) * R] = q[k];
-        }
-        return;
-    }
-    const size_t HW = (size_t)G.H * G.W;
-    const size_t pix = (size_t)py * G.W + px;
-    if (g < 3) {
-        const float rc = g == 0 ? racc0 : (g == 1 ? racc1 : racc2);
-        a.rgb[((size_t)b * 3 + g) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, rc));
-        if (a.xyz) {
-            const float xc = g == 0 ? xacc0 : (g == 1 ? xacc1 : xacc2);
-            a.xyz[((size_t)b * 3 + g) * HW + pix] = xc;
-        }
-    } else if (a.mask) {
-        a.mask[(size_t)b * HW + pix] = w_last;
-    }
-    if (a.features) {
-        float *fbp = a.features + (size_t)b * kW * HW + pix;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const uint32_t jf = 16 * t + 4 * g;
-            const f4 v = facc[t * 64 + lane];
-            fbp[(size_t)(jf + 0) * HW] = v.x;
-            fbp[(size_t)(jf + 1) * HW] = v.y;
-            fbp[(size_t)(jf + 2) * HW] = v.z;
-            fbp[(size_t)(jf + 3) * HW] = v.w;
-        }
-    }
-}
 
 // ----------------------------------------------------------------------------
 // field_x2_kernel: two waves per SIMD.
@@ -998,7 +380,14 @@ constexpr int kXStage2 = kXSliceF4 / kThreads2;     // float4 staged per thread 
 #ifndef SDFR_X2_SIDE
 #define SDFR_X2_SIDE 4
 #endif
-constexpr int kX2DmaSlots = 4;
+// SDFR_X2_SLOTS: LDS-DMA ring slots of one half-slice (16 KB); the DMA of a
+// half-slice is issued SLOTS-1 half-steps ahead of its use
+#ifndef SDFR_X2_SLOTS
+#define SDFR_X2_SLOTS 4
+#endif
+// (SIREN keeps 4: its 9 FiLM layers' vectors take 18 KB of LDS)
+template <class Net>
+constexpr int x2_slots() { return Net::kSiren ? 4 : SDFR_X2_SLOTS; }
 constexpr int kX2DmaPieces = 16 / kWaves2;          // 1 KB pieces per wave per half-slice
 
 __device__ __forceinline__ float ror8(float v) {   // lane n <- lane (n + 8) mod 16 of its row
@@ -1013,8 +402,17 @@ struct XRing2 {
     __amdgpu_buffer_rsrc_t rsrc;
     v4i drsrc;            // the packed fragments for the LDS-DMA
     uint32_t it, tid, wave;
+    uint32_t slot0;       // DMA ring slot of the pass's first half-slice (wave-uniform)
     bool late;            // waves 4-7 (SDFR_X2_STAGGER)
 };
+
+// ring slot of half-step it (0 <= it < kSlices) of the current pass
+template <class Net>
+__device__ __forceinline__ uint32_t x2_slot(const XRing2 &R, uint32_t it) {
+    constexpr uint32_t S = x2_slots<Net>();
+    if constexpr (Net::kSlices % S == 0) return it % S;  // slot0 stays 0
+    return (R.slot0 + it) % S;
+}
 
 // One 1 KB LDS-DMA piece: source byte offset sbase + soff, LDS byte address lbase +
 // loff.  The two additions run inside the asm, so the compiler keeps only the
@@ -1051,9 +449,10 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
     constexpr bool kS2 = Net::kSlice2 && !SDFR_X2_DMA;
     constexpr bool kDma = SDFR_X2_DMA;
     const uint32_t lane = R.tid & 63u;
+    constexpr uint32_t kAhead = x2_slots<Net>() - 1;
     if constexpr (kDma && (V & 4) == 0)
-        x2_dma(R, (R.it + 3u) % Net::kSlices, (R.it + 3u) % kX2DmaSlots);
-    const f4 *A = kDma ? R.lds + (R.it % kX2DmaSlots) * kXSliceF4 + lane
+        x2_dma(R, (R.it + kAhead) % Net::kSlices, x2_slot<Net>(R, R.it + kAhead));
+    const f4 *A = kDma ? R.lds + x2_slot<Net>(R, R.it) * kXSliceF4 + lane
                 : kS2  ? R.lds + ((R.it >> 1) & 1u) * (2 * kXSliceF4) + H * kXSliceF4 + lane
                        : R.lds + (R.it % 3u) * kXSliceF4 + lane;
     // A fragments in groups of two tiles, the next group's LDS reads issued ahead of
@@ -1103,7 +502,8 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
     if constexpr (kDma) {
         // own pieces of half-slice it+1 (issued two half-steps ago) have landed; the
         // barrier publishes every wave's (and closes this slot for the DMA of it+4)
-        if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kX2DmaPieces) : "memory");
+        if constexpr ((V & 4) == 0)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((x2_slots<Net>() - 2) * kX2DmaPieces) : "memory");
         if constexpr ((V & 1) == 0) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
@@ -1176,9 +576,9 @@ struct NoAct2 {
 
 template <int V, class Net>
 __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs a) {
-    constexpr int NL = Net::kLayers, NF = Net::kFilmN;
-    __shared__ f4 ring_lds[(SDFR_X2_DMA ? kX2DmaSlots : (Net::kSlice2 ? 4 : 3)) * kXSliceF4];
-    __shared__ float cst[(NL + 5) * kW];                   // bias_s[NL] (ngp layer 0 unscaled), 1/su0, sigma_w, rgb_w[3]
+    constexpr int NF = Net::kFilmN;
+    __shared__ f4 ring_lds[(SDFR_X2_DMA ? x2_slots<Net>() : (Net::kSlice2 ? 4 : 3)) * kXSliceF4];
+    __shared__ float cst[6 * kW];                          // ngp layer-0 bias, 1/su0, sigma_w, rgb_w[3]
     __shared__ float film_lds[NF * 2 * kW];                // the workgroup's face
     __shared__ f4 facc_lds[kWaves2][16 * 32];              // 64 KB: [tile][g][ray8] feature sums
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -1247,17 +647,18 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
     R.late = R.wave >= 4;
     R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
     R.it = 0;
-    for (uint32_t i = tid; i < (NL + 5) * kW; i += kThreads2) {
+    for (uint32_t i = tid; i < 6 * kW; i += kThreads2) {
         float v;
-        if (i < NL * kW) v = a.bias_s[i];
-        else if (i < (NL + 1) * kW) v = __fdiv_rn(1.0f, a.su[i - NL * kW]);
-        else if (i < (NL + 2) * kW) v = a.sigma_w[i - (NL + 1) * kW];
-        else v = a.rgb_w[i - (NL + 2) * kW];
+        if (i < kW) v = Net::kSiren ? 0.0f : a.bias_s[i];     // raw input_linear bias
+        else if (i < 2 * kW) v = __fdiv_rn(1.0f, a.su[i - kW]);
+        else if (i < 3 * kW) v = a.sigma_w[i - 2 * kW];
+        else v = a.rgb_w[i - 3 * kW];
         cst[i] = v;
     }
     if constexpr (SDFR_X2_DMA) {
-        // prologue: half-slices 0-2 -> slots 0-2 (slice 3 is issued by the first step)
-        for (uint32_t k = 0; k < 3; ++k) x2_dma(R, k % Net::kSlices, k);
+        // prologue: half-slices 0 .. SLOTS-2 -> their slots (the first step issues the next)
+        R.slot0 = 0;
+        for (uint32_t k = 0; k + 1 < (uint32_t)x2_slots<Net>(); ++k) x2_dma(R, k % Net::kSlices, k);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if constexpr (Net::kSlice2) {
         // prologue: K-step 0 (half-slices 0, 1) -> slot 0; K-step 1 -> registers
@@ -1282,9 +683,9 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
 
     float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
     float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
-    const float *bias_l = cst;
-    const float *inv_su0 = cst + NL * kW;
-    const float *sig_w = cst + (NL + 1) * kW, *rgb_w = cst + (NL + 2) * kW;
+    const float *bias0 = cst;
+    const float *inv_su0 = cst + kW;
+    const float *sig_w = cst + 2 * kW, *rgb_w = cst + 3 * kW;
     auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
     auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
     const float sig_b = a.sigma_b[0];
@@ -1321,11 +722,13 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
     load_inputs(2 * p_begin);
 
     for (uint32_t p = p_begin; p < p_end; ++p) {
-        // a pass consumes exactly Net::kSlices half-slices, a multiple of every ring's
-        // slot count (68 = 17 x 4 ngp, 132 = 44 x 3 siren): restarting the step counter
-        // keeps the slot cycle and makes every slot / slice index a compile-time constant
-        static_assert(Net::kSlices % kX2DmaSlots == 0 && Net::kSlices % 3 == (Net::kSiren ? 0 : 2),
+        // a pass consumes exactly Net::kSlices half-slices (68 ngp, 132 siren):
+        // restarting the step counter makes every slice index a compile-time constant;
+        // the register rings' slot counts divide kSlices, the DMA ring carries its slot
+        // base across passes (x2_slot)
+        static_assert(Net::kSlices % 3 == (Net::kSiren ? 0 : 2) && Net::kSlices % 4 == 0,
                       "ring slot cycle");
+        if (p != p_begin) R.slot0 = (R.slot0 + Net::kSlices) % (uint32_t)x2_slots<Net>();
         R.it = 0;
         f4 X[16], Y[16];
         f4 eh, el;
@@ -1357,36 +760,37 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
                 act_film(0)(za, zb, q);
             } else {
                 float dummy = 0.0f;
-                act_pair<0, V>(za, zb, q, inv_su0, bias_l, nullptr, dummy, g, es);
+                act_pair<0, V>(za, zb, q, inv_su0, bias0, nullptr, dummy, g, es);
             }
         };
 
-        if constexpr (Net::kSiren) init_acc(X, bias_l, g);
-        else zero_acc(X);
+        // every layer accumulates from zero: ngp layer 0 adds its bias in act_pair<0>,
+        // the FiLM layers' biases are folded into beta'' (xprep_kernel)
+        zero_acc(X);
         xstep2<V, Net, 0>(R, X, eh, el, [] {});
         xstep2<V, Net, 1>(R, X, eh, el, [&] { act_l0(X[0], X[1], 0); });
         if constexpr (Net::kSiren) {
-            init_acc(Y, bias_l + 1 * kW, g);
+            zero_acc(Y);
             dense_layer2<V, Net>(R, X, Y, act_l0, act_film(1));
             for (int l = 2; l < 6; l += 2) {
-                init_acc(X, bias_l + l * kW, g);
+                zero_acc(X);
                 dense_layer2<V, Net>(R, Y, X, act_film(l - 1), act_film(l));
-                init_acc(Y, bias_l + (l + 1) * kW, g);
+                zero_acc(Y);
                 dense_layer2<V, Net>(R, X, Y, act_film(l), act_film(l + 1));
             }
-            init_acc(X, bias_l + 6 * kW, g);
+            zero_acc(X);
             dense_layer2<V, Net>(R, Y, X, act_film(5), act_film(6));
-            init_acc(Y, bias_l + 7 * kW, g);
+            zero_acc(Y);
             dense_layer2<V, Net>(R, X, Y, act_film(6), act_sdf(7));
         } else {
-            init_acc(Y, bias_l + kW, g);
+            zero_acc(Y);
             dense_layer2<V, Net>(R, X, Y, act_l0, act_film(0));
-            init_acc(X, bias_l + 2 * kW, g);
+            zero_acc(X);
             dense_layer2<V, Net>(R, Y, X, act_film(0), act_film(1));
-            init_acc(Y, bias_l + 3 * kW, g);
+            zero_acc(Y);
             dense_layer2<V, Net>(R, X, Y, act_film(1), act_sdf(2));
         }
-        init_acc(X, bias_l + (NL - 1) * kW, g);
+        zero_acc(X);
         dense_layer2<V, Net>(R, Y, X, act_sdf(NF - 2), NoAct2{});
         xstep2<V, Net, 0>(R, X, vxh, vxl, [] {});
         xstep2<V, Net, 1>(R, X, vxh, vxl, [] {});
@@ -1577,17 +981,6 @@ __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
 // ----------------------------------------------------------------------------
 // host
 // ----------------------------------------------------------------------------
-// field kernel generation: 2 = field_x2_kernel (two waves per SIMD, default),
-// 1 = field_x_kernel (one wave per SIMD); SDFR_FIELD_KERNEL=1 selects the latter
-// (A/B timing only)
-static int field_kernel_gen() {
-    static const int gen = [] {
-        const char *e = std::getenv("SDFR_FIELD_KERNEL");
-        return (e && e[0] == '1') ? 1 : 2;
-    }();
-    return gen;
-}
-
 static uint32_t g_field_split_max = 4;
 void set_field_split_max(uint32_t m) { g_field_split_max = m; }
 
@@ -1652,7 +1045,10 @@ static int launch_xprep(const NetPtrs &P, const sdfr_ngp_render_args *a, char *x
         p.bw[f] = P.bw[f];
         p.bb[f] = P.bb[f];
     }
-    for (int l = 0; l < Net::kLayers; ++l) p.w[l] = P.w[l];
+    for (int l = 0; l < Net::kLayers; ++l) {
+        p.w[l] = P.w[l];
+        p.lb[l] = P.b[l];
+    }
     p.su = su;
     p.film = film;
     p.packed = packed;
@@ -1689,41 +1085,22 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background) : 1;
     f.part = part;
     const uint32_t blocks = g.B * ((g.tiles_per_face + kWaves - 1) / kWaves) * f.nseg;
-    if (field_kernel_gen() == 2) {
-        switch (field_variant()) {
+    switch (field_variant()) {
 #ifdef SDFR_ABLATION
 #define SDFR_X2FIELD_CASE(V)                                                                   \
     case V:                                                                                    \
         hipLaunchKernelGGL((field_x2_kernel<V, Net>), dim3(blocks), dim3(kThreads2), 0, st, f); \
         break;
-            SDFR_X2FIELD_CASE(1)
-            SDFR_X2FIELD_CASE(2)
-            SDFR_X2FIELD_CASE(4)
-            SDFR_X2FIELD_CASE(8)
-            SDFR_X2FIELD_CASE(16)
-            SDFR_X2FIELD_CASE(31)
+        SDFR_X2FIELD_CASE(1)
+        SDFR_X2FIELD_CASE(2)
+        SDFR_X2FIELD_CASE(4)
+        SDFR_X2FIELD_CASE(8)
+        SDFR_X2FIELD_CASE(16)
+        SDFR_X2FIELD_CASE(31)
 #undef SDFR_X2FIELD_CASE
 #endif
-            default:
-                hipLaunchKernelGGL((field_x2_kernel<0, Net>), dim3(blocks), dim3(kThreads2), 0, st,
-                                   f);
-        }
-    } else switch (field_variant()) {
-#ifdef SDFR_ABLATION
-#define SDFR_XFIELD_CASE(V)                                                                  \
-    case V:                                                                                  \
-        hipLaunchKernelGGL((field_x_kernel<V, Net>), dim3(blocks), dim3(kThreads), 0, st, f); \
-        break;
-        SDFR_XFIELD_CASE(1)
-        SDFR_XFIELD_CASE(2)
-        SDFR_XFIELD_CASE(4)
-        SDFR_XFIELD_CASE(8)
-        SDFR_XFIELD_CASE(16)
-        SDFR_XFIELD_CASE(31)
-#undef SDFR_XFIELD_CASE
-#endif
         default:
-            hipLaunchKernelGGL((field_x_kernel<0, Net>), dim3(blocks), dim3(kThreads), 0, st, f);
+            hipLaunchKernelGGL((field_x2_kernel<0, Net>), dim3(blocks), dim3(kThreads2), 0, st, f);
     }
     int rc = check_launch("render: field (f16x3)");
     if (rc || f.nseg == 1) return rc;

@@ -25,9 +25,12 @@ DEV = "cuda:0"
 TOL = {"rgb": (2e-6, 5e-7), "features": (1.2e-4, 1.5e-5), "sdf": (5e-6, 1e-6),
        "xyz": (5e-7, 6e-8), "mask": (2e-6, 5e-7), "image": (1e-4, 1.5e-5),
        # the op-by-op PyTorch-ROCm path (training / eikonal), not the HIP kernels
-       "module_rgb": (5e-4, 2e-5), "module_features": (1e-2, 5e-4),
-       # the module path on the golden's own rays (bit-exact rays_d): GEMM-order only
-       "module_golden_rgb": (5e-6, 1e-6), "module_golden_features": (3e-4, 3e-5)}
+       # the op-by-op PyTorch-ROCm path (training / eikonal): with the reference's
+       # left-to-right rays_d (bit-exact, test_get_rays_on_device_bit_exact) its error
+       # is GEMM-order rounding like the fused kernel's (round 1 bounded it at 1e-2
+       # when torch-ROCm's reduction rounded rays_d differently)
+       "module_rgb": (2e-6, 5e-7), "module_features": (1.2e-4, 1.5e-5),
+       "module_golden_rgb": (2e-6, 5e-7), "module_golden_features": (1.2e-4, 1.5e-5)}
 
 _record = {}
 

@@ -84,7 +84,9 @@ def test_eikonal_term_vs_reference(sdfr, golden_dir):
     net = gen.renderer.network
     _rel("eikonal_grad_sigma_w", net.sigma_linear.weight.grad.cpu(), g["grad_sigma_w"], 1e-4)
     _rel("eikonal_grad_input_w", net.input_linear.weight.grad.cpu(), g["grad_input_w"], 1e-4)
-    _rel("eikonal_grad_beta", gen.renderer.sigmoid_beta.grad.cpu(), g["grad_beta"], 1e-4)
+    # a scalar summed over 3,072 samples with cancellation (|sum| ~ 3e-4 of its terms'
+    # scale): bounded relative to the sum itself
+    _rel("eikonal_grad_beta", gen.renderer.sigmoid_beta.grad.cpu(), g["grad_beta"], 1e-3)
     n_dense = g["grad_table_dense"].shape[0]
     _rel("eikonal_grad_table_dense", net.encoder.embeddings.grad[:n_dense].cpu(),
          g["grad_table_dense"], 1e-4)
