@@ -27,11 +27,14 @@ with torch.no_grad():
     lat = g.style(torch.randn(B, 256, device=dev))
     for r in range(8):
         ren.stage_events = evs
-        ren(ext, focal, near, far, styles=lat)
+        torch.manual_seed(5)
+        out = ren(ext, focal, near, far, styles=lat)
         torch.cuda.synchronize()
         if r >= 2: ts.append(evs[2].elapsed_time(evs[3]))
 med = statistics.median(ts)
-print(f"{med:.3f} ms  {550912 * B * 4096 * 24 / med / 1e9:.1f} TFLOP/s")
+import hashlib
+h = hashlib.sha1(b"".join(t.detach().float().cpu().numpy().tobytes() for t in out[:2])).hexdigest()[:12]
+print(f"out {h}  {med:.3f} ms  {550912 * B * 4096 * 24 / med / 1e9:.1f} TFLOP/s")
 '''
 
 
