@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 4
+#define SDFR_ABI_VERSION 5
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -364,6 +364,29 @@ int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *a, void *stream);
 int sdfr_rgb_finish(float *rgb, const float *partial, uint32_t nparts, const float *rgb_b,
                     const float *skip, const float *fir, uint32_t B, uint32_t H, uint32_t W,
                     void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Marching cubes (sdf_mesh.py's surface extraction: sdf_utils.py:188-205, which
+ * calls scikit-image's marching_cubes(sdf_vol, 0) on the host; csrc/mesh.hip).
+ *
+ * Volume: n0 x n1 x n2 fp32 points (each >= 2, 4 n0 n1 n2 + 1 < 2^32) on the
+ * device, point (i, j, k) at vol[i s0 + j s1 + k s2] (element strides, so the
+ * reference's permute(1, 0, 2) is a stride swap).  A corner is inside when its
+ * value < level; vertices lie on the sign-changing grid edges by linear
+ * interpolation, in index coordinates (x = i + t ...).
+ *
+ *   sdfr_mc_count:  classify + scan into ws; writes counts[0] = vertices,
+ *                   counts[1] = triangles to HOST memory (synchronises stream)
+ *   sdfr_mc_emit:   same volume and ws (after sdfr_mc_count): verts [V,3] fp32,
+ *                   faces [F,3] int32 (vertex ids), device
+ * ------------------------------------------------------------------------- */
+size_t sdfr_mc_workspace_bytes(uint32_t n0, uint32_t n1, uint32_t n2);
+int sdfr_mc_count(const float *vol, uint32_t n0, uint32_t n1, uint32_t n2, int64_t s0,
+                  int64_t s1, int64_t s2, float level, void *ws, size_t ws_bytes,
+                  uint32_t *counts, void *stream);
+int sdfr_mc_emit(const float *vol, uint32_t n0, uint32_t n1, uint32_t n2, int64_t s0,
+                 int64_t s1, int64_t s2, float level, const void *ws, size_t ws_bytes,
+                 float *verts, int32_t *faces, void *stream);
 
 #ifdef __cplusplus
 }

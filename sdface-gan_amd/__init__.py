@@ -9,8 +9,8 @@ Drop-in surface (reference: im2scene/sdf/models/):
   GridEncoder, grid_encode                              (gridencoder/grid.py)
   SHEncoder, sh_encode                                  (shencoder/sphere_harmonics.py)
   generate_camera_params                                (sdf_utils.py:97-159)
-  align_volume, extract_mesh_with_marching_cubes,
-  xyz2mesh                                              (sdf_utils.py:164-223)
+  align_volume, extract_mesh_with_marching_cubes (+ marching_cubes, Mesh:
+  HIP, csrc/mesh.hip), xyz2mesh                       (sdf_utils.py:164-223)
   SDFOptions, vol_render_opt                            (sdf_utils.py:447, training_utils.py:144)
 Beyond the reference: GraphedGenerator (HIP-graph replay of the inference forward).
 """
@@ -22,7 +22,8 @@ from .generator import (Blur, Decoder, EqualLinear, FusedLeakyReLU, Generator,  
                         MappingLinear, ModulatedConv2d, NoiseInjection, PixelNorm, StyledConv,
                         ToRGB, Upsample, fused_leaky_relu, make_kernel, upfirdn2d)
 from .graphs import GraphedGenerator  # noqa: F401
-from .mesh import align_volume, extract_mesh_with_marching_cubes, xyz2mesh  # noqa: F401
+from .mesh import (Mesh, align_volume, extract_mesh_with_marching_cubes,  # noqa: F401
+                   marching_cubes, xyz2mesh)
 from .options import AttrDict, SDFOptions, vol_render_opt  # noqa: F401
 from . import training  # noqa: F401  (stage-2 DDP trainer, Discriminator, losses)
 from .renderer import (FCGenerator, FiLMSiren, LinearLayer, NGPSIRENGenerator,  # noqa: F401

@@ -23,7 +23,7 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 4
+ABI_VERSION = 5
 FIELD_F16X3 = 0
 FIELD_FP32 = 1
 
@@ -41,6 +41,7 @@ EXPORTS = (
     "sdfr_modulate_to_nhwc_split",
     "sdfr_conv_pack_bytes", "sdfr_conv_pack_weights", "sdfr_conv3x3_f16x3",
     "sdfr_conv3x3_f16x3_act", "sdfr_rgb_finish",
+    "sdfr_mc_workspace_bytes", "sdfr_mc_count", "sdfr_mc_emit",
 )
 
 
@@ -156,6 +157,13 @@ def lib():
     L.sdfr_conv_pack_weights.argtypes = [_vp, _f32, _u32, _u32, _vp, _vp, _vp]
     L.sdfr_conv3x3_f16x3.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _int, _vp]
     L.sdfr_conv3x3_f16x3_act.argtypes = [ctypes.POINTER(ConvActArgs), _vp]
+    _i64 = ctypes.c_int64
+    L.sdfr_mc_workspace_bytes.argtypes = [_u32, _u32, _u32]
+    L.sdfr_mc_workspace_bytes.restype = ctypes.c_size_t
+    L.sdfr_mc_count.argtypes = [_vp, _u32, _u32, _u32, _i64, _i64, _i64, _f32, _vp,
+                                ctypes.c_size_t, ctypes.POINTER(_u32), _vp]
+    L.sdfr_mc_emit.argtypes = [_vp, _u32, _u32, _u32, _i64, _i64, _i64, _f32, _vp,
+                               ctypes.c_size_t, _vp, _vp, _vp]
     L.sdfr_rgb_finish.argtypes = [_vp, _vp, _u32, _vp, _vp, ctypes.POINTER(_f32), _u32, _u32,
                                   _u32, _vp]
     v = L.sdfr_abi_version()

@@ -1,13 +1,15 @@
-"""Surface extraction helpers of sdf_mesh.py (im2scene/sdf/models/sdf_utils.py:164-223).
+"""Surface extraction of sdf_mesh.py (im2scene/sdf/models/sdf_utils.py:164-223).
 
 The SDF volume itself comes from the fused renderer: sdf_mesh.py builds a second
 Generator at 128^2 rays x 128 samples with return_sdf / return_xyz
 (sdf_mesh.py:244-252), whose forward runs ``sdfr_render_ngp_forward`` like any
 other render and returns the per-sample SDF as a [B, H, W, N, 1] volume.
 ``align_volume`` resamples that frustum-shaped volume onto a cube (device-side
-``grid_sample``, any device).  Marching cubes stays on the host: it needs
-scikit-image (and trimesh for the .obj export), which this image does not ship,
-so ``extract_mesh_with_marching_cubes`` raises ImportError naming them.
+``grid_sample``, any device).  ``extract_mesh_with_marching_cubes`` runs the
+HIP marching cubes (csrc/mesh.hip, ``sdfr_mc_count`` / ``sdfr_mc_emit``) where
+the reference calls scikit-image on the host, applies the reference's vertex
+scaling and axis flips, and returns a ``Mesh`` whose ``export(f, file_type='obj')``
+writes the .obj that sdf_mesh.py:176-182 writes through trimesh.
 """
 from __future__ import annotations
 
@@ -48,24 +50,83 @@ def align_volume(volume: torch.Tensor, near: float = 0.88, far: float = 1.12) ->
     return out
 
 
-def extract_mesh_with_marching_cubes(sdf: torch.Tensor):
-    """Zero level set of an aligned SDF volume [1, H, W, D, 1] (sdf_utils.py:188).
-    Returns a trimesh.Trimesh like the reference; needs scikit-image + trimesh."""
-    try:
-        from skimage.measure import marching_cubes
-        import trimesh
-    except ImportError as e:  # pragma: no cover - depends on the host image
-        raise ImportError("extract_mesh_with_marching_cubes needs scikit-image and trimesh "
-                          f"(host-side marching cubes): {e}") from e
+class Mesh:
+    """Indexed triangle mesh: ``vertices`` [V, 3] float32, ``faces`` [F, 3] int64
+    (counter-clockwise about the outward normal).  Stands in for the
+    ``trimesh.Trimesh`` the reference returns; trimesh's merge / cleanup
+    processing is not applied (vertices are already unique per grid edge)."""
+
+    def __init__(self, vertices, faces):
+        self.vertices = np.asarray(vertices, np.float32)
+        self.faces = np.asarray(faces, np.int64)
+
+    def export(self, file_obj=None, file_type="obj"):
+        """Wavefront .obj text (``v x y z`` lines, then 1-based ``f a b c``);
+        written to ``file_obj`` (an open text file or a path) when given."""
+        if file_type != "obj":
+            raise ValueError(f"Mesh.export: only 'obj' is supported, not {file_type!r}")
+        lines = ["v %.8f %.8f %.8f" % tuple(v) for v in self.vertices.tolist()]
+        lines += ["f %d %d %d" % tuple(f) for f in (self.faces + 1).tolist()]
+        text = "\n".join(lines) + "\n"
+        if file_obj is None:
+            return text
+        if hasattr(file_obj, "write"):
+            file_obj.write(text)
+        else:
+            with open(file_obj, "w") as f:
+                f.write(text)
+        return text
+
+
+def marching_cubes(volume: torch.Tensor, level: float = 0.0):
+    """Zero (``level``) set of an fp32 volume [n0, n1, n2] on the GPU (any strides):
+    (verts [V, 3] fp32 in index coordinates, faces [F, 3] int32), both on the
+    volume's device.  ValueError when no grid edge crosses ``level`` (scikit-image
+    raises ValueError for a level outside the data range, which sdf_mesh.py:170-174
+    catches)."""
+    from . import _lib
+    if volume.dim() != 3:
+        raise ValueError(f"marching_cubes: expected a 3-D volume, got {tuple(volume.shape)}")
+    if not volume.is_cuda:
+        raise RuntimeError("marching_cubes: the volume must be on the GPU (HIP kernel)")
+    if volume.dtype != torch.float32:
+        volume = volume.float()
+    L = _lib.lib()
+    n0, n1, n2 = volume.shape
+    s0, s1, s2 = volume.stride()
+    ws_bytes = L.sdfr_mc_workspace_bytes(n0, n1, n2)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=volume.device)
+    counts = (_lib._u32 * 2)()
+    st = _lib.stream_of(volume)
+    args = (_lib.ptr(volume), n0, n1, n2, s0, s1, s2, float(level), _lib.ptr(ws), ws_bytes)
+    _lib.check(L.sdfr_mc_count(*args, counts, st), "marching_cubes")
+    nv, nf = int(counts[0]), int(counts[1])
+    if nv == 0:
+        raise ValueError("Surface level must be within volume data range.")
+    verts = torch.empty(nv, 3, dtype=torch.float32, device=volume.device)
+    faces = torch.empty(nf, 3, dtype=torch.int32, device=volume.device)
+    _lib.check(L.sdfr_mc_emit(*args, _lib.ptr(verts), _lib.ptr(faces), st), "marching_cubes")
+    return verts, faces
+
+
+def extract_mesh_with_marching_cubes(sdf: torch.Tensor) -> Mesh:
+    """Zero level set of an aligned SDF volume [1, H, W, D, 1] (sdf_utils.py:188-205):
+    the volume read as (x, y, z) = (W, H, D) (the reference's permute(1, 0, 2), here
+    a stride swap), vertices scaled to (v / size - 0.5) * 0.24 per axis and y, z
+    negated.  A host tensor is moved to the GPU (the reference's caller passes one,
+    sdf_mesh.py:153-170)."""
     b, h, w, d, _ = sdf.shape
-    vol = sdf[0, ..., 0].permute(1, 0, 2).cpu().numpy()
-    verts, faces, _, _ = marching_cubes(vol, 0)
-    verts[:, 0] = (verts[:, 0] / float(w) - 0.5) * 0.24
-    verts[:, 1] = (verts[:, 1] / float(h) - 0.5) * 0.24
-    verts[:, 2] = (verts[:, 2] / float(d) - 0.5) * 0.24
+    vol = sdf[0, ..., 0]
+    if not vol.is_cuda:
+        if not torch.cuda.is_available():
+            raise RuntimeError("extract_mesh_with_marching_cubes: needs the GPU (HIP kernel)")
+        vol = vol.to("cuda")
+    verts, faces = marching_cubes(vol.permute(1, 0, 2), 0.0)
+    for axis, size in enumerate((w, h, d)):
+        verts[:, axis] = (verts[:, axis] / float(size) - 0.5) * 0.24
     verts[:, 2] *= -1
     verts[:, 1] *= -1
-    return trimesh.Trimesh(verts, faces)
+    return Mesh(verts.cpu().numpy(), faces.cpu().numpy())
 
 
 def xyz2mesh(xyz: torch.Tensor):
