@@ -78,6 +78,22 @@ int sdfr_grid_encode_backward(const float *grad, const float *inputs,
                               uint32_t gridtype, int align_corners,
                               uint32_t interp, void *stream);
 
+/* The same with a caller-owned device workspace of at least
+ * sdfr_grid_encode_backward_ws_bytes(...) bytes (0 = none needed: then ws may be
+ * NULL).  With it, the table gradient of the fine levels is binned and summed in
+ * LDS instead of scattered with global atomics (csrc/encoders.hip); with ws NULL
+ * or too small, the direct-atomic path runs.  sdfr_grid_encode_backward is this
+ * function with a library-owned workspace. */
+size_t sdfr_grid_encode_backward_ws_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                                          float S, uint32_t H, int align_corners);
+int sdfr_grid_encode_backward_ws(const float *grad, const float *inputs,
+                                 const float *embeddings, const int32_t *offsets,
+                                 float *grad_embeddings, uint32_t B, uint32_t D,
+                                 uint32_t C, uint32_t L, float S, uint32_t H,
+                                 const float *dy_dx, float *grad_inputs,
+                                 uint32_t gridtype, int align_corners,
+                                 uint32_t interp, void *ws, size_t ws_bytes, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Real spherical harmonics (shencoder.cu semantics), C = degree.
  *   inputs [B, D], D must be 3; outputs [B, C*C]; dy_dx [B, D*C*C] or NULL.

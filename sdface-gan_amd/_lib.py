@@ -31,6 +31,7 @@ FIELD_FP32 = 1
 EXPORTS = (
     "sdfr_abi_version", "sdfr_last_error",
     "sdfr_grid_encode_forward", "sdfr_grid_encode_backward",
+    "sdfr_grid_encode_backward_ws_bytes", "sdfr_grid_encode_backward_ws",
     "sdfr_sh_encode_forward", "sdfr_sh_encode_backward",
     "sdfr_render_ngp_workspace_bytes", "sdfr_render_ngp_forward",
     "sdfr_render_ngp_encode_only", "sdfr_debug_set_field_variant", "sdfr_debug_sin_probe",
@@ -129,6 +130,10 @@ def lib():
                                            _u32, _vp, _u32, _int, _u32, _vp]
     L.sdfr_grid_encode_backward.argtypes = [_vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32,
                                             _f32, _u32, _vp, _vp, _u32, _int, _u32, _vp]
+    L.sdfr_grid_encode_backward_ws_bytes.argtypes = [_u32, _u32, _u32, _u32, _f32, _u32, _int]
+    L.sdfr_grid_encode_backward_ws_bytes.restype = ctypes.c_size_t
+    L.sdfr_grid_encode_backward_ws.argtypes = (L.sdfr_grid_encode_backward.argtypes[:-1]
+                                               + [_vp, ctypes.c_size_t, _vp])
     L.sdfr_sh_encode_forward.argtypes = [_vp, _vp, _u32, _u32, _u32, _vp, _vp]
     L.sdfr_sh_encode_backward.argtypes = [_vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp]
     L.sdfr_render_ngp_workspace_bytes.restype = ctypes.c_size_t

@@ -15,9 +15,13 @@
 #include <cmath>
 
 #include <cstdio>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 
 #include "sdfr_common.h"
+#include "sdfr_scan.h"
 
 namespace sdfr {
 
@@ -278,6 +282,298 @@ grid_bwd_lds_kernel(const float *__restrict__ grad, const float *__restrict__ in
     }
 }
 
+// Table gradient, binned (B >= 4096, D <= 3, with a workspace).  Direct fp32
+// atomics ran at ~15 G adds/s on the hashed levels whatever the sample order
+// (uniform random and the renderer's tile order alike: 39.7 / 35.5 ms for 3.1 M
+// samples x 16 levels x 8 corners x 2 channels), i.e. the atomic path itself,
+// not address contention, was the limit; and the coarse levels' LDS windows
+// (grid_bwd_lds_kernel) re-evaluate every sample once per window.  Here every
+// (sample, level, corner) contribution becomes one entry (row, w * grad[C]),
+// counting-sorted into 32 bins of 2^sh rows per level (sh = log2 of the LDS
+// window unless the level has more rows), and each bin is summed in LDS
+// (ds_add_f32) and added to the table once.  Five launches:
+//   grid_bin_count_kernel     per (block of samples, level): entries per bin
+//   exclusive_scan_u32        counts, laid out [level][bin][block], -> offsets
+//   grid_bin_scatter_kernel   recompute the entries, counting-sort them per
+//                             block in LDS, write each bin's run contiguously
+//   grid_bin_plan_kernel      cut every bin into work items of <= kBinChunk
+//                             entries (a coarse level's single bin holds all
+//                             of its B x 8 entries; a hashed bin ~B x 8 / 32)
+//   grid_bin_accum_kernel     per item: LDS window sums -> table, plain
+//                             read-modify-write when the item is its whole bin
+//                             (rows owned by one workgroup), else atomics on
+//                             the touched rows only.  Bound by the LDS float
+//                             atomics (4.6 ms at 3.1 M samples; 1.3 ms with
+//                             plain, racy LDS adds = the streaming floor)
+// HBM traffic per entry: 4 + 4C bytes written and read once (3.3 GB at 3.1 M
+// samples x 11 hashed levels), plus the inputs twice and the gradient once.
+// The per-entry products are grid_bwd_kernel's; the fp32 sums are
+// re-associated, as the reference's atomics are.
+constexpr uint32_t kBinCount = 32;
+constexpr uint32_t kBinThreads = 256;
+constexpr uint32_t kBinAccThreads = 1024;
+constexpr uint32_t kBinLdsBytes = 128 * 1024;
+template <uint32_t C>
+constexpr uint32_t bin_rows() { return kBinLdsBytes / (4 * C); }   // LDS window (rows)
+template <uint32_t C>
+constexpr uint32_t bin_it() { return C <= 2 ? 2 : 1; }              // samples per thread
+template <uint32_t C>
+constexpr uint32_t bin_spb() { return kBinThreads * bin_it<C>(); }  // samples per block
+
+struct BinLevels {
+    uint8_t level[kMaxLevels];
+    uint32_t n;
+};
+
+// the smallest sh >= log2(window) with hsize <= kBinCount << sh
+template <uint32_t C>
+__device__ __forceinline__ uint32_t bin_shift(uint32_t hsize) {
+    uint32_t sh = 31u - __builtin_clz(bin_rows<C>());
+    while (((uint64_t)kBinCount << sh) < hsize) ++sh;
+    return sh;
+}
+
+// rows and interpolation weights of a sample's 2^D corners (grid_bwd_kernel's)
+template <uint32_t D, uint32_t C>
+__device__ __forceinline__ bool sample_corners(const float *__restrict__ inputs, uint32_t b,
+                                               const LevelParam &q, int align_corners,
+                                               uint32_t interp, uint32_t (&row)[1u << D],
+                                               float (&w)[1u << D]) {
+    float x[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) {
+        x[d] = inputs[(size_t)b * D + d];
+        if (x[d] < 0 || x[d] > 1) return false;     // grad stays 0 (gridencoder.cu:277-282)
+    }
+    LevelCoord<D, C> lc;
+    level_coord<D, C>(x, q, align_corners, interp, lc);
+#pragma unroll
+    for (uint32_t idx = 0; idx < (1u << D); ++idx) {
+        float wi = 1.0f;
+        uint32_t pl[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) {
+            if ((idx & (1u << d)) == 0) {
+                wi = __fmul_rn(wi, __fsub_rn(1.0f, lc.pos[d]));
+                pl[d] = lc.pg[d];
+            } else {
+                wi = __fmul_rn(wi, lc.pos[d]);
+                pl[d] = lc.pg[d] + 1;
+            }
+        }
+        w[idx] = wi;
+        row[idx] = grid_index<D>(q, align_corners, pl);
+    }
+    return true;
+}
+
+template <uint32_t D, uint32_t C>
+__global__ void __launch_bounds__(kBinThreads)
+grid_bin_count_kernel(const float *__restrict__ inputs, const int32_t *__restrict__ offsets,
+                      uint32_t B, const LevelTable lt, uint32_t gridtype, int align_corners,
+                      uint32_t interp, const BinLevels bl, uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t hist[kBinCount];
+    const uint32_t li = blockIdx.y, level = bl.level[li];
+    LevelParam q = lt.p[level];
+    finish_level(q, offsets, level, D, gridtype, align_corners);
+    const uint32_t sh = bin_shift<C>(q.hsize);
+    if (threadIdx.x < kBinCount) hist[threadIdx.x] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t it = 0; it < bin_it<C>(); ++it) {
+        const uint32_t b = blockIdx.x * bin_spb<C>() + it * kBinThreads + threadIdx.x;
+        uint32_t row[1u << D];
+        float w[1u << D];
+        if (b < B && sample_corners<D, C>(inputs, b, q, align_corners, interp, row, w))
+#pragma unroll
+            for (uint32_t idx = 0; idx < (1u << D); ++idx) atomicAdd(&hist[row[idx] >> sh], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kBinCount)
+        cnt[((size_t)li * kBinCount + threadIdx.x) * gridDim.x + blockIdx.x] = hist[threadIdx.x];
+}
+
+template <uint32_t D, uint32_t C>
+__global__ void __launch_bounds__(kBinThreads)
+grid_bin_scatter_kernel(const float *__restrict__ grad, const float *__restrict__ inputs,
+                        const int32_t *__restrict__ offsets, uint32_t B, const LevelTable lt,
+                        uint32_t gridtype, int align_corners, uint32_t interp, const BinLevels bl,
+                        const uint32_t *__restrict__ ofs, uint32_t *__restrict__ e_row,
+                        float *__restrict__ e_val) {
+    constexpr uint32_t K = 1u << D, IT = bin_it<C>(), E = kBinThreads * IT * K;
+    __shared__ uint32_t hist[kBinCount], lofs[kBinCount + 1];
+    __shared__ uint32_t s_row[E];
+    __shared__ float s_val[E * C];
+    const uint32_t li = blockIdx.y, level = bl.level[li];
+    LevelParam q = lt.p[level];
+    finish_level(q, offsets, level, D, gridtype, align_corners);
+    const uint32_t sh = bin_shift<C>(q.hsize);
+    if (threadIdx.x < kBinCount) hist[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t row[IT][K], slot[IT][K];
+    float w[IT][K], g[IT][C];
+    bool ok[IT];
+#pragma unroll
+    for (uint32_t it = 0; it < IT; ++it) {
+        const uint32_t b = blockIdx.x * bin_spb<C>() + it * kBinThreads + threadIdx.x;
+        ok[it] = b < B && sample_corners<D, C>(inputs, b, q, align_corners, interp, row[it], w[it]);
+        if (ok[it]) {
+#pragma unroll
+            for (uint32_t c = 0; c < C; ++c) g[it][c] = grad[((size_t)level * B + b) * C + c];
+#pragma unroll
+            for (uint32_t idx = 0; idx < K; ++idx)
+                slot[it][idx] = atomicAdd(&hist[row[it][idx] >> sh], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < kBinCount; ++k) {
+            lofs[k] = run;
+            run += hist[k];
+        }
+        lofs[kBinCount] = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t it = 0; it < IT; ++it) {
+        if (!ok[it]) continue;
+#pragma unroll
+        for (uint32_t idx = 0; idx < K; ++idx) {
+            const uint32_t p = lofs[row[it][idx] >> sh] + slot[it][idx];
+            s_row[p] = row[it][idx];
+#pragma unroll
+            for (uint32_t c = 0; c < C; ++c) s_val[p * C + c] = __fmul_rn(w[it][idx], g[it][c]);
+        }
+    }
+    __syncthreads();
+    const uint32_t total = lofs[kBinCount];
+    for (uint32_t i = threadIdx.x; i < total; i += kBinThreads) {
+        uint32_t lo = 0, hi = kBinCount;     // the last bin starting at or before i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (lofs[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        const size_t gp = ofs[((size_t)li * kBinCount + lo) * gridDim.x + blockIdx.x] + (i - lofs[lo]);
+        e_row[gp] = s_row[i];
+#pragma unroll
+        for (uint32_t c = 0; c < C; ++c) e_val[gp * C + c] = s_val[i * C + c];
+    }
+}
+
+constexpr uint32_t kBinChunk = 1u << 20;      // entries per work item (at most)
+
+struct BinItem {
+    uint32_t pair;     // level index * kBinCount + bin
+    uint32_t start, end;
+    uint32_t whole;    // the item is its bin's only one
+};
+
+// one workgroup: cut each (level, bin) entry run into items of <= kBinChunk
+__global__ void __launch_bounds__(kScanThreads)
+grid_bin_plan_kernel(const uint32_t *__restrict__ ofs, uint32_t nblk, uint32_t npairs,
+                     BinItem *__restrict__ items, uint32_t *__restrict__ nitems) {
+    uint32_t carry = 0;
+    for (uint32_t p0 = 0; p0 < npairs; p0 += kScanThreads) {
+        const uint32_t p = p0 + threadIdx.x;
+        uint32_t s = 0, e = 0, n = 0;
+        if (p < npairs) {
+            s = ofs[(size_t)p * nblk];
+            e = ofs[(size_t)(p + 1) * nblk];
+            n = (e - s + kBinChunk - 1) / kBinChunk;
+        }
+        uint32_t ex;
+        const uint32_t tot = block_exscan(n, ex);
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t a = s + k * kBinChunk;
+            items[carry + ex + k] = BinItem{p, a, min(e, a + kBinChunk), n == 1 ? 1u : 0u};
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *nitems = carry;
+}
+
+template <uint32_t C>
+__global__ void __launch_bounds__(kBinAccThreads)
+grid_bin_accum_kernel(const int32_t *__restrict__ offsets, const LevelTable lt, uint32_t D,
+                      uint32_t gridtype, int align_corners, const BinLevels bl,
+                      const BinItem *__restrict__ items, const uint32_t *__restrict__ nitems,
+                      const uint32_t *__restrict__ e_row, const float *__restrict__ e_val,
+                      float *__restrict__ grad_emb) {
+    extern __shared__ float acc[];
+    constexpr uint32_t R = bin_rows<C>();
+    constexpr uint32_t U = 4;                    // entries in flight per thread
+    if (blockIdx.x >= *nitems) return;
+    const BinItem it = items[blockIdx.x];
+    const uint32_t li = it.pair / kBinCount, bin = it.pair % kBinCount, level = bl.level[li];
+    LevelParam q = lt.p[level];
+    finish_level(q, offsets, level, D, gridtype, align_corners);
+    const uint32_t sh = bin_shift<C>(q.hsize);
+    const uint64_t base = (uint64_t)bin << sh;
+    if (base >= q.hsize) return;
+    const uint32_t end_row = (uint32_t)min((uint64_t)q.hsize, base + (1ull << sh));
+    float *gg = grad_emb + (size_t)q.offset * C;
+    // one sweep when the bin fits the LDS window (sh = log2 R), more for bigger tables
+    for (uint32_t w0 = (uint32_t)base; w0 < end_row; w0 += R) {
+        for (uint32_t i = threadIdx.x; i < R * C; i += kBinAccThreads) acc[i] = 0.0f;
+        __syncthreads();
+        for (uint32_t i0 = it.start + threadIdx.x; i0 < it.end; i0 += U * kBinAccThreads) {
+            uint32_t r[U];
+            float v[U][C];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t i = i0 + u * kBinAccThreads;
+                r[u] = i < it.end ? e_row[i] - w0 : R;
+#pragma unroll
+                for (uint32_t c = 0; c < C; ++c) v[u][c] = i < it.end ? e_val[(size_t)i * C + c] : 0.0f;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
+                if (r[u] < R)
+#pragma unroll
+                    for (uint32_t c = 0; c < C; ++c) atomicAdd(&acc[r[u] * C + c], v[u][c]);
+        }
+        __syncthreads();
+        const uint32_t n = min(R, end_row - w0) * C;
+        for (uint32_t i = threadIdx.x; i < n; i += kBinAccThreads) {
+            const float v = acc[i];
+            if (v == 0.0f) continue;
+            if (it.whole) gg[(size_t)w0 * C + i] += v;     // rows owned by this workgroup
+            else atomicAdd(gg + (size_t)w0 * C + i, v);
+        }
+        __syncthreads();
+    }
+}
+
+// workspace of the binned path: counts [n_b][32][nblk] + 1, scan scratch,
+// entries, work items
+struct BinPlan {
+    uint32_t nblk, n, max_items;
+    uint64_t M, E;
+    size_t cnt_off, bsum_off, row_off, val_off, item_off, nitem_off, bytes;
+};
+
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+template <uint32_t C>
+static BinPlan bin_plan(uint32_t B, uint32_t D, uint32_t n_b) {
+    BinPlan p{};
+    p.n = n_b;
+    p.nblk = (B + bin_spb<C>() - 1) / bin_spb<C>();
+    p.M = (uint64_t)n_b * kBinCount * p.nblk;
+    p.E = (uint64_t)B * (1u << D) * n_b;
+    p.cnt_off = 0;
+    p.bsum_off = align256((p.M + 1) * sizeof(uint32_t));
+    p.row_off = p.bsum_off + align256((size_t)scan_block_sums(p.M) * sizeof(uint32_t));
+    p.val_off = p.row_off + align256(p.E * sizeof(uint32_t));
+    p.max_items = (uint32_t)(n_b * kBinCount + (p.E + kBinChunk - 1) / kBinChunk);
+    p.item_off = p.val_off + align256(p.E * C * sizeof(float));
+    p.nitem_off = p.item_off + align256((size_t)p.max_items * sizeof(BinItem));
+    p.bytes = p.nitem_off + 256;
+    return p;
+}
+
 template <uint32_t D, uint32_t C>
 static int grid_fwd_launch(const float *in, const float *emb, const int32_t *off, float *out,
                            float *dydx, uint32_t B, uint32_t L, const LevelTable &lt,
@@ -289,25 +585,16 @@ static int grid_fwd_launch(const float *in, const float *emb, const int32_t *off
     return check_launch("grid_encode_forward");
 }
 
+// levels of the LDS-window path (bit mask) and the binned levels, as grid_bwd_launch plans them
 template <uint32_t D, uint32_t C>
-static int grid_bwd_launch(const float *grad, const float *in, const int32_t *off, float *gemb,
-                           const float *dydx, float *gin, uint32_t B, uint32_t L,
-                           const LevelTable &lt, uint32_t gt, int ac, uint32_t interp,
-                           hipStream_t st) {
-    // coarse levels go through LDS windows: a level holds at most (res+1)^D rows
-    // rounded up to 8 (grid.py:117-128), so a level whose bound needs at most
-    // kBwdLevelWins windows is planned that many (the device skips windows past
-    // the level's real size, from `offsets`, and the last one adds any rows
-    // beyond the plan directly).  The fine, hashed levels keep direct atomics:
-    // their rows are spread over 4 MB tables (little same-address contention),
-    // and re-reading every sample per window costs more than it saves
-    // (measured: all 16 levels windowed 65 ms vs 39.5 ms at 3.1 M samples).
-    // Below 4096 samples every level uses the direct atomics.
+static uint64_t window_levels(uint32_t B, uint32_t L, const LevelTable &lt, int ac,
+                              BwdWindows *wt) {
     const uint32_t win_rows = kBwdLdsBytes / sizeof(float) / C;
-    BwdWindows wt;
-    wt.nlevels = L;
-    wt.start[0] = 0;
     uint64_t lds_levels = 0;
+    if (wt) {
+        wt->nlevels = L;
+        wt->start[0] = 0;
+    }
     for (uint32_t l = 0; l < L; ++l) {
         uint32_t nwin = 0;
         if (B >= 4096) {
@@ -319,34 +606,110 @@ static int grid_bwd_launch(const float *grad, const float *in, const int32_t *of
                 lds_levels |= 1ull << l;
             }
         }
-        wt.start[l + 1] = (uint16_t)(wt.start[l] + nwin);
+        if (wt) wt->start[l + 1] = (uint16_t)(wt->start[l] + nwin);
     }
-    const uint32_t nwins = wt.start[L];
-    if (nwins) {
-        // ~256 workgroups over all windows, >= 4096 samples each
-        const uint32_t nblk = std::max<uint32_t>(1, std::min<uint32_t>((B + 4095) / 4096,
-                                                                     (256 + nwins - 1) / nwins));
-        const uint32_t per_block = (B + nblk - 1) / nblk;
+    return lds_levels;
+}
+
+// binned path applies: D <= 3 (LDS staging of 2^D corners per sample), B >= 4096,
+// and the entry count fits the uint32 scan; it then takes every level
+template <uint32_t D, uint32_t C>
+static bool bin_levels(uint32_t B, uint32_t L, BinLevels &bl) {
+    bl.n = 0;
+    if (D > 3 || B < 4096) return false;
+    for (uint32_t l = 0; l < L; ++l) bl.level[bl.n++] = (uint8_t)l;
+    return (uint64_t)B * (1u << D) * bl.n < (1ull << 32) - 1;
+}
+
+template <uint32_t D, uint32_t C>
+static size_t grid_bwd_ws_bytes_t(uint32_t B, uint32_t L) {
+    BinLevels bl;
+    if (!bin_levels<D, C>(B, L, bl)) return 0;
+    return bin_plan<C>(B, D, bl.n).bytes;
+}
+
+template <uint32_t D, uint32_t C>
+static int grid_bin_launch(const float *grad, const float *in, const int32_t *off, float *gemb,
+                           uint32_t B, const LevelTable &lt, uint32_t gt, int ac, uint32_t interp,
+                           const BinLevels &bl, void *ws, hipStream_t st) {
+    if constexpr (D <= 3) {
+        const BinPlan p = bin_plan<C>(B, D, bl.n);
+        char *w = (char *)ws;
+        uint32_t *cnt = (uint32_t *)(w + p.cnt_off), *bsum = (uint32_t *)(w + p.bsum_off);
+        uint32_t *e_row = (uint32_t *)(w + p.row_off);
+        float *e_val = (float *)(w + p.val_off);
+        const dim3 grid(p.nblk, bl.n);
+        hipLaunchKernelGGL((grid_bin_count_kernel<D, C>), grid, dim3(kBinThreads), 0, st, in, off,
+                           B, lt, gt, ac, interp, bl, cnt);
+        exclusive_scan_u32(cnt, p.M, bsum, st);
+        hipLaunchKernelGGL((grid_bin_scatter_kernel<D, C>), grid, dim3(kBinThreads), 0, st, grad,
+                           in, off, B, lt, gt, ac, interp, bl, cnt, e_row, e_val);
         static bool attr_set = false;   // > 64 KB of dynamic LDS must be opted into
         if (!attr_set) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&grid_bwd_lds_kernel<D, C>),
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&grid_bin_accum_kernel<C>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kBwdLdsBytes) != hipSuccess)
-                return fail(SDFR_ELAUNCH, "grid_encode_backward: LDS attribute");
+                                    (int)kBinLdsBytes) != hipSuccess)
+                return fail(SDFR_ELAUNCH, "grid_encode_backward: LDS attribute (bins)");
             attr_set = true;
         }
-        hipLaunchKernelGGL((grid_bwd_lds_kernel<D, C>), dim3(nblk, nwins), dim3(1024),
-                           kBwdLdsBytes, st, grad, in, off, gemb, B, lt, gt, ac, interp, wt,
-                           per_block);
-        int rc = check_launch("grid_encode_backward(lds windows)");
-        if (rc) return rc;
+        BinItem *items = (BinItem *)(w + p.item_off);
+        uint32_t *nitems = (uint32_t *)(w + p.nitem_off);
+        hipLaunchKernelGGL(grid_bin_plan_kernel, dim3(1), dim3(kScanThreads), 0, st, cnt, p.nblk,
+                           bl.n * kBinCount, items, nitems);
+        hipLaunchKernelGGL((grid_bin_accum_kernel<C>), dim3(p.max_items), dim3(kBinAccThreads),
+                           kBinLdsBytes, st, off, lt, D, gt, ac, bl, items, nitems, e_row, e_val,
+                           gemb);
+        return check_launch("grid_encode_backward(bins)");
+    } else {
+        return fail(SDFR_EINVAL, "grid_encode_backward: binned path needs D <= 3");
     }
+}
+
+template <uint32_t D, uint32_t C>
+static int grid_bwd_launch(const float *grad, const float *in, const int32_t *off, float *gemb,
+                           const float *dydx, float *gin, uint32_t B, uint32_t L,
+                           const LevelTable &lt, uint32_t gt, int ac, uint32_t interp,
+                           void *ws, size_t ws_bytes, hipStream_t st) {
     int rc = SDFR_OK;
-    if (lds_levels != (L == 64 ? ~0ull : (1ull << L) - 1ull)) {
-        dim3 grid((B + 255) / 256, L);
-        hipLaunchKernelGGL((grid_bwd_kernel<D, C>), grid, dim3(256), 0, st, grad, in, off, gemb,
-                           B, lt, gt, ac, interp, lds_levels);
-        rc = check_launch("grid_encode_backward");
+    BinLevels bl;
+    if (ws && bin_levels<D, C>(B, L, bl) && ws_bytes >= bin_plan<C>(B, D, bl.n).bytes) {
+        // every level binned (the per-level table gradient above)
+        rc = grid_bin_launch<D, C>(grad, in, off, gemb, B, lt, gt, ac, interp, bl, ws, st);
+    } else {
+        // without a workspace: coarse levels through LDS windows -- a level holds at
+        // most (res+1)^D rows rounded up to 8 (grid.py:117-128), so a level whose
+        // bound needs at most kBwdLevelWins windows is planned that many (the device
+        // skips windows past the level's real size, from `offsets`, and the last one
+        // adds any rows beyond the plan directly); the fine, hashed levels by direct
+        // atomics.  Below 4096 samples every level uses the direct atomics.
+        BwdWindows wt;
+        const uint64_t lds_levels = window_levels<D, C>(B, L, lt, ac, &wt);
+        const uint32_t nwins = wt.start[L];
+        if (nwins) {
+            // ~256 workgroups over all windows, >= 4096 samples each
+            const uint32_t nblk = std::max<uint32_t>(
+                1, std::min<uint32_t>((B + 4095) / 4096, (256 + nwins - 1) / nwins));
+            const uint32_t per_block = (B + nblk - 1) / nblk;
+            static bool attr_set = false;   // > 64 KB of dynamic LDS must be opted into
+            if (!attr_set) {
+                if (hipFuncSetAttribute(reinterpret_cast<const void *>(&grid_bwd_lds_kernel<D, C>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)kBwdLdsBytes) != hipSuccess)
+                    return fail(SDFR_ELAUNCH, "grid_encode_backward: LDS attribute");
+                attr_set = true;
+            }
+            hipLaunchKernelGGL((grid_bwd_lds_kernel<D, C>), dim3(nblk, nwins), dim3(1024),
+                               kBwdLdsBytes, st, grad, in, off, gemb, B, lt, gt, ac, interp, wt,
+                               per_block);
+            rc = check_launch("grid_encode_backward(lds windows)");
+            if (rc) return rc;
+        }
+        if (lds_levels != (L == 64 ? ~0ull : (1ull << L) - 1ull)) {
+            dim3 grid((B + 255) / 256, L);
+            hipLaunchKernelGGL((grid_bwd_kernel<D, C>), grid, dim3(256), 0, st, grad, in, off,
+                               gemb, B, lt, gt, ac, interp, lds_levels);
+            rc = check_launch("grid_encode_backward");
+        }
     }
     if (rc || !dydx || !gin) return rc;
     hipLaunchKernelGGL((grid_input_bwd_kernel<D, C>), dim3((B * D + 255) / 256), dim3(256), 0,
@@ -372,14 +735,25 @@ template <uint32_t D>
 static int grid_bwd_dispatch_c(uint32_t C, const float *grad, const float *in, const int32_t *off,
                                float *gemb, const float *dydx, float *gin, uint32_t B, uint32_t L,
                                const LevelTable &lt, uint32_t gt, int ac, uint32_t interp,
-                               hipStream_t st) {
+                               void *ws, size_t wsb, hipStream_t st) {
     switch (C) {
-        case 1: return grid_bwd_launch<D, 1>(grad, in, off, gemb, dydx, gin, B, L, lt, gt, ac, interp, st);
-        case 2: return grid_bwd_launch<D, 2>(grad, in, off, gemb, dydx, gin, B, L, lt, gt, ac, interp, st);
-        case 4: return grid_bwd_launch<D, 4>(grad, in, off, gemb, dydx, gin, B, L, lt, gt, ac, interp, st);
-        case 8: return grid_bwd_launch<D, 8>(grad, in, off, gemb, dydx, gin, B, L, lt, gt, ac, interp, st);
+        case 1: return grid_bwd_launch<D, 1>(grad, in, off, gemb, dydx, gin, B, L, lt, gt, ac, interp, ws, wsb, st);
+        case 2: return grid_bwd_launch<D, 2>(grad, in, off, gemb, dydx, gin, B, L, lt, gt, ac, interp, ws, wsb, st);
+        case 4: return grid_bwd_launch<D, 4>(grad, in, off, gemb, dydx, gin, B, L, lt, gt, ac, interp, ws, wsb, st);
+        case 8: return grid_bwd_launch<D, 8>(grad, in, off, gemb, dydx, gin, B, L, lt, gt, ac, interp, ws, wsb, st);
     }
     return fail(SDFR_EINVAL, "GridEncoding: C must be 1, 2, 4, or 8.");
+}
+
+template <uint32_t D>
+static size_t grid_bwd_ws_dispatch_c(uint32_t C, uint32_t B, uint32_t L) {
+    switch (C) {
+        case 1: return grid_bwd_ws_bytes_t<D, 1>(B, L);
+        case 2: return grid_bwd_ws_bytes_t<D, 2>(B, L);
+        case 4: return grid_bwd_ws_bytes_t<D, 4>(B, L);
+        case 8: return grid_bwd_ws_bytes_t<D, 8>(B, L);
+    }
+    return 0;
 }
 
 // ----------------------------------------------------------------------------
@@ -521,11 +895,23 @@ int sdfr_grid_encode_forward(const float *inputs, const float *embeddings,
     }
 }
 
-int sdfr_grid_encode_backward(const float *grad, const float *inputs, const float *embeddings,
-                              const int32_t *offsets, float *grad_embeddings, uint32_t B,
-                              uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
-                              const float *dy_dx, float *grad_inputs, uint32_t gridtype,
-                              int align_corners, uint32_t interp, void *stream) {
+size_t sdfr_grid_encode_backward_ws_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                                          float S, uint32_t H, int align_corners) {
+    if (D < 2 || D > 3 || !(C == 1 || C == 2 || C == 4 || C == 8) || L == 0 ||
+        L > (uint32_t)kMaxLevels)
+        return 0;
+    (void)S;
+    (void)H;
+    (void)align_corners;
+    return D == 2 ? grid_bwd_ws_dispatch_c<2>(C, B, L) : grid_bwd_ws_dispatch_c<3>(C, B, L);
+}
+
+int sdfr_grid_encode_backward_ws(const float *grad, const float *inputs, const float *embeddings,
+                                 const int32_t *offsets, float *grad_embeddings, uint32_t B,
+                                 uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                                 const float *dy_dx, float *grad_inputs, uint32_t gridtype,
+                                 int align_corners, uint32_t interp, void *ws, size_t ws_bytes,
+                                 void *stream) {
     (void)embeddings;
     if (D < 2 || D > 5) return fail(SDFR_EINVAL, "GridEncoding: D must be 2, 3, 4, or 5.");
     if (!(C == 1 || C == 2 || C == 4 || C == 8))
@@ -541,11 +927,46 @@ int sdfr_grid_encode_backward(const float *grad, const float *inputs, const floa
     LevelTable lt;
     make_level_table(L, S, H, lt);
     switch (D) {
-        case 2: return grid_bwd_dispatch_c<2>(C, grad, inputs, offsets, grad_embeddings, dy_dx, grad_inputs, B, L, lt, gridtype, align_corners, interp, st);
-        case 3: return grid_bwd_dispatch_c<3>(C, grad, inputs, offsets, grad_embeddings, dy_dx, grad_inputs, B, L, lt, gridtype, align_corners, interp, st);
-        case 4: return grid_bwd_dispatch_c<4>(C, grad, inputs, offsets, grad_embeddings, dy_dx, grad_inputs, B, L, lt, gridtype, align_corners, interp, st);
-        default: return grid_bwd_dispatch_c<5>(C, grad, inputs, offsets, grad_embeddings, dy_dx, grad_inputs, B, L, lt, gridtype, align_corners, interp, st);
+        case 2: return grid_bwd_dispatch_c<2>(C, grad, inputs, offsets, grad_embeddings, dy_dx, grad_inputs, B, L, lt, gridtype, align_corners, interp, ws, ws_bytes, st);
+        case 3: return grid_bwd_dispatch_c<3>(C, grad, inputs, offsets, grad_embeddings, dy_dx, grad_inputs, B, L, lt, gridtype, align_corners, interp, ws, ws_bytes, st);
+        case 4: return grid_bwd_dispatch_c<4>(C, grad, inputs, offsets, grad_embeddings, dy_dx, grad_inputs, B, L, lt, gridtype, align_corners, interp, ws, ws_bytes, st);
+        default: return grid_bwd_dispatch_c<5>(C, grad, inputs, offsets, grad_embeddings, dy_dx, grad_inputs, B, L, lt, gridtype, align_corners, interp, ws, ws_bytes, st);
     }
+}
+
+// The reference signature has no workspace: the binned path then uses a
+// library-owned device buffer, grown on demand (hipMalloc, one per device) and
+// kept for later calls.  Calls from several host threads on different streams
+// would share it: such callers use sdfr_grid_encode_backward_ws.
+static void *grid_bwd_internal_ws(size_t bytes) {
+    static std::mutex mu;
+    static std::map<int, std::pair<void *, size_t>> bufs;
+    std::lock_guard<std::mutex> lock(mu);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    auto &b = bufs[dev];
+    if (b.second < bytes) {
+        if (b.first) (void)hipFree(b.first);
+        b = {nullptr, 0};
+        if (hipMalloc(&b.first, bytes) != hipSuccess) {
+            b.first = nullptr;
+            return nullptr;                 // -> direct atomics
+        }
+        b.second = bytes;
+    }
+    return b.first;
+}
+
+int sdfr_grid_encode_backward(const float *grad, const float *inputs, const float *embeddings,
+                              const int32_t *offsets, float *grad_embeddings, uint32_t B,
+                              uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                              const float *dy_dx, float *grad_inputs, uint32_t gridtype,
+                              int align_corners, uint32_t interp, void *stream) {
+    const size_t wsb = B ? sdfr_grid_encode_backward_ws_bytes(B, D, C, L, S, H, align_corners) : 0;
+    void *ws = wsb ? grid_bwd_internal_ws(wsb) : nullptr;
+    return sdfr_grid_encode_backward_ws(grad, inputs, embeddings, offsets, grad_embeddings, B, D,
+                                        C, L, S, H, dy_dx, grad_inputs, gridtype, align_corners,
+                                        interp, ws, ws ? wsb : 0, stream);
 }
 
 int sdfr_sh_encode_forward(const float *inputs, float *outputs, uint32_t B, uint32_t D,

@@ -64,10 +64,14 @@ class _GridEncode(Function):
         grad = grad.view(B, L, C).permute(1, 0, 2).contiguous()
         grad_embeddings = torch.zeros_like(embeddings)
         grad_inputs = torch.zeros_like(inputs, dtype=embeddings.dtype) if dy_dx is not None else None
-        _lib.check(_lib.lib().sdfr_grid_encode_backward(
+        # binned table gradient (csrc/encoders.hip) in a workspace from torch's allocator
+        L_ = _lib.lib()
+        wsb = L_.sdfr_grid_encode_backward_ws_bytes(B, D, C, L, S, H, int(align_corners))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=grad.device) if wsb else None
+        _lib.check(L_.sdfr_grid_encode_backward_ws(
             _lib.ptr(grad), _lib.ptr(inputs), _lib.ptr(embeddings), _lib.ptr(offsets),
             _lib.ptr(grad_embeddings), B, D, C, L, S, H, _lib.ptr(dy_dx), _lib.ptr(grad_inputs),
-            gridtype, int(align_corners), interpolation, _lib.stream_of(grad)),
+            gridtype, int(align_corners), interpolation, _lib.ptr(ws), wsb, _lib.stream_of(grad)),
             "sdfr_grid_encode_backward")
         if grad_inputs is not None:
             grad_inputs = grad_inputs.to(inputs.dtype)

@@ -163,10 +163,9 @@ def test_device_sin_rev_accuracy(sdfr):
 
 
 def test_grid_backward_large_privatised_levels(sdfr, oracle_mod, table):
-    """200 k samples in the renderer's coordinate range: the coarse levels'
-    gradients go through the LDS-privatised kernel (one global add per row and
-    workgroup), the rest through direct atomics; both are order-dependent fp32
-    sums of the same per-sample products."""
+    """200 k samples in the renderer's coordinate range through the module path
+    (GridEncoder's workspace: every level binned, summed in LDS); order-dependent
+    fp32 sums of the oracle's per-sample products."""
     offsets, pls, emb = table
     rng = np.random.default_rng(9)
     n = 200_000
@@ -184,3 +183,69 @@ def test_grid_backward_large_privatised_levels(sdfr, oracle_mod, table):
     got = et.grad.cpu().numpy()
     np.testing.assert_allclose(got, ge, rtol=1e-4, atol=2e-5 * float(np.abs(ge).max()))
     assert np.count_nonzero(got) == np.count_nonzero(ge)
+
+
+def _grid_bwd_ws(sdfr, g_lbc, x, emb, offsets, pls, binned):
+    """sdfr_grid_encode_backward_ws with (binned) or without (direct atomics) a workspace."""
+    lib = sdfr._lib
+    L_ = lib.lib()
+    gt = torch.from_numpy(np.ascontiguousarray(g_lbc)).to(DEV)
+    xt = torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+    ot = torch.from_numpy(np.ascontiguousarray(offsets, dtype=np.int32)).to(DEV)
+    L, B, C = g_lbc.shape
+    S = float(np.float32(np.log2(pls)))
+    ge = torch.zeros(emb.shape, device=DEV)
+    wsb = L_.sdfr_grid_encode_backward_ws_bytes(B, 3, C, L, S, 16, 0) if binned else 0
+    ws = torch.empty(wsb, dtype=torch.uint8, device=DEV) if wsb else None
+    assert (wsb > 0) == binned
+    lib.check(L_.sdfr_grid_encode_backward_ws(
+        lib.ptr(gt), lib.ptr(xt), None, lib.ptr(ot), lib.ptr(ge), B, 3, C, L, S, 16, None, None,
+        0, 0, 0, lib.ptr(ws), wsb, lib.stream_of(gt)), "grid bwd ws")
+    torch.cuda.synchronize()
+    return ge.cpu().numpy()
+
+
+@pytest.mark.parametrize("C,log2_hash", [(2, 19), (2, 20), (1, 19), (4, 18), (8, 17)])
+def test_grid_backward_binned_vs_direct_and_oracle(sdfr, oracle_mod, C, log2_hash):
+    """The binned table gradient (count, scan, LDS counting sort, work items, LDS sums)
+    against the workspace-less path (LDS windows for the coarse levels, direct atomics
+    for the rest) and the oracle, for every C and for tables larger than 32 LDS windows
+    per level (log2_hash 20 at C = 2: two sweeps per bin).  Order-dependent fp32 sums
+    on all three sides."""
+    offsets, pls = oracle_mod.grid_offsets(level_dim=C, log2_hashmap_size=log2_hash)
+    emb = W.det_table(int(offsets[-1]), C, seed=11)
+    rng = np.random.default_rng(C + log2_hash)
+    n = 65_536
+    x = rng.uniform(0.05, 0.95, size=(n, 3)).astype(np.float32)
+    x[:3] = [[-0.1, 0.5, 0.5], [1.0, 1.0, 1.0], [0.0, 0.0, 0.0]]
+    g_lbc = rng.normal(size=(16, n, C)).astype(np.float32)
+    ref, _ = oracle_mod.grid_encode_backward(g_lbc, x, emb, offsets, pls, 16)
+    tol = dict(rtol=1e-4, atol=2e-5 * float(np.abs(ref).max()))
+    binned = _grid_bwd_ws(sdfr, g_lbc, x, emb, offsets, pls, True)
+    direct = _grid_bwd_ws(sdfr, g_lbc, x, emb, offsets, pls, False)
+    np.testing.assert_allclose(binned, ref, **tol)
+    np.testing.assert_allclose(direct, ref, **tol)
+    assert np.count_nonzero(binned) == np.count_nonzero(ref)
+
+
+def test_grid_backward_accumulates_into_existing(sdfr, oracle_mod, table):
+    """grad_embeddings is added to, not overwritten (the reference atomically adds into
+    the caller's zeros): two binned calls give twice one call."""
+    offsets, pls, emb = table
+    rng = np.random.default_rng(3)
+    n = 8192
+    x = rng.uniform(0.1, 0.9, size=(n, 3)).astype(np.float32)
+    g_lbc = rng.normal(size=(16, n, 2)).astype(np.float32)
+    lib = sdfr._lib
+    L_ = lib.lib()
+    S = float(np.float32(np.log2(pls)))
+    gt, xt = torch.from_numpy(g_lbc).to(DEV), torch.from_numpy(x).to(DEV)
+    ot = torch.from_numpy(np.asarray(offsets, np.int32)).to(DEV)
+    ge = torch.zeros(emb.shape, device=DEV)
+    for _ in range(2):
+        lib.check(L_.sdfr_grid_encode_backward(lib.ptr(gt), lib.ptr(xt), None, lib.ptr(ot),
+                                               lib.ptr(ge), n, 3, 2, 16, S, 16, None, None, 0, 0,
+                                               0, lib.stream_of(gt)), "grid bwd")
+    ref, _ = oracle_mod.grid_encode_backward(g_lbc, x, emb, offsets, pls, 16)
+    np.testing.assert_allclose(ge.cpu().numpy(), 2 * ref, rtol=1e-4,
+                               atol=4e-5 * float(np.abs(ref).max()))
