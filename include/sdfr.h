@@ -264,6 +264,17 @@ int sdfr_fused_bias_act(float *out, const float *x, const float *bias, const flo
                         uint64_t size_x, uint32_t step_b, uint32_t size_b, int act,
                         int grad, float alpha, float scale, void *stream);
 
+/* sdfr_mapping_linear: one mapping-network layer for inference (sdf_model.py:437-466
+ * MappingLinear, EqualLinear + fused_leaky_relu, PixelNorm):
+ *   x' = pixelnorm ? x * rsqrt(mean(x^2) + 1e-8) : x           (per sample)
+ *   y  = x' . (W * wscale)^T + b * bscale                       (b NULL: no bias)
+ *   out = act ? (y > 0 ? y : y * slope) * act_scale : y
+ * x [B, K], W [O, K] (16-B aligned), b [O], out [B, O]; K % 64 == 0, K <= 512.
+ * fp32 throughout; summation order differs from a GEMM's (fp32 rounding level). */
+int sdfr_mapping_linear(float *out, const float *x, const float *w, const float *b, uint32_t B,
+                        uint32_t K, uint32_t O, float wscale, float bscale, int act, float slope,
+                        float act_scale, int pixelnorm, void *stream);
+
 /* sdfr_upfirdn2d <- upfirdn2d (upfirdn2d.cpp:12, upfirdn2d_kernel.cu; caller
  * sdf_op.py:230): input viewed as [major, in_h, in_w] (minor = 1), kernel
  * [kernel_h, kernel_w] (device), out [major, out_h, out_w] with
@@ -370,9 +381,16 @@ typedef struct sdfr_conv_act_args {
     void *y_split;                /* [B,H,W,Cout/8,2,8] fp16 or NULL                */
     const float *rgb_w;           /* [B,3,Cout] modulated ToRGB weight or NULL      */
     float *rgb_partial;           /* [Cout/128,B,3,H,W] fp32 (with rgb_w)           */
+    void *ws;                     /* split-K partials or NULL                       */
+    size_t ws_bytes;              /* >= sdfr_conv_act_ws_bytes(...) to split        */
 } sdfr_conv_act_args;
 
 int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *a, void *stream);
+/* Workspace that lets sdfr_conv3x3_f16x3_act split K when B*H*W/256 * Cout/128
+ * workgroups would leave CUs idle (0: no split for this shape): the K-steps are
+ * shared by 2 or 4 workgroups per tile, whose fp32 partial tiles a second kernel
+ * sums in a fixed order before the epilogue. */
+size_t sdfr_conv_act_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout);
 
 /* ToRGB finish: rgb [B,3,H,W] = sum_k partial[k] + rgb_b[o]
  *   + upfirdn2d(skip, outer(fir,fir), up 2, pad (2,1)) when skip != NULL

@@ -38,10 +38,10 @@ EXPORTS = (
     "sdfr_debug_sin_rev_probe",
     "sdfr_debug_set_encode_mode", "sdfr_debug_set_field_split",
     "sdfr_render_siren_workspace_bytes", "sdfr_render_siren_forward",
-    "sdfr_fused_bias_act", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
+    "sdfr_fused_bias_act", "sdfr_mapping_linear", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
     "sdfr_modulate_to_nhwc_split",
     "sdfr_conv_pack_bytes", "sdfr_conv_pack_weights", "sdfr_conv3x3_f16x3",
-    "sdfr_conv3x3_f16x3_act", "sdfr_rgb_finish",
+    "sdfr_conv3x3_f16x3_act", "sdfr_conv_act_ws_bytes", "sdfr_rgb_finish",
     "sdfr_mc_workspace_bytes", "sdfr_mc_count", "sdfr_mc_emit",
 )
 
@@ -108,6 +108,7 @@ class ConvActArgs(ctypes.Structure):
         ("demod", _vp), ("noise", _vp), ("noise_weight", _vp), ("bias", _vp),
         ("negative_slope", _f32), ("act_scale", _f32),
         ("s_next", _vp), ("y_split", _vp), ("rgb_w", _vp), ("rgb_partial", _vp),
+        ("ws", _vp), ("ws_bytes", ctypes.c_size_t),
     ]
 
 
@@ -153,6 +154,8 @@ def lib():
     L.sdfr_debug_sin_rev_probe.argtypes = [_vp, _vp, _u32, _vp]
     L.sdfr_fused_bias_act.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_uint64, _u32, _u32, _int, _int,
                                       _f32, _f32, _vp]
+    L.sdfr_mapping_linear.argtypes = [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _f32, _f32, _int, _f32,
+                                      _f32, _int, _vp]
     L.sdfr_upfirdn2d.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32] + [_int] * 8 + [_vp]
     L.sdfr_styled_epilogue.argtypes = [ctypes.POINTER(StyledEpilogueArgs), _vp]
     L.sdfr_modulate_to_nhwc.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _vp]
@@ -162,6 +165,8 @@ def lib():
     L.sdfr_conv_pack_weights.argtypes = [_vp, _f32, _u32, _u32, _vp, _vp, _vp]
     L.sdfr_conv3x3_f16x3.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _int, _vp]
     L.sdfr_conv3x3_f16x3_act.argtypes = [ctypes.POINTER(ConvActArgs), _vp]
+    L.sdfr_conv_act_ws_bytes.argtypes = [_u32, _u32, _u32, _u32]
+    L.sdfr_conv_act_ws_bytes.restype = ctypes.c_size_t
     _i64 = ctypes.c_int64
     L.sdfr_mc_workspace_bytes.argtypes = [_u32, _u32, _u32]
     L.sdfr_mc_workspace_bytes.restype = ctypes.c_size_t

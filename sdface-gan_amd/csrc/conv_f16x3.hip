@@ -155,6 +155,9 @@ struct ConvArgs {
     int dy[9], dx[9];              // input pixel = (a + dy, c + dx)
     uint32_t tap[9];               // packed weight tap (3 ky + kx)
     ActEpi e;                      // conv_x_kernel<true> only
+    uint32_t ksplit;               // split-K factor (1: the epilogue runs in the conv kernel)
+    uint32_t grid;                 // workgroup slots per split (padded class tiles)
+    f4 *partial;                   // [ksplit][grid][16 (i, j)][512 threads] f4 when ksplit > 1
 };
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -303,6 +306,29 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4]
     }
 }
 
+// Workgroup slot -> (class, tile); false for a padding slot.  Class ranges start at
+// multiples of 8, so slot % 8 is the XCD.
+__device__ __forceinline__ bool slot_tile(const ConvArgs &a, uint32_t slot, uint32_t &ci,
+                                          uint32_t &tile) {
+    ci = 0;
+    for (uint32_t i = 1; i < a.ncls; ++i)
+        if (slot >= a.cls[i].tile0) ci = i;
+    const ConvClass &cl = a.cls[ci];
+    const uint32_t loc = slot - cl.tile0;
+#if CONV_XCD
+    // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs; give
+    // each XCD one contiguous run of the class's tiles, with the Cout block fastest,
+    // so the tiles that re-read an activation row (the other Cout blocks of the same
+    // pixels, the rows above and below through the taps) run on the same XCD at
+    // about the same time and hit its L2.  (The K splits of a slot, blockIdx.y, sit
+    // on the same XCD: the grid's x extent is a multiple of 8.)
+    tile = (loc & 7u) * ((cl.ntiles + 7) >> 3) + (loc >> 3);
+#else
+    tile = loc;
+#endif
+    return tile < cl.ntiles;
+}
+
 template <bool ACT>
 __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     __shared__ f4 As[kStages][kStepF4];       // [mt 8][hi,lo][64]
@@ -310,30 +336,18 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
     const uint32_t wm = wave & 1u, wn = wave >> 1;
-    // this workgroup's class (ranges start at multiples of 8: blockIdx.x % 8 is the XCD)
-    uint32_t ci = 0;
-    for (uint32_t i = 1; i < a.ncls; ++i)
-        if (blockIdx.x >= a.cls[i].tile0) ci = i;
+    uint32_t ci, tile;
+    if (!slot_tile(a, blockIdx.x, ci, tile)) return;  // padding slot (whole workgroup)
     const ConvClass &cl = a.cls[ci];
     const uint32_t Hc = cl.Hc, Wc = cl.Wc, py = cl.py, px = cl.px;
-    const uint32_t ntaps = cl.ntaps, ntiles = cl.ntiles;
+    const uint32_t ntaps = cl.ntaps;
     const uint32_t npix = a.B * Hc * Wc;
     const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT;
-    const uint32_t loc = blockIdx.x - cl.tile0;
-#if CONV_XCD
-    // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs; give
-    // each XCD one contiguous run of the class's tiles, with the Cout block fastest,
-    // so the tiles that re-read an activation row (the other Cout blocks of the same
-    // pixels, the rows above and below through the taps) run on the same XCD at
-    // about the same time and hit its L2.
-    const uint32_t tile = (loc & 7u) * ((ntiles + 7) >> 3) + (loc >> 3);
-#else
-    const uint32_t tile = loc;
-#endif
-    if (tile >= ntiles) return;                       // padding slot (whole workgroup)
     const uint32_t cb = tile % nB;
     const uint32_t pix0 = (tile / nB) * kPT;
-    const uint32_t nk = nC * ntaps;
+    // split-K: blockIdx.y's share of the class's K-steps (channel group x tap)
+    const uint32_t nk_all = nC * ntaps, split = blockIdx.y;
+    const uint32_t k_begin = split * nk_all / a.ksplit, nk = (split + 1) * nk_all / a.ksplit - k_begin;
 
     // LDS-DMA sources (6 pieces of 1 KB per wave per K-step).  Weights: the K-step's
     // 16 KB block is contiguous; wave w moves pieces 2w, 2w+1.  Activations: the 32
@@ -380,7 +394,7 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     // The address work (SALU tap decode, VALU offsets) is done in prep_step, ahead
     // of the barrier and overlapped with MFMAs; fire_step after the barrier only
     // moves M0 and issues the six DMAs.
-    uint32_t nx_c = 0, nx_t = 0;
+    uint32_t nx_c = k_begin / ntaps, nx_t = k_begin % ntaps;
     struct StepDma {
         uint32_t wsoff;           // weight pieces: global offset of this wave's first
         uint32_t offs[4];         // activation pieces: per-lane global offsets
@@ -548,7 +562,45 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     }
 #endif
 
+    if (a.ksplit > 1) {      // partial sums; conv_splitk_kernel adds them and runs the epilogue
+        f4 *pp = a.partial + ((size_t)split * a.grid + blockIdx.x) * 16 * 512 + tid;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pp[(i * 4 + j) * 512] = acc[i][j];
+        return;
+    }
     conv_epilogue<ACT>(a, acc, lane, wm, wn, cb, pix0, npix, Hc, Wc, py, px);
+}
+
+// Split-K finish: the ksplit partial tiles summed in split order (deterministic),
+// then the tile's epilogue, with the conv kernel's slot -> tile mapping and lane
+// roles.  Used when the unsplit grid would leave CUs idle (eval.py's batch of 1:
+// 64 workgroups at 64^2, 128 at 128^2, for 256 CUs).
+template <bool ACT>
+__global__ void __launch_bounds__(512, 1) conv_splitk_kernel(const ConvArgs a) {
+    uint32_t ci, tile;
+    if (!slot_tile(a, blockIdx.x, ci, tile)) return;
+    const ConvClass &cl = a.cls[ci];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t wm = wave & 1u, wn = wave >> 1;
+    const uint32_t nB = a.Cout / kCT, cb = tile % nB, pix0 = (tile / nB) * kPT;
+    f4 acc[4][4];
+    const f4 *pp = a.partial + (size_t)blockIdx.x * 16 * 512 + tid;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = pp[(i * 4 + j) * 512];
+    for (uint32_t s = 1; s < a.ksplit; ++s) {
+        const f4 *q = pp + (size_t)s * a.grid * 16 * 512;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] += q[(i * 4 + j) * 512];
+    }
+    conv_epilogue<ACT>(a, acc, lane, wm, wn, cb, pix0, a.B * cl.Hc * cl.Wc, cl.Hc, cl.Wc, cl.py,
+                       cl.px);
 }
 
 
@@ -584,9 +636,21 @@ namespace {
 
 // Shared setup of both entry points: shape checks, tap tables, classes; launches
 // conv_x_kernel<ACT>.
+// split-K factor: the largest of 4, 2 that keeps every split's grid within one
+// round of workgroups on the 256 CUs (one 512-thread workgroup per CU)
+uint32_t conv_ksplit(uint32_t grid) {
+    for (uint32_t k = 4; k > 1; k >>= 1)
+        if (grid * k <= 256) return k;
+    return 1;
+}
+
+uint32_t conv_grid(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {   // regular conv
+    return ((B * H * W + kPT - 1) / kPT * (Cout / kCT) + 7) & ~7u;
+}
+
 int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B, uint32_t H,
                 uint32_t W, uint32_t Cin, uint32_t Cout, int transposed, bool act,
-                hipStream_t st, const char *what) {
+                hipStream_t st, const char *what, void *ws = nullptr, size_t ws_bytes = 0) {
     if (!x_split || !packed) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
     if (B == 0 || H == 0 || W == 0 || Cout % kCT || Cin % 32 || Cin == 0 || Cout == 0)
         return fail(SDFR_EINVAL, "conv3x3_f16x3: bad shape (Cout % 128, Cin % 32)");
@@ -651,8 +715,20 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
                 add_class(py ? H : H + 1, px ? W : W + 1, py, px, nt);
             }
     }
-    if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid), dim3(512), 0, st, a);
+    a.grid = grid;
+    a.ksplit = 1;
+    a.partial = nullptr;
+    const uint32_t ks = conv_ksplit(grid);
+    if (ws && ks > 1 && ws_bytes >= (size_t)ks * grid * 16 * 512 * sizeof(f4)) {
+        a.ksplit = ks;
+        a.partial = reinterpret_cast<f4 *>(ws);
+    }
+    if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
+    if (a.ksplit > 1) {
+        if (act) hipLaunchKernelGGL(conv_splitk_kernel<true>, dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL(conv_splitk_kernel<false>, dim3(grid), dim3(512), 0, st, a);
+    }
     return check_launch(what);
 }
 
@@ -695,7 +771,13 @@ int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *p, void *stream) {
     a.e.rgb_w = s.rgb_w;
     a.e.rgbp = s.rgb_partial;
     return conv_launch(a, s.x_split, s.packed, s.B, s.H, s.W, s.Cin, s.Cout, 0, true,
-                       (hipStream_t)stream, "conv3x3_f16x3_act");
+                       (hipStream_t)stream, "conv3x3_f16x3_act", s.ws, s.ws_bytes);
+}
+
+size_t sdfr_conv_act_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
+    if (Cout % kCT || B == 0 || H == 0 || W == 0) return 0;
+    const uint32_t grid = conv_grid(B, H, W, Cout), ks = conv_ksplit(grid);
+    return ks > 1 ? (size_t)ks * grid * 16 * 512 * sizeof(f4) : 0;
 }
 
 }  // extern "C"

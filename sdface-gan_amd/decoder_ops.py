@@ -357,10 +357,11 @@ def conv3x3_f16x3(x_split, packed, Cout, transposed=False):
 
 def conv3x3_f16x3_act(x_split, packed, Cout, *, demod, bias, noise_weight, noise=None,
                       s_next=None, store_y=True, rgb_w=None, negative_slope=0.2,
-                      act_scale=math.sqrt(2)):
+                      act_scale=math.sqrt(2), split_k=True):
     """Regular conv with the plain styled epilogue fused (sdfr_conv3x3_f16x3_act):
     returns (y split-NHWC [B,H,W,Cout/8,2,8] or None, ToRGB partial sums
-    [Cout/128,B,3,H,W] or None).  demod must already carry 1/su."""
+    [Cout/128,B,3,H,W] or None).  demod must already carry 1/su.  ``split_k``: give
+    the kernel a workspace so that small batches split K over 2 or 4 workgroups."""
     _require_cuda(x_split)
     if x_split.dtype != torch.float16 or x_split.dim() != 6 or x_split.shape[4:] != (2, 8) \
             or not x_split.is_contiguous():
@@ -394,6 +395,9 @@ def conv3x3_f16x3_act(x_split, packed, Cout, *, demod, bias, noise_weight, noise
     a.y_split = _lib.ptr(ys)
     a.rgb_w = cptr(rgb_w)
     a.rgb_partial = _lib.ptr(part)
+    wsb = _lib.lib().sdfr_conv_act_ws_bytes(B, H, W, Cout) if split_k else 0
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev) if wsb else None
+    a.ws, a.ws_bytes = _lib.ptr(ws), wsb
     _lib.check(_lib.lib().sdfr_conv3x3_f16x3_act(a, _lib.stream_of(x_split)), "conv3x3_f16x3_act")
     return ys, part
 

@@ -111,6 +111,45 @@ class EqualLinear(nn.Module):
         return f"{self.__class__.__name__}({self.weight.shape[1]}, {self.weight.shape[0]})"
 
 
+def mapping_forward(seq, x):
+    """A mapping network (nn.Sequential of PixelNorm / EqualLinear / MappingLinear) on
+    the inference path: one HIP launch per linear layer (``sdfr_mapping_linear``,
+    PixelNorm folded into the next layer) when ``x`` is on the GPU and no gradient
+    is recorded; the modules themselves otherwise.  Same per-element arithmetic
+    (W * scale, b * lr_mul, x + b, leaky ReLU, * scale); the dot products are
+    summed in a different order than the GEMM's (fp32 rounding level)."""
+    if not (x.is_cuda and not torch.is_grad_enabled() and x.dtype == torch.float32
+            and x.dim() == 2):
+        return seq(x)
+    from . import _lib
+    L = _lib.lib()
+    pixelnorm = 0
+    for m in seq:
+        if isinstance(m, PixelNorm):
+            pixelnorm = 1
+            continue
+        if isinstance(m, EqualLinear):
+            wscale, bscale, act_scale = m.scale, m.lr_mul, 2 ** 0.5
+        elif isinstance(m, MappingLinear):
+            wscale, bscale, act_scale = 1.0, 1.0, 1.0
+        else:
+            return seq(x)                          # unknown layer: module path
+        w = m.weight.detach()
+        if w.shape[1] % 64 or w.shape[1] > 512 or not w.is_contiguous():
+            return seq(x)
+        x = x.contiguous()
+        out = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=torch.float32)
+        _lib.check(L.sdfr_mapping_linear(
+            _lib.ptr(out), _lib.ptr(x), _lib.ptr(w),
+            _lib.ptr(m.bias.detach()) if m.bias is not None else None, x.shape[0], w.shape[1],
+            w.shape[0], float(wscale), float(bscale), int(m.activation is not None), 0.2,
+            float(act_scale), pixelnorm, _lib.stream_of(x)), "sdfr_mapping_linear")
+        x, pixelnorm = out, 0
+    if pixelnorm:
+        return seq[-1](x)
+    return x
+
+
 class ModulatedConv2d(nn.Module):
     def __init__(self, in_channel, out_channel, kernel_size, style_dim, demodulate=True,
                  upsample=False, downsample=False, blur_kernel=(1, 3, 3, 1)):
@@ -279,7 +318,7 @@ class Decoder(nn.Module):
                                  truncation_latent=None, input_is_latent=False,
                                  randomize_noise=True):
         if not input_is_latent:
-            styles = [self.style(s) for s in styles]
+            styles = [mapping_forward(self.style, s) for s in styles]
         if noise is None:
             noise = ([None] * self.num_layers if randomize_noise else
                      [getattr(self.noises, f"noise_{i}") for i in range(self.num_layers)])
@@ -527,7 +566,7 @@ class Generator(nn.Module):
     def styles_and_noise_forward(self, styles, inject_index=None, truncation=1,
                                  truncation_latent=None, input_is_latent=False):
         if not input_is_latent:
-            styles = [self.style(s) for s in styles]
+            styles = [mapping_forward(self.style, s) for s in styles]
         if truncation < 1:
             styles = [truncation_latent[0] + truncation * (s - truncation_latent[0])
                       for s in styles]

@@ -265,7 +265,8 @@ def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, 
     rgb_w = torch.randn(B, 3, Cout, generator=g).to(DEV) if rgb else None
     rgb_b = torch.randn(3, generator=g).to(DEV)
     sk = torch.randn(B, 3, H // 2, W // 2, generator=g).to(DEV) if skip else None
-    ys, part = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_w=rgb_w, **kw)
+    ys, part = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_w=rgb_w, split_k=False,
+                                     **kw)
     out = ops.conv3x3_f16x3(xs, packed, Cout)
     y_ref, rgb_ref = ops.styled_epilogue(out, fir=fir, demod=demod, rgb_w=rgb_w,
                                          rgb_b=rgb_b if rgb else None, skip=sk,
@@ -282,6 +283,23 @@ def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, 
                1e-6 * scale)
     else:
         assert part is None
+    # split-K (small grids: K over 2 or 4 workgroups, partial tiles summed in a fixed
+    # order, then the same epilogue): fp32 summation-order rounding of the conv
+    ys2, part2 = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_w=rgb_w, **kw)
+    ys3, _ = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_w=rgb_w, **kw)
+    if store_y:
+        hi, lo = ops.unsplit_nhwc(ys2)
+        hr, lr = ops.unsplit_nhwc(y_ref)
+        y2, yr = hi.float() + lo.float(), hr.float() + lr.float()
+        scale = float(yr.abs().max())
+        _close(f"conv_act_splitk_y_{Cin}x{Cout}_{H}x{W}", y2.cpu(), yr.cpu(), 2e-6 * scale,
+               2e-7 * scale)
+        assert torch.equal(ys2, ys3)                      # deterministic
+    if rgb:
+        got2 = ops.rgb_finish(part2, rgb_b, skip=sk, fir=fir)
+        scale = float(rgb_ref.abs().max())
+        _close(f"conv_act_splitk_rgb_{Cin}x{Cout}_{H}x{W}", got2.cpu(), rgb_ref.cpu(),
+               1e-5 * scale, 1e-6 * scale)
 
 
 @pytest.mark.parametrize("conv_impl,fuse", [("f16x3", True), ("f16x3", False), ("miopen", False)])
@@ -371,3 +389,25 @@ def test_graphed_generator_recaptures_after_weight_update(sdfr):
     assert torch.equal(got, ref)
     with pytest.raises(TypeError, match="tensor"):
         gg.random_faces(1, 64, locations=torch.zeros(1, 2, device=dev))
+
+
+@pytest.mark.parametrize("B", [1, 5, 37])
+def test_mapping_linear_matches_module_path(sdfr, B):
+    """sdfr_mapping_linear (one launch per layer, PixelNorm folded in) against the
+    module path's GEMM + fused_leaky_relu, for both mapping networks of the Generator
+    (3 MappingLinear, sdf_model.py:1084) and of the Decoder (PixelNorm + 5 EqualLinear,
+    sdf_model.py:893-902).  fp32, summation order differs: bounded relative to the
+    output scale."""
+    from sdface_gan_amd.generator import mapping_forward
+    opt = sdfr.vol_render_opt()
+    torch.manual_seed(B)
+    g = sdfr.Generator(opt.model, opt.rendering).to("cuda")
+    z = torch.randn(B, 256, device="cuda")
+    for seq, x in ((g.style, z), (g.decoder.style, g.style(z).detach())):
+        with torch.no_grad():
+            got = mapping_forward(seq, x)
+        with torch.enable_grad():
+            ref = seq(x).detach()
+        assert got.shape == ref.shape
+        err = (got - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 2e-6, err
