@@ -269,7 +269,7 @@ int sdfr_fused_bias_act(float *out, const float *x, const float *bias, const flo
  *   x' = pixelnorm ? x * rsqrt(mean(x^2) + 1e-8) : x           (per sample)
  *   y  = x' . (W * wscale)^T + b * bscale                       (b NULL: no bias)
  *   out = act ? (y > 0 ? y : y * slope) * act_scale : y
- * x [B, K], W [O, K] (16-B aligned), b [O], out [B, O]; K % 64 == 0, K <= 512.
+ * x [B, K], W [O, K] (16-B aligned), b [O], out [B, O]; K = 256 or 512.
  * fp32 throughout; summation order differs from a GEMM's (fp32 rounding level). */
 int sdfr_mapping_linear(float *out, const float *x, const float *w, const float *b, uint32_t B,
                         uint32_t K, uint32_t O, float wscale, float bscale, int act, float slope,

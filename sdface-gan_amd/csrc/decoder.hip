@@ -465,11 +465,13 @@ extern "C" {
 // fused_leaky_relu, PixelNorm; the whole layer in one launch -- at eval.py's batch of
 // 1 the module path's 3-4 kernels per layer (scale multiply, GEMM, bias + act) cost
 // more than their arithmetic).
-// A workgroup owns 16 outputs; its 256 threads are 16 outputs x 16 K-slices, each
-// thread an fma chain over its slice for up to 16 samples, then the 16 slice
-// partials are summed in a fixed order (deterministic; not the GEMM's order).
+// A workgroup owns 4 outputs, one wave each; lane l of a wave takes K-slice l
+// (K/64 inputs, one contiguous piece of the weight row, so a wave reads the row as
+// one coalesced run) for up to 16 samples, and the 64 slice partials of a sample
+// are summed by a butterfly of lane exchanges (fixed order: deterministic; not
+// the GEMM's order).  128 workgroups for a 512-wide layer at any batch.
 // ----------------------------------------------------------------------------
-constexpr uint32_t kMapOut = 16, kMapSlices = 16, kMapB = 16, kMapMaxK = 512;
+constexpr uint32_t kMapOut = 4, kMapB = 16, kMapMaxK = 512;
 
 struct MapArgs {
     const float *x, *w, *b;
@@ -481,23 +483,21 @@ struct MapArgs {
 
 __global__ __launch_bounds__(256) void mapping_linear_kernel(const MapArgs a) {
     __shared__ float xs[kMapB * kMapMaxK];
-    __shared__ float part[kMapSlices][kMapOut][kMapB + 1];
     __shared__ float nrm[kMapB];
-    const uint32_t t = threadIdx.x, ol = t & 15u, ks = t >> 4;
-    const uint32_t o = blockIdx.x * kMapOut + ol;
-    const uint32_t kl = a.K / kMapSlices, k0 = ks * kl;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t o = blockIdx.x * kMapOut + wv;
+    const uint32_t kl = a.K / 64, k0 = lane * kl;
     for (uint32_t b0 = blockIdx.y * kMapB; b0 < a.B; b0 += gridDim.y * kMapB) {
         const uint32_t nb = min(kMapB, a.B - b0);
         for (uint32_t i = t; i < nb * a.K; i += 256) xs[i] = a.x[(size_t)b0 * a.K + i];
         __syncthreads();
         if (a.pixelnorm) {                       // x * rsqrt(mean(x^2) + 1e-8)
-            const uint32_t lane = t & 63u, w = t >> 6;
-            for (uint32_t b = w; b < nb; b += 4) {
-                float s = 0.0f;
-                for (uint32_t k = lane; k < a.K; k += 64) s = __fmaf_rn(xs[b * a.K + k], xs[b * a.K + k], s);
+            for (uint32_t b = wv; b < nb; b += 4) {
+                float q = 0.0f;
+                for (uint32_t k = lane; k < a.K; k += 64) q = __fmaf_rn(xs[b * a.K + k], xs[b * a.K + k], q);
 #pragma unroll
-                for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-                if (lane == 0) nrm[b] = rsqrtf(__fadd_rn(__fdiv_rn(s, (float)a.K), 1e-8f));
+                for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m);
+                if (lane == 0) nrm[b] = rsqrtf(__fadd_rn(__fdiv_rn(q, (float)a.K), 1e-8f));
             }
             __syncthreads();
             for (uint32_t i = t; i < nb * a.K; i += 256) xs[i] = __fmul_rn(xs[i], nrm[i / a.K]);
@@ -510,28 +510,35 @@ __global__ __launch_bounds__(256) void mapping_linear_kernel(const MapArgs a) {
             const float *wr = a.w + (size_t)o * a.K + k0;
             for (uint32_t k = 0; k < kl; k += 4) {
                 const float4 w4 = *reinterpret_cast<const float4 *>(wr + k);
-                const float wv[4] = {__fmul_rn(w4.x, a.wscale), __fmul_rn(w4.y, a.wscale),
+                const float wq[4] = {__fmul_rn(w4.x, a.wscale), __fmul_rn(w4.y, a.wscale),
                                      __fmul_rn(w4.z, a.wscale), __fmul_rn(w4.w, a.wscale)};
 #pragma unroll
-                for (uint32_t j = 0; j < 4; ++j)
-#pragma unroll
-                    for (uint32_t b = 0; b < kMapB; ++b)
-                        if (b < nb) acc[b] = __fmaf_rn(xs[b * a.K + k0 + k + j], wv[j], acc[b]);
+                for (uint32_t b = 0; b < kMapB; ++b) {
+                    if (b < nb) {
+                        const float4 x4 = *reinterpret_cast<const float4 *>(&xs[b * a.K + k0 + k]);
+                        acc[b] = __fmaf_rn(x4.x, wq[0], acc[b]);
+                        acc[b] = __fmaf_rn(x4.y, wq[1], acc[b]);
+                        acc[b] = __fmaf_rn(x4.z, wq[2], acc[b]);
+                        acc[b] = __fmaf_rn(x4.w, wq[3], acc[b]);
+                    }
+                }
             }
         }
 #pragma unroll
-        for (uint32_t b = 0; b < kMapB; ++b) part[ks][ol][b] = acc[b];
-        __syncthreads();
-        {
-            const uint32_t o2l = t & 15u, b = t >> 4, o2 = blockIdx.x * kMapOut + o2l;
-            if (o2 < a.O && b < nb) {
-                float y = 0.0f;
+        for (uint32_t b = 0; b < kMapB; ++b) {
+            if (b < nb) {
 #pragma unroll
-                for (uint32_t q = 0; q < kMapSlices; ++q) y = __fadd_rn(y, part[q][o2l][b]);
-                if (a.b) y = __fadd_rn(y, __fmul_rn(a.b[o2], a.bscale));
-                if (a.act) y = __fmul_rn(y > 0.0f ? y : __fmul_rn(y, a.slope), a.act_scale);
-                a.out[(size_t)(b0 + b) * a.O + o2] = y;
+                for (int m = 32; m >= 1; m >>= 1) acc[b] = __fadd_rn(acc[b], __shfl_xor(acc[b], m));
             }
+        }
+        if (o < a.O && lane < nb) {              // lane b stores sample b
+            float y = 0.0f;
+#pragma unroll
+            for (uint32_t b = 0; b < kMapB; ++b)
+                if (b == lane) y = acc[b];
+            if (a.b) y = __fadd_rn(y, __fmul_rn(a.b[o], a.bscale));
+            if (a.act) y = __fmul_rn(y > 0.0f ? y : __fmul_rn(y, a.slope), a.act_scale);
+            a.out[(size_t)(b0 + lane) * a.O + o] = y;
         }
         __syncthreads();
     }
@@ -542,8 +549,8 @@ int sdfr_mapping_linear(float *out, const float *x, const float *w, const float 
                         float act_scale, int pixelnorm, void *stream) {
     if (B == 0) return SDFR_OK;
     if (!out || !x || !w) return fail(SDFR_EINVAL, "mapping_linear: null tensor pointer");
-    if (K == 0 || K % 64 != 0 || K > kMapMaxK || O == 0)
-        return fail(SDFR_EINVAL, "mapping_linear: K must be a multiple of 64 and <= 512");
+    if (K == 0 || K % 256 != 0 || K > kMapMaxK || O == 0)
+        return fail(SDFR_EINVAL, "mapping_linear: K must be 256 or 512");
     if ((reinterpret_cast<uintptr_t>(w) & 15u) != 0)
         return fail(SDFR_EINVAL, "mapping_linear: W must be 16-byte aligned");
     MapArgs a{x, w, b, out, B, K, O, wscale, bscale, slope, act_scale, act, pixelnorm};

@@ -135,7 +135,7 @@ def mapping_forward(seq, x):
         else:
             return seq(x)                          # unknown layer: module path
         w = m.weight.detach()
-        if w.shape[1] % 64 or w.shape[1] > 512 or not w.is_contiguous():
+        if w.shape[1] not in (256, 512) or not w.is_contiguous():
             return seq(x)
         x = x.contiguous()
         out = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=torch.float32)
