@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip the B=1/8 and host-copy measurements")
     p.add_argument("--traffic-json", default=str(REPO / "profiles" / "field_traffic.json"))
+    p.add_argument("--counters-json", default=str(REPO / "profiles" / "round2_counters.json"),
+                   help="committed SQ counter summary (scripts/summarize_counters.py) quoted "
+                        "as the field kernel's MFMA-busy fraction")
     return p.parse_args()
 
 
@@ -237,6 +240,18 @@ def main():
             return None
 
     traffic = traffic_of(field_kernel)
+
+    def counters_of(kernel):
+        """MFMA-busy fraction of `kernel` from the committed SQ counter passes
+        (SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x GRBM_GUI_ACTIVE / XCDs)), or None."""
+        try:
+            ks = json.loads(Path(args.counters_json).read_text())["kernels"]
+            k = next(v for n, v in ks.items() if kernel in n)
+            return {"mfma_busy_frac": k["mfma_busy_frac"],
+                    "effective_clock_GHz": k["effective_clock_GHz"],
+                    "source": str(Path(args.counters_json).relative_to(REPO))}
+        except (OSError, KeyError, ValueError, TypeError, StopIteration):
+            return None
     if f16x3:
         # fp32-accurate GEMMs as 3 fp16 MFMA terms: the attainable fp32-equivalent
         # peak is the dense fp16 MFMA peak / 3 (DESIGN.md section 5)
@@ -245,7 +260,8 @@ def main():
                 "bound": "mfma", "achieved": field_tflops, "peak": MFMA_F16_PEAK_TFLOPS / 3,
                 "unit": "TFLOP/s", "frac": field_tflops / (MFMA_F16_PEAK_TFLOPS / 3),
                 "traffic": traffic, "mfma_dtype": "f16 (hi/lo split, fp32 accumulate)",
-                "mfma_issued_tflops": 3 * field_tflops, "mfma_peak_dtype": MFMA_F16_PEAK_TFLOPS}
+                "mfma_issued_tflops": 3 * field_tflops, "mfma_peak_dtype": MFMA_F16_PEAK_TFLOPS,
+                "counters": counters_of(field_kernel.split("<")[0])}
     else:
         roof = {"kernel": "ngp_field_kernel (MLP on v_mfma_f32_16x16x4_f32 + compositing)",
                 "bound": "mfma", "achieved": field_tflops, "peak": MFMA_F32_PEAK_TFLOPS,
@@ -291,6 +307,28 @@ def main():
                                    elev_range=opt.camera.elev, fov_ang=opt.camera.fov,
                                    dist_radius=opt.camera.dist_radius)[0]
         line["extras"] = extras(step, B, graphed_step)
+        if f16x3 and not siren:
+            # the exact-fp32 field (v_mfma_f32_16x16x4_f32) on the same workload: the
+            # cost of exact arithmetic, outside the timed region
+            g.renderer.field_precision = "fp32"
+            for _ in range(2):
+                step()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            for e in ev:
+                e.record()          # materialise the handles (as for the timed steps)
+            torch.cuda.synchronize()
+            g.renderer.stage_events = ev
+            t0 = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            g.renderer.stage_events = None
+            g.renderer.field_precision = args.field_precision
+            f32_ms = ev[2].elapsed_time(ev[3])
+            line["extras"]["fp32_field"] = {
+                "kernel": "ngp_field_kernel (v_mfma_f32_16x16x4_f32)", "faces_per_s": B / dt,
+                "field_ms": f32_ms, "field_tflops": flop * samples / (f32_ms * 1e-3) / 1e12,
+                "peak_tflops": MFMA_F32_PEAK_TFLOPS}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, siren)
     if rank == 0:

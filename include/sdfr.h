@@ -168,6 +168,11 @@ typedef struct sdfr_ngp_render_args {
      *   accuracy);
      * SDFR_FIELD_FP32 (1) v_mfma_f32_16x16x4_f32 (exact fp32 fma chain). */
     int field_precision;
+    /* NULL, or the split-fp16 weights packed beforehand by sdfr_render_ngp_pack /
+     * sdfr_render_siren_pack from the SAME weights (f16x3 only): the per-call
+     * row-scale and packing kernels are then skipped, only the per-face FiLM
+     * vectors are formed. */
+    const void *prepacked;
 } sdfr_ngp_render_args;
 
 #define SDFR_FIELD_F16X3 0
@@ -203,6 +208,13 @@ typedef struct sdfr_siren_weights {
 } sdfr_siren_weights;
 
 size_t sdfr_render_siren_workspace_bytes(uint32_t B);
+
+/* Split-fp16 weight packing of the field kernel (row scales, scaled biases, MFMA
+ * A-fragments), done once per weight version by the caller instead of per call:
+ * `packed` holds sdfr_render_pack_bytes(net) bytes (net 0 ngp, 1 siren). */
+size_t sdfr_render_pack_bytes(int net);
+int sdfr_render_ngp_pack(const sdfr_ngp_weights *w, void *packed, void *stream);
+int sdfr_render_siren_pack(const sdfr_siren_weights *w, void *packed, void *stream);
 
 int sdfr_render_siren_forward(const sdfr_siren_weights *w,
                               const sdfr_ngp_render_args *a, void *stream);
@@ -249,6 +261,16 @@ int sdfr_debug_sin_probe(const float *x, float *out_cw, float *out_hw, uint32_t 
  * revolutions (1/(2 pi) folded into the FiLM vectors): out[i] = sin(2 pi u[i]) by
  * v_fract_f32 + v_sin_f32, n elements. */
 int sdfr_debug_sin_rev_probe(const float *u, float *out, uint32_t n, void *stream);
+
+/* Camera parameters from sampled angles (generate_camera_params, sdf_utils.py:97-159,
+ * after its random draws; distance 1): viewpoint [B,2] = (azim, elev); ext [B,3,4] =
+ * [R^T | T] with T = (cos e sin a, sin e, cos e cos a), R rows = normalize(up x z),
+ * normalize(z x x), z = normalize(T), and the degenerate-x replacement of :151-154;
+ * near / far [B] = 1 -/+ dist_radius; focal [B] = half_res / tan(fov_ang pi / 180).
+ * azim, elev [B] on the device; fp32, one rounding per op. */
+int sdfr_camera_extrinsics(const float *azim, const float *elev, uint32_t B, float dist_radius,
+                           float fov_ang, float half_res, float *ext, float *focal, float *near_,
+                           float *far_, float *viewpoint, void *stream);
 
 /* ---------------------------------------------------------------------------
  * StyleGAN2 decoder ops (im2scene/sdf/models/sdf_op.py).

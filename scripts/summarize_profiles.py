@@ -11,9 +11,10 @@ Writes
 Counter units and corrections (MI355X_MICROARCH.md, "HBM [CDNA4]"): FETCH_SIZE and
 WRITE_SIZE are in KiB; FETCH_SIZE reads exactly half the bytes of a wide coalesced
 streaming read on gfx950, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane
-stores.  The field kernel's reads are 16-B-per-lane streams (encoded samples, packed
-weights), so the doubling applies to it; the encode kernel's reads are 8-B gathers
-(uncalibrated width) and are reported both raw and doubled.
+stores.  One rule for every kernel: traffic = 2 x FETCH_SIZE + WRITE_SIZE (the
+counter tallies 64 B per 128-B memory-side request).  The raw FETCH_SIZE is kept
+beside it; for the encode kernel's 8/16-B gathers the width is uncalibrated, so
+its doubled figure is an upper bound and the raw one a lower bound.
 """
 import argparse
 import csv
@@ -100,17 +101,17 @@ def main():
                           "write_bytes_per_face": fk["write_bytes"] / a.batch}
     ek = next((v for k, v in out["kernels"].items() if f"::{ENCODE}" in k), None)
     if ek and ek["fetch_bytes_raw"] is not None and ek["write_bytes"] is not None:
-        # gathers: FETCH_SIZE's gfx950 undercount is calibrated for wide streams
-        # only, so the raw count is the reported traffic, the doubled one a bound
+        # same rule as every kernel; for these gathers the width is uncalibrated, so
+        # the raw figure (a lower bound) is kept beside it
         per[ENCODE] = {"source": f"profiles/{a.tag}_traffic.json",
                        "bytes_per_launch_per_face":
-                           (ek["fetch_bytes_raw"] + ek["write_bytes"]) / a.batch,
-                       "bytes_per_launch_per_face_fetch_doubled":
                            (ek["fetch_bytes_corrected"] + ek["write_bytes"]) / a.batch,
-                       "fetch_bytes_raw_per_face": ek["fetch_bytes_raw"] / a.batch,
+                       "bytes_per_launch_per_face_fetch_raw":
+                           (ek["fetch_bytes_raw"] + ek["write_bytes"]) / a.batch,
+                       "fetch_bytes_per_face": ek["fetch_bytes_corrected"] / a.batch,
                        "write_bytes_per_face": ek["write_bytes"] / a.batch}
-    tj.write_text(json.dumps({"unit": "HBM bytes per face per launch (FETCH_SIZE x2 + WRITE_SIZE; "
-                                      "ngp_encode_kernel: FETCH_SIZE raw + WRITE_SIZE)",
+    tj.write_text(json.dumps({"unit": "HBM bytes per face per launch (2 x FETCH_SIZE + WRITE_SIZE, "
+                                      "every kernel)",
                               "kernels": per}, indent=1))
     print(json.dumps(out, indent=1))
 

@@ -35,9 +35,10 @@ EXPORTS = (
     "sdfr_sh_encode_forward", "sdfr_sh_encode_backward",
     "sdfr_render_ngp_workspace_bytes", "sdfr_render_ngp_forward",
     "sdfr_render_ngp_encode_only", "sdfr_debug_set_field_variant", "sdfr_debug_sin_probe",
-    "sdfr_debug_sin_rev_probe",
+    "sdfr_debug_sin_rev_probe", "sdfr_camera_extrinsics",
     "sdfr_debug_set_encode_mode", "sdfr_debug_set_field_split",
     "sdfr_render_siren_workspace_bytes", "sdfr_render_siren_forward",
+    "sdfr_render_pack_bytes", "sdfr_render_ngp_pack", "sdfr_render_siren_pack",
     "sdfr_fused_bias_act", "sdfr_mapping_linear", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
     "sdfr_modulate_to_nhwc_split",
     "sdfr_conv_pack_bytes", "sdfr_conv_pack_weights", "sdfr_conv3x3_f16x3",
@@ -84,7 +85,7 @@ class NgpRenderArgs(ctypes.Structure):
         ("z_normalize", _int), ("force_background", _int), ("with_sdf", _int),
         ("rgb", _vp), ("features", _vp), ("sdf", _vp), ("xyz", _vp), ("mask", _vp),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
-        ("stage_events", _vp * 4), ("field_precision", _int),
+        ("stage_events", _vp * 4), ("field_precision", _int), ("prepacked", _vp),
     ]
 
 
@@ -148,10 +149,16 @@ def lib():
     L.sdfr_debug_set_field_split.argtypes = [_int]
     L.sdfr_render_siren_workspace_bytes.restype = ctypes.c_size_t
     L.sdfr_render_siren_workspace_bytes.argtypes = [_u32]
+    L.sdfr_render_pack_bytes.argtypes = [_int]
+    L.sdfr_render_pack_bytes.restype = ctypes.c_size_t
+    L.sdfr_render_ngp_pack.argtypes = [ctypes.POINTER(NgpWeights), _vp, _vp]
+    L.sdfr_render_siren_pack.argtypes = [ctypes.POINTER(SirenWeights), _vp, _vp]
     L.sdfr_render_siren_forward.argtypes = [ctypes.POINTER(SirenWeights),
                                             ctypes.POINTER(NgpRenderArgs), _vp]
     L.sdfr_debug_sin_probe.argtypes = [_vp, _vp, _vp, _u32, _vp]
     L.sdfr_debug_sin_rev_probe.argtypes = [_vp, _vp, _u32, _vp]
+    L.sdfr_camera_extrinsics.argtypes = [_vp, _vp, _u32, _f32, _f32, _f32, _vp, _vp, _vp, _vp,
+                                         _vp, _vp]
     L.sdfr_fused_bias_act.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_uint64, _u32, _u32, _int, _int,
                                       _f32, _f32, _vp]
     L.sdfr_mapping_linear.argtypes = [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _f32, _f32, _int, _f32,

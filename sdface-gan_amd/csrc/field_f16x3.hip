@@ -1032,26 +1032,31 @@ struct NetPtrs {
     const float *sigma_w, *sigma_b, *rgb_w, *rgb_b, *sigmoid_beta;
 };
 
+// Row scales, scaled biases and the packed MFMA A-fragments (xscale_kernel + the
+// packing blocks of xprep_kernel) into `xws`; with styles/film the per-face FiLM
+// blocks too.  pack_only: no FiLM (sdfr_render_*_pack).
 template <class Net>
-static int launch_xprep(const NetPtrs &P, const sdfr_ngp_render_args *a, char *xws, float *film,
-                        hipStream_t st) {
+static int launch_xpack(const NetPtrs &P, uint32_t B, const float *styles, char *xws, float *film,
+                        bool pack, hipStream_t st) {
     f4 *packed = reinterpret_cast<f4 *>(xws);
     float *su = reinterpret_cast<float *>(xws + (size_t)Net::kSlices * kXSliceF4 * sizeof(f4));
     float *bias_s = su + Net::kLayers * kW;
-    XScaleArgs sa;
-    for (int l = 0; l < Net::kLayers; ++l) {
-        sa.w[l] = P.w[l];
-        sa.b[l] = P.b[l];
-        sa.K[l] = Net::K(l);
+    if (pack) {
+        XScaleArgs sa;
+        for (int l = 0; l < Net::kLayers; ++l) {
+            sa.w[l] = P.w[l];
+            sa.b[l] = P.b[l];
+            sa.K[l] = Net::K(l);
+        }
+        sa.su = su;
+        sa.bias_s = bias_s;
+        sa.raw_bias0 = !Net::kSiren;
+        hipLaunchKernelGGL(xscale_kernel, dim3(Net::kLayers, kW / 4), dim3(256), 0, st, sa);
+        int rc = check_launch("render: xscale");
+        if (rc) return rc;
     }
-    sa.su = su;
-    sa.bias_s = bias_s;
-    sa.raw_bias0 = !Net::kSiren;
-    hipLaunchKernelGGL(xscale_kernel, dim3(Net::kLayers, kW / 4), dim3(256), 0, st, sa);
-    int rc = check_launch("render: xscale");
-    if (rc) return rc;
     XPrepArgs p;
-    p.styles = a->styles;
+    p.styles = styles;
     for (int f = 0; f < Net::kFilmN; ++f) {
         p.gw[f] = P.gw[f];
         p.gb[f] = P.gb[f];
@@ -1065,10 +1070,24 @@ static int launch_xprep(const NetPtrs &P, const sdfr_ngp_render_args *a, char *x
     p.su = su;
     p.film = film;
     p.packed = packed;
-    p.B = a->B;
-    const uint32_t blocks = a->B * Net::kFilmN * 2 + (Net::kSlices * 512 + 255) / 256;
+    p.B = film ? B : 0;
+    // blocks [0, B films x 2): FiLM rows; then (pack) the fragment packing
+    const uint32_t nfilm = p.B * Net::kFilmN * 2;
+    const uint32_t blocks = nfilm + (pack ? (Net::kSlices * 512 + 255) / 256 : 0);
+    if (blocks == 0) return SDFR_OK;
     hipLaunchKernelGGL(xprep_kernel<Net>, dim3(blocks), dim3(256), 0, st, p);
     return check_launch("render: xprep");
+}
+
+// Per call: FiLM vectors of the batch, and the weight packing unless the caller
+// passed weights packed beforehand (a->prepacked, f16x3 only).
+template <class Net>
+static int launch_xprep(const NetPtrs &P, const sdfr_ngp_render_args *a, char *xws, float *film,
+                        hipStream_t st) {
+    if (a->prepacked)
+        return launch_xpack<Net>(P, a->B, a->styles, const_cast<char *>(
+                                     reinterpret_cast<const char *>(a->prepacked)), film, false, st);
+    return launch_xpack<Net>(P, a->B, a->styles, xws, film, true, st);
 }
 
 template <class Net>
@@ -1078,6 +1097,7 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     XFieldArgs f;
     f.g = g;
     f.enc = enc;
+    if (a->prepacked) xws = const_cast<char *>(reinterpret_cast<const char *>(a->prepacked));
     f.packed = reinterpret_cast<const f4 *>(xws);
     f.su = reinterpret_cast<const float *>(xws + (size_t)Net::kSlices * kXSliceF4 * sizeof(f4));
     f.bias_s = f.su + Net::kLayers * kW;
@@ -1171,6 +1191,30 @@ static size_t siren_ws_layout(uint32_t B, size_t *o_x) {
     return off + align256x(xws_bytes<SirenNet>());
 }
 
+static NetPtrs siren_ptrs(const sdfr_siren_weights *w) {
+    NetPtrs P{};
+    for (int l = 0; l < 8; ++l) {
+        P.w[l] = w->pts_w[l];
+        P.b[l] = w->pts_b[l];
+        P.gw[l] = w->pts_gw[l];
+        P.gb[l] = w->pts_gb[l];
+        P.bw[l] = w->pts_bw[l];
+        P.bb[l] = w->pts_bb[l];
+    }
+    P.w[8] = w->views_w;
+    P.b[8] = w->views_b;
+    P.gw[8] = w->views_gw;
+    P.gb[8] = w->views_gb;
+    P.bw[8] = w->views_bw;
+    P.bb[8] = w->views_bb;
+    P.sigma_w = w->sigma_w;
+    P.sigma_b = w->sigma_b;
+    P.rgb_w = w->rgb_w;
+    P.rgb_b = w->rgb_b;
+    P.sigmoid_beta = w->sigmoid_beta;
+    return P;
+}
+
 static int siren_validate(const sdfr_siren_weights *w, const sdfr_ngp_render_args *a) {
     if (!w || !a) return fail(SDFR_EINVAL, "render_siren: null args");
     if (w->depth != 8 || w->width != 256)
@@ -1205,6 +1249,22 @@ extern "C" {
 
 size_t sdfr_render_siren_workspace_bytes(uint32_t B) { return siren_ws_layout(B, nullptr); }
 
+size_t sdfr_render_pack_bytes(int net) {
+    return net ? xws_bytes<SirenNet>() : xws_bytes<NgpNet>();
+}
+
+int sdfr_render_ngp_pack(const sdfr_ngp_weights *w, void *packed, void *stream) {
+    if (!w || !packed) return fail(SDFR_EINVAL, "render_ngp_pack: null pointer");
+    return launch_xpack<NgpNet>(ngp_ptrs(w), 0, nullptr, reinterpret_cast<char *>(packed), nullptr,
+                                true, (hipStream_t)stream);
+}
+
+int sdfr_render_siren_pack(const sdfr_siren_weights *w, void *packed, void *stream) {
+    if (!w || !packed) return fail(SDFR_EINVAL, "render_siren_pack: null pointer");
+    return launch_xpack<SirenNet>(siren_ptrs(w), 0, nullptr, reinterpret_cast<char *>(packed),
+                                  nullptr, true, (hipStream_t)stream);
+}
+
 int sdfr_render_siren_forward(const sdfr_siren_weights *w, const sdfr_ngp_render_args *a,
                               void *stream) {
     int rc = siren_validate(w, a);
@@ -1214,26 +1274,7 @@ int sdfr_render_siren_forward(const sdfr_siren_weights *w, const sdfr_ngp_render
     siren_ws_layout(a->B, &o_x);
     char *ws = reinterpret_cast<char *>(a->workspace);
     float *film = reinterpret_cast<float *>(ws);
-    NetPtrs P{};
-    for (int l = 0; l < 8; ++l) {
-        P.w[l] = w->pts_w[l];
-        P.b[l] = w->pts_b[l];
-        P.gw[l] = w->pts_gw[l];
-        P.gb[l] = w->pts_gb[l];
-        P.bw[l] = w->pts_bw[l];
-        P.bb[l] = w->pts_bb[l];
-    }
-    P.w[8] = w->views_w;
-    P.b[8] = w->views_b;
-    P.gw[8] = w->views_gw;
-    P.gb[8] = w->views_gb;
-    P.bw[8] = w->views_bw;
-    P.bb[8] = w->views_bb;
-    P.sigma_w = w->sigma_w;
-    P.sigma_b = w->sigma_b;
-    P.rgb_w = w->rgb_w;
-    P.rgb_b = w->rgb_b;
-    P.sigmoid_beta = w->sigmoid_beta;
+    const NetPtrs P = siren_ptrs(w);
     GeomArgs g;
     fill_geom_args(a, 1.0f, g);
     record_event(a->stage_events[0], st);

@@ -346,6 +346,67 @@ __global__ void sin_rev_probe_kernel(const float *__restrict__ u, float *__restr
     if (i < n) out[i] = sin_rev(u[i]);
 }
 
+// Camera extrinsics from sampled angles (sdf_utils.py:136-159, after the random
+// draws), one thread per camera: the op chain of generate_camera_params in one
+// launch instead of ~25 elementwise / reduction kernels.  Each op rounds once,
+// as the tensor ops do; the library's sinf / cosf / sqrtf and the order of the
+// 3-term norm may differ from torch's kernels by an ulp.
+struct CamArgs {
+    const float *azim, *elev;      // [B]
+    float *ext, *vp;               // [B,3,4], [B,2]
+    float *focal, *near_, *far_;   // [B] each
+    float radius, fov_ang, half_res;
+    uint32_t B;
+};
+
+__device__ __forceinline__ void cam_normalize(float (&v)[3]) {   // F.normalize(eps = 1e-5)
+    const float n = fmaxf(__fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(v[0], v[0]), __fmul_rn(v[1], v[1])),
+                                               __fmul_rn(v[2], v[2]))), 1e-5f);
+    v[0] = __fdiv_rn(v[0], n);
+    v[1] = __fdiv_rn(v[1], n);
+    v[2] = __fdiv_rn(v[2], n);
+}
+
+__device__ __forceinline__ void cam_cross(const float (&a)[3], const float (&b)[3], float (&c)[3]) {
+    c[0] = __fsub_rn(__fmul_rn(a[1], b[2]), __fmul_rn(a[2], b[1]));
+    c[1] = __fsub_rn(__fmul_rn(a[2], b[0]), __fmul_rn(a[0], b[2]));
+    c[2] = __fsub_rn(__fmul_rn(a[0], b[1]), __fmul_rn(a[1], b[0]));
+}
+
+__global__ void camera_kernel(const CamArgs c) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= c.B) return;
+    const float az = c.azim[b], el = c.elev[b];
+    c.vp[2 * b] = az;
+    c.vp[2 * b + 1] = el;
+    // dist = 1: near / far = dist -/+ radius; fov = fov_ang * pi / 180; focal = 0.5 res / tan(fov)
+    c.near_[b] = __fsub_rn(1.0f, c.radius);
+    c.far_[b] = __fadd_rn(1.0f, c.radius);
+    const float fov = __fdiv_rn(__fmul_rn(c.fov_ang, (float)M_PI), 180.0f);
+    c.focal[b] = __fdiv_rn(c.half_res, tanf(fov));
+    const float ce = cosf(el);
+    float dir[3] = {__fmul_rn(ce, sinf(az)), sinf(el), __fmul_rn(ce, cosf(az))};
+    const float up[3] = {0.0f, 1.0f, 0.0f};
+    float z[3] = {dir[0], dir[1], dir[2]}, x[3], y[3];
+    cam_normalize(z);
+    cam_cross(up, z, x);
+    cam_normalize(x);
+    cam_cross(z, x, y);
+    cam_normalize(y);
+    if (fabsf(x[0]) <= 5e-3f && fabsf(x[1]) <= 5e-3f && fabsf(x[2]) <= 5e-3f) {   // isclose(x, 0)
+        cam_cross(y, z, x);
+        cam_normalize(x);
+    }
+    float *e = c.ext + 12 * (size_t)b;       // [R^T | T], R rows = x, y, z; T = 1 * dir
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        e[4 * i + 0] = x[i];
+        e[4 * i + 1] = y[i];
+        e[4 * i + 2] = z[i];
+        e[4 * i + 3] = dir[i];
+    }
+}
+
 // Streaming state for the weight ring: slot s of `lds` holds one K-slice.
 struct Ring {
     f4 *lds;              // [3][kSliceF4]
@@ -887,6 +948,18 @@ int sdfr_debug_sin_rev_probe(const float *u, float *out, uint32_t n, void *strea
     hipLaunchKernelGGL(sin_rev_probe_kernel, dim3((n + 255) / 256), dim3(256), 0,
                        (hipStream_t)stream, u, out, n);
     return check_launch("sin_rev_probe");
+}
+
+int sdfr_camera_extrinsics(const float *azim, const float *elev, uint32_t B, float dist_radius,
+                           float fov_ang, float half_res, float *ext, float *focal, float *near_,
+                           float *far_, float *viewpoint, void *stream) {
+    if (B == 0) return SDFR_OK;
+    if (!azim || !elev || !ext || !viewpoint || !focal || !near_ || !far_)
+        return fail(SDFR_EINVAL, "camera_extrinsics: null tensor pointer");
+    hipLaunchKernelGGL(camera_kernel, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                       CamArgs{azim, elev, ext, viewpoint, focal, near_, far_, dist_radius,
+                               fov_ang, half_res, B});
+    return check_launch("camera_extrinsics");
 }
 
 int sdfr_debug_set_field_split(int max_segments) {

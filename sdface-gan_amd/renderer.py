@@ -580,6 +580,8 @@ class VolumeFeatureRenderer(nn.Module):
         if self.stage_events is not None:
             for k, ev in enumerate(self.stage_events):
                 a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)
+        if self.field_precision == "f16x3":
+            a.prepacked = _lib.ptr(self._prepacked(siren, cam))
         if siren:
             if encode_only:
                 raise RuntimeError("the siren renderer has no hash-grid encode stage")
@@ -596,6 +598,28 @@ class VolumeFeatureRenderer(nn.Module):
         if encode_only:
             return ws
         return rgb, features, sdf, mask, xyz, None
+
+    def _prepacked(self, siren, like):
+        """The field kernel's split-fp16 weight packing (row scales, scaled biases,
+        MFMA fragments: sdfr_render_*_pack), redone only when a network parameter
+        changed (data pointer or in-place version), not per call."""
+        key = (siren,) + tuple((p.data_ptr(), p._version) for p in self.network.parameters())
+        cache = getattr(self, "_pack_cache", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        L = _lib.lib()
+        buf = torch.empty(L.sdfr_render_pack_bytes(int(siren)), dtype=torch.uint8,
+                          device=like.device)
+        if siren:
+            w = self._siren_weight_struct()
+            _lib.check(L.sdfr_render_siren_pack(ctypes.byref(w), _lib.ptr(buf),
+                                                _lib.stream_of(like)), "sdfr_render_siren_pack")
+        else:
+            w = self._ngp_weight_struct()
+            _lib.check(L.sdfr_render_ngp_pack(ctypes.byref(w), _lib.ptr(buf), _lib.stream_of(like)),
+                       "sdfr_render_ngp_pack")
+        self._pack_cache = (key, buf)
+        return buf
 
     # ---------------------------------------------------------------- API
     def forward(self, cam_poses, focal, near, far, styles=None, return_eikonal=False,
