@@ -586,19 +586,26 @@ __global__ void __launch_bounds__(512, 1) conv_splitk_kernel(const ConvArgs a) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t wm = wave & 1u, wn = wave >> 1;
     const uint32_t nB = a.Cout / kCT, cb = tile % nB, pix0 = (tile / nB) * kPT;
-    f4 acc[4][4];
+    // every split's 16 f4 loaded before the first add (all 64 loads in flight)
+    f4 acc[4][4], t[3][16];
     const f4 *pp = a.partial + (size_t)blockIdx.x * 16 * 512 + tid;
+    const size_t sstride = (size_t)a.grid * 16 * 512;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = pp[(i * 4 + j) * 512];
-    for (uint32_t s = 1; s < a.ksplit; ++s) {
-        const f4 *q = pp + (size_t)s * a.grid * 16 * 512;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+    for (uint32_t s = 1; s < 4; ++s)
+        if (s < a.ksplit)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] += q[(i * 4 + j) * 512];
-    }
+            for (int q = 0; q < 16; ++q) t[s - 1][q] = pp[s * sstride + q * 512];
+#pragma unroll
+    for (uint32_t s = 1; s < 4; ++s)
+        if (s < a.ksplit)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] += t[s - 1][i * 4 + j];
     conv_epilogue<ACT>(a, acc, lane, wm, wn, cb, pix0, a.B * cl.Hc * cl.Wc, cl.Hc, cl.Wc, cl.py,
                        cl.px);
 }

@@ -79,16 +79,19 @@ __device__ __forceinline__ float sin_hw(float x) {
     return __builtin_amdgcn_sinf(f);
 }
 
-// sin of an argument given in REVOLUTIONS (u = x / 2pi): v_fract_f32 (exact) then
-// the hardware v_sin_f32.  The split-fp16 field kernel folds 1/(2pi) into its FiLM
-// vectors (xprep_kernel), so a FiLM activation sin(gamma x + beta) is ONE fma, this
-// fract and the sin (the reduction of sin_hw costs 4 more VALU per element).  The
-// rounding of the folded argument, |u| 2^-24 revolutions, equals the reference's
-// own rounding of gamma x + beta in radians; accuracy of the hardware sin itself:
-// tests/test_gpu_encoders.py::test_device_sin_rev_accuracy.
-__device__ __forceinline__ float sin_rev(float u) {
-    return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(u));
-}
+// sin of an argument given in REVOLUTIONS (u = x / 2pi): the hardware v_sin_f32
+// alone.  The split-fp16 field kernel folds 1/(2pi) into its FiLM vectors
+// (xprep_kernel), so a FiLM activation sin(gamma x + beta) is ONE fma and this one
+// instruction (the radian sin_hw costs 4 more VALU per element).  v_sin_f32 reduces
+// its argument itself: measured on MI355X over |u| <= 2048 revolutions
+// (scripts/probe_sin_raw.hip, 4 M points per range) its max error against float64
+// sin(2 pi u) equals that of v_sin_f32(v_fract_f32(u)) (1.25e-7), while ~6 % of the
+// results differ from that form in the last bit -- so the exact v_fract_f32 in
+// front of it (one VALU per activation) is dropped.  FiLM arguments stay within
+// |u| <= 32 (|gamma x + beta| <= 200 rad).  The rounding of the folded argument,
+// |u| 2^-24 revolutions, equals the reference's own rounding of gamma x + beta in
+// radians; accuracy: tests/test_gpu_encoders.py::test_device_sin_rev_accuracy.
+__device__ __forceinline__ float sin_rev(float u) { return __builtin_amdgcn_sinf(u); }
 
 // SH degree 4 coefficients 4g..4g+3 of a unit direction (shencoder.cu:50-68)
 __device__ __forceinline__ f4 sh_quad(float x, float y, float z, uint32_t g) {

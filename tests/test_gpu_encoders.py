@@ -147,9 +147,9 @@ def test_device_sin_accuracy(sdfr):
 
 def test_device_sin_rev_accuracy(sdfr):
     """The split-fp16 field kernel's FiLM sin: argument in revolutions (1/(2 pi) folded
-    into gamma / beta), v_fract_f32 + v_sin_f32.  Against float64 sin(2 pi u) over the
-    FiLM range (|gamma x + beta| <= 200 rad, i.e. |u| <= 32) and far beyond it (|u| up
-    to 4096, where the exact fract keeps the hardware sin in its domain)."""
+    into gamma / beta), v_sin_f32 alone (its own range reduction).  Against float64
+    sin(2 pi u) over the FiLM range (|gamma x + beta| <= 200 rad, i.e. |u| <= 32) and
+    far beyond it (|u| up to 4096)."""
     lib = sdfr._lib
     gen = torch.Generator().manual_seed(1)
     for span, tol in ((64.0, 1e-6), (8192.0, 1e-6)):
