@@ -391,7 +391,7 @@ constexpr int kXStage2 = kXSliceF4 / kThreads2;     // float4 staged per thread 
 // SDFR_X2_SIDE: the MFMA group (of 4, two tiles each) after which the register work
 // is issued when not staggered (4 = after all of them)
 #ifndef SDFR_X2_SIDE
-#define SDFR_X2_SIDE 4
+#define SDFR_X2_SIDE 1
 #endif
 // SDFR_X2_SLOTS: LDS-DMA ring slots of one half-slice (16 KB); the DMA of a
 // half-slice is issued SLOTS-1 half-steps ahead of its use
@@ -810,54 +810,64 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
             zero_acc(Y);
             dense_layer2<V, Net>(R, X, Y, act_film(1), act_sdf(2));
         }
+        // compositing weights of the pass's two samples (this lane's s = 2p + colB),
+        // front to back: formed in the views layer's last k-step, in the MFMA shadow
+        // (the sigma head sdfp is complete once the layer's last input pair is
+        // activated)
+        const uint32_t s = 2 * p + (colB ? 1u : 0u);
+        const bool s_ok = s < G.N;
+        const uint32_t sc_ = s_ok ? s : G.N - 1;
+        float sdf = 0.0f, z = 0.0f, wA = 0.0f, wB = 0.0f;
+        auto weights = [&] {
+            sdf = __fadd_rn(group_sum(sdfp), sig_b);
+            z = sample_z(G.sc, nr, fr, ray_index, sc_);
+            const float dist = (sc_ + 1 < G.N)
+                                   ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), z),
+                                               dnorm)
+                                   : __fmul_rn(1e10f, dnorm);
+            float alpha;
+            if (a.with_sdf) {
+                const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
+                alpha = 1.0f - expf(-sig * dist);
+            } else {
+                float raw = sdf;
+                if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
+                const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+                alpha = 1.0f - expf(-sp * dist);
+            }
+            if (!s_ok) alpha = 0.0f;
+            // the pair's weights, identically in both lanes (sample 2p, then 2p+1)
+            const float alpha_o = ror8(alpha);
+            const float aA = colB ? alpha_o : alpha, aB = colB ? alpha : alpha_o;
+            const bool lastA = 2 * p + 1 == G.N, lastB = 2 * p + 2 == G.N;
+            wA = aA * T;
+            if (a.force_background && lastA) wA = 1.0f - wsum;
+            T = T * ((1.0f - aA) + 1e-10f);
+            wsum += wA;
+            wB = aB * T;
+            if (a.force_background && lastB) wB = 1.0f - wsum;
+            if (2 * p + 1 < G.N) {
+                T = T * ((1.0f - aB) + 1e-10f);
+                wsum += wB;
+            } else {
+                wB = 0.0f;
+            }
+        };
+        constexpr bool kComp = (V & 16) == 0;
         zero_acc(X);
         dense_layer2<V, Net>(R, Y, X, act_sdf(NF - 2), NoAct2{});
-        xstep2<V, Net, 0>(R, X, vxh, vxl, [] {});
-        xstep2<V, Net, 1>(R, X, vxh, vxl, [] {});
+        xstep2<V, Net, 0>(R, X, vxh, vxl, [&] {
+            if constexpr (kComp) weights();
+        });
+        xstep2<V, Net, 1>(R, X, vxh, vxl, [&] {
+            if (p + 1 < p_end) load_inputs(2 * p + 2);
+        });
 
-        if (p + 1 < p_end) load_inputs(2 * p + 2);
-        if constexpr ((V & 16) != 0) {
+        if constexpr (!kComp) {
 #pragma unroll
             for (int t = 0; t < 16; ++t) racc0 += (X[t][0] + X[t][1]) + (X[t][2] + X[t][3]);
             racc0 += sdfp;
             continue;
-        }
-        // compositing of the pass's two samples (this lane's s = 2p + colB), front to back
-        const uint32_t s = 2 * p + (colB ? 1u : 0u);
-        const bool s_ok = s < G.N;
-        const uint32_t sc_ = s_ok ? s : G.N - 1;
-        const float sdf = __fadd_rn(group_sum(sdfp), sig_b);
-        const float z = sample_z(G.sc, nr, fr, ray_index, sc_);
-        const float dist = (sc_ + 1 < G.N)
-                               ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), z),
-                                           dnorm)
-                               : __fmul_rn(1e10f, dnorm);
-        float alpha;
-        if (a.with_sdf) {
-            const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
-            alpha = 1.0f - expf(-sig * dist);
-        } else {
-            float raw = sdf;
-            if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
-            const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
-            alpha = 1.0f - expf(-sp * dist);
-        }
-        if (!s_ok) alpha = 0.0f;
-        // the pair's weights, identically in both lanes (sample 2p, then 2p+1)
-        const float alpha_o = ror8(alpha);
-        const float aA = colB ? alpha_o : alpha, aB = colB ? alpha : alpha_o;
-        const bool lastA = 2 * p + 1 == G.N, lastB = 2 * p + 2 == G.N;
-        float wA = aA * T;
-        if (a.force_background && lastA) wA = 1.0f - wsum;
-        T = T * ((1.0f - aA) + 1e-10f);
-        wsum += wA;
-        float wB = aB * T;
-        if (a.force_background && lastB) wB = 1.0f - wsum;
-        if (2 * p + 1 < G.N) {
-            T = T * ((1.0f - aB) + 1e-10f);
-            wsum += wB;
-        } else {
-            wB = 0.0f;
         }
         // colour features f = sin(gamma_v x + beta_v); rgb_linear
         const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
