@@ -395,6 +395,12 @@ constexpr int kXStage2 = kXSliceF4 / kThreads2;     // float4 staged per thread 
 #endif
 // SDFR_X2_SLOTS: LDS-DMA ring slots of one half-slice (16 KB); the DMA of a
 // half-slice is issued SLOTS-1 half-steps ahead of its use
+// SDFR_X2_KSTEP_SYNC: with the LDS-DMA ring, DMA and barrier per whole k-step (two
+// half-slices, the next k-step fetched one k-step ahead: 34 barriers per ngp pass)
+// instead of per half-step (68)
+#ifndef SDFR_X2_KSTEP_SYNC
+#define SDFR_X2_KSTEP_SYNC 1
+#endif
 #ifndef SDFR_X2_SLOTS
 #define SDFR_X2_SLOTS 4
 #endif
@@ -463,8 +469,18 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
     constexpr bool kDma = SDFR_X2_DMA;
     const uint32_t lane = R.tid & 63u;
     constexpr uint32_t kAhead = x2_slots<Net>() - 1;
-    if constexpr (kDma && (V & 4) == 0)
-        x2_dma(R, (R.it + kAhead) % Net::kSlices, x2_slot<Net>(R, R.it + kAhead));
+    if constexpr (kDma && (V & 4) == 0) {
+        if constexpr (SDFR_X2_KSTEP_SYNC) {
+            // whole k-steps: at its first half the next k-step's two half-slices go
+            // into the slots of the previous k-step (closed by its barrier)
+            if constexpr (H == 0) {
+                x2_dma(R, (R.it + 2) % Net::kSlices, x2_slot<Net>(R, R.it + 2));
+                x2_dma(R, (R.it + 3) % Net::kSlices, x2_slot<Net>(R, R.it + 3));
+            }
+        } else {
+            x2_dma(R, (R.it + kAhead) % Net::kSlices, x2_slot<Net>(R, R.it + kAhead));
+        }
+    }
     const f4 *A = kDma ? R.lds + x2_slot<Net>(R, R.it) * kXSliceF4 + lane
                 : kS2  ? R.lds + ((R.it >> 1) & 1u) * (2 * kXSliceF4) + H * kXSliceF4 + lane
                        : R.lds + (R.it % 3u) * kXSliceF4 + lane;
@@ -519,7 +535,17 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
     side();
 #endif
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (kDma) {
+    if constexpr (kDma && SDFR_X2_KSTEP_SYNC) {
+        // end of a k-step: own pieces of the next k-step have landed; the barrier
+        // publishes every wave's and closes this k-step's slots
+        if constexpr (H == 1) {
+            if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr ((V & 1) == 0) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+        }
+    } else if constexpr (kDma) {
         // own pieces of half-slice it+1 (issued two half-steps ago) have landed; the
         // barrier publishes every wave's (and closes this slot for the DMA of it+4)
         if constexpr ((V & 4) == 0)
@@ -678,7 +704,8 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
     if constexpr (SDFR_X2_DMA) {
         // prologue: half-slices 0 .. SLOTS-2 -> their slots (the first step issues the next)
         R.slot0 = 0;
-        for (uint32_t k = 0; k + 1 < (uint32_t)x2_slots<Net>(); ++k) x2_dma(R, k % Net::kSlices, k);
+        const uint32_t pro = SDFR_X2_KSTEP_SYNC ? 2u : (uint32_t)x2_slots<Net>() - 1;
+        for (uint32_t k = 0; k < pro; ++k) x2_dma(R, k % Net::kSlices, k);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if constexpr (Net::kSlice2) {
         // prologue: K-step 0 (half-slices 0, 1) -> slot 0; K-step 1 -> registers
