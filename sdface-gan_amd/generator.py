@@ -452,6 +452,35 @@ class Decoder(nn.Module):
         d = torch.rsqrt(torch.baddbmm(eps, m * m, wsq))
         return {i: d[j, :, :packs[i][2].shape[1]].contiguous() for j, i in enumerate(layers)}
 
+    def _fused_noise(self, noise, B, features):
+        """The per-layer noise maps of the fused path: the given ones, and every
+        missing one (randomize_noise) sliced from ONE standard-normal draw of all of
+        their elements, layer after layer -- one launch instead of one per layer (the
+        module path draws each layer's map separately, NoiseInjection, so the two
+        paths' random maps differ; their distribution does not)."""
+        missing = [i for i, n in enumerate(noise) if n is None]
+        if not missing:
+            return noise
+        sizes = [2 ** ((i + 2 * self.log_in_size + 1) // 2) for i in range(self.num_layers)]
+        total = sum(B * sizes[i] * sizes[i] for i in missing)
+        flat = torch.randn(total, device=features.device, dtype=features.dtype)
+        out, off = list(noise), 0
+        for i in missing:
+            n = B * sizes[i] * sizes[i]
+            out[i] = flat[off:off + n].view(B, 1, sizes[i], sizes[i])
+            off += n
+        return out
+
+    def _rgb_base(self, tc):
+        """ToRGB's scaled 1x1 weight [3, C] (tc.scale * weight), once per weight version."""
+        key = (tc.weight.data_ptr(), tc.weight._version)
+        cache = getattr(tc, "_sdfr_base", None)
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                cache = (key, tc.scale * tc.weight[0, :, :, 0, 0])
+            tc._sdfr_base = cache
+        return cache[1]
+
     def _fused_forward(self, features, latent, noise):
         """Same computation as the module path: per layer one split-fp16 convolution
         (or MIOpen's) plus one sdfr_styled_epilogue on NHWC activations -- for the
@@ -463,6 +492,7 @@ class Decoder(nn.Module):
         B = features.shape[0]
         seq = [self.conv1] + list(self.convs)
         mods, rgb_mods, mods_raw = self._modulations(latent)
+        noise = self._fused_noise(noise, B, features)
         split = [self._conv_x(sc.conv) for sc in seq]     # layer i's input as hi/lo planes
         demods = self._demods(seq, split, mods_raw)
         x = (modulate_to_nhwc_split if split[0] else modulate_to_nhwc)(features, mods[0])
@@ -478,13 +508,13 @@ class Decoder(nn.Module):
                     and (x.shape[1] * x.shape[2]) % 256 == 0):
                 # regular conv with the epilogue fused: the conv output stays on chip
                 H, W = x.shape[1], x.shape[2]
-                n = noise[i] if noise[i] is not None else features.new_empty(B, 1, H, W).normal_()
+                n = noise[i]
                 rgb_w = None
                 if i % 2 == 0:
                     to_rgb = self.to_rgb1 if i == 0 else self.to_rgbs[i // 2 - 1]
                     tc = to_rgb.conv
                     s_rgb = rgb_mods[i // 2]
-                    rgb_w = (tc.scale * tc.weight[0, :, :, 0, 0])[None] * s_rgb[:, None, :]
+                    rgb_w = self._rgb_base(tc)[None] * s_rgb[:, None, :]
                 x, part = conv3x3_f16x3_act(
                     x, packed, cout, demod=demod_su, bias=sc.activate.bias,
                     noise_weight=sc.noise.weight, noise=n,
@@ -508,13 +538,13 @@ class Decoder(nn.Module):
                 H, W = out.shape[2] - 1, out.shape[3] - 1
             else:
                 H, W = out.shape[2], out.shape[3]
-            n = noise[i] if noise[i] is not None else features.new_empty(B, 1, H, W).normal_()
+            n = noise[i]
             rgb_w = rgb_b = None
             if i % 2 == 0:
                 to_rgb = self.to_rgb1 if i == 0 else self.to_rgbs[i // 2 - 1]
                 tc = to_rgb.conv
                 s_rgb = rgb_mods[i // 2]
-                rgb_w = (tc.scale * tc.weight[0, :, :, 0, 0])[None] * s_rgb[:, None, :]
+                rgb_w = self._rgb_base(tc)[None] * s_rgb[:, None, :]
                 rgb_b = to_rgb.bias
             x, rgb_new = styled_epilogue(
                 out, fir=self._fir, bias=sc.activate.bias, noise_weight=sc.noise.weight,
