@@ -297,6 +297,30 @@ int sdfr_mapping_linear(float *out, const float *x, const float *w, const float 
                         uint32_t K, uint32_t O, float wscale, float bscale, int act, float slope,
                         float act_scale, int pixelnorm, void *stream);
 
+/* sdfr_decoder_styles: the fused decoder's per-call style prep (sdf_model.py:676-699):
+ *   mods[off_k + b c_k + c] = latent[b, idx_k] . mod_w[k, c] + mod_b[k, c]
+ *     (mod_w = EqualLinear weight * scale, mod_b = bias * lr_mul; rows zero-padded to cmax)
+ *   demods[doff_j + b o_j + o] = rsqrt(dem_eps[j, o] + sum_c mods[layer_j][b, c]^2 dem_w[j, o, c])
+ *     (dem_w = su^2 sum_{ky,kx} w^2 transposed to [Cout, Cin], dem_eps = su^2 1e-8).
+ * K (style dim) and cmax are 256 or 512; L, J <= 16.  fp32, dot products summed in
+ * a fixed order that is not a GEMM's (fp32 rounding level). */
+typedef struct sdfr_style_args {
+    uint32_t B, n_latent, K;
+    const float *latent;              /* [B, n_latent, K]                        */
+    uint32_t L, cmax;
+    const float *mod_w;               /* [L, cmax, K]                            */
+    const float *mod_b;               /* [L, cmax]                               */
+    uint32_t mod_index[16], mod_c[16], mod_off[16];
+    float *mods;                      /* per layer [B, c_k] at mod_off[k]        */
+    uint32_t J, omax;
+    const float *dem_w;               /* [J, omax, cmax]                         */
+    const float *dem_eps;             /* [J, omax]                               */
+    uint32_t dem_layer[16], dem_c[16], dem_off[16];
+    float *demods;                    /* per layer [B, o_j] at dem_off[j]        */
+} sdfr_style_args;
+
+int sdfr_decoder_styles(const sdfr_style_args *a, void *stream);
+
 /* sdfr_upfirdn2d <- upfirdn2d (upfirdn2d.cpp:12, upfirdn2d_kernel.cu; caller
  * sdf_op.py:230): input viewed as [major, in_h, in_w] (minor = 1), kernel
  * [kernel_h, kernel_w] (device), out [major, out_h, out_w] with

@@ -39,7 +39,7 @@ EXPORTS = (
     "sdfr_debug_set_encode_mode", "sdfr_debug_set_field_split",
     "sdfr_render_siren_workspace_bytes", "sdfr_render_siren_forward",
     "sdfr_render_pack_bytes", "sdfr_render_ngp_pack", "sdfr_render_siren_pack",
-    "sdfr_fused_bias_act", "sdfr_mapping_linear", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
+    "sdfr_fused_bias_act", "sdfr_mapping_linear", "sdfr_decoder_styles", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
     "sdfr_modulate_to_nhwc_split",
     "sdfr_conv_pack_bytes", "sdfr_conv_pack_weights", "sdfr_conv3x3_f16x3",
     "sdfr_conv3x3_f16x3_act", "sdfr_conv_act_ws_bytes", "sdfr_rgb_finish",
@@ -98,6 +98,17 @@ class StyledEpilogueArgs(ctypes.Structure):
         ("negative_slope", _f32), ("act_scale", _f32),
         ("s_next", _vp), ("y", _vp), ("rgb_w", _vp), ("rgb_b", _vp), ("skip", _vp), ("rgb", _vp),
         ("y_split", _vp),
+    ]
+
+
+class StyleArgs(ctypes.Structure):
+    """sdfr_style_args (include/sdfr.h)."""
+    _fields_ = [
+        ("B", _u32), ("n_latent", _u32), ("K", _u32), ("latent", _vp),
+        ("L", _u32), ("cmax", _u32), ("mod_w", _vp), ("mod_b", _vp),
+        ("mod_index", _u32 * 16), ("mod_c", _u32 * 16), ("mod_off", _u32 * 16), ("mods", _vp),
+        ("J", _u32), ("omax", _u32), ("dem_w", _vp), ("dem_eps", _vp),
+        ("dem_layer", _u32 * 16), ("dem_c", _u32 * 16), ("dem_off", _u32 * 16), ("demods", _vp),
     ]
 
 
@@ -163,6 +174,7 @@ def lib():
                                       _f32, _f32, _vp]
     L.sdfr_mapping_linear.argtypes = [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _f32, _f32, _int, _f32,
                                       _f32, _int, _vp]
+    L.sdfr_decoder_styles.argtypes = [ctypes.POINTER(StyleArgs), _vp]
     L.sdfr_upfirdn2d.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32] + [_int] * 8 + [_vp]
     L.sdfr_styled_epilogue.argtypes = [ctypes.POINTER(StyledEpilogueArgs), _vp]
     L.sdfr_modulate_to_nhwc.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _vp]

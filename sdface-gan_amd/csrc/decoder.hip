@@ -544,6 +544,138 @@ __global__ __launch_bounds__(256) void mapping_linear_kernel(const MapArgs a) {
     }
 }
 
+// ----------------------------------------------------------------------------
+// Decoder style prep for inference (sdf_model.py:676-699): every layer's
+// modulation s_k = latent[:, idx_k] . (W_k scale)^T + b_k lr_mul (conv and ToRGB
+// EqualLinears) and every split-fp16 layer's demodulation / su,
+// rsqrt(eps + s^2 . wsq) -- two launches instead of the batched GEMMs, gathers,
+// copies and rsqrt of the module code.  Same structure as mapping_linear_kernel:
+// a wave per output channel, lanes over the reduction, butterfly sum.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void style_mod_kernel(const sdfr_style_args a) {
+    __shared__ float xs[kMapB * kMapMaxK];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t k = blockIdx.y, c = blockIdx.x * kMapOut + wv;
+    const uint32_t ck = a.mod_c[k], K = a.K, kl = K / 64, k0 = lane * kl;
+    for (uint32_t b0 = blockIdx.z * kMapB; b0 < a.B; b0 += gridDim.z * kMapB) {
+        const uint32_t nb = min(kMapB, a.B - b0);
+        for (uint32_t i = t; i < nb * K; i += 256) {
+            const uint32_t b = i / K, j = i - b * K;
+            xs[i] = a.latent[((size_t)(b0 + b) * a.n_latent + a.mod_index[k]) * K + j];
+        }
+        __syncthreads();
+        float acc[kMapB];
+#pragma unroll
+        for (uint32_t b = 0; b < kMapB; ++b) acc[b] = 0.0f;
+        if (c < ck) {
+            const float *wr = a.mod_w + ((size_t)k * a.cmax + c) * K + k0;
+            for (uint32_t j = 0; j < kl; j += 4) {
+                const float4 w4 = *reinterpret_cast<const float4 *>(wr + j);
+#pragma unroll
+                for (uint32_t b = 0; b < kMapB; ++b) {
+                    if (b < nb) {
+                        const float4 x4 = *reinterpret_cast<const float4 *>(&xs[b * K + k0 + j]);
+                        acc[b] = __fmaf_rn(x4.x, w4.x, acc[b]);
+                        acc[b] = __fmaf_rn(x4.y, w4.y, acc[b]);
+                        acc[b] = __fmaf_rn(x4.z, w4.z, acc[b]);
+                        acc[b] = __fmaf_rn(x4.w, w4.w, acc[b]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kMapB; ++b)
+            if (b < nb)
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) acc[b] = __fadd_rn(acc[b], __shfl_xor(acc[b], m));
+        if (c < ck && lane < nb) {
+            float y = 0.0f;
+#pragma unroll
+            for (uint32_t b = 0; b < kMapB; ++b)
+                if (b == lane) y = acc[b];
+            a.mods[a.mod_off[k] + (size_t)(b0 + lane) * ck + c] =
+                __fadd_rn(y, a.mod_b[(size_t)k * a.cmax + c]);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void style_demod_kernel(const sdfr_style_args a) {
+    __shared__ float xs[kMapB * kMapMaxK];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t j = blockIdx.y, o = blockIdx.x * kMapOut + wv;
+    const uint32_t layer = a.dem_layer[j], cin = a.mod_c[layer], oj = a.dem_c[j];
+    const uint32_t C = a.cmax, kl = C / 64, k0 = lane * kl;
+    const float *mk = a.mods + a.mod_off[layer];
+    for (uint32_t b0 = blockIdx.z * kMapB; b0 < a.B; b0 += gridDim.z * kMapB) {
+        const uint32_t nb = min(kMapB, a.B - b0);
+        for (uint32_t i = t; i < nb * C; i += 256) {
+            const uint32_t b = i / C, cc = i - b * C;
+            const float m = cc < cin ? mk[(size_t)(b0 + b) * cin + cc] : 0.0f;
+            xs[i] = __fmul_rn(m, m);
+        }
+        __syncthreads();
+        float acc[kMapB];
+#pragma unroll
+        for (uint32_t b = 0; b < kMapB; ++b) acc[b] = 0.0f;
+        if (o < oj) {
+            const float *wr = a.dem_w + ((size_t)j * a.omax + o) * C + k0;
+            for (uint32_t q = 0; q < kl; q += 4) {
+                const float4 w4 = *reinterpret_cast<const float4 *>(wr + q);
+#pragma unroll
+                for (uint32_t b = 0; b < kMapB; ++b) {
+                    if (b < nb) {
+                        const float4 x4 = *reinterpret_cast<const float4 *>(&xs[b * C + k0 + q]);
+                        acc[b] = __fmaf_rn(x4.x, w4.x, acc[b]);
+                        acc[b] = __fmaf_rn(x4.y, w4.y, acc[b]);
+                        acc[b] = __fmaf_rn(x4.z, w4.z, acc[b]);
+                        acc[b] = __fmaf_rn(x4.w, w4.w, acc[b]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kMapB; ++b)
+            if (b < nb)
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) acc[b] = __fadd_rn(acc[b], __shfl_xor(acc[b], m));
+        if (o < oj && lane < nb) {
+            float y = 0.0f;
+#pragma unroll
+            for (uint32_t b = 0; b < kMapB; ++b)
+                if (b == lane) y = acc[b];
+            a.demods[a.dem_off[j] + (size_t)(b0 + lane) * oj + o] =
+                rsqrtf(__fadd_rn(a.dem_eps[(size_t)j * a.omax + o], y));
+        }
+        __syncthreads();
+    }
+}
+
+int sdfr_decoder_styles(const sdfr_style_args *p, void *stream) {
+    if (!p) return fail(SDFR_EINVAL, "decoder_styles: null args");
+    const sdfr_style_args &a = *p;
+    if (a.B == 0) return SDFR_OK;
+    if (a.L == 0 || a.L > 16 || a.J > 16)
+        return fail(SDFR_EINVAL, "decoder_styles: 1 <= L <= 16 and J <= 16 layers");
+    if (a.K % 256 != 0 || a.K > kMapMaxK || a.cmax % 256 != 0 || a.cmax > kMapMaxK)
+        return fail(SDFR_EINVAL, "decoder_styles: style dim and widest layer must be 256 or 512");
+    if (!a.latent || !a.mod_w || !a.mod_b || !a.mods || (a.J && (!a.dem_w || !a.dem_eps || !a.demods)))
+        return fail(SDFR_EINVAL, "decoder_styles: null tensor pointer");
+    for (uint32_t k = 0; k < a.L; ++k)
+        if (a.mod_c[k] > a.cmax || a.mod_index[k] >= a.n_latent)
+            return fail(SDFR_EINVAL, "decoder_styles: layer width / latent index out of range");
+    for (uint32_t j = 0; j < a.J; ++j)
+        if (a.dem_layer[j] >= a.L || a.dem_c[j] > a.omax)
+            return fail(SDFR_EINVAL, "decoder_styles: demodulation layer out of range");
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t bz = std::min<uint32_t>((a.B + kMapB - 1) / kMapB, 64);
+    style_mod_kernel<<<dim3(a.cmax / kMapOut, a.L, bz), 256, 0, st>>>(a);
+    int rc = check_launch("decoder_styles: modulations");
+    if (rc || a.J == 0) return rc;
+    style_demod_kernel<<<dim3((a.omax + kMapOut - 1) / kMapOut, a.J, bz), 256, 0, st>>>(a);
+    return check_launch("decoder_styles: demodulations");
+}
+
 int sdfr_mapping_linear(float *out, const float *x, const float *w, const float *b, uint32_t B,
                         uint32_t K, uint32_t O, float wscale, float bscale, int act, float slope,
                         float act_scale, int pixelnorm, void *stream) {

@@ -452,6 +452,79 @@ class Decoder(nn.Module):
         d = torch.rsqrt(torch.baddbmm(eps, m * m, wsq))
         return {i: d[j, :, :packs[i][2].shape[1]].contiguous() for j, i in enumerate(layers)}
 
+    def _styles_fused(self, latent, seq, split):
+        """_modulations + _demods in two HIP launches (sdfr_decoder_styles): the
+        stacked, scaled weights are built once per weight version; the per-layer
+        modulations and demodulations come back as contiguous slices of two flat
+        buffers.  fp32, fixed summation order (not the batched GEMM's)."""
+        from . import _lib
+        rgbs = [self.to_rgb1] + list(self.to_rgbs)
+        lins = [sc.conv.modulation for sc in seq] + [t.conv.modulation for t in rgbs]
+        nconv = len(seq)
+        key = tuple((m.weight.data_ptr(), m.weight._version, m.bias._version) for m in lins)
+        cache = getattr(self, "_sty_mod", None)
+        if cache is None or cache[0] != key:
+            cmax = max(256, max(m.weight.shape[0] for m in lins))
+            w0 = lins[0].weight
+            mw = w0.new_zeros(len(lins), cmax, w0.shape[1])
+            mb = w0.new_zeros(len(lins), cmax)
+            with torch.no_grad():
+                for k, m in enumerate(lins):
+                    c = m.weight.shape[0]
+                    mw[k, :c] = m.weight * m.scale
+                    mb[k, :c] = m.bias * m.lr_mul
+            idx = list(range(nconv)) + [2 * k + 1 for k in range(len(rgbs))]
+            cache = (key, mw, mb, idx, [m.weight.shape[0] for m in lins], cmax)
+            self._sty_mod = cache
+        _, mw, mb, idx, couts, cmax = cache
+        layers = [i for i, sc in enumerate(seq) if split[i] and sc.conv.demodulate]
+        packs = {i: self._pack(i, seq[i].conv) for i in layers}
+        dkey = tuple(self._packs[i][0] for i in layers)
+        dcache = getattr(self, "_sty_dem", None)
+        if layers and (dcache is None or dcache[0] != dkey):
+            omax = max(packs[i][2].shape[1] for i in layers)
+            w0 = packs[layers[0]][2]
+            dw = w0.new_zeros(len(layers), omax, cmax)
+            de = w0.new_zeros(len(layers), omax)
+            for j, i in enumerate(layers):
+                cin, cout = packs[i][2].shape
+                dw[j, :cout, :cin] = packs[i][2].t()
+                de[j, :cout] = packs[i][3]
+            dcache = (dkey, dw, de, omax)
+            self._sty_dem = dcache
+        B = latent.shape[0]
+        lat = latent.contiguous()
+        a = _lib.StyleArgs()
+        a.B, a.n_latent, a.K, a.latent = B, lat.shape[1], lat.shape[2], _lib.ptr(lat)
+        a.L, a.cmax, a.mod_w, a.mod_b = len(lins), cmax, _lib.ptr(mw), _lib.ptr(mb)
+        offs, off = [], 0
+        for k, c in enumerate(couts):
+            a.mod_index[k], a.mod_c[k], a.mod_off[k] = idx[k], c, off
+            offs.append(off)
+            off += B * c
+        mflat = torch.empty(off, device=lat.device)
+        a.mods = _lib.ptr(mflat)
+        dflat = None
+        if layers:
+            _, dw, de, omax = dcache
+            a.J, a.omax, a.dem_w, a.dem_eps = len(layers), omax, _lib.ptr(dw), _lib.ptr(de)
+            doffs, doff = [], 0
+            for j, i in enumerate(layers):
+                cout = packs[i][2].shape[1]
+                a.dem_layer[j], a.dem_c[j], a.dem_off[j] = i, cout, doff
+                doffs.append(doff)
+                doff += B * cout
+            dflat = torch.empty(doff, device=lat.device)
+            a.demods = _lib.ptr(dflat)
+        _lib.check(_lib.lib().sdfr_decoder_styles(a, _lib.stream_of(lat)), "sdfr_decoder_styles")
+        mods = [mflat[o:o + B * c].view(B, c) for o, c in zip(offs, couts)]
+        demods = {}
+        if layers:
+            for j, i in enumerate(layers):
+                cout = packs[i][2].shape[1]
+                demods[i] = dflat[doffs[j]:doffs[j] + B * cout].view(B, cout)
+        return mods[:nconv], mods[nconv:], demods
+
     def _fused_noise(self, noise, B, features):
         """The per-layer noise maps of the fused path: the given ones, and every
         missing one (randomize_noise) sliced from ONE standard-normal draw of all of
@@ -491,10 +564,13 @@ class Decoder(nn.Module):
         cl = torch.channels_last
         B = features.shape[0]
         seq = [self.conv1] + list(self.convs)
-        mods, rgb_mods, mods_raw = self._modulations(latent)
         noise = self._fused_noise(noise, B, features)
         split = [self._conv_x(sc.conv) for sc in seq]     # layer i's input as hi/lo planes
-        demods = self._demods(seq, split, mods_raw)
+        if latent.is_cuda and latent.dtype == torch.float32 and self.style_dim in (256, 512):
+            mods, rgb_mods, demods = self._styles_fused(latent, seq, split)
+        else:
+            mods, rgb_mods, mods_raw = self._modulations(latent)
+            demods = self._demods(seq, split, mods_raw)
         x = (modulate_to_nhwc_split if split[0] else modulate_to_nhwc)(features, mods[0])
         rgb = None
         for i, sc in enumerate(seq):
