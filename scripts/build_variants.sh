@@ -11,6 +11,7 @@ FIXED=""
 for s in $ALL; do [ "$s" = "$SRC" ] || FIXED="$FIXED build/$s.o"; done
 make -s $FIXED
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall"
+[ "$SRC" = field_f16x3 ] && FLAGS="$FLAGS -fno-slp-vectorize"   # as the Makefile
 pids=()
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
