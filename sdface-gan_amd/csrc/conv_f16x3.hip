@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "sdfr_common.h"
 
@@ -121,6 +122,9 @@ static_assert(CONV_REGDB || kStages == 3, "the single-register-set ring assumes 
 #endif
 #ifndef CONV_ABL
 #define CONV_ABL 0        // timing ablations (wrong results), see the #if CONV_ABL sites
+#endif
+#ifndef CONV_HALO
+#define CONV_HALO 1       // regular convs with the fused epilogue on conv_h_kernel
 #endif
 
 // One output-pixel class: the plain convolution has one (every pixel, 9 taps); the
@@ -226,13 +230,15 @@ template <bool ACT>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4], uint32_t lane,
                                               uint32_t wm, uint32_t wn, uint32_t cb, uint32_t pix0,
                                               uint32_t npix, uint32_t Hc, uint32_t Wc, uint32_t py,
-                                              uint32_t px) {
+                                              uint32_t px, uint32_t rs = 16) {
     // epilogue: lane (n, g) of tile (i, j) holds channels 16 mt + 4 g .. +3 of pixel 16 nt + n
     const uint32_t n = lane & 15u, g = lane >> 4;
     if constexpr (ACT) {
         // Styled epilogue on the accumulators (regular conv, H W % 256 == 0: one face
         // per workgroup): v = lrelu(acc demod + nw noise + bias) scale; y = v s_next
         // as split-NHWC; ToRGB partial over this workgroup's 128 channels -> rgbp.
+        // n-tile row r = 4 wn + j holds pixels pix0 + r rs + n (rs = 16: a 256-pixel
+        // strip; rs = W: a 16 x 16 block, conv_h_kernel).
         __shared__ float red[4][4][16][3];          // [wn][j][n][o] from the wm = 1 waves
         const ActEpi &e = a.e;
         const uint32_t HW = Hc * Wc, b = pix0 / HW;
@@ -254,7 +260,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4]
                                 : f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t P = pix0 + (4 * wn + j) * 16 + n;
+                const uint32_t P = pix0 + (4 * wn + j) * rs + n;
                 const float nz = e.noise ? nw * e.noise[P] : 0.0f;
                 f4 v;
 #pragma unroll
@@ -284,7 +290,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4]
             if (wm == 0 && g < 3) {                 // lane (n, g = o) stores channel o
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const uint32_t P = pix0 + (4 * wn + j) * 16 + n;
+                    const uint32_t P = pix0 + (4 * wn + j) * rs + n;
                     const float s = (g == 0 ? part[j][0] : g == 1 ? part[j][1] : part[j][2]) +
                                     red[wn][j][n][g];
                     e.rgbp[(((size_t)cb * a.B + b) * 3 + g) * HW + (P - b * HW)] = s;
@@ -610,6 +616,212 @@ __global__ void __launch_bounds__(512, 1) conv_splitk_kernel(const ConvArgs a) {
                        cl.px);
 }
 
+// ----------------------------------------------------------------------------
+// conv_h_kernel: the regular 3x3 convolution with the styled epilogue, on 16 x 16
+// pixel blocks whose 18 x 18 input halo is staged ONCE per channel group and read
+// at the nine tap offsets (conv_x_kernel stages every tap's 256 shifted pixels:
+// 9 x 32 KB of activations per channel group against 41 KB here; with the 16 KB of
+// weights per K-step the L2 -> LDS stream per K-step drops from 48 KB to ~21 KB).
+//
+// Halo image per channel group: [hy 18][hx 18] pixels of 128 B (the group's 32
+// channels as split-NHWC quads q = 2 g + lo), quad q stored at slot q ^ swz(hx)
+// with swz(hx) = (hx & 4) | (hx >> 1 & 1): the 16 lanes of every ds_read_b128
+// lane group then hit 16 distinct bank quads whatever the tap's column shift
+// (checked exhaustively for all shifts).  The LDS-DMA applies the swizzle through
+// each lane's source address (a piece's destinations are fixed: 8 consecutive
+// image pixels).  Zero padding: out-of-image lanes read past num_records.
+// A fragment address is a per-lane base (one of 3 column shifts x hi/lo, plus the
+// buffer) and a compile-time offset (row and column of the tap and n-tile), so the
+// unrolled tap loop reads fragments without address VALU.  The weight ring and the
+// mid-step barrier / next-step fragment schedule are conv_x_kernel's (CONV_REGDB);
+// the nine taps of a channel group are unrolled (stage = tap % 3), two groups per
+// loop iteration so the register sets alternate.
+// ----------------------------------------------------------------------------
+constexpr uint32_t kHaloW = 18;
+constexpr uint32_t kHaloPx = kHaloW * kHaloW;          // 324
+constexpr uint32_t kHaloPieces = 48;                  // 6 per wave; 41 carry pixels
+constexpr uint32_t kHaloF4 = kHaloPieces * 64;        // 48 KB per buffer
+
+__device__ __forceinline__ uint32_t halo_swz(uint32_t hx) { return (hx & 4u) | ((hx >> 1) & 1u); }
+
+typedef __attribute__((address_space(3))) f4 lds_f4_t;
+__device__ __forceinline__ f4 lds_f4(uint32_t byte_addr) {   // LDS byte address -> f4
+    return *(const lds_f4_t *)(size_t)byte_addr;
+}
+
+__global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
+    __shared__ f4 As[3][kStepF4];        // weight ring [mt 8][hi,lo][64]
+    __shared__ f4 Hs[2][kHaloF4];        // halo images, by channel-group parity
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t wm = wave & 1u, wn = wave >> 1;
+    uint32_t ci, tile;
+    if (!slot_tile(a, blockIdx.x, ci, tile)) return;
+    const uint32_t H = a.Hin, W = a.Win;
+    const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT;
+    const uint32_t cb = tile % nB;
+    const uint32_t nbx = W / 16, nby = H / 16;
+    uint32_t blk = tile / nB;
+    const uint32_t bx = blk % nbx;
+    blk /= nbx;
+    const uint32_t by = blk % nby, b = blk / nby;
+    const uint32_t pix0 = (b * H + by * 16) * W + bx * 16;
+
+    const v4i rw = make_rsrc(a.wpk, 9u * nC * nB * kStepF4 * 16u);
+    const v4i rx = make_rsrc(a.xs, a.B * H * W * a.Cin * 4);
+    // this wave's halo pieces k = wave + 8 i: per-lane source offsets at channel group 0
+    // (the group moves the buffer's soffset by 128 B)
+    uint32_t hoff[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const uint32_t h = 8u * (wave + 8u * i) + (lane >> 3);
+        const uint32_t hy = h / kHaloW, hx = h - hy * kHaloW;
+        const uint32_t q = (lane & 7u) ^ halo_swz(hx);
+        const int y = (int)(by * 16 + hy) - 1, x = (int)(bx * 16 + hx) - 1;
+        const bool ok = h < kHaloPx && y >= 0 && y < (int)H && x >= 0 && x < (int)W;
+        hoff[i] = ok ? (((b * H + (uint32_t)y) * W + (uint32_t)x) * a.Cin * 4u + q * 16u) : 0x7FFFFFF0u;
+    }
+    const uint32_t n = lane & 15u, g = lane >> 4;
+    // fragment lane bases (bytes within a halo buffer): [column shift dx + 1][lo]
+    uint32_t fb0[3][2];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int lo = 0; lo < 2; ++lo)
+            fb0[d][lo] = (4u * wn * kHaloW + n) * 128u + (((2u * g + lo) ^ halo_swz(n + d)) << 4);
+    const uint32_t hs0 = lds_addr(&Hs[0][0]), hs1 = lds_addr(&Hs[1][0]);
+
+    auto fire_w = [&](uint32_t c, uint32_t tap, uint32_t stage) {
+        const uint32_t wsoff = ((tap * nC + c) * nB + cb) * kStepF4 * 16u + 2 * wave * 1024u;
+        set_m0(lds_addr(&As[stage][2 * wave * 64]));
+        dma16<0>(rw, lane * 16u, wsoff);
+        dma16<1024>(rw, lane * 16u, wsoff);
+    };
+    uint32_t hsoff = 0;                   // soffset of the group being fetched (c * 128 B)
+    auto fire_h = [&](int buf, int i) {
+        set_m0(lds_addr(&Hs[buf][(wave + 8u * i) * 64]));
+        dma16<0>(rx, hoff[i], hsoff);
+    };
+
+    f4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    // fragments of tap T of a channel group whose halo lies at byte hs: A from stage
+    // T % 3, B at the tap's offset (dy, dx) = (T / 3 - 1, T % 3 - 1)
+    auto read_frags = [&](f4 (&R)[16], auto tapc, uint32_t hs) {
+        constexpr int T = decltype(tapc)::value;
+        constexpr uint32_t st = T % 3, dyp = T / 3, dxp = T % 3;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            R[i] = As[st][((4 * wm + i) * 2) * 64 + lane];
+            R[4 + i] = As[st][((4 * wm + i) * 2 + 1) * 64 + lane];
+        }
+        const uint32_t bh = hs + fb0[dxp][0], bl = hs + fb0[dxp][1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t imm = ((j + dyp) * kHaloW + dxp) * 128u;
+            R[8 + j] = lds_f4(bh + imm);
+            R[12 + j] = lds_f4(bl + imm);
+        }
+    };
+    auto mfma_rows = [&](const f4 (&R)[16], int i0, int nr) {
+#pragma unroll
+        for (int i = i0; i < i0 + nr; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[4 + i], R[8 + j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[i], R[12 + j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(R[i], R[8 + j], acc[i][j]);
+        }
+    };
+
+    // K-step (c, T): MFMAs of rows 0-1; wait for step (c, T)+1 (in flight may stay only
+    // what step (c, T)-1 fired); barrier; fire step +3's weights (into stage T % 3) and,
+    // at taps 0-5, halo piece T of group c + 1 (into the buffer group c - 1 used, whose
+    // last fragment reads were before the barrier of (c - 1, 8)); read step +1's
+    // fragments; MFMAs of rows 2-3.
+    // P: parity of group c (its halo buffer), compile-time in the unrolled loop
+    auto step = [&](uint32_t c, auto tapc, auto parc, const f4 (&R)[16], f4 (&Rn)[16]) {
+        constexpr int T = decltype(tapc)::value;
+        constexpr int P = decltype(parc)::value;
+        const uint32_t s = c * 9 + T, nk = nC * 9;
+        const bool prev_w = s + 2 < nk;                     // step s-1 fired weights
+        const bool prev_h = T != 0 && T - 1 <= 5 && c + 1 < nC;   // ... and a halo piece
+        mfma_rows(R, 0, 2);
+        if (prev_w && prev_h) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+        else if (prev_w) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (s + 3 < nk) {
+            constexpr uint32_t T3 = (T + 3) % 9;
+            fire_w(c + (T + 3) / 9, T3, T % 3);
+        }
+        if constexpr (T <= 5) {
+            if (c + 1 < nC) fire_h(1 - P, T);
+        }
+        if (s + 1 < nk) {
+            if constexpr (T == 8) read_frags(Rn, std::integral_constant<int, 0>{}, P ? hs0 : hs1);
+            else read_frags(Rn, std::integral_constant<int, T + 1>{}, P ? hs1 : hs0);
+        }
+        mfma_rows(R, 2, 2);
+    };
+
+    // prologue: halo of group 0, weights of steps 0-2; wait for all but step 2's
+    const uint32_t nk = nC * 9;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) fire_h(0, i);
+    hsoff = 128u;                         // next: group 1
+    fire_w(0, 0, 0);
+    fire_w(0, 1, 1);
+    fire_w(0, 2, 2);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    (void)nk;
+    f4 R0[16], R1[16];
+    read_frags(R0, std::integral_constant<int, 0>{}, hs0);
+    // two channel groups per iteration: 18 steps alternate R0 / R1
+    uint32_t c = 0;
+    for (; c + 1 < nC; c += 2) {
+        step(c, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, R0, R1);
+        step(c, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}, R1, R0);
+        step(c, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{}, R0, R1);
+        step(c, std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{}, R1, R0);
+        step(c, std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{}, R0, R1);
+        step(c, std::integral_constant<int, 5>{}, std::integral_constant<int, 0>{}, R1, R0);
+        hsoff += 128u;
+        step(c, std::integral_constant<int, 6>{}, std::integral_constant<int, 0>{}, R0, R1);
+        step(c, std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, R1, R0);
+        step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
+        step(c + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, R1, R0);
+        step(c + 1, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, R0, R1);
+        step(c + 1, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{}, R1, R0);
+        step(c + 1, std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{}, R0, R1);
+        step(c + 1, std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, R1, R0);
+        step(c + 1, std::integral_constant<int, 5>{}, std::integral_constant<int, 1>{}, R0, R1);
+        hsoff += 128u;
+        step(c + 1, std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{}, R1, R0);
+        step(c + 1, std::integral_constant<int, 7>{}, std::integral_constant<int, 1>{}, R0, R1);
+        step(c + 1, std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{}, R1, R0);
+    }
+    if (c < nC) {
+        step(c, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, R0, R1);
+        step(c, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}, R1, R0);
+        step(c, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{}, R0, R1);
+        step(c, std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{}, R1, R0);
+        step(c, std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{}, R0, R1);
+        step(c, std::integral_constant<int, 5>{}, std::integral_constant<int, 0>{}, R1, R0);
+        step(c, std::integral_constant<int, 6>{}, std::integral_constant<int, 0>{}, R0, R1);
+        step(c, std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, R1, R0);
+        step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
+    }
+    // the epilogue's LDS reduction buffer is its own; no DMA is left in flight
+    conv_epilogue<true>(a, acc, lane, wm, wn, cb, pix0, a.B * H * W, H, W, 0, 0, W);
+}
+
 
 }  // namespace
 }  // namespace sdfr
@@ -730,7 +942,9 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
         a.ksplit = ks;
         a.partial = reinterpret_cast<f4 *>(ws);
     }
-    if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
+    if (CONV_HALO && act && !transposed && a.ksplit == 1 && H % 16 == 0 && W % 16 == 0)
+        hipLaunchKernelGGL(conv_h_kernel, dim3(grid), dim3(512), 0, st, a);
+    else if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     if (a.ksplit > 1) {
         if (act) hipLaunchKernelGGL(conv_splitk_kernel<true>, dim3(grid), dim3(512), 0, st, a);

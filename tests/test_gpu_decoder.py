@@ -245,6 +245,8 @@ def test_conv3x3_f16x3_vs_fp64(ops, B, Cin, Cout, H, W, transposed):
     (1, 256, 512, 16, 32, True, False, True),   # four Cout blocks (partials), no skip
     (2, 128, 256, 32, 8, True, True, False),    # last layer: rgb only
     (1, 32, 256, 16, 16, False, False, True),   # y only
+    (2, 96, 128, 32, 48, True, True, True),     # halo kernel: odd channel-group count, 2x3 blocks
+    (1, 256, 256, 64, 64, True, False, True),   # halo kernel: decoder-sized layer
 ])
 def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, store_y):
     """sdfr_conv3x3_f16x3_act (+ sdfr_rgb_finish) against sdfr_conv3x3_f16x3 followed by
