@@ -16,5 +16,5 @@ P2="GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLIC
 FIELD=${FIELD_PREC:-f16x3}
 PMC=$P1 run field_sq1 field_x2_kernel python3 "$R/scripts/render_only.py" $FIELD &&
 PMC=$P2 run field_sq2 field_x2_kernel python3 "$R/scripts/render_only.py" $FIELD &&
-PMC=$P1 run conv_sq1 conv_x_kernel python3 "$R/scripts/decoder_only.py" &&
-PMC=$P2 run conv_sq2 conv_x_kernel python3 "$R/scripts/decoder_only.py"
+PMC=$P1 run conv_sq1 "conv_[xh]_kernel" python3 "$R/scripts/decoder_only.py" &&
+PMC=$P2 run conv_sq2 "conv_[xh]_kernel" python3 "$R/scripts/decoder_only.py"

@@ -126,6 +126,12 @@ static_assert(CONV_REGDB || kStages == 3, "the single-register-set ring assumes 
 #ifndef CONV_HALO
 #define CONV_HALO 1       // regular convs with the fused epilogue on conv_h_kernel
 #endif
+#ifndef CONV_HABL
+#define CONV_HABL 0       // conv_h_kernel timing ablations (wrong results)
+#endif
+#ifndef CONV_HPERSIST
+#define CONV_HPERSIST 0   // conv_h_kernel: one round of workgroups walking their tiles
+#endif
 
 // One output-pixel class: the plain convolution has one (every pixel, 9 taps); the
 // stride-2 transposed one has four parity classes (4, 2, 2 and 1 taps) that share
@@ -655,32 +661,33 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t wm = wave & 1u, wn = wave >> 1;
-    uint32_t ci, tile;
-    if (!slot_tile(a, blockIdx.x, ci, tile)) return;
     const uint32_t H = a.Hin, W = a.Win;
     const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT;
-    const uint32_t cb = tile % nB;
     const uint32_t nbx = W / 16, nby = H / 16;
-    uint32_t blk = tile / nB;
-    const uint32_t bx = blk % nbx;
-    blk /= nbx;
-    const uint32_t by = blk % nby, b = blk / nby;
-    const uint32_t pix0 = (b * H + by * 16) * W + bx * 16;
-
     const v4i rw = make_rsrc(a.wpk, 9u * nC * nB * kStepF4 * 16u);
     const v4i rx = make_rsrc(a.xs, a.B * H * W * a.Cin * 4);
-    // this wave's halo pieces k = wave + 8 i: per-lane source offsets at channel group 0
-    // (the group moves the buffer's soffset by 128 B)
-    uint32_t hoff[6];
+    // tile -> Cout block cb, first pixel pix0 and this wave's halo pieces k = wave + 8 i
+    // (per-lane source offsets at channel group 0; the group moves the buffer's
+    // soffset by 128 B)
+    uint32_t cb = 0, pix0 = 0, hoff[6];
+    auto setup = [&](uint32_t tile) {
+        cb = tile % nB;
+        uint32_t blk = tile / nB;
+        const uint32_t bx = blk % nbx;
+        blk /= nbx;
+        const uint32_t by = blk % nby, b = blk / nby;
+        pix0 = (b * H + by * 16) * W + bx * 16;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const uint32_t h = 8u * (wave + 8u * i) + (lane >> 3);
-        const uint32_t hy = h / kHaloW, hx = h - hy * kHaloW;
-        const uint32_t q = (lane & 7u) ^ halo_swz(hx);
-        const int y = (int)(by * 16 + hy) - 1, x = (int)(bx * 16 + hx) - 1;
-        const bool ok = h < kHaloPx && y >= 0 && y < (int)H && x >= 0 && x < (int)W;
-        hoff[i] = ok ? (((b * H + (uint32_t)y) * W + (uint32_t)x) * a.Cin * 4u + q * 16u) : 0x7FFFFFF0u;
-    }
+        for (int i = 0; i < 6; ++i) {
+            const uint32_t h = 8u * (wave + 8u * i) + (lane >> 3);
+            const uint32_t hy = h / kHaloW, hx = h - hy * kHaloW;
+            const uint32_t q = (lane & 7u) ^ halo_swz(hx);
+            const int y = (int)(by * 16 + hy) - 1, x = (int)(bx * 16 + hx) - 1;
+            const bool ok = h < kHaloPx && y >= 0 && y < (int)H && x >= 0 && x < (int)W;
+            hoff[i] = ok ? (((b * H + (uint32_t)y) * W + (uint32_t)x) * a.Cin * 4u + q * 16u)
+                         : 0x7FFFFFF0u;
+        }
+    };
     const uint32_t n = lane & 15u, g = lane >> 4;
     // fragment lane bases (bytes within a halo buffer): [column shift dx + 1][lo]
     uint32_t fb0[3][2];
@@ -704,10 +711,6 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     };
 
     f4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
     // fragments of tap T of a channel group whose halo lies at byte hs: A from stage
     // T % 3, B at the tap's offset (dy, dx) = (T / 3 - 1, T % 3 - 1)
@@ -755,12 +758,14 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         if (prev_w && prev_h) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
         else if (prev_w) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#if CONV_HABL != 2     // 2: ablation without the per-step barrier
         __builtin_amdgcn_s_barrier();
-        if (s + 3 < nk) {
+#endif
+        if (CONV_HABL != 3 && s + 3 < nk) {   // 3: ablation without in-loop staging
             constexpr uint32_t T3 = (T + 3) % 9;
             fire_w(c + (T + 3) / 9, T3, T % 3);
         }
-        if constexpr (T <= 5) {
+        if constexpr (T <= 5 && CONV_HABL != 3) {
             if (c + 1 < nC) fire_h(1 - P, T);
         }
         if (s + 1 < nk) {
@@ -770,17 +775,34 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         mfma_rows(R, 2, 2);
     };
 
-    // prologue: halo of group 0, weights of steps 0-2; wait for all but step 2's
-    const uint32_t nk = nC * 9;
+    // prologue of a tile: halo of group 0, weights of steps 0-2 (every LDS buffer is
+    // free once all waves passed the previous tile's last barrier)
+    auto prologue = [&] {
+        hsoff = 0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) fire_h(0, i);
-    hsoff = 128u;                         // next: group 1
-    fire_w(0, 0, 0);
-    fire_w(0, 1, 1);
-    fire_w(0, 2, 2);
+        for (int i = 0; i < 6; ++i) fire_h(0, i);
+        hsoff = 128u;                     // next: group 1
+        fire_w(0, 0, 0);
+        fire_w(0, 1, 1);
+        fire_w(0, 2, 2);
+    };
+    // CONV_HPERSIST: the grid covers at most one round of CUs and each workgroup walks
+    // its slots blockIdx.x + k gridDim.x (same XCD); the next tile's prologue DMAs are
+    // issued before this tile's epilogue, so they land while it computes and stores
+    uint32_t slot = blockIdx.x, ci, tile;
+    while (slot < a.grid && !slot_tile(a, slot, ci, tile)) slot += gridDim.x;
+    if (slot >= a.grid) return;
+    setup(tile);
+    prologue();
+    for (;;) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    // all but step 2's weights landed (younger epilogue stores of the previous tile
+    // may be waited for too)
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    (void)nk;
     f4 R0[16], R1[16];
     read_frags(R0, std::integral_constant<int, 0>{}, hs0);
     // two channel groups per iteration: 18 steps alternate R0 / R1
@@ -819,7 +841,31 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
     }
     // the epilogue's LDS reduction buffer is its own; no DMA is left in flight
-    conv_epilogue<true>(a, acc, lane, wm, wn, cb, pix0, a.B * H * W, H, W, 0, 0, W);
+#if CONV_HABL == 1     // ablation: no epilogue (one store keeps the accumulators live)
+    {
+        f4 t = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t += acc[i][j];
+        if (t.x == 1234.5f) a.e.rgbp[tid] = t.y;
+    }
+    return;
+#endif
+    const uint32_t cb_cur = cb, pix0_cur = pix0;
+    bool more = false;
+    if (CONV_HPERSIST) {
+        slot += gridDim.x;
+        while (slot < a.grid && !slot_tile(a, slot, ci, tile)) slot += gridDim.x;
+        more = slot < a.grid;
+        if (more) {
+            setup(tile);
+            prologue();
+        }
+    }
+    conv_epilogue<true>(a, acc, lane, wm, wn, cb_cur, pix0_cur, a.B * H * W, H, W, 0, 0, W);
+    if (!more) return;
+    }
 }
 
 
@@ -943,7 +989,8 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
         a.partial = reinterpret_cast<f4 *>(ws);
     }
     if (CONV_HALO && act && !transposed && a.ksplit == 1 && H % 16 == 0 && W % 16 == 0)
-        hipLaunchKernelGGL(conv_h_kernel, dim3(grid), dim3(512), 0, st, a);
+        hipLaunchKernelGGL(conv_h_kernel, dim3(CONV_HPERSIST && grid > 256 ? 256 : grid), dim3(512), 0,
+                           st, a);
     else if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     if (a.ksplit > 1) {
