@@ -40,6 +40,7 @@ GATHER_BYTES_PER_SAMPLE = 1024    # 16 levels x 8 corners x 2 x fp32
 MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
 MFMA_F16_PEAK_TFLOPS = 2500.0     # MI355X dense fp16/bf16 MFMA peak (no sparsity)
 HBM_PEAK_GBPS = 8000.0            # MI355X HBM3E peak
+MFMA_CLOCK_GHZ = 2.4              # clock the MFMA peaks are quoted at
 
 
 def parse():
@@ -262,6 +263,11 @@ def main():
                 "traffic": traffic, "mfma_dtype": "f16 (hi/lo split, fp32 accumulate)",
                 "mfma_issued_tflops": 3 * field_tflops, "mfma_peak_dtype": MFMA_F16_PEAK_TFLOPS,
                 "counters": counters_of(field_kernel.split("<")[0])}
+        clk = (roof["counters"] or {}).get("effective_clock_GHz")
+        if clk:
+            # the same time against the peak at the clock the chip holds under this body
+            # (committed GRBM_GUI_ACTIVE pass; the headline frac stays at 2.4 GHz)
+            roof["frac_at_measured_clock"] = roof["frac"] * MFMA_CLOCK_GHZ / clk
     else:
         roof = {"kernel": "ngp_field_kernel (MLP on v_mfma_f32_16x16x4_f32 + compositing)",
                 "bound": "mfma", "achieved": field_tflops, "peak": MFMA_F32_PEAK_TFLOPS,

@@ -216,18 +216,30 @@ __device__ __forceinline__ float act1(float c, float dm, float nz, float b, floa
     return v * scale;
 }
 
-// Round-to-nearest hi/lo split of 4 channels at NHWC element index idx (C % 8 == 0)
-// into split-NHWC (decoder.hip store_split4).
-__device__ __forceinline__ void store_split4(_Float16 *ys, size_t idx, f4 v) {
+// Round-to-nearest hi/lo split into split-NHWC (decoder.hip store_split4) for lane
+// groups g = 2k, 2k+1 holding channels 4g..4g+3 of the same 8-channel group and
+// pixel (lanes 16 g + n): one v_permlane16_swap per dword
+// gives the even group both hi halves and the odd group both lo halves, so every
+// lane issues ONE 16-B store (hi of the 8 channels at idx8, lo 16 B after it) instead
+// of two 8-B stores.  idx8 = NHWC element index of the group's channel 0.  All lanes
+// must execute it (cross-lane).
+__device__ __forceinline__ void store_split8_pair(_Float16 *ys, size_t idx8, f4 v, uint32_t g) {
     h4 h, l;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         h[r] = (_Float16)v[r];
         l[r] = (_Float16)(v[r] - (float)h[r]);
     }
-    const size_t o = 2 * idx - (idx & 7u);
-    *reinterpret_cast<h4 *>(ys + o) = h;
-    *reinterpret_cast<h4 *>(ys + o + 8) = l;
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    const u2 hd = __builtin_bit_cast(u2, h), ld = __builtin_bit_cast(u2, l);
+    uint32_t q[4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const auto r = __builtin_amdgcn_permlane16_swap(hd[k], ld[k], false, false);
+        q[k] = r[0];          // even group: own hi / odd group: partner's lo
+        q[2 + k] = r[1];      // even group: partner's hi / odd group: own lo
+    }
+    *reinterpret_cast<f4 *>(ys + 2 * idx8 + (g & 1u) * 8) = __builtin_bit_cast(f4, q);
 }
 
 // Epilogue of one workgroup tile: raw fp32 output (NHWC, class pixel placement) or,
@@ -271,7 +283,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4]
                 f4 v;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = act1(acc[i][j][r], dm[r], nz, bs[r], e.slope, e.scale);
-                if (e.ys) store_split4(e.ys, (size_t)P * a.Cout + ch, v * sn);
+                if (e.ys) store_split8_pair(e.ys, (size_t)P * a.Cout + (ch & ~7u), v * sn, g);
 #pragma unroll
                 for (int o = 0; o < 3; ++o)
 #pragma unroll
@@ -698,16 +710,21 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
             fb0[d][lo] = (4u * wn * kHaloW + n) * 128u + (((2u * g + lo) ^ halo_swz(n + d)) << 4);
     const uint32_t hs0 = lds_addr(&Hs[0][0]), hs1 = lds_addr(&Hs[1][0]);
 
+    auto uni = [](v4i r) {     // keep the resources in SGPRs (the inline asm needs them there)
+        return v4i{__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),
+                   __builtin_amdgcn_readfirstlane(r.z), __builtin_amdgcn_readfirstlane(r.w)};
+    };
     auto fire_w = [&](uint32_t c, uint32_t tap, uint32_t stage) {
-        const uint32_t wsoff = ((tap * nC + c) * nB + cb) * kStepF4 * 16u + 2 * wave * 1024u;
+        const uint32_t wsoff = __builtin_amdgcn_readfirstlane(
+            ((tap * nC + c) * nB + cb) * kStepF4 * 16u + 2 * wave * 1024u);
         set_m0(lds_addr(&As[stage][2 * wave * 64]));
-        dma16<0>(rw, lane * 16u, wsoff);
-        dma16<1024>(rw, lane * 16u, wsoff);
+        dma16<0>(uni(rw), lane * 16u, wsoff);
+        dma16<1024>(uni(rw), lane * 16u, wsoff);
     };
     uint32_t hsoff = 0;                   // soffset of the group being fetched (c * 128 B)
     auto fire_h = [&](int buf, int i) {
         set_m0(lds_addr(&Hs[buf][(wave + 8u * i) * 64]));
-        dma16<0>(rx, hoff[i], hsoff);
+        dma16<0>(uni(rx), hoff[i], __builtin_amdgcn_readfirstlane(hsoff));
     };
 
     f4 acc[4][4];
@@ -789,8 +806,14 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     // CONV_HPERSIST: the grid covers at most one round of CUs and each workgroup walks
     // its slots blockIdx.x + k gridDim.x (same XCD); the next tile's prologue DMAs are
     // issued before this tile's epilogue, so they land while it computes and stores
-    uint32_t slot = blockIdx.x, ci, tile;
-    while (slot < a.grid && !slot_tile(a, slot, ci, tile)) slot += gridDim.x;
+    // one class (slot_tile's XCD-aware order without the class search)
+    const uint32_t ntiles = a.cls[0].ntiles, per_xcd = (ntiles + 7) >> 3;
+    auto slot_ok = [&](uint32_t sl, uint32_t &t) {
+        t = __builtin_amdgcn_readfirstlane((sl & 7u) * per_xcd + (sl >> 3));   // uniform (SGPR)
+        return t < ntiles;
+    };
+    uint32_t slot = blockIdx.x, tile;
+    while (slot < a.grid && !slot_ok(slot, tile)) slot += gridDim.x;
     if (slot >= a.grid) return;
     setup(tile);
     prologue();
@@ -856,14 +879,20 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     bool more = false;
     if (CONV_HPERSIST) {
         slot += gridDim.x;
-        while (slot < a.grid && !slot_tile(a, slot, ci, tile)) slot += gridDim.x;
+        while (slot < a.grid && !slot_ok(slot, tile)) slot += gridDim.x;
         more = slot < a.grid;
         if (more) {
             setup(tile);
             prologue();
         }
     }
-    conv_epilogue<true>(a, acc, lane, wm, wn, cb_cur, pix0_cur, a.B * H * W, H, W, 0, 0, W);
+    {
+        // the epilogue's kernel arguments are loaded here, not hoisted out of the tile
+        // loop (SGPRs live across the K loop spilled)
+        const ConvArgs *ap = &a;
+        if (CONV_HPERSIST) asm volatile("" : "+s"(ap));
+        conv_epilogue<true>(*ap, acc, lane, wm, wn, cb_cur, pix0_cur, a.B * H * W, H, W, 0, 0, W);
+    }
     if (!more) return;
     }
 }

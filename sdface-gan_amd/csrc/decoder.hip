@@ -149,6 +149,37 @@ __device__ __forceinline__ void store_y(const EpiArgs &a, size_t idx, float4 v) 
     else *reinterpret_cast<float4 *>(a.y + idx) = v;
 }
 
+// store_y for threads whose neighbour lane (lane ^ 1) holds channels c ^ 4 of the same
+// pixel (epi_blur_kernel: channel quad fastest, C % 8 == 0): the split store goes out
+// as ONE 16-B store per lane -- the even lane writes the 8 channels' hi halves, the
+// odd lane their lo halves -- after one DPP quad_perm [1,0,3,2] exchange per dword
+// instead of two 8-B stores per lane.  Both lanes of a pair must execute it.
+__device__ __forceinline__ void store_y_pair(const EpiArgs &a, size_t idx, float4 v) {
+    if (!a.ys) {
+        *reinterpret_cast<float4 *>(a.y + idx) = v;
+        return;
+    }
+    h4v h, l;
+    h[0] = (_Float16)v.x; h[1] = (_Float16)v.y; h[2] = (_Float16)v.z; h[3] = (_Float16)v.w;
+    l[0] = (_Float16)(v.x - (float)h[0]);
+    l[1] = (_Float16)(v.y - (float)h[1]);
+    l[2] = (_Float16)(v.z - (float)h[2]);
+    l[3] = (_Float16)(v.w - (float)h[3]);
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    const u2 hd = __builtin_bit_cast(u2, h), ld = __builtin_bit_cast(u2, l);
+    const bool odd = (idx & 4u) != 0;
+    uint32_t q[4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t send = odd ? hd[k] : ld[k];     // what the partner lane keeps
+        const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
+        q[k] = odd ? recv : hd[k];                     // even: own hi, partner hi
+        q[2 + k] = odd ? ld[k] : recv;                 // odd: partner lo, own lo
+    }
+    const size_t i8 = idx & ~(size_t)7;
+    *reinterpret_cast<uint4 *>(a.ys + 2 * i8 + (odd ? 8 : 0)) = __builtin_bit_cast(uint4, q);
+}
+
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
 __device__ __forceinline__ float act1(float c, float dm, float nz, float b, float slope,
@@ -375,8 +406,8 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg)
                     s.w = fmaf(h3.w, f3, fmaf(h2[k].w, f2, fmaf(h1[k].w, f1, h0[k].w * f0)));
                     const size_t pix = ((size_t)b * a.H + oy) * a.W + ox0 + k;
                     const float4 vv = act4(s, dm, nz[g][k], bs, a.slope, a.act_scale);
-                    store_y(a, pix * C + c,
-                            make_float4(vv.x * sn.x, vv.y * sn.y, vv.z * sn.z, vv.w * sn.w));
+                    store_y_pair(a, pix * C + c,
+                                 make_float4(vv.x * sn.x, vv.y * sn.y, vv.z * sn.z, vv.w * sn.w));
                 }
                 h0[k] = h1[k];
                 h1[k] = h2[k];
