@@ -405,6 +405,15 @@ int sdfr_conv_pack_weights(const float *w, float scale, uint32_t Cout, uint32_t 
 int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
                        uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
                        int transposed, void *stream);
+/* The same with a workspace: when the grid would leave CUs idle (small batches,
+ * e.g. eval.py's one face) the K-steps of every tile are shared by 2-4 workgroups
+ * whose fp32 partial tiles a second kernel sums in a fixed order (deterministic).
+ * ws_bytes >= sdfr_conv_ws_bytes(B, H, W, Cout, transposed) enables it (0: no split
+ * for this shape; a smaller or NULL workspace runs unsplit). */
+int sdfr_conv3x3_f16x3_ws(float *out, const void *x_split, const void *packed,
+                          uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
+                          int transposed, void *ws, size_t ws_bytes, void *stream);
+size_t sdfr_conv_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout, int transposed);
 
 /* The regular (transposed = 0) convolution with the plain styled epilogue fused
  * into it (the conv output never goes to memory): per pixel and channel

@@ -42,6 +42,7 @@ EXPORTS = (
     "sdfr_fused_bias_act", "sdfr_mapping_linear", "sdfr_decoder_styles", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
     "sdfr_modulate_to_nhwc_split",
     "sdfr_conv_pack_bytes", "sdfr_conv_pack_weights", "sdfr_conv3x3_f16x3",
+    "sdfr_conv3x3_f16x3_ws", "sdfr_conv_ws_bytes",
     "sdfr_conv3x3_f16x3_act", "sdfr_conv_act_ws_bytes", "sdfr_rgb_finish",
     "sdfr_mc_workspace_bytes", "sdfr_mc_count", "sdfr_mc_emit",
 )
@@ -183,6 +184,10 @@ def lib():
     L.sdfr_conv_pack_bytes.argtypes = [_u32, _u32]
     L.sdfr_conv_pack_weights.argtypes = [_vp, _f32, _u32, _u32, _vp, _vp, _vp]
     L.sdfr_conv3x3_f16x3.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _int, _vp]
+    L.sdfr_conv3x3_f16x3_ws.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _int, _vp,
+                                        ctypes.c_size_t, _vp]
+    L.sdfr_conv_ws_bytes.argtypes = [_u32, _u32, _u32, _u32, _int]
+    L.sdfr_conv_ws_bytes.restype = ctypes.c_size_t
     L.sdfr_conv3x3_f16x3_act.argtypes = [ctypes.POINTER(ConvActArgs), _vp]
     L.sdfr_conv_act_ws_bytes.argtypes = [_u32, _u32, _u32, _u32]
     L.sdfr_conv_act_ws_bytes.restype = ctypes.c_size_t

@@ -933,13 +933,21 @@ namespace {
 // split-K factor: the largest of 4, 2 that keeps every split's grid within one
 // round of workgroups on the 256 CUs (one 512-thread workgroup per CU)
 uint32_t conv_ksplit(uint32_t grid) {
-    for (uint32_t k = 4; k > 1; k >>= 1)
+    for (uint32_t k = 4; k > 1; --k)
         if (grid * k <= 256) return k;
     return 1;
 }
 
 uint32_t conv_grid(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {   // regular conv
     return ((B * H * W + kPT - 1) / kPT * (Cout / kCT) + 7) & ~7u;
+}
+
+uint32_t conv_grid_t(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {  // transposed (4 classes)
+    uint32_t g = 0;
+    for (uint32_t py = 0; py < 2; ++py)
+        for (uint32_t px = 0; px < 2; ++px)
+            g += ((B * (py ? H : H + 1) * (px ? W : W + 1) + kPT - 1) / kPT * (Cout / kCT) + 7) & ~7u;
+    return g;
 }
 
 int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B, uint32_t H,
@@ -1033,14 +1041,28 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
 
 extern "C" {
 
-int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
-                       uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
-                       int transposed, void *stream) {
+int sdfr_conv3x3_f16x3_ws(float *out, const void *x_split, const void *packed,
+                          uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
+                          int transposed, void *ws, size_t ws_bytes, void *stream) {
     if (!out) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
     ConvArgs a{};
     a.out = out;
     return conv_launch(a, x_split, packed, B, H, W, Cin, Cout, transposed, false,
-                       (hipStream_t)stream, "conv3x3_f16x3");
+                       (hipStream_t)stream, "conv3x3_f16x3", ws, ws_bytes);
+}
+
+int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
+                       uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
+                       int transposed, void *stream) {
+    return sdfr_conv3x3_f16x3_ws(out, x_split, packed, B, H, W, Cin, Cout, transposed, nullptr, 0,
+                                 stream);
+}
+
+size_t sdfr_conv_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout, int transposed) {
+    if (Cout % kCT || B == 0 || H == 0 || W == 0) return 0;
+    const uint32_t grid = transposed ? conv_grid_t(B, H, W, Cout) : conv_grid(B, H, W, Cout);
+    const uint32_t ks = conv_ksplit(grid);
+    return ks > 1 ? (size_t)ks * grid * 16 * 512 * sizeof(f4) : 0;
 }
 
 int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *p, void *stream) {

@@ -336,10 +336,12 @@ def unsplit_nhwc(xs):
     return xs[:, :, :, :, 0].reshape(B, H, W, -1), xs[:, :, :, :, 1].reshape(B, H, W, -1)
 
 
-def conv3x3_f16x3(x_split, packed, Cout, transposed=False):
+def conv3x3_f16x3(x_split, packed, Cout, transposed=False, split_k=True):
     """x_split = split-NHWC fp16 [B, H, W, Cin/8, 2, 8] (split_nhwc) -> channels_last
     fp32 [B, Cout, H, W] (conv2d, pad 1) or [B, Cout, 2H+1, 2W+1] (conv_transpose2d
-    stride 2), scaled by su (conv_pack_weights)."""
+    stride 2), scaled by su (conv_pack_weights).  ``split_k``: give the kernel a
+    workspace so that small batches split K over 2-4 workgroups
+    (sdfr_conv3x3_f16x3_ws)."""
     _require_cuda(x_split)
     if x_split.dtype != torch.float16 or x_split.dim() != 6 or x_split.shape[4:] != (2, 8) \
             or not x_split.is_contiguous():
@@ -348,9 +350,12 @@ def conv3x3_f16x3(x_split, packed, Cout, transposed=False):
     B, H, W, Cin = x_split.shape[0], x_split.shape[1], x_split.shape[2], 8 * x_split.shape[3]
     Ho, Wo = (2 * H + 1, 2 * W + 1) if transposed else (H, W)
     out = torch.empty(B, Cout, Ho, Wo, device=x_split.device, memory_format=torch.channels_last)
-    _lib.check(_lib.lib().sdfr_conv3x3_f16x3(_lib.ptr(out), _lib.ptr(x_split),
-                                             _lib.ptr(packed), B, H, W, Cin, Cout,
-                                             int(bool(transposed)), _lib.stream_of(x_split)),
+    wsb = _lib.lib().sdfr_conv_ws_bytes(B, H, W, Cout, int(bool(transposed))) if split_k else 0
+    ws = torch.empty(wsb, dtype=torch.uint8, device=x_split.device) if wsb else None
+    _lib.check(_lib.lib().sdfr_conv3x3_f16x3_ws(_lib.ptr(out), _lib.ptr(x_split),
+                                                _lib.ptr(packed), B, H, W, Cin, Cout,
+                                                int(bool(transposed)), _lib.ptr(ws), wsb,
+                                                _lib.stream_of(x_split)),
                "conv3x3_f16x3")
     return out
 

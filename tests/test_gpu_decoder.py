@@ -238,6 +238,15 @@ def test_conv3x3_f16x3_vs_fp64(ops, B, Cin, Cout, H, W, transposed):
     name = f"conv_f16x3_B{B}_{Cin}x{Cout}_{H}x{W}_{'T' if transposed else 'N'}"
     _record[name] = [e16, e32]
     assert e16 <= 4 * e32 + 1e-6, (e16, e32)
+    # split-K (small grids: K shared by 2-4 workgroups, partials summed in a fixed
+    # order): the unsplit result to fp32 summation-order rounding, deterministic
+    xs = ops.split_nhwc(x.to(DEV))
+    o1 = ops.conv3x3_f16x3(xs, packed, Cout, transposed=transposed, split_k=False)
+    o2 = ops.conv3x3_f16x3(xs, packed, Cout, transposed=transposed)
+    o3 = ops.conv3x3_f16x3(xs, packed, Cout, transposed=transposed)
+    assert torch.equal(o2, o3)
+    scale = float(o1.abs().max())
+    _close(f"{name}_splitk", o2.cpu(), o1.cpu(), 2e-6 * scale, 2e-7 * scale)
 
 
 @pytest.mark.parametrize("B,Cin,Cout,H,W,rgb,skip,store_y", [
@@ -269,7 +278,7 @@ def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, 
     sk = torch.randn(B, 3, H // 2, W // 2, generator=g).to(DEV) if skip else None
     ys, part = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_w=rgb_w, split_k=False,
                                      **kw)
-    out = ops.conv3x3_f16x3(xs, packed, Cout)
+    out = ops.conv3x3_f16x3(xs, packed, Cout, split_k=False)
     y_ref, rgb_ref = ops.styled_epilogue(out, fir=fir, demod=demod, rgb_w=rgb_w,
                                          rgb_b=rgb_b if rgb else None, skip=sk,
                                          split_y=store_y, **kw)
