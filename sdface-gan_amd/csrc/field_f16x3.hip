@@ -174,29 +174,28 @@ struct XPrepArgs {
     uint32_t B;
 };
 
-// blocks [0, B*films*2): FiLM rows; then packing, one (slice, t8, lane) per thread
+// blocks [0, B*films*2*256/4): FiLM rows, one wave per output row (lanes over K,
+// butterfly sum); then packing, one (slice, t8, lane) per thread
 template <class Net>
 __global__ void __launch_bounds__(256) xprep_kernel(const XPrepArgs a) {
     constexpr int NF = Net::kFilmN;
     const uint32_t blk = blockIdx.x, j = threadIdx.x;
-    const uint32_t nfilm = a.B * NF * 2;
+    const uint32_t nfilm = a.B * NF * 2 * kW / 4;
     if (blk < nfilm) {
-        const uint32_t b = blk / (NF * 2), rem = blk % (NF * 2);
+        const uint32_t lane = j & 63u, row_id = blk * 4 + (j >> 6);
+        const uint32_t jr = row_id % kW, rest = row_id / kW;
+        const uint32_t b = rest / (NF * 2), rem = rest % (NF * 2);
         const uint32_t f = rem >> 1, which = rem & 1;
-        const float *W = which ? a.bw[f] : a.gw[f];
-        const float *bias = which ? a.bb[f] : a.gb[f];
-        const f4 *wr = reinterpret_cast<const f4 *>(W + (size_t)j * kW);
-        const f4 *sr = reinterpret_cast<const f4 *>(a.styles + (size_t)b * kW);
-        float acc = 0.0f;
-#pragma unroll 8
-        for (uint32_t k = 0; k < kW / 4; ++k) {
-            const f4 w4 = wr[k], s4 = sr[k];
-            acc = __fmaf_rn(s4.x, w4.x, acc);
-            acc = __fmaf_rn(s4.y, w4.y, acc);
-            acc = __fmaf_rn(s4.z, w4.z, acc);
-            acc = __fmaf_rn(s4.w, w4.w, acc);
-        }
-        const float lin = __fadd_rn(acc, bias[j]);
+        const f4 s4 = reinterpret_cast<const f4 *>(a.styles + (size_t)b * kW)[lane];
+        // one 256-long dot product per wave: lane l holds k = 4l .. 4l+3
+        auto dot = [&](const float *W) {
+            const f4 w4 = reinterpret_cast<const f4 *>(W + (size_t)jr * kW)[lane];
+            float p = __fmaf_rn(s4.w, w4.w, __fmaf_rn(s4.z, w4.z, __fmaf_rn(s4.y, w4.y, __fmul_rn(s4.x, w4.x))));
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) p = __fadd_rn(p, __shfl_xor(p, o));
+            return p;
+        };
+        const float lin = __fadd_rn(dot(which ? a.bw[f] : a.gw[f]), (which ? a.bb[f] : a.gb[f])[jr]);
         // LinearLayer: std_init * linear + bias_init (sdf_model.py:39, 58-59).  The
         // activation sin(gamma (W x + b) + beta) of the modulated layer runs as
         // sin_rev(fma(gamma'', z, beta'')) on its bias-free, row-scaled GEMM output
@@ -206,27 +205,17 @@ __global__ void __launch_bounds__(256) xprep_kernel(const XPrepArgs a) {
         // beta'' leaves the accumulators starting from zero (no bias rows in LDS).
         constexpr double k2pi = 6.283185307179586476925;
         const int l = Net::film_layer(f);
-        const float gam = __fadd_rn(__fmul_rn(15.0f, lin), 30.0f);
         float v;
         if (which) {
-            // gamma of the same row: recomputed here (its block is another workgroup)
-            const f4 *gr = reinterpret_cast<const f4 *>(a.gw[f] + (size_t)j * kW);
-            float ga = 0.0f;
-#pragma unroll 8
-            for (uint32_t k = 0; k < kW / 4; ++k) {
-                const f4 w4 = gr[k], s4 = sr[k];
-                ga = __fmaf_rn(s4.x, w4.x, ga);
-                ga = __fmaf_rn(s4.y, w4.y, ga);
-                ga = __fmaf_rn(s4.z, w4.z, ga);
-                ga = __fmaf_rn(s4.w, w4.w, ga);
-            }
-            const float g = __fadd_rn(__fmul_rn(15.0f, __fadd_rn(ga, a.gb[f][j])), 30.0f);
+            // gamma of the same row (its wave is another one)
+            const float g = __fadd_rn(__fmul_rn(15.0f, __fadd_rn(dot(a.gw[f]), a.gb[f][jr])), 30.0f);
             const float bet = __fadd_rn(__fmul_rn(0.25f, lin), 0.0f);
-            v = (float)(((double)g * (double)a.lb[l][j] + (double)bet) / k2pi);
+            v = (float)(((double)g * (double)a.lb[l][jr] + (double)bet) / k2pi);
         } else {
-            v = (float)((double)gam / ((double)a.su[l * kW + j] * k2pi));
+            const float gam = __fadd_rn(__fmul_rn(15.0f, lin), 30.0f);
+            v = (float)((double)gam / ((double)a.su[l * kW + jr] * k2pi));
         }
-        a.film[(((size_t)b * NF + f) * 2 + which) * kW + j] = v;
+        if (lane == 0) a.film[(((size_t)b * NF + f) * 2 + which) * kW + jr] = v;
         return;
     }
     const uint32_t e = (blk - nfilm) * 256 + j;
@@ -420,6 +409,12 @@ constexpr int kXStage2 = kXSliceF4 / kThreads2;     // float4 staged per thread 
 #ifndef SDFR_X2_PIN2
 #define SDFR_X2_PIN2 1     // keep the previous group's A fragments allocated too
 #endif
+// SDFR_X2_SGB = n > 0 (with SDFR_X2_PD): the side work is issued interleaved with the
+// half-step's MFMAs, n VALU per MFMA, by sched_group_barrier (one region per
+// half-step) instead of as one block after MFMA group SDFR_X2_SIDE
+#ifndef SDFR_X2_SGB
+#define SDFR_X2_SGB 0
+#endif
 // (SIREN keeps 4: its 9 FiLM layers' vectors take 18 KB of LDS)
 template <class Net>
 constexpr int x2_slots() { return Net::kSiren ? 4 : SDFR_X2_SLOTS; }
@@ -512,6 +507,7 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
             ah[i] = R.nh[i];
             al[i] = R.nl[i];
         }
+        if constexpr (SDFR_X2_SGB > 0) side();
 #pragma unroll
         for (int grp = 0; grp < 4; ++grp) {
             const int gn = grp + PD;
@@ -541,8 +537,18 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
             asm volatile("" ::"v"(ah[i0]), "v"(ah[i1]), "v"(al[i0]), "v"(al[i1]));
             if (SDFR_X2_PIN2 && grp > 0)
                 asm volatile("" ::"v"(ah[i0 - 2]), "v"(ah[i1 - 2]), "v"(al[i0 - 2]), "v"(al[i1 - 2]));
-            __builtin_amdgcn_sched_barrier(0);
-            if (grp == (SDFR_X2_SIDE < 4 ? SDFR_X2_SIDE : 3)) side();
+            if constexpr (SDFR_X2_SGB > 0) {
+                // this group: its 4 fragment reads, then MFMA / n VALU alternating
+                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002 | 0x400, SDFR_X2_SGB, 0);
+                }
+            } else {
+                __builtin_amdgcn_sched_barrier(0);
+                if (grp == (SDFR_X2_SIDE < 4 ? SDFR_X2_SIDE : 3)) side();
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
         ++R.it;
@@ -1204,8 +1210,8 @@ static int launch_xpack(const NetPtrs &P, uint32_t B, const float *styles, char 
     p.film = film;
     p.packed = packed;
     p.B = film ? B : 0;
-    // blocks [0, B films x 2): FiLM rows; then (pack) the fragment packing
-    const uint32_t nfilm = p.B * Net::kFilmN * 2;
+    // blocks [0, B films x 2 x 256 / 4): FiLM rows; then (pack) the fragment packing
+    const uint32_t nfilm = p.B * Net::kFilmN * 2 * kW / 4;
     const uint32_t blocks = nfilm + (pack ? (Net::kSlices * 512 + 255) / 256 : 0);
     if (blocks == 0) return SDFR_OK;
     hipLaunchKernelGGL(xprep_kernel<Net>, dim3(blocks), dim3(256), 0, st, p);
