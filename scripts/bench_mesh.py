@@ -3,8 +3,10 @@
 Times the surface-extraction Generator (full_pipeline=False, return_sdf/xyz;
 sdf_mesh.py:244-252) at 128^2 rays x 128 samples (the reference setting) and at
 256^2 x 256 (a 256^3 volume, 16.8 M samples), one face per call as sdf_mesh.py
-does, plus align_volume; marching cubes (host, scikit-image) is excluded.
-Prints one JSON line per resolution."""
+does, plus align_volume ("ms_per_volume"); then the whole mesh step of
+sdf_mesh.py:160-182 -- volume, align_volume and extract_mesh_with_marching_cubes
+(GPU marching cubes, vertex scaling/flips, mesh copied to the host) --
+("ms_per_mesh").  Prints one JSON line per resolution."""
 import json
 import sys
 import time
@@ -47,11 +49,24 @@ def main(reps=5):
                     field.append(evs[2].elapsed_time(evs[3]))
         ms = sorted(times)[len(times) // 2] * 1e3
         fms = sorted(field)[len(field) // 2]
+        g.renderer.stage_events = None
+        mtimes = []
+        with torch.no_grad():
+            for r in range(reps + 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                out = g([z], ext, focal, near, far, return_sdf=True, return_xyz=True)
+                mesh = sdfr.extract_mesh_with_marching_cubes(sdfr.align_volume(out[3]))
+                if r:
+                    mtimes.append(time.perf_counter() - t0)
+        mms = sorted(mtimes)[len(mtimes) // 2] * 1e3
         samples = res * res * res
         print(json.dumps({"config": f"sdf_mesh surface extraction {res}^2 rays x {res} samples "
                                     f"({res}^3 SDF volume), 1 face per call",
                           "ms_per_volume": ms, "volumes_per_s": 1e3 / ms,
-                          "field_ms": fms,
+                          "field_ms": fms, "ms_per_mesh": mms,
+                          "mesh_vertices": int(mesh.vertices.shape[0]),
+                          "mesh_faces": int(mesh.faces.shape[0]),
                           "field_tflops": 550912 * samples / fms / 1e9,
                           "volume_shape": list(vol.shape)}), flush=True)
         del g, out, vol
