@@ -6,7 +6,8 @@ sdf_mesh.py:244-252) at 128^2 rays x 128 samples (the reference setting) and at
 does, plus align_volume ("ms_per_volume"); then the whole mesh step of
 sdf_mesh.py:160-182 -- volume, align_volume and extract_mesh_with_marching_cubes
 (GPU marching cubes, vertex scaling/flips, mesh copied to the host) --
-("ms_per_mesh").  Prints one JSON line per resolution."""
+("ms_per_mesh"; at the volume's median level, since a random-init SDF has no zero
+crossing).  Prints one JSON line per resolution."""
 import json
 import sys
 import time
@@ -56,7 +57,15 @@ def main(reps=5):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 out = g([z], ext, focal, near, far, return_sdf=True, return_xyz=True)
-                mesh = sdfr.extract_mesh_with_marching_cubes(sdfr.align_volume(out[3]))
+                vol = sdfr.align_volume(out[3])
+                # extract_mesh_with_marching_cubes's steps at the volume's median level:
+                # a random-init SDF (no sphere init) has no zero crossing
+                v3 = vol[0, ..., 0].permute(1, 0, 2)
+                verts, faces = sdfr.marching_cubes(v3, float(v3.median()))
+                for axis, size in enumerate((vol.shape[2], vol.shape[1], vol.shape[3])):
+                    verts[:, axis] = (verts[:, axis] / float(size) - 0.5) * 0.24
+                verts[:, 1:] *= -1
+                mesh = sdfr.Mesh(verts.cpu().numpy(), faces.cpu().numpy())
                 if r:
                     mtimes.append(time.perf_counter() - t0)
         mms = sorted(mtimes)[len(mtimes) // 2] * 1e3
