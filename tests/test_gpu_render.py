@@ -526,3 +526,10 @@ def test_module_path_vs_reference_golden(sdfr, golden_dir, name):
     _cmp(f"module_{name}", "rgb", rgb.cpu().numpy(), g["rgb"], "module_golden_rgb")
     _cmp(f"module_{name}", "features", feat.cpu().numpy(), g["features"],
          "module_golden_features")
+
+
+def test_graft_entry_smoke():
+    """__graft_entry__.smoke() (the round-end smoke check): the fused render against
+    the oracle and Generator.forward's thumbnail equal to the renderer's own output."""
+    import __graft_entry__
+    __graft_entry__.smoke()
