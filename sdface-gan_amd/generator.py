@@ -339,7 +339,11 @@ class Decoder(nn.Module):
 
     def forward(self, features, styles, rgbd_in=None, transform=None, return_latents=False,
                 inject_index=None, truncation=1, truncation_latent=None, input_is_latent=False,
-                noise=None, randomize_noise=True, mesh_path=None):
+                noise=None, randomize_noise=True, mesh_path=None, prepared=None):
+        if prepared is not None:         # prepare_fused() ran earlier (Generator.forward)
+            latent, noise, sty = prepared
+            return (self._fused_forward(features, latent, noise, sty),
+                    (latent if return_latents else None))
         latent, noise = self.styles_and_noise_forward(styles, noise, inject_index, truncation,
                                                       truncation_latent, input_is_latent,
                                                       randomize_noise)
@@ -371,6 +375,33 @@ class Decoder(nn.Module):
                 for t in self.to_rgbs)
             self._fir = fir if ok else False
         return self._fir is not False
+
+    def fused_ready(self, device, transform=None, rgbd_in=None):
+        """Will forward() take the fused path for features on ``device``?  (Checked
+        before the features exist, so that prepare_fused can run beside the renderer.)"""
+        if device.type != "cuda":
+            return False
+        return self._fused_ok(torch.empty(0, device=device), rgbd_in, transform)
+
+    def prepare_fused(self, styles, B, device, noise=None, inject_index=None, truncation=1,
+                      truncation_latent=None, input_is_latent=False, randomize_noise=True):
+        """Everything of the fused forward that does not depend on the features: the
+        mapping network, the noise maps and every layer's modulation / demodulation;
+        forward(..., prepared=<this>) then runs the convolutions.  The same work, in
+        the same order, as forward() does it."""
+        latent, noise = self.styles_and_noise_forward(styles, noise, inject_index, truncation,
+                                                      truncation_latent, input_is_latent,
+                                                      randomize_noise)
+        seq = [self.conv1] + list(self.convs)
+        noise = self._fused_noise(noise, B, device, torch.float32)
+        split = [self._conv_x(sc.conv) for sc in seq]
+        return latent, noise, self._fused_styles(latent, seq, split)
+
+    def _fused_styles(self, latent, seq, split):
+        if latent.is_cuda and latent.dtype == torch.float32 and self.style_dim in (256, 512):
+            return self._styles_fused(latent, seq, split)
+        mods, rgb_mods, mods_raw = self._modulations(latent)
+        return mods, rgb_mods, self._demods(seq, split, mods_raw)
 
     def _conv_x(self, mc):
         """Does this ModulatedConv2d run on the split-fp16 implicit GEMM?"""
@@ -525,7 +556,7 @@ class Decoder(nn.Module):
                 demods[i] = dflat[doffs[j]:doffs[j] + B * cout].view(B, cout)
         return mods[:nconv], mods[nconv:], demods
 
-    def _fused_noise(self, noise, B, features):
+    def _fused_noise(self, noise, B, device, dtype):
         """The per-layer noise maps of the fused path: the given ones, and every
         missing one (randomize_noise) sliced from ONE standard-normal draw of all of
         their elements, layer after layer -- one launch instead of one per layer (the
@@ -536,7 +567,7 @@ class Decoder(nn.Module):
             return noise
         sizes = [2 ** ((i + 2 * self.log_in_size + 1) // 2) for i in range(self.num_layers)]
         total = sum(B * sizes[i] * sizes[i] for i in missing)
-        flat = torch.randn(total, device=features.device, dtype=features.dtype)
+        flat = torch.randn(total, device=device, dtype=dtype)
         out, off = list(noise), 0
         for i in missing:
             n = B * sizes[i] * sizes[i]
@@ -554,7 +585,7 @@ class Decoder(nn.Module):
             tc._sdfr_base = cache
         return cache[1]
 
-    def _fused_forward(self, features, latent, noise):
+    def _fused_forward(self, features, latent, noise, sty=None):
         """Same computation as the module path: per layer one split-fp16 convolution
         (or MIOpen's) plus one sdfr_styled_epilogue on NHWC activations -- for the
         regular convolutions the epilogue runs inside the conv kernel
@@ -564,13 +595,11 @@ class Decoder(nn.Module):
         cl = torch.channels_last
         B = features.shape[0]
         seq = [self.conv1] + list(self.convs)
-        noise = self._fused_noise(noise, B, features)
         split = [self._conv_x(sc.conv) for sc in seq]     # layer i's input as hi/lo planes
-        if latent.is_cuda and latent.dtype == torch.float32 and self.style_dim in (256, 512):
-            mods, rgb_mods, demods = self._styles_fused(latent, seq, split)
-        else:
-            mods, rgb_mods, mods_raw = self._modulations(latent)
-            demods = self._demods(seq, split, mods_raw)
+        if sty is None:
+            noise = self._fused_noise(noise, B, features.device, features.dtype)
+            sty = self._fused_styles(latent, seq, split)
+        mods, rgb_mods, demods = sty
         x = (modulate_to_nhwc_split if split[0] else modulate_to_nhwc)(features, mods[0])
         rgb = None
         for i, sc in enumerate(seq):
@@ -633,6 +662,15 @@ class Decoder(nn.Module):
         return rgb
 
 
+def _tensors_of(x):
+    """Every tensor inside nested tuples / lists (Decoder.prepare_fused's result)."""
+    if isinstance(x, torch.Tensor):
+        yield x
+    elif isinstance(x, (tuple, list)):
+        for y in x:
+            yield from _tensors_of(y)
+
+
 def _has(o, k):
     return k in o.keys() if hasattr(o, "keys") else hasattr(o, k)
 
@@ -656,6 +694,22 @@ class Generator(nn.Module):
                                               out_im_res=model_opt.renderer_spatial_output_dim)
         if self.full_pipeline:
             self.decoder = Decoder(model_opt, blur_kernel=blur_kernel)
+        # fused inference: decoder style prep on a side stream beside the renderer
+        self.overlap_decoder_prep = True
+        self._side_streams = {}
+        self._dec_key = None
+
+    def _decoder_weights_unchanged(self):
+        key = tuple((p.data_ptr(), p._version) for p in self.decoder.parameters())
+        same = key == self._dec_key
+        self._dec_key = key
+        return same
+
+    def _side_stream(self, device):
+        st = self._side_streams.get(device)
+        if st is None:
+            st = self._side_streams[device] = torch.cuda.Stream(device=device)
+        return st
 
     def mean_latent(self, n_latent, device, z=None):
         if z is None:
@@ -690,17 +744,48 @@ class Generator(nn.Module):
         with torch.set_grad_enabled(self.is_train and self.train_renderer):
             latent = self.styles_and_noise_forward(styles, inject_index, truncation,
                                                    truncation_latent, input_is_latent)
+        # Fused inference: the decoder's feature-independent prep (its mapping network,
+        # noise maps, per-layer modulations / demodulations: ~12 small launches) runs
+        # before the renderer -- on a side stream beside it while the decoder's weight
+        # caches are warm (weights unchanged since the previous call), else in order
+        # on this stream, so the caches a weight update rebuilds, and the ones it
+        # frees, never cross streams.  Either way the device RNG is drawn in the same
+        # order (decoder noise, then the renderer's sampling offsets).
+        prepared, side = None, None
+        if (self.full_pipeline and cam_poses.is_cuda and not project_noise
+                and self.decoder.fused_ready(cam_poses.device)):
+            kw = dict(noise=noise, inject_index=inject_index, truncation=truncation,
+                      truncation_latent=truncation_latent, input_is_latent=input_is_latent,
+                      randomize_noise=randomize_noise)
+            B, dev = cam_poses.shape[0], cam_poses.device
+            # (a small eager batch is host-bound: the stream switch would cost more than
+            # the overlap saves; inside a graph capture it costs nothing at replay)
+            if (self.overlap_decoder_prep and (B >= 8 or torch.cuda.is_current_stream_capturing())
+                    and self._decoder_weights_unchanged()):
+                main = torch.cuda.current_stream(dev)
+                side = self._side_stream(dev)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    prepared = self.decoder.prepare_fused(latent, B, dev, **kw)
+                if not torch.cuda.is_current_stream_capturing():
+                    for t in _tensors_of(prepared):
+                        t.record_stream(main)        # made on `side`, used on `main`
+            else:
+                prepared = self.decoder.prepare_fused(latent, B, dev, **kw)
+        with torch.set_grad_enabled(self.is_train and self.train_renderer):
             lat0 = latent[0][:, 0] if input_is_latent else latent[0]
             thumb_rgb, features, sdf, mask, xyz, eikonal_term = self.renderer(
                 cam_poses, focals, near, far, styles=lat0, return_eikonal=return_eikonal,
                 t_rand=t_rand)
         if self.full_pipeline:
+            if side is not None:
+                torch.cuda.current_stream(cam_poses.device).wait_stream(side)
             rgb, decoder_latent = self.decoder(
                 features, latent, transform=cam_poses if project_noise else None,
                 return_latents=return_latents, inject_index=inject_index, truncation=truncation,
                 truncation_latent=truncation_latent, noise=noise,
                 input_is_latent=input_is_latent, randomize_noise=randomize_noise,
-                mesh_path=mesh_path)
+                mesh_path=mesh_path, prepared=prepared)
         else:
             rgb = None
         if return_latents:
