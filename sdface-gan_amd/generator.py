@@ -662,6 +662,9 @@ class Decoder(nn.Module):
         return rgb
 
 
+_SIDE_STREAMS = {}
+
+
 def _tensors_of(x):
     """Every tensor inside nested tuples / lists (Decoder.prepare_fused's result)."""
     if isinstance(x, torch.Tensor):
@@ -696,7 +699,6 @@ class Generator(nn.Module):
             self.decoder = Decoder(model_opt, blur_kernel=blur_kernel)
         # fused inference: decoder style prep on a side stream beside the renderer
         self.overlap_decoder_prep = True
-        self._side_streams = {}
         self._dec_key = None
 
     def _decoder_weights_unchanged(self):
@@ -705,10 +707,12 @@ class Generator(nn.Module):
         self._dec_key = key
         return same
 
-    def _side_stream(self, device):
-        st = self._side_streams.get(device)
+    @staticmethod
+    def _side_stream(device):
+        # one per device for the process (kept off the module: a Stream does not deepcopy)
+        st = _SIDE_STREAMS.get(device)
         if st is None:
-            st = self._side_streams[device] = torch.cuda.Stream(device=device)
+            st = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
         return st
 
     def mean_latent(self, n_latent, device, z=None):

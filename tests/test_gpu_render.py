@@ -533,3 +533,28 @@ def test_graft_entry_smoke():
     the oracle and Generator.forward's thumbnail equal to the renderer's own output."""
     import __graft_entry__
     __graft_entry__.smoke()
+
+
+def test_decoder_prep_overlap_matches_in_order(sdfr):
+    """Generator.forward's decoder prep on the side stream (batch >= 8, warm weight
+    caches) gives the images of the in-order prep from the same RNG state, and the
+    generator still deep-copies after it ran (the stream is kept off the module)."""
+    import copy
+    dev = torch.device("cuda", 0)
+    opt = sdfr.vol_render_opt()
+    torch.manual_seed(5)
+    g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
+    g.renderer.rng_device = "device"
+    B = 8
+    z = torch.randn(B, 256, device=dev)
+    cam, focal, near, far, _ = sdfr.generate_camera_params(64, dev, batch=B)
+    outs = []
+    for overlap in (False, True, True):       # the 2nd call warms the caches
+        g.overlap_decoder_prep = overlap
+        torch.cuda.manual_seed(21)
+        with torch.no_grad():
+            outs.append(g([z], cam, focal, near, far))
+    torch.cuda.synchronize()
+    for rgb, thumb in outs[1:]:
+        assert torch.equal(rgb, outs[0][0]) and torch.equal(thumb, outs[0][1])
+    copy.deepcopy(g)
