@@ -106,8 +106,29 @@ def timed_steps(step, steps, world, device, before_step=None):
     return elapsed
 
 
+def _cgroup_cpus():
+    """CPUs granted by the cgroup's CPU quota (cgroup v2 cpu.max / v1 cfs), or None."""
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            return -(-int(quota) // int(period))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        p = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        if q > 0:
+            return -(-q // p)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_info():
-    """Host CPU facts for the CPU baseline line: logical CPUs and the model name."""
+    """Host CPU facts for the CPU baseline line: logical CPUs, the affinity mask, the
+    physical cores in it (one per SMT sibling group), the cgroup CPU quota, the model
+    name, and `cores` = the threads the baseline runs with: every physical core of the
+    affinity mask, capped by the quota (threads beyond the quota only time-slice)."""
     model = None
     try:
         for ln in open("/proc/cpuinfo"):
@@ -116,7 +137,18 @@ def host_info():
                 break
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "cpu_model": model}
+    aff = sorted(os.sched_getaffinity(0))
+    groups = set()
+    for c in aff:
+        try:
+            groups.add(Path(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list")
+                       .read_text().strip())
+        except OSError:
+            groups.add(str(c))
+    quota = _cgroup_cpus()
+    cores = len(groups) if quota is None else max(1, min(len(groups), quota))
+    return {"nproc": os.cpu_count(), "affinity_cpus": len(aff), "physical_cores_in_affinity":
+            len(groups), "cgroup_cpu_quota": quota, "cpu_model": model, "cores": cores}
 
 
 def build_generator(sdfr, device, seed, ngp=True):
@@ -136,6 +168,9 @@ def cpu_baseline(seconds, siren=False):
     from sdfr_loader import load
     sdfr = load()
     oracle.build()
+    host = host_info()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(host["cores"])
     opt = sdfr.vol_render_opt(ngp=not siren)
     torch.manual_seed(1)
     g = sdfr.Generator(opt.model, opt.rendering).eval()
@@ -154,10 +189,13 @@ def cpu_baseline(seconds, siren=False):
             el = time.perf_counter() - t0
             if el >= seconds and faces >= 2:
                 break
-    return {"value": faces / el, "unit": "faces/s", "cores": torch.get_num_threads(),
-            "kind": "port", **host_info(),
+    used = torch.get_num_threads()
+    torch.set_num_threads(prev_threads)
+    return {"value": faces / el, "unit": "faces/s", **host, "cores": used,
+            "kind": "port",
             "sample": f"{faces} faces (64^2x24 oracle renderer + CPU decoder to 256^2), "
-                      f"1 face per call, {el:.1f}s; cores = torch intra-op threads used"}
+                      f"1 face per call, {el:.1f}s; cores = torch intra-op threads used "
+                      "(physical cores of the affinity mask, capped by the cgroup quota)"}
 
 
 def extras(step, B, graphed_step, steps=10, warm=3):

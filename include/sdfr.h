@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 5
+#define SDFR_ABI_VERSION 6
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -82,8 +82,9 @@ int sdfr_grid_encode_backward(const float *grad, const float *inputs,
  * sdfr_grid_encode_backward_ws_bytes(...) bytes (0 = none needed: then ws may be
  * NULL).  With it, the table gradient of the fine levels is binned and summed in
  * LDS instead of scattered with global atomics (csrc/encoders.hip); with ws NULL
- * or too small, the direct-atomic path runs.  sdfr_grid_encode_backward is this
- * function with a library-owned workspace. */
+ * or too small, the workspace-free path runs (LDS windows for the coarse levels,
+ * direct atomics for the hashed ones).  sdfr_grid_encode_backward is this function
+ * with ws NULL: it allocates nothing (stream-ordered, HIP-graph-capture safe). */
 size_t sdfr_grid_encode_backward_ws_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L,
                                           float S, uint32_t H, int align_corners);
 int sdfr_grid_encode_backward_ws(const float *grad, const float *inputs,
@@ -173,6 +174,13 @@ typedef struct sdfr_ngp_render_args {
      * row-scale and packing kernels are then skipped, only the per-face FiLM
      * vectors are formed. */
     const void *prepacked;
+    /* Upper bound on the sample segments per ray of the f16x3 field stage (0 = the
+     * default 4): batches too small to give every CU a workgroup split each ray's
+     * samples over up to this many workgroups and chain the segments in a merge
+     * kernel (sdf_model.py:273-289's cumprod re-associated: fp32-rounding-level
+     * differences).  1 disables the split; 2 or 4 otherwise.  The workspace size
+     * (sdfr_render_ngp_workspace_bytes) covers the default bound. */
+    uint32_t max_field_segments;
 } sdfr_ngp_render_args;
 
 #define SDFR_FIELD_F16X3 0
@@ -224,32 +232,18 @@ int sdfr_render_siren_forward(const sdfr_siren_weights *w,
 int sdfr_render_ngp_encode_only(const sdfr_ngp_weights *w,
                                 const sdfr_ngp_render_args *a, void *stream);
 
-/* Profiling hook: select an ablated build of the field kernel for the NEXT
- * sdfr_render_ngp_forward calls (process-global).  0 = the product kernel;
- * 1 no barrier, 2 no LDS A-operand reads, 4 no weight staging, 8 no
- * activations, 16 no compositing (f16x3 kernel), 15/31 MFMA only.  Non-zero
- * variants produce wrong outputs, exist only to attribute kernel time
- *  and are compiled only into `make ABLATION=1` builds;
- * the product build accepts 0 only (SDFR_EINVAL otherwise). */
+#ifdef SDFR_ABLATION
+/* Profiling hooks, exported only by `make ABLATION=1` builds (lib_abl/libsdfr.so,
+ * process-global state; never in the product library):
+ * sdfr_debug_set_field_variant selects an ablated field kernel for later calls
+ * (0 = the product kernel; 1 no barrier, 2 no LDS A-operand reads, 4 no weight
+ * staging, 8 no activations, 16 no compositing, 15/31 MFMA only -- wrong outputs,
+ * to attribute kernel time); sdfr_debug_set_encode_mode the
+ * hash-grid gather variant (default 289, or SDFR_ENC_MODE at load; 1, 2, 9, 33,
+ * 257, 289, 290 -- all bit-identical, scripts/encode_time.py). */
 int sdfr_debug_set_field_variant(int variant);
-
-/* Selects the hash-grid gather variant of the ngp encode stage for later calls
- * (process-global; default 289, overridable at load by SDFR_ENC_MODE): the low
- * bits are the levels handled per thread (1 or 2), +8 disables the paired
- * x-corner loads (mode 9), +32 gives each thread two samples, +256 pairs any
- * consecutive rows with dword-aligned 16-B loads.  Accepted: 1, 2, 9, 33, 257,
- * 289, 290.  Every mode produces bit-identical features; modes exist to measure
- * the gather (scripts/encode_time.py).  SDFR_EINVAL for any other value. */
 int sdfr_debug_set_encode_mode(int mode);
-
-/* Upper bound on the sample segments per ray of the f16x3 ngp field stage
- * (process-global, default 4): batches too small to give every CU a workgroup
- * split each ray's samples over up to this many workgroups and chain the
- * segments in a merge kernel (sdf_model.py:273-289's cumprod re-associated:
- * fp32-rounding-level differences).  1 disables the split.  The workspace size
- * (sdfr_render_ngp_workspace_bytes) already covers the default bound.
- * SDFR_EINVAL unless 1, 2 or 4. */
-int sdfr_debug_set_field_split(int max_segments);
+#endif
 
 /* Accuracy probe for the two device sin implementations the field kernel can
  * use (software Cody-Waite + polynomial, hardware v_sin_f32 after reduction):

@@ -23,20 +23,21 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 5
+ABI_VERSION = 6
 FIELD_F16X3 = 0
 FIELD_FP32 = 1
 
-# every symbol include/sdfr.h declares (tests check the .so exports all of them)
+# every symbol include/sdfr.h declares outside its SDFR_ABLATION block (tests check the
+# product .so exports all of them and nothing else with the sdfr_ prefix)
+ABLATION_EXPORTS = ("sdfr_debug_set_field_variant", "sdfr_debug_set_encode_mode")
 EXPORTS = (
     "sdfr_abi_version", "sdfr_last_error",
     "sdfr_grid_encode_forward", "sdfr_grid_encode_backward",
     "sdfr_grid_encode_backward_ws_bytes", "sdfr_grid_encode_backward_ws",
     "sdfr_sh_encode_forward", "sdfr_sh_encode_backward",
     "sdfr_render_ngp_workspace_bytes", "sdfr_render_ngp_forward",
-    "sdfr_render_ngp_encode_only", "sdfr_debug_set_field_variant", "sdfr_debug_sin_probe",
+    "sdfr_render_ngp_encode_only", "sdfr_debug_sin_probe",
     "sdfr_debug_sin_rev_probe", "sdfr_camera_extrinsics",
-    "sdfr_debug_set_encode_mode", "sdfr_debug_set_field_split",
     "sdfr_render_siren_workspace_bytes", "sdfr_render_siren_forward",
     "sdfr_render_pack_bytes", "sdfr_render_ngp_pack", "sdfr_render_siren_pack",
     "sdfr_fused_bias_act", "sdfr_mapping_linear", "sdfr_decoder_styles", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
@@ -87,6 +88,7 @@ class NgpRenderArgs(ctypes.Structure):
         ("rgb", _vp), ("features", _vp), ("sdf", _vp), ("xyz", _vp), ("mask", _vp),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
         ("stage_events", _vp * 4), ("field_precision", _int), ("prepacked", _vp),
+        ("max_field_segments", _u32),
     ]
 
 
@@ -156,9 +158,9 @@ def lib():
                                           ctypes.POINTER(NgpRenderArgs), _vp]
     L.sdfr_render_ngp_encode_only.argtypes = [ctypes.POINTER(NgpWeights),
                                               ctypes.POINTER(NgpRenderArgs), _vp]
-    L.sdfr_debug_set_field_variant.argtypes = [_int]
-    L.sdfr_debug_set_encode_mode.argtypes = [_int]
-    L.sdfr_debug_set_field_split.argtypes = [_int]
+    for name in ABLATION_EXPORTS:           # profiling builds only (make ABLATION=1)
+        if hasattr(L, name):
+            getattr(L, name).argtypes = [_int]
     L.sdfr_render_siren_workspace_bytes.restype = ctypes.c_size_t
     L.sdfr_render_siren_workspace_bytes.argtypes = [_u32]
     L.sdfr_render_pack_bytes.argtypes = [_int]

@@ -18,7 +18,10 @@ def generate_camera_params(resolution, device, batch=1, locations=None, sweep=Fa
     """Returns (extrinsics [B,3,4] = [R^T | T], focal [B,1,1], near [B,1,1],
     far [B,1,1], viewpoint [B,2] = (azim, elev))."""
     dev = torch.device(device)
-    if dev.type == "cuda":
+    scalar = all(not isinstance(v, torch.Tensor) or v.numel() == 1
+                 for v in (fov_ang, dist_radius))
+    if dev.type == "cuda" and scalar:
+        # per-view fov / radius tensors (sdf_mesh.py:46-55) take the torch ops below
         return _camera_cuda(resolution, dev, batch, locations, sweep, uniform, azim_range,
                             elev_range, fov_ang, dist_radius)
     if locations is not None:
@@ -78,6 +81,7 @@ def _camera_cuda(resolution, device, batch, locations, sweep, uniform, azim_rang
     sdf_utils.py:151-154 replaced; capture-safe (no host sync, no host->device copy)."""
     from . import _lib
     if locations is not None:
+        locations = locations.to(device, torch.float32)   # the kernel reads device memory
         azim = locations[:, 0].contiguous()
         elev = locations[:, 1].contiguous()
     elif sweep:

@@ -72,16 +72,25 @@ def trainer_payload(trainer, with_optim=True):
     return d
 
 
+def _barrier():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+
+
 def save(path, trainer, with_optim=True):
-    """Write ``{g, d, g_ema[, g_optim, d_optim, iteration, mean_path_length]}`` (rank 0)."""
-    if _rank() != 0:
-        return None
+    """Write ``{g, d, g_ema[, g_optim, d_optim, iteration, mean_path_length]}`` (rank 0).
+    Collective when a process group is up: every rank calls it and leaves only once
+    the file is in place, so no rank can read a checkpoint rank 0 is still writing
+    (stage 2 loads vol_renderer.pt right after stage 1's save_final)."""
     path = Path(path)
-    path.parent.mkdir(parents=True, exist_ok=True)
-    tmp = path.with_suffix(".tmp")
-    torch.save(trainer_payload(trainer, with_optim), tmp)
-    os.replace(tmp, path)
-    return path
+    if _rank() == 0:
+        path.parent.mkdir(parents=True, exist_ok=True)
+        tmp = path.with_suffix(".tmp")
+        torch.save(trainer_payload(trainer, with_optim), tmp)
+        os.replace(tmp, path)
+    _barrier()
+    return path if _rank() == 0 else None
 
 
 def load_file(path, map_location="cpu"):

@@ -15,8 +15,6 @@
 #include <cmath>
 
 #include <cstdio>
-#include <map>
-#include <mutex>
 #include <string>
 #include <utility>
 
@@ -644,14 +642,12 @@ static int grid_bin_launch(const float *grad, const float *in, const int32_t *of
         exclusive_scan_u32(cnt, p.M, bsum, st);
         hipLaunchKernelGGL((grid_bin_scatter_kernel<D, C>), grid, dim3(kBinThreads), 0, st, grad,
                            in, off, B, lt, gt, ac, interp, bl, cnt, e_row, e_val);
-        static bool attr_set = false;   // > 64 KB of dynamic LDS must be opted into
-        if (!attr_set) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&grid_bin_accum_kernel<C>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kBinLdsBytes) != hipSuccess)
-                return fail(SDFR_ELAUNCH, "grid_encode_backward: LDS attribute (bins)");
-            attr_set = true;
-        }
+        // > 64 KB of dynamic LDS must be opted into; the attribute is per device, so it
+        // is set on every call (a host-side call, not a stream op, capture-safe)
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&grid_bin_accum_kernel<C>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kBinLdsBytes) != hipSuccess)
+            return fail(SDFR_ELAUNCH, "grid_encode_backward: LDS attribute (bins)");
         BinItem *items = (BinItem *)(w + p.item_off);
         uint32_t *nitems = (uint32_t *)(w + p.nitem_off);
         hipLaunchKernelGGL(grid_bin_plan_kernel, dim3(1), dim3(kScanThreads), 0, st, cnt, p.nblk,
@@ -690,14 +686,11 @@ static int grid_bwd_launch(const float *grad, const float *in, const int32_t *of
             const uint32_t nblk = std::max<uint32_t>(
                 1, std::min<uint32_t>((B + 4095) / 4096, (256 + nwins - 1) / nwins));
             const uint32_t per_block = (B + nblk - 1) / nblk;
-            static bool attr_set = false;   // > 64 KB of dynamic LDS must be opted into
-            if (!attr_set) {
-                if (hipFuncSetAttribute(reinterpret_cast<const void *>(&grid_bwd_lds_kernel<D, C>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)kBwdLdsBytes) != hipSuccess)
-                    return fail(SDFR_ELAUNCH, "grid_encode_backward: LDS attribute");
-                attr_set = true;
-            }
+            // > 64 KB of dynamic LDS: opted into per call (the attribute is per device)
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&grid_bwd_lds_kernel<D, C>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kBwdLdsBytes) != hipSuccess)
+                return fail(SDFR_ELAUNCH, "grid_encode_backward: LDS attribute");
             hipLaunchKernelGGL((grid_bwd_lds_kernel<D, C>), dim3(nblk, nwins), dim3(1024),
                                kBwdLdsBytes, st, grad, in, off, gemb, B, lt, gt, ac, interp, wt,
                                per_block);
@@ -934,39 +927,19 @@ int sdfr_grid_encode_backward_ws(const float *grad, const float *inputs, const f
     }
 }
 
-// The reference signature has no workspace: the binned path then uses a
-// library-owned device buffer, grown on demand (hipMalloc, one per device) and
-// kept for later calls.  Calls from several host threads on different streams
-// would share it: such callers use sdfr_grid_encode_backward_ws.
-static void *grid_bwd_internal_ws(size_t bytes) {
-    static std::mutex mu;
-    static std::map<int, std::pair<void *, size_t>> bufs;
-    std::lock_guard<std::mutex> lock(mu);
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    auto &b = bufs[dev];
-    if (b.second < bytes) {
-        if (b.first) (void)hipFree(b.first);
-        b = {nullptr, 0};
-        if (hipMalloc(&b.first, bytes) != hipSuccess) {
-            b.first = nullptr;
-            return nullptr;                 // -> direct atomics
-        }
-        b.second = bytes;
-    }
-    return b.first;
-}
-
+// The reference signature (gridencoder.h:12) has no workspace argument: it runs the
+// workspace-free path (LDS windows for the coarse levels, direct atomics for the
+// hashed ones).  Nothing is allocated, so it is stream-ordered and capture-safe;
+// callers that can hand over scratch memory (the reference's own caller allocates
+// every buffer, grid.py:75-82) use sdfr_grid_encode_backward_ws for the binned path.
 int sdfr_grid_encode_backward(const float *grad, const float *inputs, const float *embeddings,
                               const int32_t *offsets, float *grad_embeddings, uint32_t B,
                               uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
                               const float *dy_dx, float *grad_inputs, uint32_t gridtype,
                               int align_corners, uint32_t interp, void *stream) {
-    const size_t wsb = B ? sdfr_grid_encode_backward_ws_bytes(B, D, C, L, S, H, align_corners) : 0;
-    void *ws = wsb ? grid_bwd_internal_ws(wsb) : nullptr;
     return sdfr_grid_encode_backward_ws(grad, inputs, embeddings, offsets, grad_embeddings, B, D,
                                         C, L, S, H, dy_dx, grad_inputs, gridtype, align_corners,
-                                        interp, ws, ws ? wsb : 0, stream);
+                                        interp, nullptr, 0, stream);
 }
 
 int sdfr_sh_encode_forward(const float *inputs, float *outputs, uint32_t B, uint32_t D,

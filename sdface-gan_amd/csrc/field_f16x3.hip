@@ -361,63 +361,17 @@ __device__ __forceinline__ void zero_acc(f4 (&acc)[16]) {
 // ----------------------------------------------------------------------------
 constexpr int kWaves2 = 8;
 constexpr int kThreads2 = kWaves2 * 64;
-constexpr int kXStage2 = kXSliceF4 / kThreads2;     // float4 staged per thread per half-slice
-// SDFR_X2_DMA: the weight ring is filled by LDS-DMA (buffer_load ... lds) into 4
-// half-slice slots, three half-steps ahead, one barrier per half-step (1), or
-// staged through registers + ds_write (0: ngp 2 whole-K-step slots, siren 3
-// half-slice slots).  The register path moves 32 KB per K-step through VGPRs and
-// the LDS store port (measured 16 % of the kernel by ablation).
-#ifndef SDFR_X2_DMA
-#define SDFR_X2_DMA 1
-#endif
-// SDFR_X2_STAGGER: waves 4-7 issue each half-step's register work (the next input
-// pair's activation) BEFORE their MFMAs, waves 0-3 after, so the two waves of a SIMD
-// enter every barrier interval with complementary work (matrix beside VALU)
-// instead of in lockstep (MI355X_MICROARCH.md, two waves per SIMD, item 9)
-#ifndef SDFR_X2_STAGGER
-#define SDFR_X2_STAGGER 0
-#endif
-// SDFR_X2_SIDE: the MFMA group (of 4, two tiles each) after which the register work
-// is issued when not staggered (4 = after all of them)
-#ifndef SDFR_X2_SIDE
-#define SDFR_X2_SIDE 1
-#endif
-// SDFR_X2_PRIO: static issue priority 1 for waves 4-7 (the second-dispatched half
-// loses every VALU arbitration at equal priority, MI355X_MICROARCH.md two waves per
-// SIMD item 4); no per-segment flips
-#ifndef SDFR_X2_PRIO
-#define SDFR_X2_PRIO 0
-#endif
-// SDFR_X2_SLOTS: LDS-DMA ring slots of one half-slice (16 KB); the DMA of a
-// half-slice is issued SLOTS-1 half-steps ahead of its use
-// SDFR_X2_KSTEP_SYNC: with the LDS-DMA ring, DMA and barrier per whole k-step (two
-// half-slices, the next k-step fetched one k-step ahead: 34 barriers per ngp pass)
-// instead of per half-step (68)
-#ifndef SDFR_X2_KSTEP_SYNC
-#define SDFR_X2_KSTEP_SYNC 1
-#endif
-#ifndef SDFR_X2_SLOTS
-#define SDFR_X2_SLOTS 4
-#endif
-// SDFR_X2_PD: A-fragment prefetch distance in MFMA groups across half-step and k-step
-// boundaries (0: within a half-step only, the next k-step's first group read after
-// the barrier).  With PD >= 1 the k-step's barrier moves ahead of its last PD groups'
-// MFMAs, and the next k-step's first PD groups are read behind them.
-#ifndef SDFR_X2_PD
-#define SDFR_X2_PD 1
-#endif
-#ifndef SDFR_X2_PIN2
-#define SDFR_X2_PIN2 1     // keep the previous group's A fragments allocated too
-#endif
-// SDFR_X2_SGB = n > 0 (with SDFR_X2_PD): the side work is issued interleaved with the
-// half-step's MFMAs, n VALU per MFMA, by sched_group_barrier (one region per
-// half-step) instead of as one block after MFMA group SDFR_X2_SIDE
-#ifndef SDFR_X2_SGB
-#define SDFR_X2_SGB 0
-#endif
-// (SIREN keeps 4: its 9 FiLM layers' vectors take 18 KB of LDS)
-template <class Net>
-constexpr int x2_slots() { return Net::kSiren ? 4 : SDFR_X2_SLOTS; }
+// The weight ring: 4 half-slice slots (16 KB each) filled by LDS-DMA (buffer_load
+// ... lds), DMA and barrier per whole k-step (two half-slices, the next k-step fetched
+// one k-step ahead: 34 barriers per ngp pass).  A fragments are prefetched one MFMA
+// group ahead across half-step and k-step boundaries: the k-step's barrier sits ahead
+// of its last group's MFMAs, and the next k-step's first group is read behind them.
+// The register work of a half-step (the next input pair's activation) is issued after
+// its MFMA group 1.  (Measured alternatives -- register staging through ds_write,
+// per-half-step barriers, staggered or interleaved side work, wave priorities -- are
+// in git history)
+constexpr int kX2Slots = 4;
+constexpr int kX2Side = 1;
 constexpr int kX2DmaPieces = 16 / kWaves2;          // 1 KB pieces per wave per half-slice
 
 __device__ __forceinline__ float ror8(float v) {   // lane n <- lane (n + 8) mod 16 of its row
@@ -427,20 +381,16 @@ __device__ __forceinline__ float ror8(float v) {   // lane n <- lane (n + 8) mod
 
 struct XRing2 {
     f4 *lds;
-    f4 st[2 * kXStage2];  // register path: ngp the next K-step (both halves), siren st[0..kXStage2)
-    f4 pre_h, pre_l;      // first (hi, lo) A fragment of the current slice
-    f4 nh[4], nl[4];      // SDFR_X2_PD: the next half-step's first PD groups of fragments
-    __amdgpu_buffer_rsrc_t rsrc;
+    f4 nh[2], nl[2];      // the next half-step's first group of A fragments
     v4i drsrc;            // the packed fragments for the LDS-DMA
     uint32_t it, tid, wave;
     uint32_t slot0;       // DMA ring slot of the pass's first half-slice (wave-uniform)
-    bool late;            // waves 4-7 (SDFR_X2_STAGGER)
 };
 
 // ring slot of half-step it (0 <= it < kSlices) of the current pass
 template <class Net>
 __device__ __forceinline__ uint32_t x2_slot(const XRing2 &R, uint32_t it) {
-    constexpr uint32_t S = x2_slots<Net>();
+    constexpr uint32_t S = kX2Slots;
     if constexpr (Net::kSlices % S == 0) return it % S;  // slot0 stays 0
     return (R.slot0 + it) % S;
 }
@@ -477,123 +427,49 @@ __device__ __forceinline__ void x2_dma(XRing2 &R, uint32_t slice, uint32_t slot)
 template <int V, class Net, int H, class Side>
 __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, const f4 bl,
                                        Side &&side) {
-    constexpr bool kS2 = Net::kSlice2 && !SDFR_X2_DMA;
-    constexpr bool kDma = SDFR_X2_DMA;
     const uint32_t lane = R.tid & 63u;
-    constexpr uint32_t kAhead = x2_slots<Net>() - 1;
-    if constexpr (SDFR_X2_PD > 0 && kDma && SDFR_X2_KSTEP_SYNC) {
-        constexpr int PD = SDFR_X2_PD;
-        static_assert(PD <= 2, "prefetch distance");
-        if constexpr (H == 0 && (V & 4) == 0) {
-            x2_dma(R, (R.it + 2) % Net::kSlices, x2_slot<Net>(R, R.it + 2));
-            x2_dma(R, (R.it + 3) % Net::kSlices, x2_slot<Net>(R, R.it + 3));
-        }
-        // this half-slice and the next (H = 0: the same k-step's second half, already
-        // published; H = 1: the next k-step's first, published by this step's barrier)
-        const f4 *A = R.lds + x2_slot<Net>(R, R.it) * kXSliceF4 + lane;
-        const f4 *An = R.lds + x2_slot<Net>(R, R.it + 1) * kXSliceF4 + lane;
-        f4 ah[8], al[8];
-        auto rd = [&](const f4 *src, int t, f4 &h, f4 &l) {
-            if constexpr ((V & 2) != 0) {
-                h = bh * (float)(t + 1);
-                l = bl * (float)(t + 1);
-            } else {
-                h = src[(2 * t) * 64];
-                l = src[(2 * t + 1) * 64];
-            }
-        };
-#pragma unroll
-        for (int i = 0; i < 2 * PD; ++i) {
-            ah[i] = R.nh[i];
-            al[i] = R.nl[i];
-        }
-        if constexpr (SDFR_X2_SGB > 0) side();
-#pragma unroll
-        for (int grp = 0; grp < 4; ++grp) {
-            const int gn = grp + PD;
-            if (H == 1 && gn == 4) {
-                // every read of this k-step's slots is issued: land own DMA pieces of the
-                // next k-step, drain the reads, publish / close at the barrier
-                if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if constexpr ((V & 1) == 0) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    __builtin_amdgcn_s_barrier();
-                }
-            }
-            if (gn < 4) {
-                rd(A, 2 * gn, ah[2 * gn], al[2 * gn]);
-                rd(A, 2 * gn + 1, ah[2 * gn + 1], al[2 * gn + 1]);
-            } else {
-                rd(An, 2 * (gn - 4), R.nh[2 * (gn - 4)], R.nl[2 * (gn - 4)]);
-                rd(An, 2 * (gn - 4) + 1, R.nh[2 * (gn - 4) + 1], R.nl[2 * (gn - 4) + 1]);
-            }
-            const int i0 = 2 * grp, i1 = 2 * grp + 1;
-            acc[8 * H + i0] = mfma16(al[i0], bh, acc[8 * H + i0]);
-            acc[8 * H + i1] = mfma16(al[i1], bh, acc[8 * H + i1]);
-            acc[8 * H + i0] = mfma16(ah[i0], bl, acc[8 * H + i0]);
-            acc[8 * H + i1] = mfma16(ah[i1], bl, acc[8 * H + i1]);
-            acc[8 * H + i0] = mfma16(ah[i0], bh, acc[8 * H + i0]);
-            acc[8 * H + i1] = mfma16(ah[i1], bh, acc[8 * H + i1]);
-            asm volatile("" ::"v"(ah[i0]), "v"(ah[i1]), "v"(al[i0]), "v"(al[i1]));
-            if (SDFR_X2_PIN2 && grp > 0)
-                asm volatile("" ::"v"(ah[i0 - 2]), "v"(ah[i1 - 2]), "v"(al[i0 - 2]), "v"(al[i1 - 2]));
-            if constexpr (SDFR_X2_SGB > 0) {
-                // this group: its 4 fragment reads, then MFMA / n VALU alternating
-                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002 | 0x400, SDFR_X2_SGB, 0);
-                }
-            } else {
-                __builtin_amdgcn_sched_barrier(0);
-                if (grp == (SDFR_X2_SIDE < 4 ? SDFR_X2_SIDE : 3)) side();
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        ++R.it;
-        return;
+    if constexpr (H == 0 && (V & 4) == 0) {
+        // at its first half the next k-step's two half-slices go into the slots of the
+        // previous k-step (closed by its barrier)
+        x2_dma(R, (R.it + 2) % Net::kSlices, x2_slot<Net>(R, R.it + 2));
+        x2_dma(R, (R.it + 3) % Net::kSlices, x2_slot<Net>(R, R.it + 3));
     }
-    if constexpr (kDma && (V & 4) == 0) {
-        if constexpr (SDFR_X2_KSTEP_SYNC) {
-            // whole k-steps: at its first half the next k-step's two half-slices go
-            // into the slots of the previous k-step (closed by its barrier)
-            if constexpr (H == 0) {
-                x2_dma(R, (R.it + 2) % Net::kSlices, x2_slot<Net>(R, R.it + 2));
-                x2_dma(R, (R.it + 3) % Net::kSlices, x2_slot<Net>(R, R.it + 3));
-            }
-        } else {
-            x2_dma(R, (R.it + kAhead) % Net::kSlices, x2_slot<Net>(R, R.it + kAhead));
-        }
-    }
-    const f4 *A = kDma ? R.lds + x2_slot<Net>(R, R.it) * kXSliceF4 + lane
-                : kS2  ? R.lds + ((R.it >> 1) & 1u) * (2 * kXSliceF4) + H * kXSliceF4 + lane
-                       : R.lds + (R.it % 3u) * kXSliceF4 + lane;
-    // A fragments in groups of two tiles, the next group's LDS reads issued ahead of
-    // the current group's 6 MFMAs (32 registers of fragments, not 64)
+    // this half-slice and the next (H = 0: the same k-step's second half, already
+    // published; H = 1: the next k-step's first, published by this step's barrier)
+    const f4 *A = R.lds + x2_slot<Net>(R, R.it) * kXSliceF4 + lane;
+    const f4 *An = R.lds + x2_slot<Net>(R, R.it + 1) * kXSliceF4 + lane;
     f4 ah[8], al[8];
-    auto load = [&](int i) {
+    auto rd = [&](const f4 *src, int t, f4 &h, f4 &l) {
         if constexpr ((V & 2) != 0) {
-            ah[i] = bh * (float)(i + 1);
-            al[i] = bl * (float)(i + 1);
-        } else if (!kDma && (kS2 ? H == 1 : true) && i == 0) {
-            ah[0] = R.pre_h;
-            al[0] = R.pre_l;
+            h = bh * (float)(t + 1);
+            l = bl * (float)(t + 1);
         } else {
-            ah[i] = A[(2 * i) * 64];
-            al[i] = A[(2 * i + 1) * 64];
+            h = src[(2 * t) * 64];
+            l = src[(2 * t + 1) * 64];
         }
     };
-#if SDFR_X2_STAGGER
-    if (R.late) side();
-#endif
-    load(0);
-    load(1);
+    ah[0] = R.nh[0];
+    al[0] = R.nl[0];
+    ah[1] = R.nh[1];
+    al[1] = R.nl[1];
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
-        if (grp < 3) {
-            load(2 * grp + 2);
-            load(2 * grp + 3);
+        const int gn = grp + 1;
+        if (H == 1 && gn == 4) {
+            // every read of this k-step's slots is issued: land own DMA pieces of the
+            // next k-step, drain the reads, publish / close at the barrier
+            if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr ((V & 1) == 0) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+        }
+        if (gn < 4) {
+            rd(A, 2 * gn, ah[2 * gn], al[2 * gn]);
+            rd(A, 2 * gn + 1, ah[2 * gn + 1], al[2 * gn + 1]);
+        } else {
+            rd(An, 0, R.nh[0], R.nl[0]);
+            rd(An, 1, R.nh[1], R.nl[1]);
         }
         const int i0 = 2 * grp, i1 = 2 * grp + 1;
         acc[8 * H + i0] = mfma16(al[i0], bh, acc[8 * H + i0]);
@@ -610,79 +486,9 @@ __device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, co
         if (grp > 0)
             asm volatile("" ::"v"(ah[i0 - 2]), "v"(ah[i1 - 2]), "v"(al[i0 - 2]), "v"(al[i1 - 2]));
         __builtin_amdgcn_sched_barrier(0);
-#if !SDFR_X2_STAGGER && SDFR_X2_SIDE < 4
-        if (grp == SDFR_X2_SIDE) side();
-#endif
+        if (grp == kX2Side) side();
     }
-#if SDFR_X2_STAGGER
-    if (!R.late) side();
-#elif SDFR_X2_SIDE >= 4
-    side();
-#endif
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (kDma && SDFR_X2_KSTEP_SYNC) {
-        // end of a k-step: own pieces of the next k-step have landed; the barrier
-        // publishes every wave's and closes this k-step's slots
-        if constexpr (H == 1) {
-            if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if constexpr ((V & 1) == 0) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-            }
-        }
-    } else if constexpr (kDma) {
-        // own pieces of half-slice it+1 (issued two half-steps ago) have landed; the
-        // barrier publishes every wave's (and closes this slot for the DMA of it+4)
-        if constexpr ((V & 4) == 0)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((x2_slots<Net>() - 2) * kX2DmaPieces) : "memory");
-        if constexpr ((V & 1) == 0) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-    } else if constexpr ((V & 4) != 0) {
-        if constexpr ((V & 1) == 0) __builtin_amdgcn_s_barrier();
-    } else if constexpr (kS2) {
-        const uint32_t fs = R.it >> 1;
-        f4 *wl = R.lds + ((fs + 1u) & 1u) * (2 * kXSliceF4) + H * kXSliceF4;
-#pragma unroll
-        for (int i = 0; i < kXStage2; ++i) wl[R.tid + i * kThreads2] = R.st[H * kXStage2 + i];
-        const uint32_t pf = (2u * fs + 4u + H) % Net::kSlices;
-#pragma unroll
-        for (int i = 0; i < kXStage2; ++i)
-            R.st[H * kXStage2 + i] = __builtin_bit_cast(
-                f4, __builtin_amdgcn_raw_buffer_load_b128(
-                        R.rsrc, (int)((R.tid + i * kThreads2) * sizeof(f4)),
-                        (int)(pf * kXSliceF4 * sizeof(f4)), 0));
-        if constexpr (H == 0) {
-            if constexpr ((V & 2) == 0) {
-                R.pre_h = A[kXSliceF4];
-                R.pre_l = A[kXSliceF4 + 64];
-            }
-        } else if constexpr ((V & 1) == 0) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-    } else {
-        const uint32_t wslot = (R.it + 2u) % 3u;
-#pragma unroll
-        for (int i = 0; i < kXStage2; ++i) R.lds[wslot * kXSliceF4 + R.tid + i * kThreads2] = R.st[i];
-        const uint32_t pf = (R.it + 3u) % Net::kSlices;
-#pragma unroll
-        for (int i = 0; i < kXStage2; ++i)
-            R.st[i] = __builtin_bit_cast(
-                f4, __builtin_amdgcn_raw_buffer_load_b128(
-                        R.rsrc, (int)((R.tid + i * kThreads2) * sizeof(f4)),
-                        (int)(pf * kXSliceF4 * sizeof(f4)), 0));
-        if constexpr ((V & 2) == 0) {
-            const f4 *An = R.lds + ((R.it + 1u) % 3u) * kXSliceF4 + lane;
-            R.pre_h = An[0];
-            R.pre_l = An[64];
-        }
-        if constexpr ((V & 1) == 0) {
-            asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-    }
     ++R.it;
 }
 
@@ -708,7 +514,7 @@ struct NoAct2 {
 template <int V, class Net>
 __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs a) {
     constexpr int NF = Net::kFilmN;
-    __shared__ f4 ring_lds[(SDFR_X2_DMA ? x2_slots<Net>() : (Net::kSlice2 ? 4 : 3)) * kXSliceF4];
+    __shared__ f4 ring_lds[kX2Slots * kXSliceF4];
     __shared__ float cst[6 * kW];                          // ngp layer-0 bias, 1/su0, sigma_w, rgb_w[3]
     __shared__ float film_lds[NF * 2 * kW];                // the workgroup's face
     __shared__ f4 facc_lds[kWaves2][16 * 32];              // 64 KB: [tile][g][ray8] feature sums
@@ -770,12 +576,8 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
     }
     XRing2 R;
     R.lds = ring_lds;
-    R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<f4 *>(a.packed), 0,
-                                               (int)(Net::kSlices * kXSliceF4 * sizeof(f4)),
-                                               0x00020000);
     R.tid = tid;
     R.wave = __builtin_amdgcn_readfirstlane(wave);
-    R.late = R.wave >= 4;
     R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
     R.it = 0;
     for (uint32_t i = tid; i < 6 * kW; i += kThreads2) {
@@ -786,39 +588,19 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
         else v = a.rgb_w[i - 3 * kW];
         cst[i] = v;
     }
-    if constexpr (SDFR_X2_DMA) {
-        // prologue: half-slices 0 .. SLOTS-2 -> their slots (the first step issues the next)
-        R.slot0 = 0;
-        const uint32_t pro = SDFR_X2_KSTEP_SYNC ? 2u : (uint32_t)x2_slots<Net>() - 1;
-        for (uint32_t k = 0; k < pro; ++k) x2_dma(R, k % Net::kSlices, k);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if constexpr (Net::kSlice2) {
-        // prologue: K-step 0 (half-slices 0, 1) -> slot 0; K-step 1 -> registers
-#pragma unroll
-        for (int i = 0; i < 2 * kXStage2; ++i) R.lds[tid + i * kThreads2] = a.packed[tid + i * kThreads2];
-#pragma unroll
-        for (int i = 0; i < 2 * kXStage2; ++i)
-            R.st[i] = a.packed[2 * kXSliceF4 + tid + i * kThreads2];
-    } else {
-        // prologue: slices 0, 1 -> slots 0, 1; slice 2 -> registers
-#pragma unroll
-        for (int i = 0; i < 2 * kXStage2; ++i) R.lds[tid + i * kThreads2] = a.packed[tid + i * kThreads2];
-#pragma unroll
-        for (int i = 0; i < kXStage2; ++i) R.st[i] = a.packed[2 * kXSliceF4 + tid + i * kThreads2];
-    }
+    // prologue: half-slices 0, 1 (k-step 0) -> slots 0, 1 (the first step issues the next)
+    R.slot0 = 0;
+    for (uint32_t k = 0; k < 2u; ++k) x2_dma(R, k % Net::kSlices, k);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     f4 *facc = facc_lds[wave];
 #pragma unroll
     for (int t = 0; t < 8; ++t) facc[t * 64 + lane] = f4{0.0f, 0.0f, 0.0f, 0.0f};
     __syncthreads();
-    R.pre_h = R.lds[lane];
-    R.pre_l = R.lds[64 + lane];
-#if SDFR_X2_PD
 #pragma unroll
-    for (int i = 0; i < 2 * SDFR_X2_PD; ++i) {
+    for (int i = 0; i < 2; ++i) {
         R.nh[i] = R.lds[(2 * i) * 64 + lane];
         R.nl[i] = R.lds[(2 * i + 1) * 64 + lane];
     }
-#endif
 
     float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
     float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
@@ -859,9 +641,6 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
     const uint32_t pps = (npass + a.nseg - 1) / a.nseg;
     const uint32_t p_begin = seg * pps, p_end = min(npass, p_begin + pps);
     load_inputs(2 * p_begin);
-#if SDFR_X2_PRIO
-    if (R.late) __builtin_amdgcn_s_setprio(1);
-#endif
 
     for (uint32_t p = p_begin; p < p_end; ++p) {
         // a pass consumes exactly Net::kSlices half-slices (68 ngp, 132 siren):
@@ -870,7 +649,7 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
         // base across passes (x2_slot)
         static_assert(Net::kSlices % 3 == (Net::kSiren ? 0 : 2) && Net::kSlices % 4 == 0,
                       "ring slot cycle");
-        if (p != p_begin) R.slot0 = (R.slot0 + Net::kSlices) % (uint32_t)x2_slots<Net>();
+        if (p != p_begin) R.slot0 = (R.slot0 + Net::kSlices) % (uint32_t)kX2Slots;
         R.it = 0;
         f4 X[16], Y[16];
         f4 eh, el;
@@ -1047,10 +826,8 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
         }
         if (a.sdf && ray_ok && g == 0 && s_ok) a.sdf[(size_t)ray_index * G.N + s] = sdf;
     }
-#if SDFR_X2_DMA
     // the ring runs ahead across passes: no LDS-DMA may land after the workgroup ends
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     if (!ray_ok || colB) return;
     if (a.nseg > 1) {
         const size_t Rr = (size_t)G.total_tiles * kTileRays;
@@ -1133,17 +910,17 @@ __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
 // ----------------------------------------------------------------------------
 // host
 // ----------------------------------------------------------------------------
-static uint32_t g_field_split_max = 4;
-void set_field_split_max(uint32_t m) { g_field_split_max = m; }
-
-// Segments per ray: enough workgroups for every CU (>= 256), at most
-// g_field_split_max, at least one pass (two samples) in every segment, and never
-// with force_background (its last weight needs the whole ray's sum).
-uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background) {
+// Segments per ray: enough workgroups for every CU (>= 256), at most max_seg (the
+// call's max_field_segments, 0 = kFieldSplitMax), at least one pass (two samples) in
+// every segment, and never with force_background (its last weight needs the whole
+// ray's sum).
+uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background,
+                    uint32_t max_seg) {
+    if (max_seg == 0 || max_seg > kFieldSplitMax) max_seg = kFieldSplitMax;
     const uint32_t wgs = B * ((tiles_per_face + kWaves - 1) / kWaves);
     const uint32_t npass = (N + 1) / 2;
     uint32_t nseg = 1;
-    while (!force_background && wgs * nseg < 256 && 2 * nseg <= g_field_split_max) {
+    while (!force_background && wgs * nseg < 256 && 2 * nseg <= max_seg) {
         const uint32_t c = 2 * nseg, pps = (npass + c - 1) / c;
         if ((c - 1) * pps >= npass) break;            // no empty last segment
         nseg = c;
@@ -1152,7 +929,7 @@ uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_b
 }
 
 size_t field_part_bytes(uint32_t B, uint32_t tiles_per_face, uint32_t N) {
-    const uint32_t nseg = field_nseg(B, tiles_per_face, N, 0);
+    const uint32_t nseg = field_nseg(B, tiles_per_face, N, 0, kFieldSplitMax);
     return nseg > 1 ? (size_t)nseg * kPartQ * B * tiles_per_face * kTileRays * sizeof(float) : 0;
 }
 
@@ -1254,7 +1031,8 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     f.sdf = a->sdf;
     f.xyz = a->xyz;
     f.mask = a->mask;
-    f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background) : 1;
+    f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background,
+                              a->max_field_segments) : 1;
     f.part = part;
     const uint32_t blocks = g.B * ((g.tiles_per_face + kWaves - 1) / kWaves) * f.nseg;
     switch (field_variant()) {
@@ -1362,6 +1140,8 @@ static int siren_validate(const sdfr_siren_weights *w, const sdfr_ngp_render_arg
         return fail(SDFR_EUNSUPPORTED, "render_siren: only field_precision 0 (f16x3)");
     if (a->B == 0 || a->H == 0 || a->W == 0 || a->N == 0)
         return fail(SDFR_EINVAL, "render_siren: empty batch / image / sample count");
+    if (a->max_field_segments > kFieldSplitMax || a->max_field_segments == 3)
+        return fail(SDFR_EINVAL, "render_siren: max_field_segments must be 0, 1, 2 or 4");
     if (!a->cam || !a->focal || !a->near_ || !a->far_ || !a->styles || !a->pix_x ||
         !a->pix_y || !a->t_vals || !a->rgb || !a->workspace)
         return fail(SDFR_EINVAL, "render_siren: required pointer is null");

@@ -137,9 +137,10 @@ int launch_xfield_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
                       const GeomArgs &g, const float *enc, char *xws, const float *film,
                       hipStream_t st, float *part);
 // sample-segment split of the f16x3 field kernel for small batches
-uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background);
+constexpr uint32_t kFieldSplitMax = 4;   // sample segments per ray at most
+uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background,
+                    uint32_t max_seg);
 size_t field_part_bytes(uint32_t B, uint32_t tiles_per_face, uint32_t N);
-void set_field_split_max(uint32_t m);
 void fill_geom_args(const sdfr_ngp_render_args *a, float bound, GeomArgs &g);
 void record_event(void *ev, hipStream_t st);
 

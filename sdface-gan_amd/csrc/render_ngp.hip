@@ -787,6 +787,8 @@ static int validate(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a) {
         return fail(SDFR_EINVAL, "render_ngp: empty batch / image / sample count");
     if (a->field_precision != SDFR_FIELD_F16X3 && a->field_precision != SDFR_FIELD_FP32)
         return fail(SDFR_EINVAL, "render_ngp: field_precision must be 0 (f16x3) or 1 (fp32)");
+    if (a->max_field_segments > kFieldSplitMax || a->max_field_segments == 3)
+        return fail(SDFR_EINVAL, "render_ngp: max_field_segments must be 0, 1, 2 or 4");
     if (!a->cam || !a->focal || !a->near_ || !a->far_ || !a->styles || !a->pix_x ||
         !a->pix_y || !a->t_vals || !a->rgb || !a->workspace)
         return fail(SDFR_EINVAL, "render_ngp: required pointer is null");
@@ -843,8 +845,12 @@ void record_event(void *ev, hipStream_t st) {
     if (ev) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev), st);
 }
 
+#ifdef SDFR_ABLATION
 static int g_field_variant = 0;   // profiling ablations only (see ABL_*)
 int field_variant() { return g_field_variant; }
+#else
+int field_variant() { return 0; }
+#endif
 
 static void launch_field(int v, dim3 grid, hipStream_t st, const FieldArgs &f) {
     switch (v) {
@@ -896,10 +902,12 @@ static int launch_prep(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
     return check_launch("render_ngp: prep");
 }
 
+#ifdef SDFR_ABLATION
 static uint32_t g_encode_mode = [] {
     const char *e = std::getenv("SDFR_ENC_MODE");   // ablations only
     return e ? (uint32_t)std::atoi(e) : kEncDefault;
 }();
+#endif
 
 template <bool PAIR, bool A8, uint32_t LPT, uint32_t SPT>
 static void launch_encode_mode(hipStream_t st, const EncodeArgs &e) {
@@ -917,6 +925,7 @@ static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *
     e.enc = enc;
     e.pair_ok = (reinterpret_cast<uintptr_t>(w->embeddings) & 15u) == 0;
     make_level_table(16, w->log2_per_level_scale, w->base_resolution, e.lt);
+#ifdef SDFR_ABLATION
     switch (g_encode_mode) {
         case 8 | 1: launch_encode_mode<false, false, 1, 1>(st, e); break;
         case 1: launch_encode_mode<true, false, 1, 1>(st, e); break;
@@ -926,6 +935,10 @@ static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *
         case 256 | 32 | 2: launch_encode_mode<true, true, 2, 2>(st, e); break;
         default: launch_encode_mode<true, true, 1, 2>(st, e); break;   // 289
     }
+#else
+    static_assert(kEncDefault == (256 | 32 | 1), "product gather: A8, 1 level, 2 samples");
+    launch_encode_mode<true, true, 1, 2>(st, e);
+#endif
     return check_launch("render_ngp: encode");
 }
 
@@ -962,13 +975,8 @@ int sdfr_camera_extrinsics(const float *azim, const float *elev, uint32_t B, flo
     return check_launch("camera_extrinsics");
 }
 
-int sdfr_debug_set_field_split(int max_segments) {
-    if (max_segments != 1 && max_segments != 2 && max_segments != 4)
-        return fail(SDFR_EINVAL, "sdfr_debug_set_field_split: max_segments must be 1, 2 or 4");
-    set_field_split_max((uint32_t)max_segments);
-    return SDFR_OK;
-}
-
+#ifdef SDFR_ABLATION
+// profiling hooks (make ABLATION=1 builds only; process-global)
 int sdfr_debug_set_encode_mode(int mode) {
     const int ok[] = {1, 2, 9, 33, 257, 289, 290};
     bool found = false;
@@ -981,11 +989,7 @@ int sdfr_debug_set_encode_mode(int mode) {
 }
 
 int sdfr_debug_set_field_variant(int variant) {
-#ifdef SDFR_ABLATION
     const int ok[] = {0, 1, 2, 4, 8, 15, 16, 31};
-#else
-    const int ok[] = {0};   // ablated kernels are only built with `make ABLATION=1`
-#endif
     for (int v : ok)
         if (v == variant) {
             g_field_variant = variant;
@@ -994,6 +998,7 @@ int sdfr_debug_set_field_variant(int variant) {
     return fail(SDFR_EINVAL,
                 "sdfr_debug_set_field_variant: variant must be 0,1,2,4,8,15,16,31");
 }
+#endif
 
 size_t sdfr_render_ngp_workspace_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t N,
                                        uint32_t num_levels) {
@@ -1062,7 +1067,7 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     f.xyz = a->xyz;
     f.mask = a->mask;
     const uint32_t blocks = (g.total_tiles + kWaves - 1) / kWaves;
-    launch_field(g_field_variant, dim3(blocks), st, f);
+    launch_field(field_variant(), dim3(blocks), st, f);
     if ((rc = check_launch("render_ngp: field"))) return rc;
     record_event(a->stage_events[3], st);
     return SDFR_OK;

@@ -341,9 +341,13 @@ class Decoder(nn.Module):
                 inject_index=None, truncation=1, truncation_latent=None, input_is_latent=False,
                 noise=None, randomize_noise=True, mesh_path=None, prepared=None):
         if prepared is not None:         # prepare_fused() ran earlier (Generator.forward)
-            latent, noise, sty = prepared
-            return (self._fused_forward(features, latent, noise, sty),
-                    (latent if return_latents else None))
+            if self._fused_ok(features, rgbd_in, transform):
+                latent, noise_f, sty = prepared
+                return (self._fused_forward(features, latent, noise_f, sty),
+                        (latent if return_latents else None))
+            # the features turned out to need the autograd path (they require grad):
+            # drop the prep and run the module path below, so no gradient is lost
+            prepared = None
         latent, noise = self.styles_and_noise_forward(styles, noise, inject_index, truncation,
                                                       truncation_latent, input_is_latent,
                                                       randomize_noise)
@@ -756,7 +760,12 @@ class Generator(nn.Module):
         # frees, never cross streams.  Either way the device RNG is drawn in the same
         # order (decoder noise, then the renderer's sampling offsets).
         prepared, side = None, None
-        if (self.full_pipeline and cam_poses.is_cuda and not project_noise
+        # features needing grad (renderer trained, or latents requiring grad) take the
+        # decoder's autograd path: no prep then (Decoder.forward re-checks as well)
+        render_grad = (self.is_train and self.train_renderer) and (
+            any(p.requires_grad for p in self.renderer.parameters())
+            or any(s.requires_grad for s in latent))
+        if (self.full_pipeline and cam_poses.is_cuda and not project_noise and not render_grad
                 and self.decoder.fused_ready(cam_poses.device)):
             kw = dict(noise=noise, inject_index=inject_index, truncation=truncation,
                       truncation_latent=truncation_latent, input_is_latent=input_is_latent,

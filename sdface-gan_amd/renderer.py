@@ -308,6 +308,9 @@ class VolumeFeatureRenderer(nn.Module):
         # optional 4 torch.cuda.Event(enable_timing=True) recorded around the
         # fused stages (prep | hash grid | field | end), see include/sdfr.h
         self.stage_events = None
+        # upper bound on the per-ray sample segments of the fused field stage at small
+        # batches (0 = the library default 4; 1 = whole rays), include/sdfr.h
+        self.max_field_segments = 0
 
     # ---------------------------------------------------------------- reference structure
     def get_rays(self, focal, c2w):
@@ -577,6 +580,7 @@ class VolumeFeatureRenderer(nn.Module):
             raise ValueError(f"field_precision must be 'f16x3' or 'fp32', "
                              f"got {self.field_precision!r}")
         a.field_precision = _lib.FIELD_FP32 if self.field_precision == "fp32" else _lib.FIELD_F16X3
+        a.max_field_segments = int(self.max_field_segments)
         if self.stage_events is not None:
             for k, ev in enumerate(self.stage_events):
                 a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)

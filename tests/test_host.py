@@ -2,6 +2,7 @@
 import ast
 import ctypes
 import re
+import subprocess
 from pathlib import Path
 
 import numpy as np
@@ -13,9 +14,24 @@ from tests.golden import weights as W
 REPO = Path(__file__).resolve().parents[1]
 
 
-def header_symbols():
+def header_symbols(ablation=False):
+    """Functions include/sdfr.h declares: the product ones, or (ablation=True) only
+    those of its `#ifdef SDFR_ABLATION` block (profiling builds)."""
     txt = (REPO / "include" / "sdfr.h").read_text()
+    blocks = re.findall(r"#ifdef SDFR_ABLATION\n(.*?)#endif", txt, re.S)
+    if ablation:
+        txt = "\n".join(blocks)
+    else:
+        txt = re.sub(r"#ifdef SDFR_ABLATION\n.*?#endif", "", txt, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:int|size_t|const char \*)\s*(sdfr_\w+)\s*\(", txt, re.M)))
+
+
+def library_symbols(path):
+    """Global text symbols with the sdfr_ prefix that a shared library exports."""
+    out = subprocess.run(["nm", "-D", "--defined-only", str(path)], capture_output=True,
+                         text=True, check=True).stdout
+    return sorted({ln.split()[-1] for ln in out.splitlines()
+                   if ln.split()[-2:-1] == ["T"] and ln.split()[-1].startswith("sdfr_")})
 
 
 def test_library_exports_every_header_symbol(sdfr):
@@ -26,6 +42,12 @@ def test_library_exports_every_header_symbol(sdfr):
         assert hasattr(lib, s), s
     assert set(syms) == set(sdfr._lib.EXPORTS)
     assert lib.sdfr_abi_version() == sdfr._lib.ABI_VERSION
+    # the product library exports exactly the documented entry points: no profiling
+    # hooks (process-global state) outside `make ABLATION=1` builds
+    assert library_symbols(sdfr._lib.LIB_PATH) == syms
+    assert header_symbols(ablation=True) == sorted(sdfr._lib.ABLATION_EXPORTS)
+    for s in sdfr._lib.ABLATION_EXPORTS:
+        assert not hasattr(lib, s), s
 
 
 def test_argument_errors_mirror_reference(sdfr):
@@ -43,9 +65,6 @@ def test_argument_errors_mirror_reference(sdfr):
     assert rc == sdfr._lib.SDFR_EINVAL
     rc = lib.sdfr_sh_encode_forward(nul, nul, 4, 3, 6, nul, nul)
     assert rc == sdfr._lib.SDFR_EUNSUPPORTED
-    for bad in (0, 3, 4, 8, 10, 18):
-        assert lib.sdfr_debug_set_encode_mode(bad) == sdfr._lib.SDFR_EINVAL
-    assert lib.sdfr_debug_set_encode_mode(289) == sdfr._lib.SDFR_OK
     w, a = sdfr._lib.NgpWeights(), sdfr._lib.NgpRenderArgs()
     rc = lib.sdfr_render_ngp_forward(ctypes.byref(w), ctypes.byref(a), nul)
     assert rc in (sdfr._lib.SDFR_EINVAL, sdfr._lib.SDFR_EUNSUPPORTED)
@@ -65,7 +84,14 @@ def test_workspace_size(sdfr):
     assert enc + fixed + xfixed + part <= n <= enc + fixed + xfixed + part + 1280
     n32 = lib.sdfr_render_ngp_workspace_bytes(32, 64, 64, 24, 16)   # >= 256 workgroups: no split
     assert n32 <= 16 * enc + fixed + 32 * 8 * 256 * 4 + xfixed + 1280
-    assert lib.sdfr_debug_set_field_split(3) == sdfr._lib.SDFR_EINVAL
+    # the per-call sample-split bound is validated before anything is launched
+    w, a = sdfr._lib.NgpWeights(), sdfr._lib.NgpRenderArgs()
+    w.num_levels, a.B, a.H, a.W, a.N = 16, 1, 8, 8, 24
+    for bad in (3, 5, 8):
+        a.max_field_segments = bad
+        assert lib.sdfr_render_ngp_forward(ctypes.byref(w), ctypes.byref(a), None) == \
+            sdfr._lib.SDFR_EINVAL
+        assert b"max_field_segments" in lib.sdfr_last_error()
 
 
 def test_conv_split_k_workspace(sdfr):
