@@ -41,10 +41,7 @@ typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 constexpr int kCT = 128;        // output channels per workgroup
 constexpr int kPT = 256;        // output pixels per workgroup
 constexpr int kStepF4 = 1024;   // f4 of weight fragments per K-step (16 KB)
-#ifndef CONV_STAGES
-#define CONV_STAGES 3
-#endif
-constexpr int kStages = CONV_STAGES;   // LDS-DMA ring depth (kStages - 1 K-steps in flight)
+constexpr int kStages = 3;   // LDS-DMA ring depth (kStages - 1 K-steps in flight)
 
 __device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a),
@@ -113,25 +110,6 @@ __global__ void __launch_bounds__(256) conv_pack_kernel(const float *__restrict_
 // ----------------------------------------------------------------------------
 // implicit GEMM
 // ----------------------------------------------------------------------------
-#ifndef CONV_REGDB
-#define CONV_REGDB 1      // fragments of step ks+1 read into a second register set mid-step
-#endif
-static_assert(CONV_REGDB || kStages == 3, "the single-register-set ring assumes 3 stages");
-#ifndef CONV_XCD
-#define CONV_XCD 1
-#endif
-#ifndef CONV_ABL
-#define CONV_ABL 0        // timing ablations (wrong results), see the #if CONV_ABL sites
-#endif
-#ifndef CONV_HALO
-#define CONV_HALO 1       // regular convs with the fused epilogue on conv_h_kernel
-#endif
-#ifndef CONV_HABL
-#define CONV_HABL 0       // conv_h_kernel timing ablations (wrong results)
-#endif
-#ifndef CONV_HPERSIST
-#define CONV_HPERSIST 0   // conv_h_kernel: one round of workgroups walking their tiles
-#endif
 
 // One output-pixel class: the plain convolution has one (every pixel, 9 taps); the
 // stride-2 transposed one has four parity classes (4, 2, 2 and 1 taps) that share
@@ -339,7 +317,6 @@ __device__ __forceinline__ bool slot_tile(const ConvArgs &a, uint32_t slot, uint
         if (slot >= a.cls[i].tile0) ci = i;
     const ConvClass &cl = a.cls[ci];
     const uint32_t loc = slot - cl.tile0;
-#if CONV_XCD
     // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs; give
     // each XCD one contiguous run of the class's tiles, with the Cout block fastest,
     // so the tiles that re-read an activation row (the other Cout blocks of the same
@@ -347,9 +324,6 @@ __device__ __forceinline__ bool slot_tile(const ConvArgs &a, uint32_t slot, uint
     // about the same time and hit its L2.  (The K splits of a slot, blockIdx.y, sit
     // on the same XCD: the grid's x extent is a multiple of 8.)
     tile = (loc & 7u) * ((cl.ntiles + 7) >> 3) + (loc >> 3);
-#else
-    tile = loc;
-#endif
     return tile < cl.ntiles;
 }
 
@@ -437,17 +411,7 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const bool ok = (tmask[k] >> tl) & 1u;
-#if CONV_ABL == 1   // ablation: activations from a tiny L2-resident window
-            const uint32_t off = ((lane & 7u) * a.Cin * 4u + c * 128u + loff) + 0 * (ok ? 1u : 0u);
-#else
-            uint32_t off = ok ? xoff[k] + toff : 0x7FFFFFF0u;   // past num_records: zero fill
-#if CONV_ABL == 7      // ablation: same pattern folded into a 2 MB (L2-resident) window
-            off &= 0x1FFFFFu;
-#elif CONV_ABL == 8    // ... into a 64 MB window (Infinity-Cache resident)
-            off &= 0x3FFFFFFu;
-#endif
-#endif
-            r.offs[k] = off;
+            r.offs[k] = ok ? xoff[k] + toff : 0x7FFFFFF0u;   // past num_records: zero fill
         }
         return r;
     };
@@ -500,7 +464,6 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
         }
     };
 
-#if CONV_REGDB
     // Ring: step ks lives in stage ks % 3 and is read into registers half a step
     // early.  Half-way through step ks (rows 0-1 done) the wave waits for its pieces
     // of step ks+1 (ks+2's 6 may stay in flight), drains its LDS reads and meets the
@@ -518,20 +481,12 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(pr.offs[k]));
         mfma_rows(R, 0, 2);
-#if CONV_ABL == 4      // ablation: never wait for the DMA
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
         if (more) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#endif
-#if CONV_ABL != 5      // 5: ablation without the barrier
         __builtin_amdgcn_s_barrier();
-#endif
         const uint32_t st = st_ks, st1 = st_ks == kStages - 1 ? 0u : st_ks + 1;
         st_ks = st1;                                   // ks % kStages, carried
-#if CONV_ABL != 6      // 6: ablation without in-loop staging
         if (fire) fire_step(pr, st);
-#endif
         if (ks + 1 < nk) read_frags(Rn, st1);
         mfma_rows(R, 2, 2);
     };
@@ -550,41 +505,6 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
         step(ks + 1, R1, R0);
     }
     if (ks < nk) step(ks, R0, R1);
-#if CONV_ABL == 4
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-#else
-    // Ring: step ks in stage ks % 3; steps ks+1, ks+2 in flight while ks computes.
-    // Stage (ks+2) % 3 last held step ks-1, whose reads every wave completed before
-    // the barrier that closed step ks-1.
-    issue_step(0, 0);
-    if (nk > 1) issue_step(1, 1);
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    uint32_t cur = 0;
-    for (uint32_t ks = 0; ks < nk; ++ks) {
-        const bool more = ks + 2 < nk;
-#if CONV_ABL == 2 || CONV_ABL == 3   // ablation: no staging in the loop (stale LDS)
-        (void)more;
-#else
-        if (more) issue_step(ks + 2, cur == 0 ? 2u : cur - 1);
-#endif
-        f4 R[16];
-        read_frags(R, cur);
-        mfma_rows(R, 0, 4);
-        // step ks+1 must have landed (only ks+2's 6 pieces may stay in flight), and
-        // this wave's fragment reads of stage `cur` must be done, before the barrier
-#if CONV_ABL == 3   // ablation: no staging, no barrier
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-        if (more) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-#endif
-        cur = cur == 2 ? 0 : cur + 1;
-    }
-#endif
 
     if (a.ksplit > 1) {      // partial sums; conv_splitk_kernel adds them and runs the epilogue
         f4 *pp = a.partial + ((size_t)split * a.grid + blockIdx.x) * 16 * 512 + tid;
@@ -651,7 +571,7 @@ __global__ void __launch_bounds__(512, 1) conv_splitk_kernel(const ConvArgs a) {
 // A fragment address is a per-lane base (one of 3 column shifts x hi/lo, plus the
 // buffer) and a compile-time offset (row and column of the tap and n-tile), so the
 // unrolled tap loop reads fragments without address VALU.  The weight ring and the
-// mid-step barrier / next-step fragment schedule are conv_x_kernel's (CONV_REGDB);
+// mid-step barrier / next-step fragment schedule are conv_x_kernel's;
 // the nine taps of a channel group are unrolled (stage = tap % 3), two groups per
 // loop iteration so the register sets alternate.
 // ----------------------------------------------------------------------------
@@ -775,14 +695,12 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         if (prev_w && prev_h) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
         else if (prev_w) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#if CONV_HABL != 2     // 2: ablation without the per-step barrier
         __builtin_amdgcn_s_barrier();
-#endif
-        if (CONV_HABL != 3 && s + 3 < nk) {   // 3: ablation without in-loop staging
+        if (s + 3 < nk) {
             constexpr uint32_t T3 = (T + 3) % 9;
             fire_w(c + (T + 3) / 9, T3, T % 3);
         }
-        if constexpr (T <= 5 && CONV_HABL != 3) {
+        if constexpr (T <= 5) {
             if (c + 1 < nC) fire_h(1 - P, T);
         }
         if (s + 1 < nk) {
@@ -803,27 +721,18 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         fire_w(0, 1, 1);
         fire_w(0, 2, 2);
     };
-    // CONV_HPERSIST: the grid covers at most one round of CUs and each workgroup walks
-    // its slots blockIdx.x + k gridDim.x (same XCD); the next tile's prologue DMAs are
-    // issued before this tile's epilogue, so they land while it computes and stores
-    // one class (slot_tile's XCD-aware order without the class search)
+    // XCD-aware tile order (slot_tile's, one class)
     const uint32_t ntiles = a.cls[0].ntiles, per_xcd = (ntiles + 7) >> 3;
-    auto slot_ok = [&](uint32_t sl, uint32_t &t) {
-        t = __builtin_amdgcn_readfirstlane((sl & 7u) * per_xcd + (sl >> 3));   // uniform (SGPR)
-        return t < ntiles;
-    };
-    uint32_t slot = blockIdx.x, tile;
-    while (slot < a.grid && !slot_ok(slot, tile)) slot += gridDim.x;
-    if (slot >= a.grid) return;
+    const uint32_t slot = blockIdx.x;
+    const uint32_t tile = __builtin_amdgcn_readfirstlane((slot & 7u) * per_xcd + (slot >> 3));
+    if (tile >= ntiles) return;    // padding slot (whole workgroup)
     setup(tile);
     prologue();
-    for (;;) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    // all but step 2's weights landed (younger epilogue stores of the previous tile
-    // may be waited for too)
+    // everything but step 2's weights has landed
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     f4 R0[16], R1[16];
@@ -864,37 +773,7 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
     }
     // the epilogue's LDS reduction buffer is its own; no DMA is left in flight
-#if CONV_HABL == 1     // ablation: no epilogue (one store keeps the accumulators live)
-    {
-        f4 t = f4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) t += acc[i][j];
-        if (t.x == 1234.5f) a.e.rgbp[tid] = t.y;
-    }
-    return;
-#endif
-    const uint32_t cb_cur = cb, pix0_cur = pix0;
-    bool more = false;
-    if (CONV_HPERSIST) {
-        slot += gridDim.x;
-        while (slot < a.grid && !slot_ok(slot, tile)) slot += gridDim.x;
-        more = slot < a.grid;
-        if (more) {
-            setup(tile);
-            prologue();
-        }
-    }
-    {
-        // the epilogue's kernel arguments are loaded here, not hoisted out of the tile
-        // loop (SGPRs live across the K loop spilled)
-        const ConvArgs *ap = &a;
-        if (CONV_HPERSIST) asm volatile("" : "+s"(ap));
-        conv_epilogue<true>(*ap, acc, lane, wm, wn, cb_cur, pix0_cur, a.B * H * W, H, W, 0, 0, W);
-    }
-    if (!more) return;
-    }
+    conv_epilogue<true>(a, acc, lane, wm, wn, cb, pix0, a.B * H * W, H, W, 0, 0, W);
 }
 
 
@@ -1025,9 +904,8 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
         a.ksplit = ks;
         a.partial = reinterpret_cast<f4 *>(ws);
     }
-    if (CONV_HALO && act && !transposed && a.ksplit == 1 && H % 16 == 0 && W % 16 == 0)
-        hipLaunchKernelGGL(conv_h_kernel, dim3(CONV_HPERSIST && grid > 256 ? 256 : grid), dim3(512), 0,
-                           st, a);
+    if (act && !transposed && a.ksplit == 1 && H % 16 == 0 && W % 16 == 0)
+        hipLaunchKernelGGL(conv_h_kernel, dim3(grid), dim3(512), 0, st, a);
     else if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     if (a.ksplit > 1) {
