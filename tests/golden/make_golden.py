@@ -333,6 +333,33 @@ def case_mesh(sdf_model, sdf_utils):
     print("mesh128.npz", sdf.shape, aligned.shape)
 
 
+def case_mesh256(sdf_model, sdf_utils):
+    """BASELINE configs[3]: sdf_mesh.py's surface query at 256^2 rays x 256 samples
+    (sdf_mesh.py:243-252 with 256 for its 128; the options of :211-214: static
+    viewdirs, force_background, perturb 0) on every 16th pixel row and column.  The
+    reference's own get_rays runs at the full 256^2 resolution; its rays are then
+    subsampled before render_rays, which treats every ray independently -- so the
+    stored 16 x 16 x 256 SDF values are exactly those of the full 256^3 volume."""
+    g, opt = _generator(sdf_model, sdf_utils, res=256, n_samples=256, full_pipeline=False,
+                        return_sdf=True, return_xyz=True, static_viewdirs=True,
+                        force_background=True, perturb=0)
+    r = g.renderer
+    full_get_rays = r.get_rays
+    sub = slice(0, None, 16)
+    r.get_rays = lambda focal, c2w: tuple(t[:, sub, sub] for t in full_get_rays(focal, c2w))
+    ext, focal, near, far, vp = _cams(sdf_utils, 1, 256, 61)
+    torch.manual_seed(62)
+    z = torch.randn(1, 256)
+    with torch.no_grad():
+        _, thumb, xyz, sdf, mask = g([z], ext, focal, near, far, return_sdf=True,
+                                     return_xyz=True)
+    np.savez_compressed(OUT / "mesh256_sub.npz", z=_t2n(z), ext=_t2n(ext), focal=_t2n(focal),
+                        near=_t2n(near), far=_t2n(far), thumb_sub=_t2n(thumb),
+                        xyz_sub=_t2n(xyz), mask_sub=_t2n(mask), sdf_sub=_t2n(sdf),
+                        stride=np.int64(16), res=np.int64(256), n_samples=np.int64(256))
+    print("mesh256_sub.npz", tuple(sdf.shape))
+
+
 def case_siren(sdf_model, sdf_utils):
     """rendering.type == 'sdf' (SirenGenerator, 100 % reference code on CPU)."""
     case_render(sdf_model, sdf_utils, "render_siren_small", B=2, res=8, n_samples=24,
@@ -390,6 +417,11 @@ def case_eikonal(sdf_model, sdf_utils):
     loss.backward()
     net = g.renderer.network
     n_dense = int(net.encoder.offsets[2])                  # levels 0-1: dense rows
+    # the hashed levels (5-15, grid.py:117-128): every 4th row that received gradient
+    gt = net.encoder.embeddings.grad
+    first_hashed = int(net.encoder.offsets[5])
+    hit = torch.nonzero(gt[first_hashed:].abs().sum(1) > 0).flatten() + first_hashed
+    hashed_rows = hit[::4].numpy().astype(np.int64)
     np.savez_compressed(
         OUT / "eikonal.npz", z=_t2n(z), ext=_t2n(ext), focal=_t2n(focal), near=_t2n(near),
         far=_t2n(far), t_rand=_t2n(rr.draws[0]), thumb=_t2n(thumb), sdf=_t2n(sdf),
@@ -399,6 +431,7 @@ def case_eikonal(sdf_model, sdf_utils):
         grad_input_w=_t2n(net.input_linear.weight.grad),
         grad_beta=_t2n(g.renderer.sigmoid_beta.grad),
         grad_table_dense=_t2n(net.encoder.embeddings.grad[:n_dense]),
+        grad_table_hashed_rows=hashed_rows, grad_table_hashed=_t2n(gt[hashed_rows]),
         res=np.int64(res), n_samples=np.int64(N), table_amp=np.float64(0.05))
     print("eikonal.npz", tuple(eik.shape), "eik requires_grad:", eik.requires_grad)
 
@@ -513,6 +546,7 @@ def main():
                 intermediates=False, seed=41, return_sdf=True, return_xyz=True)
     case_generator(sdf_model, sdf_utils)
     case_mesh(sdf_model, sdf_utils)
+    case_mesh256(sdf_model, sdf_utils)
     case_siren(sdf_model, sdf_utils)
     case_table_scales(sdf_model, sdf_utils)
     case_eikonal(sdf_model, sdf_utils)

@@ -54,6 +54,29 @@ def test_mesh128_vs_reference(sdfr, golden_dir, prec):
     _cmp("aligned", aligned[:, ::8, ::8].cpu(), g["aligned_sub"])
 
 
+def test_mesh256_vs_reference_subsampled(sdfr, golden_dir):
+    """configs[3] at its full size: 256^2 rays x 256 samples in one fused call with
+    sdf_mesh.py's options (static viewdirs, force_background, perturb 0), compared
+    on every 16th pixel row and column -- all 256 samples of those rays -- with the
+    reference run on the same inputs (tests/golden/mesh256_sub.npz)."""
+    g = np.load(golden_dir / "mesh256_sub.npz")
+    gen = surface_generator(sdfr, 256, 256, "f16x3")
+    gen.renderer.static_viewdirs = True
+    gen.renderer.force_background = True
+    gen.renderer.perturb = 0
+    t = lambda k: torch.from_numpy(g[k]).to(DEV)  # noqa: E731
+    st = int(g["stride"])
+    with torch.no_grad():
+        rgb, thumb, xyz, sdf, mask = gen([t("z")], t("ext"), t("focal"), t("near"), t("far"),
+                                         return_sdf=True, return_xyz=True)
+    torch.cuda.synchronize()
+    assert sdf.shape == (1, 256, 256, 256, 1)
+    _cmp("sdf", sdf[:, ::st, ::st].cpu(), g["sdf_sub"])
+    _cmp("thumb", thumb[:, :, ::st, ::st].cpu(), g["thumb_sub"])
+    _cmp("xyz", xyz[:, :, ::st, ::st].cpu(), g["xyz_sub"])
+    _cmp("mask", mask[:, :, ::st, ::st].cpu(), g["mask_sub"])
+
+
 def test_sdf_volume_256_properties(sdfr):
     """The 256^3 configuration (16.8 M samples in one call): shape, finiteness,
     and batch-independence of a 32-row crop against a separate 32-row render is

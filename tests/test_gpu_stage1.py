@@ -90,6 +90,11 @@ def test_eikonal_term_vs_reference(sdfr, golden_dir):
     n_dense = g["grad_table_dense"].shape[0]
     _rel("eikonal_grad_table_dense", net.encoder.embeddings.grad[:n_dense].cpu(),
          g["grad_table_dense"], 1e-4)
+    # the hashed levels 5-15 (every 4th row that the reference's backward reached):
+    # the binned HIP table gradient vs the reference's atomics, order-dependent sums
+    rows = torch.from_numpy(g["grad_table_hashed_rows"]).to(DEV)
+    _rel("eikonal_grad_table_hashed", net.encoder.embeddings.grad[rows].cpu(),
+         g["grad_table_hashed"], 1e-4)
 
 
 def test_sphere_init_pass_vs_reference(sdfr, golden_dir):

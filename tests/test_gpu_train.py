@@ -137,3 +137,101 @@ def test_bench_multi_rank_timing_world2():
     assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["scaling"] == "weak"
     assert rec["value"] > 0
     assert abs(rec["value"] - 2 * 4 * 3 / (rec["ms_per_step"] * 3 / 1e3)) < 1e-6 * rec["value"]
+
+
+# ------------------------------------------------------------------ ngp DDP gradients
+# Stage 1 on the ngp network (the 12.66 M-row hash table: the dominant all-reduce of
+# SURVEY.md §5), world 2 over gloo with both ranks on cuda:0: after one d_backward and
+# one g_backward with perturb 0, every gradient equals a single process's on the
+# concatenated batch (discriminator: equal; generator: x 1/2, per-chunk losses summed
+# over 2x the chunks) -- training_utils.py:346-440, sdf_utils.py:344-379.
+def _ngp_stage1_opt(sdfr):
+    from tests.test_train_renderer import stage1_opt
+    opt = stage1_opt(sdfr, ngp=True, res=16, samples=8, batch=2, chunk=1)
+    opt.rendering.perturb = 0
+    return opt
+
+
+def _to_dev(x):
+    if isinstance(x, torch.Tensor):
+        return x.to(DEV)
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_dev(v) for v in x)
+    return x
+
+
+def _ngp_grads(tr, noise, cams, real, chunks):
+    tr.d_backward(_to_dev(noise), _to_dev(cams), _to_dev(real))
+    d = {n: p.grad.detach().cpu() for n, p in tr.d_module.named_parameters()}
+    tr.g_backward(iter(_to_dev(chunks)), len(chunks))
+    g = {n: p.grad.detach().cpu() for n, p in tr.g_module.named_parameters()
+         if p.grad is not None}
+    return d, g
+
+
+def _ngp_grad_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, str(REPO))
+    from sdfr_loader import load
+    sdfr = load()
+    from sdface_gan_amd.training import RendererTrainer
+    from tests.test_train_renderer import _stage1_inputs
+    opt = _ngp_stage1_opt(sdfr)
+    tr = RendererTrainer(opt, DEV, seed=5)
+    d, g = _ngp_grads(tr, *_stage1_inputs(sdfr, opt, rank))
+    torch.save({"d": d, "g": g}, os.path.join(out_dir, f"ngp_grad{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ngp_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path):
+    from sdface_gan_amd.training import RendererTrainer
+    from tests.test_train_renderer import _stage1_inputs
+    mp.spawn(_ngp_grad_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    opt = _ngp_stage1_opt(sdfr)
+    ins = [_stage1_inputs(sdfr, opt, r) for r in (0, 1)]
+    noise = [torch.cat([ins[0][0][0], ins[1][0][0]])]
+    cams = tuple(torch.cat([a, b]) for a, b in zip(ins[0][1], ins[1][1]))
+    real = torch.cat([ins[0][2], ins[1][2]])
+    chunks = ins[0][3] + ins[1][3]
+    opt.training.batch *= 2
+    tr = RendererTrainer(opt, DEV, seed=5)
+    d, g = _ngp_grads(tr, noise, cams, real, chunks)
+    table = "renderer.network.encoder.embeddings"
+    assert table in g and float(g[table].abs().max()) > 0
+    for rank in (0, 1):
+        r = torch.load(tmp_path / f"ngp_grad{rank}.pt", weights_only=True)
+        for what, got, ref, scale in (("discriminator", r["d"], d, 1.0),
+                                      ("generator", r["g"], g, 0.5)):
+            assert set(got) == set(ref), what
+            for k, v in got.items():
+                want = ref[k] * scale
+                # fp32 sums in a different order (atomics / binned table gradient,
+                # the all-reduce): relative to the tensor's largest entry
+                tol = 2e-5 * max(1e-6, float(want.abs().max()))
+                assert torch.allclose(v, want, rtol=2e-4, atol=tol), \
+                    f"{what} {k}: max |diff| {float((v - want).abs().max()):.3e}"
+        # the hashed levels (5-15) carry most of the table's gradient rows
+        off = int(tr.g_module.renderer.network.encoder.offsets[5])
+        hashed = r["g"][table][off:]
+        assert int((hashed != 0).any(1).sum()) > 1000
+
+
+def test_renderer_grads_survive_frozen_decoder(sdfr):
+    """Grad enabled, decoder frozen, renderer trainable: the decoder takes
+    its autograd path (not the fused inference path) so the renderer gets gradients."""
+    opt = sdfr.vol_render_opt(train_renderer=True)
+    torch.manual_seed(0)
+    g = sdfr.Generator(opt.model, opt.rendering).to(DEV)
+    g.is_train, g.train_renderer = True, True
+    for p in g.decoder.parameters():
+        p.requires_grad_(False)
+    cam, focal, near, far, _ = sdfr.generate_camera_params(64, DEV, batch=1)
+    z = torch.randn(1, 256, device=DEV)
+    rgb, thumb = g([z], cam, focal, near, far)
+    assert rgb.requires_grad
+    rgb.mean().backward()
+    w = g.renderer.network.views_linears.weight
+    assert w.grad is not None and float(w.grad.abs().max()) > 0
+    assert g.renderer.network.encoder.embeddings.grad is not None
