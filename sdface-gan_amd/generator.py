@@ -701,8 +701,11 @@ class Generator(nn.Module):
                                               out_im_res=model_opt.renderer_spatial_output_dim)
         if self.full_pipeline:
             self.decoder = Decoder(model_opt, blur_kernel=blur_kernel)
-        # fused inference: decoder style prep on a side stream beside the renderer
-        self.overlap_decoder_prep = True
+        # fused inference: decoder style prep on a side stream beside the renderer.
+        # Off by default: measured in one process (scripts/overlap_ab.py,
+        # profiles/round3_overlap_ab.json) it saves 0.04 ms of 11.4 per 32 faces, within
+        # noise, and slows the hash-grid gather beside it (0.774 -> 0.801 ms)
+        self.overlap_decoder_prep = False
         self._dec_key = None
 
     def _decoder_weights_unchanged(self):

@@ -160,6 +160,20 @@ def _to_dev(x):
     return x
 
 
+def _chunk_seeded_smoothness():
+    """The smoothness term draws its voxel block from the CPU RNG (smoothLoss.py:5-27):
+    seed it from the chunk's own latents so that a rank and the single process draw
+    the same block for the same chunk."""
+    from sdface_gan_amd import training
+    orig = training.smoothness
+
+    def smoothness(generator, box, styles, device, *a, **k):
+        torch.manual_seed(int(abs(float(styles[0].flatten()[0])) * 1e6) % (2 ** 31))
+        return orig(generator, box, styles, device, *a, **k)
+    training.smoothness = smoothness
+    return orig
+
+
 def _ngp_grads(tr, noise, cams, real, chunks):
     tr.d_backward(_to_dev(noise), _to_dev(cams), _to_dev(real))
     d = {n: p.grad.detach().cpu() for n, p in tr.d_module.named_parameters()}
@@ -180,6 +194,7 @@ def _ngp_grad_worker(rank, world, port, out_dir):
     from tests.test_train_renderer import _stage1_inputs
     opt = _ngp_stage1_opt(sdfr)
     tr = RendererTrainer(opt, DEV, seed=5)
+    _chunk_seeded_smoothness()
     d, g = _ngp_grads(tr, *_stage1_inputs(sdfr, opt, rank))
     torch.save({"d": d, "g": g}, os.path.join(out_dir, f"ngp_grad{rank}.pt"))
     dist.destroy_process_group()
@@ -197,7 +212,12 @@ def test_ngp_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path):
     chunks = ins[0][3] + ins[1][3]
     opt.training.batch *= 2
     tr = RendererTrainer(opt, DEV, seed=5)
-    d, g = _ngp_grads(tr, noise, cams, real, chunks)
+    from sdface_gan_amd import training
+    orig = _chunk_seeded_smoothness()
+    try:
+        d, g = _ngp_grads(tr, noise, cams, real, chunks)
+    finally:
+        training.smoothness = orig
     table = "renderer.network.encoder.embeddings"
     assert table in g and float(g[table].abs().max()) > 0
     for rank in (0, 1):
