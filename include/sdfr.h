@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 6
+#define SDFR_ABI_VERSION 7
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -265,6 +265,32 @@ int sdfr_debug_sin_rev_probe(const float *u, float *out, uint32_t n, void *strea
 int sdfr_camera_extrinsics(const float *azim, const float *elev, uint32_t B, float dist_radius,
                            float fov_ang, float half_res, float *ext, float *focal, float *near_,
                            float *far_, float *viewpoint, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Renderer MLP linear layers for training (no reference native op: they replace
+ * the rocBLAS fp32 GEMMs of F.linear in FiLMSiren / LinearLayer, sdf_model.py:23-69,
+ * and of their autograd backward, on the op-by-op path stage-1 training takes,
+ * training_utils.py:396-451).  Split-fp16 MFMA, fp32 accumulation, fp32-level
+ * accuracy (rows / columns scaled by powers of two so no fp16 lo part goes
+ * subnormal).  Row-major fp32 tensors, 16-B aligned rows.
+ *
+ * sdfr_linear_pack: B [N,K] = w (transposed = 0; w is [N,K]) or w^T (transposed = 1;
+ *   w is [K,N]) -> sdfr_linear_pack_bytes(N, K) bytes of split fragments + row scales.
+ * sdfr_linear_f16x3: out [M,N] = x [M,K] . B^T (+ bias [N], NULL = none).  Forward
+ *   (B = W [N,K]) and input gradient (B = W^T).  Shapes: (N, K) = (256, K <= 32 |
+ *   <= 256 | <= 288) or (N <= 32 | <= 256 | <= 272, K <= 256), N and K multiples of 4.
+ * sdfr_linear_wgrad_f16x3: gw [N,K] = dy[M,N]^T . x[M,K] (weight gradient), N = 256,
+ *   K <= 288; ws >= sdfr_linear_wgrad_ws_bytes(M, N, K).  The sum over M is split
+ *   over workgroups and their partials added in a fixed order (deterministic).
+ * ------------------------------------------------------------------------- */
+size_t sdfr_linear_pack_bytes(uint32_t N, uint32_t K);
+int sdfr_linear_pack(const float *w, uint32_t N, uint32_t K, int transposed, void *packed,
+                     void *stream);
+int sdfr_linear_f16x3(float *out, const float *x, const void *packed, const float *bias,
+                      uint32_t M, uint32_t N, uint32_t K, void *stream);
+size_t sdfr_linear_wgrad_ws_bytes(uint32_t M, uint32_t N, uint32_t K);
+int sdfr_linear_wgrad_f16x3(float *gw, const float *dy, const float *x, uint32_t M, uint32_t N,
+                            uint32_t K, void *ws, size_t ws_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * StyleGAN2 decoder ops (im2scene/sdf/models/sdf_op.py).

@@ -23,7 +23,7 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 6
+ABI_VERSION = 7
 FIELD_F16X3 = 0
 FIELD_FP32 = 1
 
@@ -46,6 +46,8 @@ EXPORTS = (
     "sdfr_conv3x3_f16x3_ws", "sdfr_conv_ws_bytes",
     "sdfr_conv3x3_f16x3_act", "sdfr_conv_act_ws_bytes", "sdfr_rgb_finish",
     "sdfr_mc_workspace_bytes", "sdfr_mc_count", "sdfr_mc_emit",
+    "sdfr_linear_pack_bytes", "sdfr_linear_pack", "sdfr_linear_f16x3",
+    "sdfr_linear_wgrad_ws_bytes", "sdfr_linear_wgrad_f16x3",
 )
 
 
@@ -202,6 +204,14 @@ def lib():
                                ctypes.c_size_t, _vp, _vp, _vp]
     L.sdfr_rgb_finish.argtypes = [_vp, _vp, _u32, _vp, _vp, ctypes.POINTER(_f32), _u32, _u32,
                                   _u32, _vp]
+    L.sdfr_linear_pack_bytes.argtypes = [_u32, _u32]
+    L.sdfr_linear_pack_bytes.restype = ctypes.c_size_t
+    L.sdfr_linear_pack.argtypes = [_vp, _u32, _u32, _int, _vp, _vp]
+    L.sdfr_linear_f16x3.argtypes = [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp]
+    L.sdfr_linear_wgrad_ws_bytes.argtypes = [_u32, _u32, _u32]
+    L.sdfr_linear_wgrad_ws_bytes.restype = ctypes.c_size_t
+    L.sdfr_linear_wgrad_f16x3.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _vp, ctypes.c_size_t,
+                                          _vp]
     v = L.sdfr_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"libsdfr ABI {v} != expected {ABI_VERSION}; rebuild the library")

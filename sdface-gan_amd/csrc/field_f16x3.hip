@@ -37,11 +37,10 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "f16x3.h"
 #include "render_ngp.h"
 
 namespace sdfr {
-
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 t_out][hi,lo][64 lanes] x 16 B
 // ----------------------------------------------------------------------------
@@ -94,37 +93,8 @@ __device__ __forceinline__ int xperm_k(int l, uint32_t q, uint32_t g, uint32_t j
     return (int)(16 * (2 * q + (j >> 2)) + 4 * g + (j & 3));
 }
 
-__device__ __forceinline__ h8 as_h8(f4 v) { return __builtin_bit_cast(h8, v); }
 __device__ __forceinline__ void xpin(f4 &x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void xpin(float &x) { asm volatile("" : "+v"(x)); }
-__device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(a), as_h8(b), c, 0, 0, 0);
-}
-
-// 8 fp32 -> (hi, lo) fp16x8, round-to-nearest both.  hi: v_cvt_pk_f16_f32 per
-// pair.  x - hi is exact in fp32 (|x - hi| <= half an fp16 ulp of x), so
-// lo = RN16(x - hi) is ONE v_fma_mix{lo,hi}_f16 per value: fma(hi, -1, x) with the
-// packed f16 hi as a mixed-precision source, bit-identical to cvt(x - cvt(hi)) and
-// half its VALU (the compiler canonicalises a written-out fma(-hi, 1, x) back to
-// the sub, hence the asm).
-__device__ __forceinline__ void split8(const float (&v)[8], f4 &hi, f4 &lo) {
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    uint32_t hp[4], lp[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        h2 H;
-        H[0] = (_Float16)v[2 * j];
-        H[1] = (_Float16)v[2 * j + 1];
-        hp[j] = __builtin_bit_cast(uint32_t, H);
-        uint32_t l;
-        asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hp[j]), "v"(v[2 * j]));
-        asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-            : "+v"(l) : "v"(hp[j]), "v"(v[2 * j + 1]));
-        lp[j] = l;
-    }
-    hi = __builtin_bit_cast(f4, hp);
-    lo = __builtin_bit_cast(f4, lp);
-}
 
 // ----------------------------------------------------------------------------
 // prep 1: per-row power-of-two scales and scaled biases (one wave per row)

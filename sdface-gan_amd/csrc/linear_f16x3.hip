@@ -1,0 +1,494 @@
+// linear_f16x3.hip -- the renderer MLP's linear layers for TRAINING (stage 1,
+// training_utils.py:396-451): when the renderer needs gradients the reference runs
+// NGPSIRENGenerator / SirenGenerator op by op (sdf_model.py:1566-1592, 44-69, 23-41),
+// i.e. F.linear over S = chunk x 64^2 x 24 = 196,608 samples at a time, and its
+// backward.  Those three GEMM shapes run here on split-fp16 MFMA at fp32-level
+// accuracy (f16x3.h), instead of rocBLAS's fp32 GEMMs:
+//
+//   sdfr_linear_f16x3        out[M,N] = x[M,K] . B[N,K]^T (+ bias[N])
+//                            forward (B = W) and input gradient (B = W^T, no bias)
+//   sdfr_linear_wgrad_f16x3  gw[N,K] = sum_m dy[m,n] x[m,k]   (weight gradient)
+//
+// Forward / input gradient: a workgroup is 8 waves over 128 rows of x (16 per wave:
+// MFMA N = 16 columns = rows m of x); a wave holds its 16 rows' K values in
+// registers, scales each row by a power of two (max |x_m| into [0.5, 1): the fp16
+// lo parts stay normal at any magnitude, activations and gradients alike) and splits
+// them per k-step; the B fragments (pre-split, row-scaled by su[n], packed in MFMA
+// A-fragment order by sdfr_linear_pack) stream through a two-slot LDS ring shared by
+// the 8 waves.  Outputs accumulate in fp32 and are unscaled exactly.
+//
+// Weight gradient: the sum over m is split over workgroups (a contiguous range of
+// rows each), each accumulating an [N,K] partial in fp32; a second kernel adds the
+// partials in a fixed order (deterministic).  Every column of dy and of x is scaled
+// by a power of two from its maximum over all M (column-max kernel), the scales are
+// undone exactly on the partials.  Per m-step of 32 rows both operands are staged
+// transposed into LDS as split-fp16 MFMA fragments.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "f16x3.h"
+#include "sdfr_common.h"
+
+namespace sdfr {
+namespace {
+
+constexpr uint32_t kLinWaves = 8;
+constexpr uint32_t kLinThreads = kLinWaves * 64;
+constexpr uint32_t kLinRows = kLinWaves * 16;          // rows of x per workgroup
+constexpr uint32_t kTileF4 = 128;                      // one 16-row tile: [hi,lo][64 lanes]
+
+__host__ __device__ constexpr uint32_t ceil_div(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// power of two s with max |.| * s in [0.5, 1) (1 for zero / non-finite maxima)
+__device__ __forceinline__ float pow2_scale(float m) {
+    if (!(m > 0.0f && m < 3.0e38f)) return 1.0f;
+    int ex = __builtin_amdgcn_frexp_expf(m);
+    ex = ex < -100 ? -100 : (ex > 100 ? 100 : ex);
+    return __builtin_ldexpf(1.0f, -ex);
+}
+
+// ----------------------------------------------------------------------------
+// packing: B [N,K] (or W [K,N] read transposed) -> su [N] and fragments
+// [ks][nt][hi,lo][lane], lane (r = lane & 15, g = lane >> 4) holding
+// B[16 nt + r][32 ks + 8 g + j] * su, j = 0..7 (zero past N / K)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ float bval(const float *w, uint32_t N, uint32_t K, int tr, uint32_t n,
+                                      uint32_t k) {
+    if (n >= N || k >= K) return 0.0f;
+    return tr ? w[(size_t)k * N + n] : w[(size_t)n * K + k];
+}
+
+__global__ void __launch_bounds__(256) lin_scale_kernel(const float *__restrict__ w, uint32_t N,
+                                                        uint32_t K, int tr, float *__restrict__ su) {
+    const uint32_t n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    float m = 0.0f;
+    if (n < N)
+        for (uint32_t k = lane; k < K; k += 64) m = fmaxf(m, fabsf(bval(w, N, K, tr, n, k)));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0 && n < N) su[n] = pow2_scale(m);
+}
+
+__global__ void __launch_bounds__(256) lin_pack_kernel(const float *__restrict__ w, uint32_t N,
+                                                       uint32_t K, int tr,
+                                                       const float *__restrict__ su,
+                                                       f4 *__restrict__ packed) {
+    const uint32_t NT = ceil_div(N, 16), KS = ceil_div(K, 32);
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;     // (ks, nt, lane)
+    if (e >= KS * NT * 64) return;
+    const uint32_t lane = e & 63u, nt = (e >> 6) % NT, ks = (e >> 6) / NT;
+    const uint32_t n = 16 * nt + (lane & 15u), g = lane >> 4;
+    const float s = n < N ? su[n] : 1.0f;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = __fmul_rn(bval(w, N, K, tr, n, 32 * ks + 8 * g + j), s);
+    f4 hi, lo;
+    split8(v, hi, lo);
+    f4 *dst = packed + ((size_t)ks * NT + nt) * kTileF4 + lane;
+    dst[0] = hi;
+    dst[64] = lo;
+}
+
+// ----------------------------------------------------------------------------
+// out = x . B^T (+ bias): NT output tiles of 16, KS k-steps of 32
+// ----------------------------------------------------------------------------
+struct LinArgs {
+    const float *x;            // [M, K]
+    const f4 *packed;          // [KS][NT][128]
+    const float *su;           // [N]
+    const float *bias;         // [N] or null
+    float *out;                // [M, N]
+    uint32_t M, N, K;
+};
+
+template <int NT, int KS>
+__global__ void __launch_bounds__(kLinThreads, 2) lin_fwd_kernel(const LinArgs a) {
+    constexpr uint32_t kSliceF4 = NT * kTileF4;                 // one k-step of B
+    constexpr uint32_t kStage = ceil_div(kSliceF4, kLinThreads);
+    __shared__ f4 ring[2][kSliceF4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t n = lane & 15u, g = lane >> 4;
+    const uint32_t m = blockIdx.x * kLinRows + wave * 16 + n;
+    const bool m_ok = m < a.M;
+
+    // this lane's K values of row m: k = 32 q + 8 g + j
+    float xv[KS][8];
+    const float *xr = a.x + (size_t)(m_ok ? m : 0) * a.K;
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+        const uint32_t k0 = 32 * q + 8 * g;
+        if (m_ok && k0 + 8 <= a.K) {
+            const f4 u = *reinterpret_cast<const f4 *>(xr + k0);
+            const f4 w = *reinterpret_cast<const f4 *>(xr + k0 + 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                xv[q][j] = u[j];
+                xv[q][4 + j] = w[j];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xv[q][j] = (m_ok && k0 + j < a.K) ? xr[k0 + j] : 0.0f;
+        }
+    }
+    // per-row power-of-two scale (the row's 4 lane groups hold all of its K)
+    float mx = 0.0f;
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(xv[q][j]));
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float xs = pow2_scale(mx);
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[q][j] = __fmul_rn(xv[q][j], xs);
+
+    // k-step 0 -> slot 0
+    f4 st[kStage];
+#pragma unroll
+    for (uint32_t i = 0; i < kStage; ++i) {
+        const uint32_t e = tid + i * kLinThreads;
+        if (e < kSliceF4) ring[0][e] = a.packed[e];
+    }
+    __syncthreads();
+
+    f4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+        const uint32_t slot = q & 1;
+        if (q + 1 < KS) {
+#pragma unroll
+            for (uint32_t i = 0; i < kStage; ++i) {
+                const uint32_t e = tid + i * kLinThreads;
+                if (e < kSliceF4) st[i] = a.packed[(size_t)(q + 1) * kSliceF4 + e];
+            }
+        }
+        f4 bh, bl;
+        split8(xv[q], bh, bl);
+        const f4 *A = ring[slot] + lane;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const f4 ah = A[t * kTileF4], al = A[t * kTileF4 + 64];
+            acc[t] = mfma16(al, bh, acc[t]);
+            acc[t] = mfma16(ah, bl, acc[t]);
+            acc[t] = mfma16(ah, bh, acc[t]);
+        }
+        if (q + 1 < KS) {
+#pragma unroll
+            for (uint32_t i = 0; i < kStage; ++i) {
+                const uint32_t e = tid + i * kLinThreads;
+                if (e < kSliceF4) ring[slot ^ 1][e] = st[i];
+            }
+            __syncthreads();
+        }
+    }
+    if (!m_ok) return;
+    // lane (n, g) of tile t holds output columns 16 t + 4 g + r of row m
+    const float inv_xs = 1.0f / xs;                        // powers of two: exact
+    float *orow = a.out + (size_t)m * a.N;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const uint32_t c0 = 16 * t + 4 * g;
+        if (c0 >= a.N) continue;
+        f4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t c = c0 + r;
+            const float s = c < a.N ? a.su[c] : 1.0f;
+            float y = __fmul_rn(__fmul_rn(acc[t][r], inv_xs), 1.0f / s);
+            if (a.bias && c < a.N) y = __fadd_rn(y, a.bias[c]);
+            v[r] = y;
+        }
+        if (c0 + 4 <= a.N) {
+            *reinterpret_cast<f4 *>(orow + c0) = v;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (c0 + r < a.N) orow[c0 + r] = v[r];
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// column maxima: cmax[c] = max_m |x[m, c]| (as uint bits: order-free, exact)
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) lin_colmax_kernel(const float *__restrict__ x, uint32_t M,
+                                                         uint32_t C, uint32_t rows_per_block,
+                                                         uint32_t *__restrict__ cmax) {
+    const uint32_t m0 = blockIdx.x * rows_per_block;
+    const uint32_t m1 = min(M, m0 + rows_per_block);
+    for (uint32_t c = threadIdx.x; c < C; c += 256) {
+        float mx = 0.0f;
+        for (uint32_t m = m0; m < m1; ++m) mx = fmaxf(mx, fabsf(x[(size_t)m * C + c]));
+        atomicMax(cmax + c, __float_as_uint(mx));
+    }
+}
+
+// ----------------------------------------------------------------------------
+// weight gradient partials: part[p][n][k] = sum over the workgroup's rows of
+// dy[m, n] x[m, k]; N = 256 (wave w: n-tiles 2w, 2w+1), KT k-tiles of 16
+// ----------------------------------------------------------------------------
+struct WgradArgs {
+    const float *dy;           // [M, N]
+    const float *x;            // [M, K]
+    const uint32_t *cmax_dy;   // [N] float bits
+    const uint32_t *cmax_x;    // [K]
+    float *part;               // [P][N][K]
+    uint32_t M, N, K, rows;    // rows per workgroup (multiple of 32)
+};
+
+template <int KT>
+__global__ void __launch_bounds__(kLinThreads, 1) lin_wgrad_kernel(const WgradArgs a) {
+    constexpr uint32_t NTn = 16;                            // N = 256
+    constexpr uint32_t kA = NTn * kTileF4, kB = KT * kTileF4;
+    __shared__ f4 As[2][kA];
+    __shared__ f4 Bs[2][kB];
+    __shared__ float sd[256], sx[KT * 16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t m_begin = blockIdx.x * a.rows;
+    const uint32_t m_end = min(a.M, m_begin + a.rows);
+    for (uint32_t c = tid; c < 256; c += kLinThreads) sd[c] = pow2_scale(__uint_as_float(a.cmax_dy[c]));
+    for (uint32_t c = tid; c < KT * 16; c += kLinThreads)
+        sx[c] = c < a.K ? pow2_scale(__uint_as_float(a.cmax_x[c])) : 1.0f;
+    __syncthreads();
+
+    // staging tasks per m-step: (row group g8 of 8 rows, column c) -> one lane of one
+    // fragment tile, columns fastest (a wave's load of one row is 64 consecutive
+    // floats): dy tasks [0, 4 x 256), x tasks [.., + 4 x 16 KT)
+    constexpr uint32_t kTasks = (NTn + KT) * 16 * 4;
+    constexpr uint32_t kPer = ceil_div(kTasks, kLinThreads);
+    float stv[kPer][8];
+    auto task_of = [&](uint32_t task, bool &is_dy, uint32_t &c, uint32_t &g8) {
+        is_dy = task < NTn * 64;
+        const uint32_t tt = is_dy ? task : task - NTn * 64;
+        const uint32_t width = is_dy ? NTn * 16 : KT * 16;
+        g8 = tt / width;
+        c = tt % width;
+    };
+    auto load = [&](uint32_t m0) {
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint32_t task = tid + i * kLinThreads;
+            bool is_dy;
+            uint32_t c, g8;
+            task_of(task, is_dy, c, g8);
+            const uint32_t C = is_dy ? a.N : a.K;
+            const float *src = is_dy ? a.dy : a.x;
+            const float s = task < kTasks ? (is_dy ? sd[c] : sx[c < KT * 16 ? c : 0]) : 0.0f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t m = m0 + 8 * g8 + j;
+                const bool ok = task < kTasks && c < C && m < m_end;
+                stv[i][j] = ok ? __fmul_rn(src[(size_t)m * C + c], s) : 0.0f;
+            }
+        }
+    };
+    auto store = [&](uint32_t slot) {
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint32_t task = tid + i * kLinThreads;
+            if (task >= kTasks) continue;
+            bool is_dy;
+            uint32_t c, g8;
+            task_of(task, is_dy, c, g8);
+            const uint32_t l = (g8 << 4) | (c & 15u);
+            f4 hi, lo;
+            split8(stv[i], hi, lo);
+            f4 *dst = (is_dy ? As[slot] : Bs[slot]) + (c >> 4) * kTileF4 + l;
+            dst[0] = hi;
+            dst[64] = lo;
+        }
+    };
+
+    f4 acc[2][KT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < KT; ++t) acc[i][t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    const uint32_t nsteps = ceil_div(m_end > m_begin ? m_end - m_begin : 0, 32);
+    if (nsteps > 0) {
+        load(m_begin);
+        store(0);
+    }
+    __syncthreads();
+    for (uint32_t s = 0; s < nsteps; ++s) {
+        const uint32_t slot = s & 1u;
+        if (s + 1 < nsteps) load(m_begin + 32 * (s + 1));
+        const f4 *A = As[slot] + (2 * wave) * kTileF4 + lane;
+        const f4 a0h = A[0], a0l = A[64], a1h = A[kTileF4], a1l = A[kTileF4 + 64];
+        const f4 *Bp = Bs[slot] + lane;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+            const f4 bh = Bp[t * kTileF4], bl = Bp[t * kTileF4 + 64];
+            acc[0][t] = mfma16(a0l, bh, acc[0][t]);
+            acc[1][t] = mfma16(a1l, bh, acc[1][t]);
+            acc[0][t] = mfma16(a0h, bl, acc[0][t]);
+            acc[1][t] = mfma16(a1h, bl, acc[1][t]);
+            acc[0][t] = mfma16(a0h, bh, acc[0][t]);
+            acc[1][t] = mfma16(a1h, bh, acc[1][t]);
+        }
+        if (s + 1 < nsteps) store(slot ^ 1u);
+        __syncthreads();
+    }
+    // lane (kc = lane & 15, g) of (n-tile i, k-tile t) holds n = 16 (2 wave + i) + 4 g + r,
+    // k = 16 t + kc; unscale (exact) and store the partial
+    const uint32_t kc = lane & 15u, g = lane >> 4;
+    float *pp = a.part + (size_t)blockIdx.x * a.N * a.K;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+            const uint32_t k = 16 * t + kc;
+            if (k >= a.K) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t nn = 16 * (2 * wave + i) + 4 * g + r;
+                pp[(size_t)nn * a.K + k] = __fmul_rn(acc[i][t][r], 1.0f / (sd[nn] * sx[k]));
+            }
+        }
+}
+
+__global__ void __launch_bounds__(256) lin_reduce_kernel(const float *__restrict__ part, uint32_t P,
+                                                         uint32_t count, float *__restrict__ out) {
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= count) return;
+    float s = 0.0f;
+    for (uint32_t p = 0; p < P; ++p) s += part[(size_t)p * count + e];   // fixed order
+    out[e] = s;
+}
+
+uint32_t wgrad_rows(uint32_t M) {
+    // at most 256 workgroups (one round on the 256 CUs, 256 partials), whole m-steps
+    const uint32_t r = ceil_div(ceil_div(M, 256), 32) * 32;
+    return r < 32 ? 32 : r;
+}
+
+template <int NT, int KS>
+int launch_fwd(const LinArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL((lin_fwd_kernel<NT, KS>), dim3(ceil_div(a.M, kLinRows)), dim3(kLinThreads),
+                       0, st, a);
+    return check_launch("linear_f16x3");
+}
+
+template <int KT>
+int launch_wgrad(const WgradArgs &a, uint32_t P, hipStream_t st) {
+    hipLaunchKernelGGL((lin_wgrad_kernel<KT>), dim3(P), dim3(kLinThreads), 0, st, a);
+    return check_launch("linear_wgrad_f16x3");
+}
+
+}  // namespace
+}  // namespace sdfr
+
+using namespace sdfr;
+
+extern "C" {
+
+size_t sdfr_linear_pack_bytes(uint32_t N, uint32_t K) {
+    return (size_t)ceil_div(K, 32) * ceil_div(N, 16) * kTileF4 * sizeof(f4) + (size_t)N * 4;
+}
+
+int sdfr_linear_pack(const float *w, uint32_t N, uint32_t K, int transposed, void *packed,
+                     void *stream) {
+    if (!w || !packed) return fail(SDFR_EINVAL, "linear_pack: null pointer");
+    if (N == 0 || K == 0) return fail(SDFR_EINVAL, "linear_pack: empty matrix");
+    hipStream_t st = (hipStream_t)stream;
+    const size_t frag = (size_t)ceil_div(K, 32) * ceil_div(N, 16) * kTileF4 * sizeof(f4);
+    float *su = reinterpret_cast<float *>(static_cast<char *>(packed) + frag);
+    hipLaunchKernelGGL(lin_scale_kernel, dim3(ceil_div(N, 4)), dim3(256), 0, st, w, N, K,
+                       transposed ? 1 : 0, su);
+    int rc = check_launch("linear_pack: scale");
+    if (rc) return rc;
+    const uint32_t total = ceil_div(K, 32) * ceil_div(N, 16) * 64;
+    hipLaunchKernelGGL(lin_pack_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, w, N, K,
+                       transposed ? 1 : 0, su, reinterpret_cast<f4 *>(packed));
+    return check_launch("linear_pack: pack");
+}
+
+int sdfr_linear_f16x3(float *out, const float *x, const void *packed, const float *bias,
+                      uint32_t M, uint32_t N, uint32_t K, void *stream) {
+    if (M == 0) return SDFR_OK;
+    if (!out || !x || !packed) return fail(SDFR_EINVAL, "linear_f16x3: null pointer");
+    if (K % 4 || N % 4 || (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) % 16)
+        return fail(SDFR_EINVAL, "linear_f16x3: K, N multiples of 4, 16-B aligned rows");
+    LinArgs a;
+    a.x = x;
+    a.packed = static_cast<const f4 *>(packed);
+    a.su = reinterpret_cast<const float *>(static_cast<const char *>(packed) +
+                                           (size_t)ceil_div(K, 32) * ceil_div(N, 16) * kTileF4 *
+                                               sizeof(f4));
+    a.bias = bias;
+    a.out = out;
+    a.M = M;
+    a.N = N;
+    a.K = K;
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t NT = ceil_div(N, 16), KS = ceil_div(K, 32);
+    // the renderer networks' shapes: K in {32, 256, 272} -> N 256; N in {32, 256, 272} <- K 256
+    if (NT == 16 && KS == 1) return launch_fwd<16, 1>(a, st);
+    if (NT == 16 && KS == 8) return launch_fwd<16, 8>(a, st);
+    if (NT == 16 && KS == 9) return launch_fwd<16, 9>(a, st);
+    if (NT == 2 && KS == 8) return launch_fwd<2, 8>(a, st);
+    if (NT == 17 && KS == 8) return launch_fwd<17, 8>(a, st);
+    return fail(SDFR_EUNSUPPORTED, "linear_f16x3: (N, K) must be (256, <=32 | <=256 | <=288) or "
+                                   "(<=32 | <=272, <=256)");
+}
+
+size_t sdfr_linear_wgrad_ws_bytes(uint32_t M, uint32_t N, uint32_t K) {
+    if (M == 0 || N == 0 || K == 0) return 0;
+    const uint32_t P = ceil_div(M, wgrad_rows(M));
+    return (size_t)(N + ceil_div(K, 16) * 16) * 4 + 256 + (size_t)P * N * K * 4;
+}
+
+int sdfr_linear_wgrad_f16x3(float *gw, const float *dy, const float *x, uint32_t M, uint32_t N,
+                            uint32_t K, void *ws, size_t ws_bytes, void *stream) {
+    if (!gw || (M && (!dy || !x))) return fail(SDFR_EINVAL, "linear_wgrad_f16x3: null pointer");
+    if (N != 256 || K == 0 || K > 288)
+        return fail(SDFR_EUNSUPPORTED, "linear_wgrad_f16x3: N must be 256 and K <= 288");
+    hipStream_t st = (hipStream_t)stream;
+    if (M == 0) {
+        if (hipMemsetAsync(gw, 0, (size_t)N * K * 4, st) != hipSuccess)
+            return fail(SDFR_ELAUNCH, "linear_wgrad_f16x3: memset");
+        return SDFR_OK;
+    }
+    if (!ws || ws_bytes < sdfr_linear_wgrad_ws_bytes(M, N, K))
+        return fail(SDFR_EINVAL, "linear_wgrad_f16x3: workspace too small");
+    const uint32_t Kp = ceil_div(K, 16) * 16;
+    uint32_t *cmax = static_cast<uint32_t *>(ws);
+    float *part = reinterpret_cast<float *>(static_cast<char *>(ws) +
+                                            ((size_t)(N + Kp) * 4 + 255) / 256 * 256);
+    if (hipMemsetAsync(cmax, 0, (size_t)(N + Kp) * 4, st) != hipSuccess)
+        return fail(SDFR_ELAUNCH, "linear_wgrad_f16x3: memset");
+    const uint32_t rpb = 256;
+    hipLaunchKernelGGL(lin_colmax_kernel, dim3(ceil_div(M, rpb)), dim3(256), 0, st, dy, M, N, rpb,
+                       cmax);
+    hipLaunchKernelGGL(lin_colmax_kernel, dim3(ceil_div(M, rpb)), dim3(256), 0, st, x, M, K, rpb,
+                       cmax + N);
+    int rc = check_launch("linear_wgrad_f16x3: column max");
+    if (rc) return rc;
+    WgradArgs a;
+    a.dy = dy;
+    a.x = x;
+    a.cmax_dy = cmax;
+    a.cmax_x = cmax + N;
+    a.part = part;
+    a.M = M;
+    a.N = N;
+    a.K = K;
+    a.rows = wgrad_rows(M);
+    const uint32_t P = ceil_div(M, a.rows);
+    const uint32_t KT = ceil_div(K, 16);
+    if (KT <= 2) rc = launch_wgrad<2>(a, P, st);              // input_linear (K = 32)
+    else if (KT <= 16) rc = launch_wgrad<16>(a, P, st);       // dense layers (K = 256)
+    else if (KT <= 17) rc = launch_wgrad<17>(a, P, st);       // views (K = 272, 259)
+    else rc = launch_wgrad<18>(a, P, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(lin_reduce_kernel, dim3(ceil_div(N * K, 256)), dim3(256), 0, st, part, P,
+                       N * K, gw);
+    return check_launch("linear_wgrad_f16x3: reduce");
+}
+
+}  // extern "C"

@@ -28,6 +28,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .encoders import GridEncoder, SHEncoder
+from .linear import linear
 
 
 # ---------------------------------------------------------------------------
@@ -54,7 +55,9 @@ class LinearLayer(nn.Module):
         self.std_init = std_init
 
     def forward(self, input):
-        return self.std_init * F.linear(input, self.weight, bias=self.bias) + self.bias_init
+        # linear(): F.linear, or the split-fp16 MFMA kernels for the renderer MLP's
+        # training shapes (linear.py)
+        return self.std_init * linear(input, self.weight, self.bias) + self.bias_init
 
 
 class FiLMSiren(nn.Module):
@@ -78,7 +81,7 @@ class FiLMSiren(nn.Module):
 
     def forward(self, input, style):
         batch, features = style.shape
-        out = F.linear(input, self.weight, bias=self.bias)
+        out = linear(input, self.weight, self.bias)
         shape = (batch,) + (1,) * (input.dim() - 2) + (features,)
         gamma = self.gamma(style).view(shape)
         beta = self.beta(style).view(shape)

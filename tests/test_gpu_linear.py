@@ -1,0 +1,115 @@
+"""GPU: the renderer MLP's training GEMMs on split-fp16 MFMA (csrc/linear_f16x3.hip,
+linear.py) against float64 references of the same op, and the stage-1 gradients of a
+whole renderer with the kernels on and off.
+
+Accuracy bound, per output element: |got - exact| <= c * 2^-24 * sum_k |x_k w_k|
+(the scale of an fp32 dot product's rounding), with c small; the PyTorch fp32
+product on the same inputs is measured beside it."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+U = 2.0 ** -24
+
+
+def _rand(shape, mag, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(*shape, generator=g)
+    if mag == "rows":                       # per-row magnitudes 1e-8 .. 1e2
+        x = x * 10.0 ** (torch.rand(shape[0], 1, generator=g) * 10 - 8)
+    elif mag == "tiny":
+        x = x * 1e-6
+    return x
+
+
+def _bound_check(name, got, exact, scale, c=32.0):
+    err = (got.double().cpu() - exact).abs()
+    bound = c * U * scale + 1e-30
+    ratio = float((err / bound).max())
+    assert ratio <= 1.0, f"{name}: max err / bound = {ratio:.3f}"
+    return ratio
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 32), (3000, 256, 256), (2048, 256, 272),
+                                   (1001, 256, 256)])
+@pytest.mark.parametrize("mag", ["unit", "rows", "tiny"])
+def test_linear_forward_and_backward_vs_float64(sdfr, M, N, K, mag):
+    from sdface_gan_amd.linear import _LinearF16x3
+    x = _rand((M, K), mag, 1).to(DEV).requires_grad_(True)
+    w = (_rand((N, K), "unit", 2) * 0.05).to(DEV).requires_grad_(True)
+    b = (_rand((N,), "unit", 3) * 0.1).to(DEV).requires_grad_(True)
+    gy = _rand((M, N), mag, 4).to(DEV)
+    y = _LinearF16x3.apply(x, w, b)
+    y.backward(gy)
+    torch.cuda.synchronize()
+    xd, wd, bd, gyd = (t.detach().double().cpu() for t in (x, w, b, gy))
+    yd = xd @ wd.t() + bd
+    _bound_check("forward", y.detach(), yd, xd.abs() @ wd.abs().t() + bd.abs())
+    _bound_check("input grad", x.grad, gyd @ wd, gyd.abs() @ wd.abs())
+    _bound_check("weight grad", w.grad, gyd.t() @ xd, gyd.abs().t() @ xd.abs())
+    np.testing.assert_allclose(b.grad.cpu().numpy(), gyd.sum(0).numpy(),
+                               rtol=1e-5, atol=1e-5 * float(gyd.abs().sum(0).max()))
+    # for scale: PyTorch's fp32 forward on the same data meets the same kind of bound
+    y32 = torch.nn.functional.linear(x.detach(), w.detach(), b.detach())
+    _bound_check("torch fp32 forward", y32, yd, xd.abs() @ wd.abs().t() + bd.abs(), c=64.0)
+
+
+def test_linear_routing_and_deterministic(sdfr):
+    """linear() takes the kernels only for the MLP's training shapes; the weight
+    gradient's split reduction is deterministic run to run."""
+    from sdface_gan_amd import linear as lin
+    x = torch.randn(196608 // 16, 256, device=DEV, requires_grad=True)
+    w = torch.randn(256, 256, device=DEV, requires_grad=True)
+    y = lin.linear(x, w)
+    assert y.grad_fn is not None and "LinearF16x3" in type(y.grad_fn).__name__
+    with torch.no_grad():
+        assert lin.linear(x, w).grad_fn is None             # inference: F.linear
+    s = torch.randn(8, 256, device=DEV)
+    assert "LinearF16x3" not in type(lin.linear(s.requires_grad_(), w).grad_fn).__name__
+    grads = []
+    for _ in range(2):
+        w.grad = None
+        lin.linear(x, w).square().sum().backward()
+        grads.append(w.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("ngp", [True, False], ids=["ngp", "siren"])
+def test_stage1_gradients_kernels_vs_torch_gemm(sdfr, ngp):
+    """One stage-1 generator backward (adversarial + eikonal + minimal-surface +
+    smoothness terms, perturb 0) with the renderer MLP's GEMMs on the HIP kernels and
+    on rocBLAS fp32: every gradient agrees to fp32 rounding level."""
+    from sdface_gan_amd import linear as lin
+    from sdface_gan_amd import training
+    from sdface_gan_amd.training import RendererTrainer
+    from tests.test_train_renderer import stage1_opt
+    opt = stage1_opt(sdfr, ngp=ngp, res=32, samples=24, batch=2, chunk=2)
+    opt.rendering.perturb = 0
+    torch.manual_seed(0)
+    noise = [torch.randn(2, 256, device=DEV)]
+    cams = sdfr.generate_camera_params(32, DEV, batch=2)
+    grads = {}
+    orig = training.smoothness
+    for mode in ("torch", "f16x3"):
+        lin.set_train_gemm(mode)
+        tr = RendererTrainer(opt, DEV, seed=5)
+
+        def smooth(*a, **k):
+            torch.manual_seed(7)                       # the same voxel block both times
+            return orig(*a, **k)
+        training.smoothness = smooth
+        try:
+            tr.g_backward(iter([(noise, cams)]), 1)
+        finally:
+            training.smoothness = orig
+            lin.set_train_gemm("f16x3")
+        grads[mode] = {n: p.grad.detach().clone() for n, p in tr.g_module.named_parameters()
+                       if p.grad is not None}
+    assert set(grads["torch"]) == set(grads["f16x3"])
+    for k, ref in grads["torch"].items():
+        got = grads["f16x3"][k]
+        scale = float(ref.abs().max())
+        err = float((got - ref).abs().max())
+        assert err <= 2e-4 * scale + 1e-12, f"{k}: max |diff| {err:.3e} (max |g| {scale:.3e})"
