@@ -302,14 +302,29 @@ static void orc_sh_one(const float *in, float *o, uint32_t C, float *dx,
     }
 }
 
+/* Bands 4..7 (degrees 5..8, shencoder.cu:74-123 and the matching dy_dx terms): the
+ * Legendre-recurrence form that csrc/sh_gen.py generates for the HIP kernel (the same
+ * header, so this C restatement and the kernel agree bit for bit); pinned against the
+ * reference's own degree-8 formulas evaluated in fp32 (tests/golden/sh_deg8.npz) and
+ * against scipy's spherical harmonics (tests/test_oracle.py). */
+#include "../../sdface-gan_amd/csrc/sh_bands.h"
+
 int orc_sh_encode_forward(const float *inputs, float *outputs, uint32_t B,
                           uint32_t D, uint32_t C, float *dy_dx) {
-    if (D != 3 || C < 1 || C > 4) return ORC_EINVAL;
+    if (D != 3 || C < 1 || C > 8) return ORC_EINVAL;
     uint32_t C2 = C * C;
     for (uint32_t b = 0; b < B; b++) {
-        float *dx = dy_dx ? dy_dx + (size_t)b * D * C2 : NULL;
-        orc_sh_one(inputs + (size_t)b * D, outputs + (size_t)b * C2, C, dx,
-                   dx ? dx + C2 : NULL, dx ? dx + 2 * C2 : NULL);
+        float o[64], dxs[3][64];
+        float *dx = dy_dx ? dxs[0] : NULL;
+        const float *in = inputs + (size_t)b * D;
+        orc_sh_one(in, o, C < 4 ? C : 4, dx, dx ? dxs[1] : NULL, dx ? dxs[2] : NULL);
+        if (C > 4) sdfr_sh_bands_4_7(in[0], in[1], in[2], C, o, dx, dx ? dxs[1] : NULL,
+                                     dx ? dxs[2] : NULL);
+        for (uint32_t i = 0; i < C2; i++) outputs[(size_t)b * C2 + i] = o[i];
+        if (dy_dx)
+            for (uint32_t d = 0; d < 3; d++)
+                for (uint32_t i = 0; i < C2; i++)
+                    dy_dx[(size_t)b * D * C2 + d * C2 + i] = dxs[d][i];
     }
     return ORC_OK;
 }
@@ -319,7 +334,7 @@ int orc_sh_encode_backward(const float *grad, const float *inputs, uint32_t B,
                            uint32_t D, uint32_t C, const float *dy_dx,
                            float *grad_inputs) {
     (void)inputs;
-    if (D != 3 || C < 1 || C > 4) return ORC_EINVAL;
+    if (D != 3 || C < 1 || C > 8) return ORC_EINVAL;
     uint32_t C2 = C * C;
     for (uint32_t b = 0; b < B; b++)
         for (uint32_t d = 0; d < D; d++) {

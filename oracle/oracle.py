@@ -170,7 +170,7 @@ def sh_encode_forward(inputs, degree=4, calc_dy_dx=False):
     out = np.empty((B, degree * degree), np.float32)
     dydx = np.empty((B, D * degree * degree), np.float32) if calc_dy_dx else None
     if lib().orc_sh_encode_forward(_p(x), _p(out), B, D, degree, _p(dydx)) != 0:
-        raise RuntimeError("SH oracle supports input_dim 3, degree 1..4")
+        raise RuntimeError("SH oracle supports input_dim 3, degree 1..8")
     return out, dydx
 
 
@@ -180,7 +180,7 @@ def sh_encode_backward(grad, inputs, degree, dy_dx):
     B, D = x.shape
     gin = np.zeros_like(x)
     if lib().orc_sh_encode_backward(_p(g), _p(x), B, D, degree, _p(_f32(dy_dx)), _p(gin)) != 0:
-        raise RuntimeError("SH oracle supports input_dim 3, degree 1..4")
+        raise RuntimeError("SH oracle supports input_dim 3, degree 1..8")
     return gin
 
 

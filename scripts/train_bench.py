@@ -41,6 +41,11 @@ def main():
     p.add_argument("--miopen-find", action="store_true",
                    help="torch.backends.cudnn.benchmark = True (MIOpen find per conv shape "
                         "during warmup instead of its heuristics)")
+    p.add_argument("--train-gemm", default="f16x3", choices=["f16x3", "torch"],
+                   help="stage 1: renderer-MLP GEMMs on the split-fp16 MFMA kernels or on "
+                        "rocBLAS fp32 (linear.py)")
+    p.add_argument("--coord-pad", type=int, default=8,
+                   help="stage-1 discriminator CoordConv channel padding (training.py; 1 = off)")
     a = p.parse_args()
     torch.backends.cudnn.benchmark = a.miopen_find
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -51,7 +56,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     sdfr = load()
+    from sdface_gan_amd.linear import set_train_gemm
     from sdface_gan_amd.training import FullPipelineTrainer, RendererTrainer
+    set_train_gemm(a.train_gemm)
+    from sdface_gan_amd.training import CoordConv2d
+    CoordConv2d.pad_to = a.coord_pad
     opt = sdfr.vol_render_opt(ngp=a.net == "ngp", batch=a.batch, chunk=a.chunk,
                               train_renderer=a.stage == 1)
     if a.stage == 1:

@@ -750,7 +750,8 @@ static size_t grid_bwd_ws_dispatch_c(uint32_t C, uint32_t B, uint32_t L) {
 }
 
 // ----------------------------------------------------------------------------
-// SH encoder (degree <= 4), shencoder.cu:27-123
+// SH encoder, shencoder.cu:27-355 (bands 0..3 term by term below, bands 4..7 from
+// sh_bands.h)
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ void sh_eval(float x, float y, float z, uint32_t C, float *o) {
     const float xy = __fmul_rn(x, y), xz = __fmul_rn(x, z), yz = __fmul_rn(y, z);
@@ -817,6 +818,14 @@ __device__ __forceinline__ void sh_eval_d(float x, float y, float z, uint32_t C,
     dz[15] = 0.0f;
 }
 
+// bands 4..7 (degrees 5..8): generated by csrc/sh_gen.py from the Legendre
+// recurrence, same band convention as the terms above
+#define SDFR_SH_FN static __device__ __forceinline__
+#include "sh_bands.h"
+#undef SDFR_SH_FN
+
+// MAXC2 = 16 (degree <= 4, SDFace's) or 64 (degrees 5..8)
+template <uint32_t MAXC2>
 __global__ void __launch_bounds__(256)
 sh_fwd_kernel(const float *__restrict__ inputs, float *__restrict__ outputs,
               float *__restrict__ dy_dx, uint32_t B, uint32_t C) {
@@ -825,12 +834,14 @@ sh_fwd_kernel(const float *__restrict__ inputs, float *__restrict__ outputs,
     const float x = inputs[(size_t)b * 3], y = inputs[(size_t)b * 3 + 1],
                 z = inputs[(size_t)b * 3 + 2];
     const uint32_t C2 = C * C;
-    float o[16];
+    float o[MAXC2];
     sh_eval(x, y, z, C, o);
+    if constexpr (MAXC2 > 16) sdfr_sh_bands_4_7(x, y, z, C, o, nullptr, nullptr, nullptr);
     for (uint32_t i = 0; i < C2; ++i) outputs[(size_t)b * C2 + i] = o[i];
     if (dy_dx) {
-        float dx[16], dy[16], dz[16];
+        float dx[MAXC2], dy[MAXC2], dz[MAXC2];
         sh_eval_d(x, y, z, C, dx, dy, dz);
+        if constexpr (MAXC2 > 16) sdfr_sh_bands_4_7(x, y, z, C, o, dx, dy, dz);
         float *p = dy_dx + (size_t)b * 3 * C2;
         for (uint32_t i = 0; i < C2; ++i) {
             p[i] = dx[i];
@@ -946,11 +957,14 @@ int sdfr_sh_encode_forward(const float *inputs, float *outputs, uint32_t B, uint
                            uint32_t C, float *dy_dx, void *stream) {
     if (D != 3) return fail(SDFR_EINVAL, "SH encoder only support input dim == 3");
     if (C < 1 || C > 8) return fail(SDFR_EINVAL, "SH encoder only supports degree in [1, 8]");
-    if (C > 4) return fail(SDFR_EUNSUPPORTED, "sdfr: SH degree > 4 not implemented");
     if (B == 0) return SDFR_OK;
     if (!inputs || !outputs) return fail(SDFR_EINVAL, "sh_encode_forward: null tensor pointer");
-    hipLaunchKernelGGL(sh_fwd_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                       inputs, outputs, dy_dx, B, C);
+    if (C <= 4)
+        hipLaunchKernelGGL(sh_fwd_kernel<16>, dim3((B + 255) / 256), dim3(256), 0,
+                           (hipStream_t)stream, inputs, outputs, dy_dx, B, C);
+    else
+        hipLaunchKernelGGL(sh_fwd_kernel<64>, dim3((B + 255) / 256), dim3(256), 0,
+                           (hipStream_t)stream, inputs, outputs, dy_dx, B, C);
     return check_launch("sh_encode_forward");
 }
 
@@ -959,7 +973,6 @@ int sdfr_sh_encode_backward(const float *grad, const float *inputs, uint32_t B, 
     (void)inputs;
     if (D != 3) return fail(SDFR_EINVAL, "SH encoder only support input dim == 3");
     if (C < 1 || C > 8) return fail(SDFR_EINVAL, "SH encoder only supports degree in [1, 8]");
-    if (C > 4) return fail(SDFR_EUNSUPPORTED, "sdfr: SH degree > 4 not implemented");
     if (B == 0) return SDFR_OK;
     if (!grad || !dy_dx || !grad_inputs)
         return fail(SDFR_EINVAL, "sh_encode_backward: null tensor pointer");

@@ -424,7 +424,16 @@ class AddCoords(nn.Module):
 
 
 class CoordConv2d(nn.Module):
-    """sdf_model.py:1278-1296."""
+    """sdf_model.py:1278-1296.
+
+    On the GPU the convolution's input channels (C + 2 coordinate channels: 130, 258,
+    402 in the stage-1 discriminator) are zero-padded to a multiple of ``pad_to``,
+    input and weight alike: the extra channels contribute exact zeros, the
+    parameters and state-dict keys are unchanged, and MIOpen can pick its
+    implicit-GEMM / Winograd solvers instead of the naive fallback it uses for
+    channel counts that are not a multiple of 4 (``pad_to = 1`` turns it off)."""
+
+    pad_to = 8
 
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True):
         super().__init__()
@@ -433,7 +442,14 @@ class CoordConv2d(nn.Module):
                               padding=padding, bias=bias)
 
     def forward(self, input_tensor):
-        return self.conv(self.addcoords(input_tensor))
+        x = self.addcoords(input_tensor)
+        c = x.shape[1]
+        pad = -c % self.pad_to
+        if not x.is_cuda or pad == 0:
+            return self.conv(x)
+        w = F.pad(self.conv.weight, (0, 0, 0, 0, 0, pad))
+        return F.conv2d(F.pad(x, (0, 0, 0, 0, 0, pad)), w, self.conv.bias,
+                        self.conv.stride, self.conv.padding)
 
 
 class CoordConvLayer(nn.Module):

@@ -225,6 +225,43 @@ def case_encoders():
     print("encoders.npz", out.shape, sh.shape)
 
 
+def case_sh_deg8():
+    """SH encoder at degree 8 (shencoder.cu:27-355: outputs[0..63] and the dy_dx lambdas
+    write_sh_dx / _dy / _dz).  The CUDA kernel cannot run here, so its formulas are read
+    from the reference source and evaluated in float32 (numpy, one rounding per
+    operation; nvcc may contract a*b+c, so the kernel itself can differ by an ulp).
+    Stored: unit directions (plus the poles and axis points), outputs [B, 64] and
+    dy_dx [B, 3, 64]."""
+    import re
+    src = (REF / "im2scene/sdf/models/shencoder/src/shencoder.cu").read_text()
+    rx = re.compile(r"^\s*(outputs|dx|dy|dz)\[(\d+)\]\s*=\s*(.*?)\s*;", re.M)
+    exprs = {"outputs": {}, "dx": {}, "dy": {}, "dz": {}}
+    for name, idx, e in rx.findall(src):
+        exprs[name][int(idx)] = re.sub(r"(\d+\.\d*(?:e[-+]?\d+)?)f", r"F(\1)", e)
+    assert all(len(v) == 64 for v in exprs.values()), {k: len(v) for k, v in exprs.items()}
+    rng = np.random.default_rng(8)
+    d = rng.normal(size=(2048, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d[:6] = np.array([[0, 0, 1], [0, 0, -1], [1, 0, 0], [0, 1, 0], [-1, 0, 0],
+                      [0.6, 0.0, 0.8]], np.float32)
+    F = np.float32
+    x, y, z = (d[:, i].copy() for i in range(3))
+    env = dict(F=F, pow=lambda a, n: np.power(a, np.float32(n)), x=x, y=y, z=z, xy=x * y, xz=x * z, yz=y * z, x2=x * x, y2=y * y, z2=z * z)
+    env.update(xyz=env["xy"] * z, x4=env["x2"] * env["x2"], y4=env["y2"] * env["y2"],
+               z4=env["z2"] * env["z2"])
+    env.update(x6=env["x4"] * env["x2"], y6=env["y4"] * env["y2"], z6=env["z4"] * env["z2"])
+
+    def ev(e):
+        v = eval(e, {"__builtins__": {}}, env)       # reference arithmetic on float32 arrays
+        return np.broadcast_to(np.asarray(v, np.float32), x.shape)
+    out = np.stack([ev(exprs["outputs"][i]) for i in range(64)], 1)
+    dydx = np.stack([np.stack([ev(exprs[k][i]) for i in range(64)], 1)
+                     for k in ("dx", "dy", "dz")], 1)
+    assert out.dtype == np.float32 and dydx.dtype == np.float32
+    np.savez_compressed(OUT / "sh_deg8.npz", dirs=d, sh_out=out, dy_dx=dydx)
+    print("sh_deg8.npz", out.shape, dydx.shape)
+
+
 def case_camera(sdf_utils):
     res = {}
     for name, kw in [("gauss", {}), ("uniform", {"uniform": True}), ("sweep", {"sweep": True})]:
@@ -536,6 +573,7 @@ def main():
         return
     case_init_stats(sdf_model, sdf_utils)
     case_encoders()
+    case_sh_deg8()
     case_camera(sdf_utils)
     case_render(sdf_model, sdf_utils, "render_small", B=2, res=8, n_samples=24,
                 intermediates=True, seed=11)

@@ -130,6 +130,26 @@ def test_sh_forward_backward_bit_exact(sdfr, oracle_mod, golden_dir):
         np.testing.assert_array_equal(o.cpu().numpy(), oracle_mod.sh_encode_forward(x, deg)[0])
 
 
+@pytest.mark.parametrize("deg", [5, 6, 7, 8])
+def test_sh_degrees_5_to_8_bit_exact(sdfr, oracle_mod, golden_dir, deg):
+    """The reference's _shencoder accepts degrees 1..8 (sphere_harmonics.py:62-86):
+    the HIP kernel's bands 4..7 equal the oracle bit for bit (forward, dy_dx, input
+    backward), and the reference's own degree-8 formulas to fp32 rounding."""
+    g = np.load(golden_dir / "sh_deg8.npz")
+    x = g["dirs"]
+    xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    out = sdfr.sh_encode(xt, deg, True)
+    ref, dref = oracle_mod.sh_encode_forward(x, deg, calc_dy_dx=True)
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), ref)
+    c2 = deg * deg
+    scale = np.abs(g["sh_out"][:, :c2]).max(0) + 1e-30
+    assert (np.abs(out.detach().cpu().numpy() - g["sh_out"][:, :c2]) / scale).max() < 1e-5
+    grad = np.random.default_rng(deg).normal(size=ref.shape).astype(np.float32)
+    out.backward(torch.from_numpy(grad).to(DEV))
+    np.testing.assert_array_equal(xt.grad.cpu().numpy(),
+                                  oracle_mod.sh_encode_backward(grad, x, deg, dref))
+
+
 def test_device_sin_accuracy(sdfr):
     """The field kernel's sin (hardware v_sin_f32 after an fma 2pi reduction) and
     the polynomial alternative, against float64 over the FiLM argument range."""

@@ -126,6 +126,46 @@ def test_sh_dydx_finite_difference(oracle_mod):
         np.testing.assert_allclose(dd[:, d, :], fd, atol=2e-2, rtol=1e-2)
 
 
+def test_sh_degree8_vs_reference_formulas(oracle_mod, golden_dir):
+    """Degrees 5..8 (shencoder.cu:27-355): the oracle's generated bands (csrc/sh_gen.py)
+    against the reference's own formulas evaluated in fp32 (tests/golden/sh_deg8.npz,
+    make_golden.py case_sh_deg8) -- same functions in a different expression form
+    (and, for bands 0..3, with the fma contraction nvcc applies where the numpy
+    evaluation rounds twice), so agreement is to fp32 rounding, relative to each
+    output's largest magnitude."""
+    g = np.load(golden_dir / "sh_deg8.npz")
+    for deg in (5, 6, 7, 8):
+        c2 = deg * deg
+        out, dd = oracle_mod.sh_encode_forward(g["dirs"], deg, calc_dy_dx=True)
+        ref = g["sh_out"][:, :c2]
+        scale = np.abs(ref).max(0, keepdims=True) + 1e-30
+        assert (np.abs(out - ref) / scale).max() < 1e-5, deg
+        dref = g["dy_dx"][:, :, :c2]
+        dd = dd.reshape(-1, 3, c2)
+        dscale = np.abs(dref).max(0, keepdims=True) + 1e-3
+        assert (np.abs(dd - dref) / dscale).max() < 1e-5, deg
+
+
+def test_sh_degree8_vs_scipy(oracle_mod):
+    """An independent pin of the band convention: real SH from scipy's complex
+    spherical harmonics (Condon-Shortley phase) -- sqrt(2) Re Y_l^m (m > 0),
+    Y_l^0, sqrt(2) Im Y_l^|m| (m < 0) -- equal the oracle's 64 outputs at degree 8
+    to fp32 accuracy, for every band (0..3 are the reference's own terms)."""
+    from scipy.special import sph_harm_y
+    rng = np.random.default_rng(11)
+    d = rng.normal(size=(512, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    out, _ = oracle_mod.sh_encode_forward(d.astype(np.float32), 8)
+    theta = np.arccos(np.clip(d[:, 2], -1, 1))          # polar
+    phi = np.arctan2(d[:, 1], d[:, 0])                  # azimuth
+    for l in range(8):
+        for m in range(-l, l + 1):
+            y = sph_harm_y(l, abs(m), theta, phi)
+            ref = y.real if m == 0 else np.sqrt(2) * (y.real if m > 0 else y.imag)
+            np.testing.assert_allclose(out[:, l * l + l + m], ref, atol=3e-6 * max(1, l),
+                                       err_msg=f"l={l} m={m}")
+
+
 @pytest.mark.parametrize("name", ["render_small"])
 def test_ray_sampling_bit_exact(oracle_mod, golden_dir, name):
     g = np.load(golden_dir / f"{name}.npz")
