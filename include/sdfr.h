@@ -292,6 +292,23 @@ size_t sdfr_linear_wgrad_ws_bytes(uint32_t M, uint32_t N, uint32_t K);
 int sdfr_linear_wgrad_f16x3(float *gw, const float *dy, const float *x, uint32_t M, uint32_t N,
                             uint32_t K, void *ws, size_t ws_bytes, void *stream);
 
+/* FiLMSiren.forward / backward (sdf_model.py:62-67) around the same GEMM, F faces of
+ * rows_per_face consecutive rows each (M = F rows_per_face), N = 256:
+ * sdfr_film_linear_f16x3: y_save = x . W^T + bias; out = sin(gamma[f] * y + beta[f])
+ *   (gamma, beta [F,N]; one rounding per op, as the reference's separate ops).
+ * sdfr_film_backward: with u = gamma[f] y + beta[f] recomputed, du = ds cos(u):
+ *   dy = du gamma[f] [M,N] (the input of the two GEMM gradients), dgamma[f] = sum du y,
+ *   dbeta[f] = sum du, dbf[f] = sum dy (the bias gradient, per face) [F,N] each;
+ *   every sum in a fixed order; ws >= sdfr_film_backward_ws_bytes(M, N, rows_per_face). */
+int sdfr_film_linear_f16x3(float *out, float *y_save, const float *x, const void *packed,
+                           const float *bias, const float *gamma, const float *beta, uint32_t M,
+                           uint32_t N, uint32_t K, uint32_t rows_per_face, void *stream);
+size_t sdfr_film_backward_ws_bytes(uint32_t M, uint32_t N, uint32_t rows_per_face);
+int sdfr_film_backward(float *dy, float *dgamma, float *dbeta, float *dbf, const float *ds,
+                       const float *y, const float *gamma, const float *beta, uint32_t M,
+                       uint32_t N, uint32_t rows_per_face, void *ws, size_t ws_bytes,
+                       void *stream);
+
 /* ---------------------------------------------------------------------------
  * StyleGAN2 decoder ops (im2scene/sdf/models/sdf_op.py).
  *

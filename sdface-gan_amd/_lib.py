@@ -48,6 +48,7 @@ EXPORTS = (
     "sdfr_mc_workspace_bytes", "sdfr_mc_count", "sdfr_mc_emit",
     "sdfr_linear_pack_bytes", "sdfr_linear_pack", "sdfr_linear_f16x3",
     "sdfr_linear_wgrad_ws_bytes", "sdfr_linear_wgrad_f16x3",
+    "sdfr_film_linear_f16x3", "sdfr_film_backward_ws_bytes", "sdfr_film_backward",
 )
 
 
@@ -212,6 +213,10 @@ def lib():
     L.sdfr_linear_wgrad_ws_bytes.restype = ctypes.c_size_t
     L.sdfr_linear_wgrad_f16x3.argtypes = [_vp, _vp, _vp, _u32, _u32, _u32, _vp, ctypes.c_size_t,
                                           _vp]
+    L.sdfr_film_linear_f16x3.argtypes = [_vp] * 7 + [_u32] * 4 + [_vp]
+    L.sdfr_film_backward_ws_bytes.argtypes = [_u32, _u32, _u32]
+    L.sdfr_film_backward_ws_bytes.restype = ctypes.c_size_t
+    L.sdfr_film_backward.argtypes = [_vp] * 8 + [_u32] * 3 + [_vp, ctypes.c_size_t, _vp]
     v = L.sdfr_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"libsdfr ABI {v} != expected {ABI_VERSION}; rebuild the library")

@@ -100,9 +100,14 @@ struct LinArgs {
     const float *bias;         // [N] or null
     float *out;                // [M, N]
     uint32_t M, N, K;
+    // FiLM epilogue (FILM kernels): out = sin(gamma[f] * y + beta[f]), y = x B^T + bias
+    // saved to y_save; f = m / rows_per_face
+    const float *gamma, *beta; // [F, N]
+    float *y_save;             // [M, N]
+    uint32_t rows_per_face;
 };
 
-template <int NT, int KS>
+template <int NT, int KS, bool FILM>
 __global__ void __launch_bounds__(kLinThreads, 2) lin_fwd_kernel(const LinArgs a) {
     constexpr uint32_t kSliceF4 = NT * kTileF4;                 // one k-step of B
     constexpr uint32_t kStage = ceil_div(kSliceF4, kLinThreads);
@@ -190,26 +195,115 @@ __global__ void __launch_bounds__(kLinThreads, 2) lin_fwd_kernel(const LinArgs a
     // lane (n, g) of tile t holds output columns 16 t + 4 g + r of row m
     const float inv_xs = 1.0f / xs;                        // powers of two: exact
     float *orow = a.out + (size_t)m * a.N;
+    const size_t frow = FILM ? (size_t)(m / a.rows_per_face) * a.N : 0;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const uint32_t c0 = 16 * t + 4 * g;
         if (c0 >= a.N) continue;
-        f4 v;
+        f4 v, yv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t c = c0 + r;
             const float s = c < a.N ? a.su[c] : 1.0f;
             float y = __fmul_rn(__fmul_rn(acc[t][r], inv_xs), 1.0f / s);
             if (a.bias && c < a.N) y = __fadd_rn(y, a.bias[c]);
-            v[r] = y;
+            yv[r] = y;
+            if constexpr (FILM) {
+                // FiLMSiren.forward (sdf_model.py:62-67): sin(gamma * out + beta), one
+                // rounding per op as the reference's separate elementwise ops
+                const float gm = c < a.N ? a.gamma[frow + c] : 0.0f;
+                const float bt = c < a.N ? a.beta[frow + c] : 0.0f;
+                v[r] = sinf(__fadd_rn(__fmul_rn(gm, y), bt));
+            } else {
+                v[r] = y;
+            }
         }
         if (c0 + 4 <= a.N) {
             *reinterpret_cast<f4 *>(orow + c0) = v;
+            if constexpr (FILM) *reinterpret_cast<f4 *>(a.y_save + (size_t)m * a.N + c0) = yv;
         } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                if (c0 + r < a.N) orow[c0 + r] = v[r];
+                if (c0 + r < a.N) {
+                    orow[c0 + r] = v[r];
+                    if constexpr (FILM) a.y_save[(size_t)m * a.N + c0 + r] = yv[r];
+                }
         }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// FiLM backward (elementwise part): with u = gamma[f] y + beta[f] (as the forward),
+//   du = ds cos(u),  dy = du gamma[f]     (written: the GEMMs' input)
+//   per-block column sums  du y (-> dgamma[f]),  du (-> dbeta[f]),  dy (-> db)
+// Block (f, j) covers rows [f R + j rpb, ...) of face f; thread = column (N = 256).
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) film_bwd_kernel(const float *__restrict__ ds,
+                                                       const float *__restrict__ y,
+                                                       const float *__restrict__ gamma,
+                                                       const float *__restrict__ beta,
+                                                       float *__restrict__ dy, uint32_t N,
+                                                       uint32_t rows_per_face, uint32_t rpb,
+                                                       float *__restrict__ part) {
+    const uint32_t f = blockIdx.y, j = blockIdx.x, c = threadIdx.x;
+    const uint32_t r0 = j * rpb, r1 = min(rows_per_face, r0 + rpb);
+    const float gm = gamma[(size_t)f * N + c], bt = beta[(size_t)f * N + c];
+    float sg = 0.0f, sb = 0.0f, sd = 0.0f;
+    const size_t base = (size_t)f * rows_per_face;
+    uint32_t r = r0;
+    for (; r + 4 <= r1; r += 4) {
+        float dsv[4], yv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            dsv[k] = ds[(base + r + k) * N + c];
+            yv[k] = y[(base + r + k) * N + c];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float u = __fadd_rn(__fmul_rn(gm, yv[k]), bt);
+            const float du = __fmul_rn(dsv[k], cosf(u));
+            const float d = __fmul_rn(du, gm);
+            dy[(base + r + k) * N + c] = d;
+            sg = __fadd_rn(sg, __fmul_rn(du, yv[k]));
+            sb = __fadd_rn(sb, du);
+            sd = __fadd_rn(sd, d);
+        }
+    }
+    for (; r < r1; ++r) {
+        const float yv = y[(base + r) * N + c];
+        const float u = __fadd_rn(__fmul_rn(gm, yv), bt);
+        const float du = __fmul_rn(ds[(base + r) * N + c], cosf(u));
+        const float d = __fmul_rn(du, gm);
+        dy[(base + r) * N + c] = d;
+        sg = __fadd_rn(sg, __fmul_rn(du, yv));
+        sb = __fadd_rn(sb, du);
+        sd = __fadd_rn(sd, d);
+    }
+    float *p = part + ((size_t)f * gridDim.x + j) * 3 * N;
+    p[c] = sg;
+    p[N + c] = sb;
+    p[2 * N + c] = sd;
+}
+
+// per face f (block f): dgamma[f], dbeta[f], dbf[f] (the bias gradient's share of
+// face f) = the face's block partials summed in order
+__global__ void __launch_bounds__(256) film_bwd_reduce_kernel(const float *__restrict__ part,
+                                                              uint32_t nb, uint32_t N,
+                                                              float *__restrict__ dgamma,
+                                                              float *__restrict__ dbeta,
+                                                              float *__restrict__ dbf) {
+    const uint32_t f = blockIdx.x;
+    for (uint32_t c = threadIdx.x; c < N; c += 256) {
+        float sg = 0.0f, sb = 0.0f, sd = 0.0f;
+        for (uint32_t j = 0; j < nb; ++j) {
+            const float *p = part + ((size_t)f * nb + j) * 3 * N;
+            sg += p[c];
+            sb += p[N + c];
+            sd += p[2 * N + c];
+        }
+        dgamma[(size_t)f * N + c] = sg;
+        dbeta[(size_t)f * N + c] = sb;
+        dbf[(size_t)f * N + c] = sd;
     }
 }
 
@@ -367,11 +461,18 @@ uint32_t wgrad_rows(uint32_t M) {
     return r < 32 ? 32 : r;
 }
 
-template <int NT, int KS>
+template <int NT, int KS, bool FILM = false>
 int launch_fwd(const LinArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL((lin_fwd_kernel<NT, KS>), dim3(ceil_div(a.M, kLinRows)), dim3(kLinThreads),
-                       0, st, a);
+    hipLaunchKernelGGL((lin_fwd_kernel<NT, KS, FILM>), dim3(ceil_div(a.M, kLinRows)),
+                       dim3(kLinThreads), 0, st, a);
     return check_launch("linear_f16x3");
+}
+
+uint32_t film_blocks_per_face(uint32_t F, uint32_t rows_per_face) {
+    // ~512 blocks in all, at least 64 rows each
+    uint32_t nb = ceil_div(512, F);
+    const uint32_t maxb = ceil_div(rows_per_face, 64);
+    return nb < 1 ? 1 : (nb > maxb ? maxb : nb);
 }
 
 template <int KT>
@@ -406,6 +507,69 @@ int sdfr_linear_pack(const float *w, uint32_t N, uint32_t K, int transposed, voi
     hipLaunchKernelGGL(lin_pack_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, w, N, K,
                        transposed ? 1 : 0, su, reinterpret_cast<f4 *>(packed));
     return check_launch("linear_pack: pack");
+}
+
+int sdfr_film_linear_f16x3(float *out, float *y_save, const float *x, const void *packed,
+                           const float *bias, const float *gamma, const float *beta, uint32_t M,
+                           uint32_t N, uint32_t K, uint32_t rows_per_face, void *stream) {
+    if (M == 0) return SDFR_OK;
+    if (!out || !y_save || !x || !packed || !gamma || !beta)
+        return fail(SDFR_EINVAL, "film_linear_f16x3: null pointer");
+    if (rows_per_face == 0 || M % rows_per_face)
+        return fail(SDFR_EINVAL, "film_linear_f16x3: M must be a multiple of rows_per_face");
+    if (K % 4 || N != 256 ||
+        (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+         reinterpret_cast<uintptr_t>(y_save)) % 16)
+        return fail(SDFR_EINVAL, "film_linear_f16x3: N = 256, K multiple of 4, 16-B aligned rows");
+    LinArgs a;
+    a.x = x;
+    a.packed = static_cast<const f4 *>(packed);
+    a.su = reinterpret_cast<const float *>(static_cast<const char *>(packed) +
+                                           (size_t)ceil_div(K, 32) * 16 * kTileF4 * sizeof(f4));
+    a.bias = bias;
+    a.out = out;
+    a.M = M;
+    a.N = N;
+    a.K = K;
+    a.gamma = gamma;
+    a.beta = beta;
+    a.y_save = y_save;
+    a.rows_per_face = rows_per_face;
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t KS = ceil_div(K, 32);
+    if (KS == 8) return launch_fwd<16, 8, true>(a, st);
+    if (KS == 9) return launch_fwd<16, 9, true>(a, st);
+    return fail(SDFR_EUNSUPPORTED, "film_linear_f16x3: K must be <= 256 or 257..288");
+}
+
+size_t sdfr_film_backward_ws_bytes(uint32_t M, uint32_t N, uint32_t rows_per_face) {
+    if (M == 0 || rows_per_face == 0) return 0;
+    const uint32_t F = M / rows_per_face;
+    return (size_t)F * film_blocks_per_face(F, rows_per_face) * 3 * N * 4;
+}
+
+int sdfr_film_backward(float *dy, float *dgamma, float *dbeta, float *dbf, const float *ds,
+                       const float *y, const float *gamma, const float *beta, uint32_t M,
+                       uint32_t N, uint32_t rows_per_face, void *ws, size_t ws_bytes,
+                       void *stream) {
+    if (M == 0) return SDFR_OK;
+    if (!dy || !dgamma || !dbeta || !dbf || !ds || !y || !gamma || !beta)
+        return fail(SDFR_EINVAL, "film_backward: null pointer");
+    if (N != 256 || rows_per_face == 0 || M % rows_per_face)
+        return fail(SDFR_EINVAL, "film_backward: N = 256, M a multiple of rows_per_face");
+    if (!ws || ws_bytes < sdfr_film_backward_ws_bytes(M, N, rows_per_face))
+        return fail(SDFR_EINVAL, "film_backward: workspace too small");
+    const uint32_t F = M / rows_per_face, nb = film_blocks_per_face(F, rows_per_face);
+    const uint32_t rpb = ceil_div(rows_per_face, nb);
+    hipStream_t st = (hipStream_t)stream;
+    float *part = static_cast<float *>(ws);
+    hipLaunchKernelGGL(film_bwd_kernel, dim3(nb, F), dim3(256), 0, st, ds, y, gamma, beta, dy, N,
+                       rows_per_face, rpb, part);
+    int rc = check_launch("film_backward");
+    if (rc) return rc;
+    hipLaunchKernelGGL(film_bwd_reduce_kernel, dim3(F), dim3(256), 0, st, part, nb, N, dgamma,
+                       dbeta, dbf);
+    return check_launch("film_backward: reduce");
 }
 
 int sdfr_linear_f16x3(float *out, const float *x, const void *packed, const float *bias,

@@ -7,6 +7,8 @@ per chunk, forward and backward.  ``linear`` routes those products to the HIP
 kernels of ``csrc/linear_f16x3.hip`` (three fp16 MFMA terms per fp32 product,
 fp32 accumulation, power-of-two row / column scaling: fp32-level accuracy):
 
+  FiLM forward     s = sin(g (x W^T + b) + be) sdfr_film_linear_f16x3 (GEMM + epilogue)
+  FiLM backward    dy, dg, dbe, db             sdfr_film_backward (one elementwise pass)
   forward          out = x W^T + b             sdfr_linear_f16x3 (B = W)
   input gradient   gx  = gy W                  sdfr_linear_f16x3 (B = W^T)
   weight gradient  gW  = gy^T x                sdfr_linear_wgrad_f16x3
@@ -104,6 +106,73 @@ class _LinearF16x3(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = gy2.sum(0)
         return gx, gw, gb
+
+
+class _FiLMLinearF16x3(torch.autograd.Function):
+    """sin(gamma[f] * (x W^T + b) + beta[f]) over F faces of equal row count: the GEMM
+    with the FiLM activation in its epilogue (y = x W^T + b saved), and a backward whose
+    elementwise part is one HIP kernel (dy, dgamma, dbeta, db) before the two GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta):
+        N, K = weight.shape
+        F_ = gamma.shape[0]
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, K).contiguous()
+        M = x2.shape[0]
+        w = weight.contiguous()
+        g2, b2 = gamma.reshape(F_, N).contiguous(), beta.reshape(F_, N).contiguous()
+        out = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        _lib.check(_lib.lib().sdfr_film_linear_f16x3(
+            _lib.ptr(out), _lib.ptr(y), _lib.ptr(x2), _lib.ptr(_pack(w, False)),
+            _lib.ptr(bias.contiguous() if bias is not None else None), _lib.ptr(g2),
+            _lib.ptr(b2), M, N, K, M // F_, _lib.stream_of(x2)), "sdfr_film_linear_f16x3")
+        ctx.save_for_backward(x2, w, y, g2, b2)
+        ctx.meta = (lead, bias is not None, gamma.shape, beta.shape)
+        return out.view(*lead, N)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, ds):
+        x2, w, y, g2, b2 = ctx.saved_tensors
+        lead, has_bias, gshape, bshape = ctx.meta
+        N, K = w.shape
+        M, F_ = x2.shape[0], g2.shape[0]
+        ds2 = ds.reshape(-1, N).contiguous()
+        L = _lib.lib()
+        dy = torch.empty(M, N, device=ds.device, dtype=torch.float32)
+        dg = torch.empty(F_, N, device=ds.device, dtype=torch.float32)
+        db_ = torch.empty(F_, N, device=ds.device, dtype=torch.float32)
+        dbf = torch.empty(F_, N, device=ds.device, dtype=torch.float32)
+        nws = L.sdfr_film_backward_ws_bytes(M, N, M // F_)
+        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=ds.device)
+        _lib.check(L.sdfr_film_backward(
+            _lib.ptr(dy), _lib.ptr(dg), _lib.ptr(db_), _lib.ptr(dbf), _lib.ptr(ds2), _lib.ptr(y),
+            _lib.ptr(g2), _lib.ptr(b2), M, N, M // F_, _lib.ptr(ws), nws, _lib.stream_of(ds2)),
+            "sdfr_film_backward")
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = _gemm(dy, _pack(w, True), None, K).view(*lead, K)
+        if ctx.needs_input_grad[1]:
+            gw = _wgrad(dy, x2)
+        if has_bias and ctx.needs_input_grad[2]:
+            gb = dbf.sum(0)
+        gg = dg.view(gshape) if ctx.needs_input_grad[3] else None
+        gbt = db_.view(bshape) if ctx.needs_input_grad[4] else None
+        return gx, gw, gb, gg, gbt
+
+
+def film_linear(x, weight, bias, gamma, beta):
+    """FiLMSiren's ``sin(gamma * F.linear(x, weight, bias) + beta)`` (sdf_model.py:62-67),
+    gamma / beta [F, 1, ..., 1, N] broadcast over each face's samples: fused on the HIP
+    kernels for the renderer MLP's training shapes, the reference's ops otherwise."""
+    F_ = gamma.shape[0]
+    if (_routable(x, weight) and x.shape[0] == F_ and gamma.shape[-1] == weight.shape[0]
+            and gamma.numel() == F_ * weight.shape[0] and beta.shape == gamma.shape
+            and weight.shape[1] > 32):
+        return _FiLMLinearF16x3.apply(x, weight, bias, gamma, beta)
+    return torch.sin(gamma * linear(x, weight, bias) + beta)
 
 
 def _routable(x: torch.Tensor, weight: torch.Tensor) -> bool:

@@ -28,7 +28,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .encoders import GridEncoder, SHEncoder
-from .linear import linear
+from .linear import film_linear, linear
 
 
 # ---------------------------------------------------------------------------
@@ -81,11 +81,12 @@ class FiLMSiren(nn.Module):
 
     def forward(self, input, style):
         batch, features = style.shape
-        out = linear(input, self.weight, self.bias)
         shape = (batch,) + (1,) * (input.dim() - 2) + (features,)
         gamma = self.gamma(style).view(shape)
         beta = self.beta(style).view(shape)
-        return self.activation(gamma * out + beta)
+        # film_linear(): the reference's ops, or for the MLP's training shapes the GEMM
+        # with the activation fused on the HIP kernels (linear.py)
+        return film_linear(input, self.weight, self.bias, gamma, beta)
 
 
 # ---------------------------------------------------------------------------

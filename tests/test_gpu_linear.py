@@ -113,3 +113,36 @@ def test_stage1_gradients_kernels_vs_torch_gemm(sdfr, ngp):
         scale = float(ref.abs().max())
         err = float((got - ref).abs().max())
         assert err <= 2e-4 * scale + 1e-12, f"{k}: max |diff| {err:.3e} (max |g| {scale:.3e})"
+
+
+@pytest.mark.parametrize("F_,R,K", [(2, 1536, 256), (3, 700, 272)])
+def test_film_linear_vs_float64(sdfr, F_, R, K):
+    """FiLMSiren with the FiLM activation fused into the GEMM epilogue and its backward's
+    elementwise part in one kernel: sin(gamma (x W^T + b) + beta) and the gradients of
+    x, W, b, gamma, beta against float64 autograd of the reference's ops."""
+    from sdface_gan_amd.linear import _FiLMLinearF16x3
+    N = 256
+    x = (_rand((F_, R, K), "unit", 5) * 0.5).to(DEV).requires_grad_(True)
+    w = (_rand((N, K), "unit", 6) * 0.05).to(DEV).requires_grad_(True)
+    b = (_rand((N,), "unit", 7) * 0.1).to(DEV).requires_grad_(True)
+    gam = (30 + 15 * _rand((F_, 1, N), "unit", 8) * 0.2).to(DEV).requires_grad_(True)
+    bet = (0.25 * _rand((F_, 1, N), "unit", 9)).to(DEV).requires_grad_(True)
+    ds = _rand((F_, R, N), "unit", 10).to(DEV)
+    s = _FiLMLinearF16x3.apply(x, w, b, gam, bet)
+    s.backward(ds)
+    torch.cuda.synchronize()
+    xd, wd, bd, gd, btd = (t.detach().double().cpu().requires_grad_(True)
+                           for t in (x, w, b, gam, bet))
+    y = xd @ wd.t() + bd
+    sd = torch.sin(gd * y + btd)
+    sd.backward(ds.double().cpu())
+    # the sin argument is ~30x the GEMM output: compare through its own scale
+    yscale = (xd.detach().abs() @ wd.detach().abs().t() + bd.detach().abs())
+    arg_err = 64 * U * (gd.detach().abs() * yscale + btd.detach().abs()) + 4e-7
+    assert float(((s.detach().cpu().double() - sd.detach()).abs() - arg_err).max()) <= 0
+    for name, got, ref in (("x", x.grad, xd.grad), ("W", w.grad, wd.grad), ("b", b.grad, bd.grad),
+                           ("gamma", gam.grad, gd.grad), ("beta", bet.grad, btd.grad)):
+        ref = ref.detach()
+        err = float((got.cpu().double() - ref).abs().max())
+        scale = float(ref.abs().max())
+        assert err <= 2e-4 * scale, f"{name}: max |diff| {err:.3e} vs max |g| {scale:.3e}"
