@@ -67,7 +67,9 @@ int sdfr_grid_encode_forward(const float *inputs, const float *embeddings,
                              uint32_t interp, void *stream);
 
 /*   grad            [L, B, C]
- *   grad_embeddings [offsets[L], C], must be zeroed by the caller (grid.py:75)
+ *   grad_embeddings [offsets[L], C], must be zeroed by the caller (grid.py:75); may be
+ *                   NULL when grad_inputs is given (input gradient only: the eikonal
+ *                   term's pass, whose table gradient autograd.grad discards)
  *   dy_dx / grad_inputs: both NULL, or dy_dx [B, L*D*C] and grad_inputs [B, D]
  *   (grad_inputs is overwritten). */
 int sdfr_grid_encode_backward(const float *grad, const float *inputs,

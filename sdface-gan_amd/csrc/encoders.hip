@@ -668,7 +668,9 @@ static int grid_bwd_launch(const float *grad, const float *in, const int32_t *of
                            void *ws, size_t ws_bytes, hipStream_t st) {
     int rc = SDFR_OK;
     BinLevels bl;
-    if (ws && bin_levels<D, C>(B, L, bl) && ws_bytes >= bin_plan<C>(B, D, bl.n).bytes) {
+    if (!gemb) {
+        // input gradient only (grad_embeddings NULL): the table gradient is skipped
+    } else if (ws && bin_levels<D, C>(B, L, bl) && ws_bytes >= bin_plan<C>(B, D, bl.n).bytes) {
         // every level binned (the per-level table gradient above)
         rc = grid_bin_launch<D, C>(grad, in, off, gemb, B, lt, gt, ac, interp, bl, ws, st);
     } else {
@@ -923,7 +925,7 @@ int sdfr_grid_encode_backward_ws(const float *grad, const float *inputs, const f
     if (L == 0 || L > (uint32_t)kMaxLevels)
         return fail(SDFR_EINVAL, "GridEncoding: 1 <= L <= 64 levels supported.");
     if (B == 0) return SDFR_OK;
-    if (!grad || !inputs || !offsets || !grad_embeddings)
+    if (!grad || !inputs || !offsets || (!grad_embeddings && !grad_inputs))
         return fail(SDFR_EINVAL, "grid_encode_backward: null tensor pointer");
     if ((dy_dx == nullptr) != (grad_inputs == nullptr))
         return fail(SDFR_EINVAL, "grid_encode_backward: dy_dx and grad_inputs go together");

@@ -24,11 +24,12 @@
 // divided by su (gamma' x_scaled == gamma x, bit for bit), and NGP's identity
 // input layer multiplies by 1/su.
 //
-// Work unit: a wave owns 16 rays and evaluates TWO samples per pass (MFMA
-// N = 2 x 16), so each A fragment read from LDS feeds 6 MFMAs and the weight
-// stream (1.1 MB ngp / 2.1 MB siren per pass, shared by the 4 waves of a
-// workgroup through a 3-slot LDS ring) is amortised over 128 ray-samples.  The
-// accumulator of layer l is the B operand of layer l+1 with no lane movement:
+// Work unit (field_x2_kernel below): a workgroup of 8 waves, two per SIMD; a wave
+// owns one MFMA sample column of N = 16 = 8 rays x 2 samples, so each A fragment
+// read from LDS feeds 3 MFMAs, and the weight stream (1.1 MB ngp / 2.1 MB siren per
+// pass, shared by the 8 waves through a 4-slot LDS-DMA ring of 16 KB half-slices) is
+// amortised over 128 ray-samples.  The accumulator of layer l is the B operand of
+// layer l+1 with no lane movement:
 // after a pair of 16-row tiles (2q, 2q+1) is activated, its 8 values per lane
 // are split in place into (hi, lo) fp16x8, which is exactly the k-step q
 // fragment (the packed weights permute K to match, xprep_kernel).

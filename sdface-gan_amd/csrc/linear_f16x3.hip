@@ -28,14 +28,25 @@
 #include <cstdint>
 
 #include "f16x3.h"
+#include "render_ngp.h"
 #include "sdfr_common.h"
 
 namespace sdfr {
 namespace {
 
+// cos as sin_hw (render_ngp.h): 2 pi reduction by fma, then v_cos_f32 (revolutions)
+__device__ __forceinline__ float cos_hw(float x) {
+    constexpr float c_hi = 0.15915493667125702f;    // fl(1/(2pi))
+    constexpr float c_lo = 6.4206382432985265e-09f;  // 1/(2pi) - c_hi
+    const float k = __builtin_rintf(x * c_hi);
+    float f = __fmaf_rn(x, c_hi, -k);
+    f = __fmaf_rn(x, c_lo, f);
+    return __builtin_amdgcn_cosf(f);
+}
+
 constexpr uint32_t kLinWaves = 8;
 constexpr uint32_t kLinThreads = kLinWaves * 64;
-constexpr uint32_t kLinRows = kLinWaves * 16;          // rows of x per workgroup
+constexpr uint32_t kLinRows = 64;                      // rows of x per forward workgroup
 constexpr uint32_t kTileF4 = 128;                      // one 16-row tile: [hi,lo][64 lanes]
 
 __host__ __device__ constexpr uint32_t ceil_div(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
@@ -108,87 +119,98 @@ struct LinArgs {
 };
 
 template <int NT, int KS, bool FILM>
-__global__ void __launch_bounds__(kLinThreads, 2) lin_fwd_kernel(const LinArgs a) {
+__global__ void __launch_bounds__(kLinThreads, 4) lin_fwd_kernel(const LinArgs a) {
+    // 8 waves: 4 row groups of 16 rows x 2 halves of the NT output tiles, so a wave
+    // holds NTH accumulator tiles and two workgroups fit a CU (<= 128 VGPRs, 4 waves
+    // per SIMD hide the LDS and load latencies)
+    constexpr int NTH = (NT + 1) / 2;
     constexpr uint32_t kSliceF4 = NT * kTileF4;                 // one k-step of B
-    constexpr uint32_t kStage = ceil_div(kSliceF4, kLinThreads);
+    constexpr uint32_t kPieces = 2 * NT;                        // 1 KB LDS-DMA pieces
     __shared__ f4 ring[2][kSliceF4];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t rg = wave >> 1, nh = wave & 1u;
+    const uint32_t t_begin = nh * NTH;
+    const uint32_t t_count = NT - t_begin < (uint32_t)NTH ? NT - t_begin : NTH;
     const uint32_t n = lane & 15u, g = lane >> 4;
-    const uint32_t m = blockIdx.x * kLinRows + wave * 16 + n;
+    const uint32_t m = blockIdx.x * kLinRows + rg * 16 + n;
     const bool m_ok = m < a.M;
-
-    // this lane's K values of row m: k = 32 q + 8 g + j
-    float xv[KS][8];
     const float *xr = a.x + (size_t)(m_ok ? m : 0) * a.K;
-#pragma unroll
-    for (int q = 0; q < KS; ++q) {
+
+    // this lane's 8 K values of k-step q: k = 32 q + 8 g + j
+    auto load_x = [&](int q, float (&v)[8]) {
         const uint32_t k0 = 32 * q + 8 * g;
         if (m_ok && k0 + 8 <= a.K) {
             const f4 u = *reinterpret_cast<const f4 *>(xr + k0);
             const f4 w = *reinterpret_cast<const f4 *>(xr + k0 + 4);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                xv[q][j] = u[j];
-                xv[q][4 + j] = w[j];
+                v[j] = u[j];
+                v[4 + j] = w[j];
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) xv[q][j] = (m_ok && k0 + j < a.K) ? xr[k0 + j] : 0.0f;
+            for (int j = 0; j < 8; ++j) v[j] = (m_ok && k0 + j < a.K) ? xr[k0 + j] : 0.0f;
         }
-    }
-    // per-row power-of-two scale (the row's 4 lane groups hold all of its K)
+    };
+    // the B fragments of a slice by LDS-DMA (no VGPRs): pieces wave, wave + 8, ...
+    const v4i rs = make_rsrc(a.packed, KS * kSliceF4 * 16u);
+    auto dma_slice = [&](int q, uint32_t slot) {
+        for (uint32_t p = wave; p < kPieces; p += kLinWaves)
+            dma16(rs, lane * 16u, (uint32_t)((q * kSliceF4 + p * 64) * 16),
+                  lds_addr(&ring[slot][p * 64]));
+    };
+    dma_slice(0, 0);
+
+    // pass 1: the row's power-of-two scale (max |x_m| into [0.5, 1): the fp16 lo parts
+    // stay normal at any magnitude; the row's 4 lane groups hold all of its K)
     float mx = 0.0f;
 #pragma unroll
-    for (int q = 0; q < KS; ++q)
+    for (int q = 0; q < KS; ++q) {
+        float v[8];
+        load_x(q, v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(xv[q][j]));
+        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[j]));
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 16));
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     const float xs = pow2_scale(mx);
-#pragma unroll
-    for (int q = 0; q < KS; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv[q][j] = __fmul_rn(xv[q][j], xs);
 
-    // k-step 0 -> slot 0
-    f4 st[kStage];
-#pragma unroll
-    for (uint32_t i = 0; i < kStage; ++i) {
-        const uint32_t e = tid + i * kLinThreads;
-        if (e < kSliceF4) ring[0][e] = a.packed[e];
-    }
+    float xa[8];
+    load_x(0, xa);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    f4 acc[NT];
+    f4 acc[NTH];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int t = 0; t < NTH; ++t) acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int q = 0; q < KS; ++q) {
         const uint32_t slot = q & 1;
+        float xn[8];
         if (q + 1 < KS) {
-#pragma unroll
-            for (uint32_t i = 0; i < kStage; ++i) {
-                const uint32_t e = tid + i * kLinThreads;
-                if (e < kSliceF4) st[i] = a.packed[(size_t)(q + 1) * kSliceF4 + e];
-            }
+            dma_slice(q + 1, slot ^ 1u);          // slot^1 was last read before the barrier
+            load_x(q + 1, xn);
         }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xa[j] = __fmul_rn(xa[j], xs);
         f4 bh, bl;
-        split8(xv[q], bh, bl);
-        const f4 *A = ring[slot] + lane;
+        split8(xa, bh, bl);
+        const f4 *A = ring[slot] + t_begin * kTileF4 + lane;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const f4 ah = A[t * kTileF4], al = A[t * kTileF4 + 64];
-            acc[t] = mfma16(al, bh, acc[t]);
-            acc[t] = mfma16(ah, bl, acc[t]);
-            acc[t] = mfma16(ah, bh, acc[t]);
+        for (int t = 0; t < NTH; ++t) {
+            if (t < (int)t_count) {
+                const f4 ah = A[t * kTileF4], al = A[t * kTileF4 + 64];
+                acc[t] = mfma16(al, bh, acc[t]);
+                acc[t] = mfma16(ah, bl, acc[t]);
+                acc[t] = mfma16(ah, bh, acc[t]);
+            }
         }
         if (q + 1 < KS) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of q+1 landed
+            __syncthreads();                                     // everyone's; slot free
 #pragma unroll
-            for (uint32_t i = 0; i < kStage; ++i) {
-                const uint32_t e = tid + i * kLinThreads;
-                if (e < kSliceF4) ring[slot ^ 1][e] = st[i];
-            }
-            __syncthreads();
+            for (int j = 0; j < 8; ++j) xa[j] = xn[j];
         }
     }
     if (!m_ok) return;
@@ -197,7 +219,9 @@ __global__ void __launch_bounds__(kLinThreads, 2) lin_fwd_kernel(const LinArgs a
     float *orow = a.out + (size_t)m * a.N;
     const size_t frow = FILM ? (size_t)(m / a.rows_per_face) * a.N : 0;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
+    for (int tt = 0; tt < NTH; ++tt) {
+        if (tt >= (int)t_count) continue;
+        const int t = (int)t_begin + tt;
         const uint32_t c0 = 16 * t + 4 * g;
         if (c0 >= a.N) continue;
         f4 v, yv;
@@ -205,7 +229,7 @@ __global__ void __launch_bounds__(kLinThreads, 2) lin_fwd_kernel(const LinArgs a
         for (int r = 0; r < 4; ++r) {
             const uint32_t c = c0 + r;
             const float s = c < a.N ? a.su[c] : 1.0f;
-            float y = __fmul_rn(__fmul_rn(acc[t][r], inv_xs), 1.0f / s);
+            float y = __fmul_rn(__fmul_rn(acc[tt][r], inv_xs), 1.0f / s);
             if (a.bias && c < a.N) y = __fadd_rn(y, a.bias[c]);
             yv[r] = y;
             if constexpr (FILM) {
@@ -213,7 +237,7 @@ __global__ void __launch_bounds__(kLinThreads, 2) lin_fwd_kernel(const LinArgs a
                 // rounding per op as the reference's separate elementwise ops
                 const float gm = c < a.N ? a.gamma[frow + c] : 0.0f;
                 const float bt = c < a.N ? a.beta[frow + c] : 0.0f;
-                v[r] = sinf(__fadd_rn(__fmul_rn(gm, y), bt));
+                v[r] = sin_hw(__fadd_rn(__fmul_rn(gm, y), bt));
             } else {
                 v[r] = y;
             }
@@ -261,7 +285,7 @@ __global__ void __launch_bounds__(256) film_bwd_kernel(const float *__restrict__
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const float u = __fadd_rn(__fmul_rn(gm, yv[k]), bt);
-            const float du = __fmul_rn(dsv[k], cosf(u));
+            const float du = __fmul_rn(dsv[k], cos_hw(u));
             const float d = __fmul_rn(du, gm);
             dy[(base + r + k) * N + c] = d;
             sg = __fadd_rn(sg, __fmul_rn(du, yv[k]));
@@ -272,7 +296,7 @@ __global__ void __launch_bounds__(256) film_bwd_kernel(const float *__restrict__
     for (; r < r1; ++r) {
         const float yv = y[(base + r) * N + c];
         const float u = __fadd_rn(__fmul_rn(gm, yv), bt);
-        const float du = __fmul_rn(ds[(base + r) * N + c], cosf(u));
+        const float du = __fmul_rn(ds[(base + r) * N + c], cos_hw(u));
         const float d = __fmul_rn(du, gm);
         dy[(base + r) * N + c] = d;
         sg = __fadd_rn(sg, __fmul_rn(du, yv));
@@ -285,21 +309,33 @@ __global__ void __launch_bounds__(256) film_bwd_kernel(const float *__restrict__
     p[2 * N + c] = sd;
 }
 
-// per face f (block f): dgamma[f], dbeta[f], dbf[f] (the bias gradient's share of
-// face f) = the face's block partials summed in order
+// per face f: dgamma[f], dbeta[f], dbf[f] (the bias gradient's share of face f) =
+// the face's block partials summed in a fixed order: block (32 columns, f), thread
+// (column, group jg of the blocks j = jg mod 8), the 8 group sums added in order
 __global__ void __launch_bounds__(256) film_bwd_reduce_kernel(const float *__restrict__ part,
                                                               uint32_t nb, uint32_t N,
                                                               float *__restrict__ dgamma,
                                                               float *__restrict__ dbeta,
                                                               float *__restrict__ dbf) {
-    const uint32_t f = blockIdx.x;
-    for (uint32_t c = threadIdx.x; c < N; c += 256) {
-        float sg = 0.0f, sb = 0.0f, sd = 0.0f;
-        for (uint32_t j = 0; j < nb; ++j) {
-            const float *p = part + ((size_t)f * nb + j) * 3 * N;
-            sg += p[c];
-            sb += p[N + c];
-            sd += p[2 * N + c];
+    __shared__ float red[3][8][32];
+    const uint32_t f = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31u);
+    const uint32_t jg = threadIdx.x >> 5;
+    float sg = 0.0f, sb = 0.0f, sd = 0.0f;
+    for (uint32_t j = jg; j < nb; j += 8) {
+        const float *p = part + ((size_t)f * nb + j) * 3 * N;
+        sg += p[c];
+        sb += p[N + c];
+        sd += p[2 * N + c];
+    }
+    red[0][jg][threadIdx.x & 31u] = sg;
+    red[1][jg][threadIdx.x & 31u] = sb;
+    red[2][jg][threadIdx.x & 31u] = sd;
+    __syncthreads();
+    if (jg == 0) {
+        for (uint32_t k = 1; k < 8; ++k) {
+            sg += red[0][k][threadIdx.x];
+            sb += red[1][k][threadIdx.x];
+            sd += red[2][k][threadIdx.x];
         }
         dgamma[(size_t)f * N + c] = sg;
         dbeta[(size_t)f * N + c] = sb;
@@ -308,17 +344,46 @@ __global__ void __launch_bounds__(256) film_bwd_reduce_kernel(const float *__res
 }
 
 // ----------------------------------------------------------------------------
-// column maxima: cmax[c] = max_m |x[m, c]| (as uint bits: order-free, exact)
+// column maxima: cmax[c] = max_m |x[m, c]| (as uint bits: order-free, exact).
+// Thread = (column quad, row slot): 16-B loads, the block's row slots combined in LDS.
 // ----------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) lin_colmax_kernel(const float *__restrict__ x, uint32_t M,
                                                          uint32_t C, uint32_t rows_per_block,
                                                          uint32_t *__restrict__ cmax) {
+    __shared__ f4 red[256];
+    const uint32_t nq = C / 4, slots = 256 / nq;           // C % 4 == 0, C <= 1024
+    const uint32_t t = threadIdx.x, q = t % nq, slot = t / nq;
     const uint32_t m0 = blockIdx.x * rows_per_block;
     const uint32_t m1 = min(M, m0 + rows_per_block);
-    for (uint32_t c = threadIdx.x; c < C; c += 256) {
-        float mx = 0.0f;
-        for (uint32_t m = m0; m < m1; ++m) mx = fmaxf(mx, fabsf(x[(size_t)m * C + c]));
-        atomicMax(cmax + c, __float_as_uint(mx));
+    f4 mx = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (slot < slots) {
+        const f4 *src = reinterpret_cast<const f4 *>(x) + q;
+        uint32_t m = m0 + slot;
+        for (; m + 3 * slots < m1; m += 4 * slots) {
+            f4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = src[(size_t)(m + k * slots) * nq];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mx[r] = fmaxf(mx[r], fabsf(v[k][r]));
+        }
+        for (; m < m1; m += slots) {
+            const f4 v = src[(size_t)m * nq];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mx[r] = fmaxf(mx[r], fabsf(v[r]));
+        }
+    }
+    red[t] = mx;
+    __syncthreads();
+    if (slot == 0) {
+        for (uint32_t s2 = 1; s2 < slots; ++s2) {
+            const f4 o = red[s2 * nq + q];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mx[r] = fmaxf(mx[r], o[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicMax(cmax + 4 * q + r, __float_as_uint(mx[r]));
     }
 }
 
@@ -567,8 +632,8 @@ int sdfr_film_backward(float *dy, float *dgamma, float *dbeta, float *dbf, const
                        rows_per_face, rpb, part);
     int rc = check_launch("film_backward");
     if (rc) return rc;
-    hipLaunchKernelGGL(film_bwd_reduce_kernel, dim3(F), dim3(256), 0, st, part, nb, N, dgamma,
-                       dbeta, dbf);
+    hipLaunchKernelGGL(film_bwd_reduce_kernel, dim3(N / 32, F), dim3(256), 0, st, part, nb, N,
+                       dgamma, dbeta, dbf);
     return check_launch("film_backward: reduce");
 }
 
@@ -610,8 +675,11 @@ size_t sdfr_linear_wgrad_ws_bytes(uint32_t M, uint32_t N, uint32_t K) {
 int sdfr_linear_wgrad_f16x3(float *gw, const float *dy, const float *x, uint32_t M, uint32_t N,
                             uint32_t K, void *ws, size_t ws_bytes, void *stream) {
     if (!gw || (M && (!dy || !x))) return fail(SDFR_EINVAL, "linear_wgrad_f16x3: null pointer");
-    if (N != 256 || K == 0 || K > 288)
-        return fail(SDFR_EUNSUPPORTED, "linear_wgrad_f16x3: N must be 256 and K <= 288");
+    if (N != 256 || K == 0 || K > 288 || K % 4)
+        return fail(SDFR_EUNSUPPORTED,
+                    "linear_wgrad_f16x3: N must be 256 and K <= 288 a multiple of 4");
+    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) % 16)
+        return fail(SDFR_EINVAL, "linear_wgrad_f16x3: 16-B aligned rows required");
     hipStream_t st = (hipStream_t)stream;
     if (M == 0) {
         if (hipMemsetAsync(gw, 0, (size_t)N * K * 4, st) != hipSuccess)
@@ -626,7 +694,7 @@ int sdfr_linear_wgrad_f16x3(float *gw, const float *dy, const float *x, uint32_t
                                             ((size_t)(N + Kp) * 4 + 255) / 256 * 256);
     if (hipMemsetAsync(cmax, 0, (size_t)(N + Kp) * 4, st) != hipSuccess)
         return fail(SDFR_ELAUNCH, "linear_wgrad_f16x3: memset");
-    const uint32_t rpb = 256;
+    const uint32_t rpb = ceil_div(ceil_div(M, 512), 8) * 8;     // ~512 blocks
     hipLaunchKernelGGL(lin_colmax_kernel, dim3(ceil_div(M, rpb)), dim3(256), 0, st, dy, M, N, rpb,
                        cmax);
     hipLaunchKernelGGL(lin_colmax_kernel, dim3(ceil_div(M, rpb)), dim3(256), 0, st, x, M, K, rpb,

@@ -29,6 +29,25 @@ def _check_cuda(t: torch.Tensor, name: str):
         raise RuntimeError(f"{name} must be a CUDA tensor")
 
 
+_INPUT_GRAD_ONLY = [False]
+
+
+class input_grad_only:
+    """Context for an autograd.grad call that asks for the grid encoder's INPUT
+    gradient only (VolumeFeatureRenderer.get_eikonal_term, sdf_model.py:224-229):
+    the reference's backward also computes the table gradient there, which
+    autograd.grad then discards; here it is not computed.  Process-wide while active
+    (the autograd engine may run the backward on its device thread)."""
+
+    def __enter__(self):
+        self.prev = _INPUT_GRAD_ONLY[0]
+        _INPUT_GRAD_ONLY[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _INPUT_GRAD_ONLY[0] = self.prev
+
+
 class _GridEncode(Function):
     @staticmethod
     def forward(ctx, inputs, embeddings, offsets, per_level_scale, base_resolution,
@@ -62,11 +81,15 @@ class _GridEncode(Function):
         inputs, embeddings, offsets, dy_dx = ctx.saved_tensors
         B, D, C, L, S, H, gridtype, interpolation, align_corners = ctx.dims
         grad = grad.view(B, L, C).permute(1, 0, 2).contiguous()
-        grad_embeddings = torch.zeros_like(embeddings)
         grad_inputs = torch.zeros_like(inputs, dtype=embeddings.dtype) if dy_dx is not None else None
+        # inside input_grad_only() (the eikonal term's autograd.grad, which returns the
+        # points' gradient only) the table gradient would be discarded: skip it
+        skip = _INPUT_GRAD_ONLY[0] and grad_inputs is not None
+        grad_embeddings = None if skip else torch.zeros_like(embeddings)
         # binned table gradient (csrc/encoders.hip) in a workspace from torch's allocator
         L_ = _lib.lib()
-        wsb = L_.sdfr_grid_encode_backward_ws_bytes(B, D, C, L, S, H, int(align_corners))
+        wsb = 0 if skip else L_.sdfr_grid_encode_backward_ws_bytes(B, D, C, L, S, H,
+                                                                   int(align_corners))
         ws = torch.empty(wsb, dtype=torch.uint8, device=grad.device) if wsb else None
         _lib.check(L_.sdfr_grid_encode_backward_ws(
             _lib.ptr(grad), _lib.ptr(inputs), _lib.ptr(embeddings), _lib.ptr(offsets),

@@ -19,10 +19,12 @@ Shapes the kernels take: out features 256 with in features 32 / 256 / 259..288
 3- and 1-wide heads, the per-face gamma / beta layers on the styles, CPU tensors,
 inference) stays on F.linear.  ``set_train_gemm("torch")`` turns the routing off.
 
-The backward is first-order only (``once_differentiable``): SDFace-GAN never
-differentiates through it twice -- the eikonal term leaves autograd inside the
-grid encoder's backward (grid.py:65-89), so it carries no gradient (as in the
-reference), and R1 / path-length regularisation touch only D and the decoder.
+The backward is first-order only (``once_differentiable``), so only the ngp network
+routes here (``NGPSIRENGenerator`` marks its layers ``train_kernels = True``): its
+eikonal term leaves autograd inside the grid encoder's backward (grid.py:65-89) and
+carries no gradient (as in the reference), so nothing differentiates these ops twice.
+The SIREN network's eikonal loss does reach its weights through a double backward
+(the points feed the MLP directly), so SirenGenerator keeps F.linear.
 """
 from __future__ import annotations
 
@@ -163,16 +165,17 @@ class _FiLMLinearF16x3(torch.autograd.Function):
         return gx, gw, gb, gg, gbt
 
 
-def film_linear(x, weight, bias, gamma, beta):
+def film_linear(x, weight, bias, gamma, beta, kernels=True):
     """FiLMSiren's ``sin(gamma * F.linear(x, weight, bias) + beta)`` (sdf_model.py:62-67),
     gamma / beta [F, 1, ..., 1, N] broadcast over each face's samples: fused on the HIP
-    kernels for the renderer MLP's training shapes, the reference's ops otherwise."""
+    kernels for the renderer MLP's training shapes (and ``kernels``), the reference's
+    ops otherwise."""
     F_ = gamma.shape[0]
-    if (_routable(x, weight) and x.shape[0] == F_ and gamma.shape[-1] == weight.shape[0]
+    if (kernels and _routable(x, weight) and x.shape[0] == F_ and gamma.shape[-1] == weight.shape[0]
             and gamma.numel() == F_ * weight.shape[0] and beta.shape == gamma.shape
             and weight.shape[1] > 32):
         return _FiLMLinearF16x3.apply(x, weight, bias, gamma, beta)
-    return torch.sin(gamma * linear(x, weight, bias) + beta)
+    return torch.sin(gamma * linear(x, weight, bias, kernels) + beta)
 
 
 def _routable(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -186,9 +189,9 @@ def _routable(x: torch.Tensor, weight: torch.Tensor) -> bool:
     return x.numel() // K >= 1024            # the per-face gamma / beta layers stay on F.linear
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, kernels=True) -> torch.Tensor:
     """F.linear(x, weight, bias), on the split-fp16 MFMA kernels for the renderer MLP's
-    training shapes (module docstring), on F.linear otherwise."""
-    if _routable(x, weight):
+    training shapes (module docstring) when ``kernels``, on F.linear otherwise."""
+    if kernels and _routable(x, weight):
         return _LinearF16x3.apply(x, weight, bias)
     return F.linear(x, weight, bias)

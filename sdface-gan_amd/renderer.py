@@ -27,7 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .encoders import GridEncoder, SHEncoder
+from .encoders import GridEncoder, SHEncoder, input_grad_only
 from .linear import film_linear, linear
 
 
@@ -54,14 +54,20 @@ class LinearLayer(nn.Module):
         self.bias_init = bias_init
         self.std_init = std_init
 
+    # the ngp network's layers take the training kernels (linear.py); others F.linear
+    train_kernels = False
+
     def forward(self, input):
         # linear(): F.linear, or the split-fp16 MFMA kernels for the renderer MLP's
         # training shapes (linear.py)
-        return self.std_init * linear(input, self.weight, self.bias) + self.bias_init
+        return self.std_init * linear(input, self.weight, self.bias,
+                                      self.train_kernels) + self.bias_init
 
 
 class FiLMSiren(nn.Module):
     """``sin(gamma(style) * (x W^T + b) + beta(style))`` (sdf_model.py:44-69)."""
+
+    train_kernels = False         # set by NGPSIRENGenerator (linear.py)
 
     def __init__(self, in_channel, out_channel, style_dim, is_first=False):
         super().__init__()
@@ -85,8 +91,8 @@ class FiLMSiren(nn.Module):
         gamma = self.gamma(style).view(shape)
         beta = self.beta(style).view(shape)
         # film_linear(): the reference's ops, or for the MLP's training shapes the GEMM
-        # with the activation fused on the HIP kernels (linear.py)
-        return film_linear(input, self.weight, self.bias, gamma, beta)
+        # with the activation fused on the HIP kernels (linear.py, ngp network only)
+        return film_linear(input, self.weight, self.bias, gamma, beta, self.train_kernels)
 
 
 # ---------------------------------------------------------------------------
@@ -163,6 +169,10 @@ class NGPSIRENGenerator(nn.Module):
         self.views_linears = FiLMSiren(self.in_dim_dir + self.W, self.W, style_dim=style_dim)
         self.rgb_linear = LinearLayer(self.W, 3, freq_init=True)
         self.sigma_linear = LinearLayer(W, 1, freq_init=True)
+        # training GEMMs on the split-fp16 kernels (first-order backward suffices here:
+        # the eikonal term leaves autograd in the grid encoder's backward, linear.py)
+        for m in [self.input_linear, *self.pts_linears, self.views_linears]:
+            m.train_kernels = True
 
     def forward(self, x, styles):
         pts, views = torch.split(x, [self.input_ch, self.input_ch_views], dim=-1)
@@ -333,8 +343,10 @@ class VolumeFeatureRenderer(nn.Module):
         return rays_o, rays_d, viewdirs
 
     def get_eikonal_term(self, pts, sdf):
-        return autograd.grad(outputs=sdf, inputs=pts, grad_outputs=torch.ones_like(sdf),
-                             create_graph=True)[0]
+        # only d sdf / d pts is returned: the grid encoder skips its table gradient
+        with input_grad_only():
+            return autograd.grad(outputs=sdf, inputs=pts, grad_outputs=torch.ones_like(sdf),
+                                 create_graph=True)[0]
 
     def sdf_activation(self, input):
         return torch.sigmoid(input / self.sigmoid_beta) / self.sigmoid_beta

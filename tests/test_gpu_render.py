@@ -271,7 +271,8 @@ def test_generator_vs_reference_golden(sdfr, golden_dir):
         rgb, thumb = g([t("z")], t("ext"), t("focal"), t("near"), t("far"),
                        randomize_noise=False, t_rand=torch.from_numpy(z["t_rand"]))
     _cmp("generator", "thumb", thumb.cpu().numpy(), z["thumb"], "rgb")
-    # the 256^2 image goes through the PyTorch-ROCm decoder on top (MIOpen fp32)
+    # the 256^2 image: the fused HIP decoder on top (split-fp16 implicit-GEMM convolutions
+    # with the styled epilogues, csrc/conv_f16x3.hip, csrc/decoder.hip)
     _cmp("generator", "image", rgb.cpu().numpy(), z["rgb"])
 
 

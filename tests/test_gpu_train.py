@@ -241,7 +241,7 @@ def test_ngp_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path):
 def test_renderer_grads_survive_frozen_decoder(sdfr):
     """Grad enabled, decoder frozen, renderer trainable: the decoder takes
     its autograd path (not the fused inference path) so the renderer gets gradients."""
-    opt = sdfr.vol_render_opt(train_renderer=True)
+    opt = sdfr.vol_render_opt()                      # full pipeline (features out)
     torch.manual_seed(0)
     g = sdfr.Generator(opt.model, opt.rendering).to(DEV)
     g.is_train, g.train_renderer = True, True
