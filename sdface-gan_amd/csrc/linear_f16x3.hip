@@ -388,8 +388,15 @@ __global__ void __launch_bounds__(256) lin_colmax_kernel(const float *__restrict
 }
 
 // ----------------------------------------------------------------------------
-// weight gradient partials: part[p][n][k] = sum over the workgroup's rows of
-// dy[m, n] x[m, k]; N = 256 (wave w: n-tiles 2w, 2w+1), KT k-tiles of 16
+// weight gradient partials: part[p][n][k] = sum over workgroup p's rows of
+// dy[m, n] x[m, k] (N = 256; blockIdx.y = which 128 of the n).  16 waves in two roles
+// per 32-row m-step, double-buffered in LDS with one barrier per step:
+//   waves 8..15 (producers): load the next step's dy[32 x 128] and x[32 x K] (loads
+//     issued a step ahead), scale by the column's power of two, split into hi/lo
+//     fp16 and store them as MFMA fragments (m = the MFMA K dimension);
+//   waves 0..7 (consumers): 2 n-tiles x one half of the k-tiles each, 3 MFMAs per
+//     fragment pair, accumulated in fp32 over the workgroup's rows.
+// The conversion VALU of the producers runs beside the consumers' MFMAs on every SIMD.
 // ----------------------------------------------------------------------------
 struct WgradArgs {
     const float *dy;           // [M, N]
@@ -400,113 +407,142 @@ struct WgradArgs {
     uint32_t M, N, K, rows;    // rows per workgroup (multiple of 32)
 };
 
+constexpr uint32_t kWgWaves = 16, kWgThreads = kWgWaves * 64;
+
 template <int KT>
-__global__ void __launch_bounds__(kLinThreads, 1) lin_wgrad_kernel(const WgradArgs a) {
-    constexpr uint32_t NTn = 16;                            // N = 256
+__global__ void __launch_bounds__(kWgThreads) lin_wgrad_kernel(const WgradArgs a) {
+    constexpr uint32_t NTn = 8;                             // n-tiles per workgroup
+    constexpr uint32_t KH = (KT + 1) / 2;                   // k-tiles per consumer wave
     constexpr uint32_t kA = NTn * kTileF4, kB = KT * kTileF4;
+    constexpr uint32_t kTasks = (NTn + KT) * 16 * 4;        // (row group, column) per step
+    constexpr uint32_t kPer = ceil_div(kTasks, 512);        // per producer thread
     __shared__ f4 As[2][kA];
     __shared__ f4 Bs[2][kB];
-    __shared__ float sd[256], sx[KT * 16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    __shared__ float sd[NTn * 16], sx[KT * 16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t n0 = blockIdx.y * NTn * 16;
     const uint32_t m_begin = blockIdx.x * a.rows;
     const uint32_t m_end = min(a.M, m_begin + a.rows);
-    for (uint32_t c = tid; c < 256; c += kLinThreads) sd[c] = pow2_scale(__uint_as_float(a.cmax_dy[c]));
-    for (uint32_t c = tid; c < KT * 16; c += kLinThreads)
+    for (uint32_t c = tid; c < NTn * 16; c += kWgThreads)
+        sd[c] = pow2_scale(__uint_as_float(a.cmax_dy[n0 + c]));
+    for (uint32_t c = tid; c < KT * 16; c += kWgThreads)
         sx[c] = c < a.K ? pow2_scale(__uint_as_float(a.cmax_x[c])) : 1.0f;
     __syncthreads();
+    const uint32_t nsteps = ceil_div(m_end > m_begin ? m_end - m_begin : 0, 32);
+    const bool producer = wave >= 8;
 
-    // staging tasks per m-step: (row group g8 of 8 rows, column c) -> one lane of one
-    // fragment tile, columns fastest (a wave's load of one row is 64 consecutive
-    // floats): dy tasks [0, 4 x 256), x tasks [.., + 4 x 16 KT)
-    constexpr uint32_t kTasks = (NTn + KT) * 16 * 4;
-    constexpr uint32_t kPer = ceil_div(kTasks, kLinThreads);
-    float stv[kPer][8];
+    // ---- producer: task = (row group g8, column c), columns fastest
+    const uint32_t ptid = tid - 512;
     auto task_of = [&](uint32_t task, bool &is_dy, uint32_t &c, uint32_t &g8) {
         is_dy = task < NTn * 64;
         const uint32_t tt = is_dy ? task : task - NTn * 64;
         const uint32_t width = is_dy ? NTn * 16 : KT * 16;
         g8 = tt / width;
-        c = tt % width;
+        c = tt - g8 * width;
     };
-    auto load = [&](uint32_t m0) {
+    float stv[kPer][8];
+    auto load = [&](uint32_t step) {
+        const uint32_t m0 = m_begin + 32 * step;
 #pragma unroll
         for (uint32_t i = 0; i < kPer; ++i) {
-            const uint32_t task = tid + i * kLinThreads;
+            const uint32_t task = ptid + i * 512;
             bool is_dy;
             uint32_t c, g8;
             task_of(task, is_dy, c, g8);
+            const bool tok = task < kTasks && (is_dy || c < a.K);
+            const float *src = is_dy ? a.dy + n0 + c : a.x + c;
             const uint32_t C = is_dy ? a.N : a.K;
-            const float *src = is_dy ? a.dy : a.x;
-            const float s = task < kTasks ? (is_dy ? sd[c] : sx[c < KT * 16 ? c : 0]) : 0.0f;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t m = m0 + 8 * g8 + j;
-                const bool ok = task < kTasks && c < C && m < m_end;
-                stv[i][j] = ok ? __fmul_rn(src[(size_t)m * C + c], s) : 0.0f;
+                stv[i][j] = (tok && m < m_end) ? src[(size_t)m * C] : 0.0f;
             }
         }
     };
     auto store = [&](uint32_t slot) {
 #pragma unroll
         for (uint32_t i = 0; i < kPer; ++i) {
-            const uint32_t task = tid + i * kLinThreads;
+            const uint32_t task = ptid + i * 512;
             if (task >= kTasks) continue;
             bool is_dy;
             uint32_t c, g8;
             task_of(task, is_dy, c, g8);
-            const uint32_t l = (g8 << 4) | (c & 15u);
+            const float sc = is_dy ? sd[c] : sx[c];
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = __fmul_rn(stv[i][j], sc);
             f4 hi, lo;
-            split8(stv[i], hi, lo);
-            f4 *dst = (is_dy ? As[slot] : Bs[slot]) + (c >> 4) * kTileF4 + l;
+            split8(v, hi, lo);
+            f4 *dst = (is_dy ? As[slot] : Bs[slot]) + (c >> 4) * kTileF4 + ((g8 << 4) | (c & 15u));
             dst[0] = hi;
             dst[64] = lo;
         }
     };
 
-    f4 acc[2][KT];
+    if (producer) {
+        // (each role runs its own loop with the same barriers, one per step, so the
+        // compiler never holds both roles' registers at once)
+        if (nsteps > 0) {
+            load(0);
+            store(0);
+            if (nsteps > 1) load(1);
+        }
+        __syncthreads();
+        for (uint32_t s = 0; s < nsteps; ++s) {
+            if (s + 1 < nsteps) {
+                store((s & 1u) ^ 1u);                  // step s+1 (loaded a step ago)
+                if (s + 2 < nsteps) load(s + 2);
+            }
+            __syncthreads();
+        }
+        return;
+    }
+
+    // ---- consumer: n-tiles 2 (w & 3), +1; k-tiles [KH (w >> 2), ...)
+    const uint32_t np = wave & 3u, kh = (wave >> 2) & 1u;
+    const uint32_t k_begin = kh * KH;
+    const uint32_t k_count = KT - k_begin < KH ? KT - k_begin : KH;
+    f4 acc[2][KH];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int t = 0; t < KT; ++t) acc[i][t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    const uint32_t nsteps = ceil_div(m_end > m_begin ? m_end - m_begin : 0, 32);
-    if (nsteps > 0) {
-        load(m_begin);
-        store(0);
-    }
+        for (uint32_t t = 0; t < KH; ++t) acc[i][t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
     __syncthreads();
     for (uint32_t s = 0; s < nsteps; ++s) {
         const uint32_t slot = s & 1u;
-        if (s + 1 < nsteps) load(m_begin + 32 * (s + 1));
-        const f4 *A = As[slot] + (2 * wave) * kTileF4 + lane;
+        const f4 *A = As[slot] + (2 * np) * kTileF4 + lane;
         const f4 a0h = A[0], a0l = A[64], a1h = A[kTileF4], a1l = A[kTileF4 + 64];
-        const f4 *Bp = Bs[slot] + lane;
+        const f4 *Bp = Bs[slot] + k_begin * kTileF4 + lane;
 #pragma unroll
-        for (int t = 0; t < KT; ++t) {
-            const f4 bh = Bp[t * kTileF4], bl = Bp[t * kTileF4 + 64];
-            acc[0][t] = mfma16(a0l, bh, acc[0][t]);
-            acc[1][t] = mfma16(a1l, bh, acc[1][t]);
-            acc[0][t] = mfma16(a0h, bl, acc[0][t]);
-            acc[1][t] = mfma16(a1h, bl, acc[1][t]);
-            acc[0][t] = mfma16(a0h, bh, acc[0][t]);
-            acc[1][t] = mfma16(a1h, bh, acc[1][t]);
+        for (uint32_t t = 0; t < KH; ++t) {
+            if (t < k_count) {
+                const f4 bh = Bp[t * kTileF4], bl = Bp[t * kTileF4 + 64];
+                acc[0][t] = mfma16(a0l, bh, acc[0][t]);
+                acc[1][t] = mfma16(a1l, bh, acc[1][t]);
+                acc[0][t] = mfma16(a0h, bl, acc[0][t]);
+                acc[1][t] = mfma16(a1h, bl, acc[1][t]);
+                acc[0][t] = mfma16(a0h, bh, acc[0][t]);
+                acc[1][t] = mfma16(a1h, bh, acc[1][t]);
+            }
         }
-        if (s + 1 < nsteps) store(slot ^ 1u);
         __syncthreads();
     }
-    // lane (kc = lane & 15, g) of (n-tile i, k-tile t) holds n = 16 (2 wave + i) + 4 g + r,
+    // lane (kc = lane & 15, g) of (n-tile i, k-tile t) holds n = 16 (2 np + i) + 4 g + r,
     // k = 16 t + kc; unscale (exact) and store the partial
     const uint32_t kc = lane & 15u, g = lane >> 4;
     float *pp = a.part + (size_t)blockIdx.x * a.N * a.K;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int t = 0; t < KT; ++t) {
-            const uint32_t k = 16 * t + kc;
+        for (uint32_t t = 0; t < KH; ++t) {
+            if (t >= k_count) continue;
+            const uint32_t k = 16 * (k_begin + t) + kc;
             if (k >= a.K) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const uint32_t nn = 16 * (2 * wave + i) + 4 * g + r;
-                pp[(size_t)nn * a.K + k] = __fmul_rn(acc[i][t][r], 1.0f / (sd[nn] * sx[k]));
+                const uint32_t nl = 16 * (2 * np + i) + 4 * g + r;
+                pp[(size_t)(n0 + nl) * a.K + k] = __fmul_rn(acc[i][t][r], 1.0f / (sd[nl] * sx[k]));
             }
         }
 }
@@ -521,8 +557,8 @@ __global__ void __launch_bounds__(256) lin_reduce_kernel(const float *__restrict
 }
 
 uint32_t wgrad_rows(uint32_t M) {
-    // at most 256 workgroups (one round on the 256 CUs, 256 partials), whole m-steps
-    const uint32_t r = ceil_div(ceil_div(M, 256), 32) * 32;
+    // 128 row ranges x 2 n-halves = one round of 256 workgroups, whole m-steps
+    const uint32_t r = ceil_div(ceil_div(M, 128), 32) * 32;
     return r < 32 ? 32 : r;
 }
 
@@ -542,7 +578,7 @@ uint32_t film_blocks_per_face(uint32_t F, uint32_t rows_per_face) {
 
 template <int KT>
 int launch_wgrad(const WgradArgs &a, uint32_t P, hipStream_t st) {
-    hipLaunchKernelGGL((lin_wgrad_kernel<KT>), dim3(P), dim3(kLinThreads), 0, st, a);
+    hipLaunchKernelGGL((lin_wgrad_kernel<KT>), dim3(P, 2), dim3(kWgThreads), 0, st, a);
     return check_launch("linear_wgrad_f16x3");
 }
 
