@@ -274,7 +274,8 @@ int sdfr_camera_extrinsics(const float *azim, const float *elev, uint32_t B, flo
  * and of their autograd backward, on the op-by-op path stage-1 training takes,
  * training_utils.py:396-451).  Split-fp16 MFMA, fp32 accumulation, fp32-level
  * accuracy (rows / columns scaled by powers of two so no fp16 lo part goes
- * subnormal).  Row-major fp32 tensors, 16-B aligned rows.
+ * subnormal).  Row-major fp32 tensors; x, out, y_save 16-B aligned, and bias,
+ * gamma, beta (read as 16-B vectors) 16-B aligned.
  *
  * sdfr_linear_pack: B [N,K] = w (transposed = 0; w is [N,K]) or w^T (transposed = 1;
  *   w is [K,N]) -> sdfr_linear_pack_bytes(N, K) bytes of split fragments + row scales.
@@ -283,7 +284,9 @@ int sdfr_camera_extrinsics(const float *azim, const float *elev, uint32_t B, flo
  *   <= 256 | <= 288) or (N <= 32 | <= 256 | <= 272, K <= 256), N and K multiples of 4.
  * sdfr_linear_wgrad_f16x3: gw [N,K] = dy[M,N]^T . x[M,K] (weight gradient), N = 256,
  *   K <= 288; ws >= sdfr_linear_wgrad_ws_bytes(M, N, K).  The sum over M is split
- *   over workgroups and their partials added in a fixed order (deterministic).
+ *   over workgroups and their partials added in a fixed order (deterministic); each
+ *   workgroup scales a column by the running maximum of the rows it has read, so
+ *   dy and x are each read once (no separate column-maximum pass).
  * ------------------------------------------------------------------------- */
 size_t sdfr_linear_pack_bytes(uint32_t N, uint32_t K);
 int sdfr_linear_pack(const float *w, uint32_t N, uint32_t K, int transposed, void *packed,

@@ -294,9 +294,9 @@ grid_bwd_lds_kernel(const float *__restrict__ grad, const float *__restrict__ in
 //   exclusive_scan_u32        counts, laid out [level][bin][block], -> offsets
 //   grid_bin_scatter_kernel   recompute the entries, counting-sort them per
 //                             block in LDS, write each bin's run contiguously
-//   grid_bin_plan_kernel      cut every bin into work items of <= kBinChunk
-//                             entries (a coarse level's single bin holds all
-//                             of its B x 8 entries; a hashed bin ~B x 8 / 32)
+//   grid_bin_plan_kernel      cut every bin into work items (bin_chunk: a
+//                             coarse level's single bin holds all of its B x 8
+//                             entries; a hashed bin ~B x 8 / 32)
 //   grid_bin_accum_kernel     per item: LDS window sums -> table, plain
 //                             read-modify-write when the item is its whole bin
 //                             (rows owned by one workgroup), else atomics on
@@ -460,7 +460,19 @@ grid_bin_scatter_kernel(const float *__restrict__ grad, const float *__restrict_
     }
 }
 
-constexpr uint32_t kBinChunk = 1u << 20;      // entries per work item (at most)
+// Entries per work item: bins are cut into pieces of ~2x the mean bin size, at
+// least kBinChunkMin and at most kBinChunkMax entries.  A coarse level's single
+// bin holds all of its B x 8 entries while a hashed bin holds ~B x 8 / 32, so at a
+// training chunk (~196 K samples) a fixed 1 M cut left two items per coarse level
+// -- a few CUs summing 1 M entries each while the rest idled.  Splitting costs one
+// atomic write-back of the window per extra item, so hashed bins (near the mean)
+// stay whole and keep the plain read-modify-write.
+constexpr uint32_t kBinChunkMin = 1u << 16;
+constexpr uint32_t kBinChunkMax = 1u << 20;
+static uint32_t bin_chunk(uint64_t E, uint32_t npairs) {
+    const uint64_t c = 2 * E / std::max<uint32_t>(npairs, 1u);
+    return (uint32_t)std::min<uint64_t>(kBinChunkMax, std::max<uint64_t>(kBinChunkMin, c));
+}
 
 struct BinItem {
     uint32_t pair;     // level index * kBinCount + bin
@@ -468,10 +480,10 @@ struct BinItem {
     uint32_t whole;    // the item is its bin's only one
 };
 
-// one workgroup: cut each (level, bin) entry run into items of <= kBinChunk
+// one workgroup: cut each (level, bin) entry run into items of <= chunk entries
 __global__ void __launch_bounds__(kScanThreads)
 grid_bin_plan_kernel(const uint32_t *__restrict__ ofs, uint32_t nblk, uint32_t npairs,
-                     BinItem *__restrict__ items, uint32_t *__restrict__ nitems) {
+                     uint32_t chunk, BinItem *__restrict__ items, uint32_t *__restrict__ nitems) {
     uint32_t carry = 0;
     for (uint32_t p0 = 0; p0 < npairs; p0 += kScanThreads) {
         const uint32_t p = p0 + threadIdx.x;
@@ -479,13 +491,13 @@ grid_bin_plan_kernel(const uint32_t *__restrict__ ofs, uint32_t nblk, uint32_t n
         if (p < npairs) {
             s = ofs[(size_t)p * nblk];
             e = ofs[(size_t)(p + 1) * nblk];
-            n = (e - s + kBinChunk - 1) / kBinChunk;
+            n = (e - s + chunk - 1) / chunk;
         }
         uint32_t ex;
         const uint32_t tot = block_exscan(n, ex);
         for (uint32_t k = 0; k < n; ++k) {
-            const uint32_t a = s + k * kBinChunk;
-            items[carry + ex + k] = BinItem{p, a, min(e, a + kBinChunk), n == 1 ? 1u : 0u};
+            const uint32_t a = s + k * chunk;
+            items[carry + ex + k] = BinItem{p, a, min(e, a + chunk), n == 1 ? 1u : 0u};
         }
         carry += tot;
     }
@@ -547,7 +559,7 @@ grid_bin_accum_kernel(const int32_t *__restrict__ offsets, const LevelTable lt, 
 // workspace of the binned path: counts [n_b][32][nblk] + 1, scan scratch,
 // entries, work items
 struct BinPlan {
-    uint32_t nblk, n, max_items;
+    uint32_t nblk, n, max_items, chunk;
     uint64_t M, E;
     size_t cnt_off, bsum_off, row_off, val_off, item_off, nitem_off, bytes;
 };
@@ -565,7 +577,8 @@ static BinPlan bin_plan(uint32_t B, uint32_t D, uint32_t n_b) {
     p.bsum_off = align256((p.M + 1) * sizeof(uint32_t));
     p.row_off = p.bsum_off + align256((size_t)scan_block_sums(p.M) * sizeof(uint32_t));
     p.val_off = p.row_off + align256(p.E * sizeof(uint32_t));
-    p.max_items = (uint32_t)(n_b * kBinCount + (p.E + kBinChunk - 1) / kBinChunk);
+    p.chunk = bin_chunk(p.E, n_b * kBinCount);
+    p.max_items = (uint32_t)(n_b * kBinCount + (p.E + p.chunk - 1) / p.chunk);
     p.item_off = p.val_off + align256(p.E * C * sizeof(float));
     p.nitem_off = p.item_off + align256((size_t)p.max_items * sizeof(BinItem));
     p.bytes = p.nitem_off + 256;
@@ -651,7 +664,7 @@ static int grid_bin_launch(const float *grad, const float *in, const int32_t *of
         BinItem *items = (BinItem *)(w + p.item_off);
         uint32_t *nitems = (uint32_t *)(w + p.nitem_off);
         hipLaunchKernelGGL(grid_bin_plan_kernel, dim3(1), dim3(kScanThreads), 0, st, cnt, p.nblk,
-                           bl.n * kBinCount, items, nitems);
+                           bl.n * kBinCount, p.chunk, items, nitems);
         hipLaunchKernelGGL((grid_bin_accum_kernel<C>), dim3(p.max_items), dim3(kBinAccThreads),
                            kBinLdsBytes, st, off, lt, D, gt, ac, bl, items, nitems, e_row, e_val,
                            gemb);

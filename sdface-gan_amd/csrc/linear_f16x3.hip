@@ -9,20 +9,22 @@
 //                            forward (B = W) and input gradient (B = W^T, no bias)
 //   sdfr_linear_wgrad_f16x3  gw[N,K] = sum_m dy[m,n] x[m,k]   (weight gradient)
 //
-// Forward / input gradient: a workgroup is 8 waves over 128 rows of x (16 per wave:
-// MFMA N = 16 columns = rows m of x); a wave holds its 16 rows' K values in
-// registers, scales each row by a power of two (max |x_m| into [0.5, 1): the fp16
-// lo parts stay normal at any magnitude, activations and gradients alike) and splits
-// them per k-step; the B fragments (pre-split, row-scaled by su[n], packed in MFMA
-// A-fragment order by sdfr_linear_pack) stream through a two-slot LDS ring shared by
-// the 8 waves.  Outputs accumulate in fp32 and are unscaled exactly.
+// Forward / input gradient: a workgroup is 8 waves over 64 rows of x (16 per wave:
+// MFMA N = 16 columns = rows m of x; two waves per row group, one half of the output
+// tiles each); a lane loads its row's K values into registers up front, scales the
+// row by a power of two (max |x_m| into [0.5, 1): the fp16 lo parts stay normal at any
+// magnitude, activations and gradients alike) and splits them per k-step; the B
+// fragments (pre-split, row-scaled by su[n], packed in MFMA A-fragment order by
+// sdfr_linear_pack) stream through a two-slot LDS ring by LDS-DMA.  Outputs
+// accumulate in fp32 and are unscaled exactly.
 //
 // Weight gradient: the sum over m is split over workgroups (a contiguous range of
 // rows each), each accumulating an [N,K] partial in fp32; a second kernel adds the
 // partials in a fixed order (deterministic).  Every column of dy and of x is scaled
-// by a power of two from its maximum over all M (column-max kernel), the scales are
-// undone exactly on the partials.  Per m-step of 32 rows both operands are staged
-// transposed into LDS as split-fp16 MFMA fragments.
+// by a power of two from its running maximum over the workgroup's rows (the
+// accumulators are rescaled exactly when a scale shrinks), so the operands are read
+// once.  Per m-step of 32 rows both operands are staged into LDS as split-fp16 MFMA
+// fragments.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -118,11 +120,26 @@ struct LinArgs {
     uint32_t rows_per_face;
 };
 
+// a buffer resource over `bytes` bytes at `base`: loads past the end return zeros
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes,
+                                             0x00020000);
+}
+constexpr uint32_t kOob = 0x80000000u;                  // a buffer offset that reads zeros
+
+__device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ float ld1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+
 template <int NT, int KS, bool FILM>
-__global__ void __launch_bounds__(kLinThreads, 4) lin_fwd_kernel(const LinArgs a) {
-    // 8 waves: 4 row groups of 16 rows x 2 halves of the NT output tiles, so a wave
-    // holds NTH accumulator tiles and two workgroups fit a CU (<= 128 VGPRs, 4 waves
-    // per SIMD hide the LDS and load latencies)
+__global__ void __launch_bounds__(kLinThreads, 2) lin_fwd_kernel(const LinArgs a) {
+    // 8 waves: 4 row groups of 16 rows x 2 halves of the NT output tiles.  A lane holds
+    // its row's 8 K values of every k-step in registers, all loaded up front (branch-free
+    // buffer loads: rows past M and columns past K read zeros), so x is read from HBM
+    // once and the loads of one workgroup overlap the MFMAs of the other on the CU
     constexpr int NTH = (NT + 1) / 2;
     constexpr uint32_t kSliceF4 = NT * kTileF4;                 // one k-step of B
     constexpr uint32_t kPieces = 2 * NT;                        // 1 KB LDS-DMA pieces
@@ -133,26 +150,11 @@ __global__ void __launch_bounds__(kLinThreads, 4) lin_fwd_kernel(const LinArgs a
     const uint32_t t_begin = nh * NTH;
     const uint32_t t_count = NT - t_begin < (uint32_t)NTH ? NT - t_begin : NTH;
     const uint32_t n = lane & 15u, g = lane >> 4;
-    const uint32_t m = blockIdx.x * kLinRows + rg * 16 + n;
-    const bool m_ok = m < a.M;
-    const float *xr = a.x + (size_t)(m_ok ? m : 0) * a.K;
+    const uint32_t m_blk = blockIdx.x * kLinRows;
+    const uint32_t rows = a.M - m_blk < kLinRows ? a.M - m_blk : kLinRows;
+    const uint32_t r_in = rg * 16 + n;
+    const uint32_t m = m_blk + r_in;
 
-    // this lane's 8 K values of k-step q: k = 32 q + 8 g + j
-    auto load_x = [&](int q, float (&v)[8]) {
-        const uint32_t k0 = 32 * q + 8 * g;
-        if (m_ok && k0 + 8 <= a.K) {
-            const f4 u = *reinterpret_cast<const f4 *>(xr + k0);
-            const f4 w = *reinterpret_cast<const f4 *>(xr + k0 + 4);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                v[j] = u[j];
-                v[4 + j] = w[j];
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (m_ok && k0 + j < a.K) ? xr[k0 + j] : 0.0f;
-        }
-    };
     // the B fragments of a slice by LDS-DMA (no VGPRs): pieces wave, wave + 8, ...
     const v4i rs = make_rsrc(a.packed, KS * kSliceF4 * 16u);
     auto dma_slice = [&](int q, uint32_t slot) {
@@ -162,22 +164,27 @@ __global__ void __launch_bounds__(kLinThreads, 4) lin_fwd_kernel(const LinArgs a
     };
     dma_slice(0, 0);
 
-    // pass 1: the row's power-of-two scale (max |x_m| into [0.5, 1): the fp16 lo parts
-    // stay normal at any magnitude; the row's 4 lane groups hold all of its K)
-    float mx = 0.0f;
+    const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x + (size_t)m_blk * a.K, rows * a.K * 4u);
+    f4 xv[KS][2];
 #pragma unroll
     for (int q = 0; q < KS; ++q) {
-        float v[8];
-        load_x(q, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[j]));
+        const uint32_t k0 = 32 * q + 8 * g;
+        const uint32_t off = (r_in * a.K + k0) * 4u;
+        xv[q][0] = ld4(xr, k0 + 4 <= a.K ? off : kOob);
+        xv[q][1] = ld4(xr, k0 + 8 <= a.K ? off + 16 : kOob);
     }
+    // the row's power-of-two scale (max |x_m| into [0.5, 1): the fp16 lo parts stay
+    // normal at any magnitude; the row's 4 lane groups hold all of its K)
+    float mx = 0.0f;
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mx = fmaxf(mx, fabsf(xv[q][h][j]));
     mx = fmaxf(mx, __shfl_xor(mx, 16));
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     const float xs = pow2_scale(mx);
-
-    float xa[8];
-    load_x(0, xa);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
@@ -187,15 +194,15 @@ __global__ void __launch_bounds__(kLinThreads, 4) lin_fwd_kernel(const LinArgs a
 #pragma unroll
     for (int q = 0; q < KS; ++q) {
         const uint32_t slot = q & 1;
-        float xn[8];
-        if (q + 1 < KS) {
-            dma_slice(q + 1, slot ^ 1u);          // slot^1 was last read before the barrier
-            load_x(q + 1, xn);
-        }
+        if (q + 1 < KS) dma_slice(q + 1, slot ^ 1u);   // slot^1 was last read before the barrier
+        float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xa[j] = __fmul_rn(xa[j], xs);
+        for (int j = 0; j < 4; ++j) {
+            v[j] = __fmul_rn(xv[q][0][j], xs);
+            v[4 + j] = __fmul_rn(xv[q][1][j], xs);
+        }
         f4 bh, bl;
-        split8(xa, bh, bl);
+        split8(v, bh, bl);
         const f4 *A = ring[slot] + t_begin * kTileF4 + lane;
 #pragma unroll
         for (int t = 0; t < NTH; ++t) {
@@ -209,50 +216,40 @@ __global__ void __launch_bounds__(kLinThreads, 4) lin_fwd_kernel(const LinArgs a
         if (q + 1 < KS) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of q+1 landed
             __syncthreads();                                     // everyone's; slot free
-#pragma unroll
-            for (int j = 0; j < 8; ++j) xa[j] = xn[j];
         }
     }
-    if (!m_ok) return;
-    // lane (n, g) of tile t holds output columns 16 t + 4 g + r of row m
+    if (r_in >= rows) return;
+    // lane (n, g) of tile t holds output columns 16 t + 4 g + r of row m (N % 4 == 0,
+    // so a quad is wholly inside or outside N)
     const float inv_xs = 1.0f / xs;                        // powers of two: exact
     float *orow = a.out + (size_t)m * a.N;
     const size_t frow = FILM ? (size_t)(m / a.rows_per_face) * a.N : 0;
 #pragma unroll
     for (int tt = 0; tt < NTH; ++tt) {
         if (tt >= (int)t_count) continue;
-        const int t = (int)t_begin + tt;
-        const uint32_t c0 = 16 * t + 4 * g;
+        const uint32_t c0 = 16 * (t_begin + tt) + 4 * g;
         if (c0 >= a.N) continue;
-        f4 v, yv;
+        const f4 s4 = *reinterpret_cast<const f4 *>(a.su + c0);
+        const f4 b4 = a.bias ? *reinterpret_cast<const f4 *>(a.bias + c0) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+        f4 yv, v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const uint32_t c = c0 + r;
-            const float s = c < a.N ? a.su[c] : 1.0f;
-            float y = __fmul_rn(__fmul_rn(acc[tt][r], inv_xs), 1.0f / s);
-            if (a.bias && c < a.N) y = __fadd_rn(y, a.bias[c]);
+            float y = __fmul_rn(__fmul_rn(acc[tt][r], inv_xs), 1.0f / s4[r]);
+            if (a.bias) y = __fadd_rn(y, b4[r]);
             yv[r] = y;
-            if constexpr (FILM) {
-                // FiLMSiren.forward (sdf_model.py:62-67): sin(gamma * out + beta), one
-                // rounding per op as the reference's separate elementwise ops
-                const float gm = c < a.N ? a.gamma[frow + c] : 0.0f;
-                const float bt = c < a.N ? a.beta[frow + c] : 0.0f;
-                v[r] = sin_hw(__fadd_rn(__fmul_rn(gm, y), bt));
-            } else {
-                v[r] = y;
-            }
         }
-        if (c0 + 4 <= a.N) {
-            *reinterpret_cast<f4 *>(orow + c0) = v;
-            if constexpr (FILM) *reinterpret_cast<f4 *>(a.y_save + (size_t)m * a.N + c0) = yv;
-        } else {
+        if constexpr (FILM) {
+            // FiLMSiren.forward (sdf_model.py:62-67): sin(gamma * out + beta), one
+            // rounding per op as the reference's separate elementwise ops
+            const f4 gm = *reinterpret_cast<const f4 *>(a.gamma + frow + c0);
+            const f4 bt = *reinterpret_cast<const f4 *>(a.beta + frow + c0);
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (c0 + r < a.N) {
-                    orow[c0 + r] = v[r];
-                    if constexpr (FILM) a.y_save[(size_t)m * a.N + c0 + r] = yv[r];
-                }
+            for (int r = 0; r < 4; ++r) v[r] = sin_hw(__fadd_rn(__fmul_rn(gm[r], yv[r]), bt[r]));
+            *reinterpret_cast<f4 *>(a.y_save + (size_t)m * a.N + c0) = yv;
+        } else {
+            v = yv;
         }
+        *reinterpret_cast<f4 *>(orow + c0) = v;
     }
 }
 
@@ -344,65 +341,27 @@ __global__ void __launch_bounds__(256) film_bwd_reduce_kernel(const float *__res
 }
 
 // ----------------------------------------------------------------------------
-// column maxima: cmax[c] = max_m |x[m, c]| (as uint bits: order-free, exact).
-// Thread = (column quad, row slot): 16-B loads, the block's row slots combined in LDS.
-// ----------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) lin_colmax_kernel(const float *__restrict__ x, uint32_t M,
-                                                         uint32_t C, uint32_t rows_per_block,
-                                                         uint32_t *__restrict__ cmax) {
-    __shared__ f4 red[256];
-    const uint32_t nq = C / 4, slots = 256 / nq;           // C % 4 == 0, C <= 1024
-    const uint32_t t = threadIdx.x, q = t % nq, slot = t / nq;
-    const uint32_t m0 = blockIdx.x * rows_per_block;
-    const uint32_t m1 = min(M, m0 + rows_per_block);
-    f4 mx = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (slot < slots) {
-        const f4 *src = reinterpret_cast<const f4 *>(x) + q;
-        uint32_t m = m0 + slot;
-        for (; m + 3 * slots < m1; m += 4 * slots) {
-            f4 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = src[(size_t)(m + k * slots) * nq];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) mx[r] = fmaxf(mx[r], fabsf(v[k][r]));
-        }
-        for (; m < m1; m += slots) {
-            const f4 v = src[(size_t)m * nq];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mx[r] = fmaxf(mx[r], fabsf(v[r]));
-        }
-    }
-    red[t] = mx;
-    __syncthreads();
-    if (slot == 0) {
-        for (uint32_t s2 = 1; s2 < slots; ++s2) {
-            const f4 o = red[s2 * nq + q];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mx[r] = fmaxf(mx[r], o[r]);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) atomicMax(cmax + 4 * q + r, __float_as_uint(mx[r]));
-    }
-}
-
-// ----------------------------------------------------------------------------
 // weight gradient partials: part[p][n][k] = sum over workgroup p's rows of
 // dy[m, n] x[m, k] (N = 256; blockIdx.y = which 128 of the n).  16 waves in two roles
 // per 32-row m-step, double-buffered in LDS with one barrier per step:
-//   waves 8..15 (producers): load the next step's dy[32 x 128] and x[32 x K] (loads
-//     issued a step ahead), scale by the column's power of two, split into hi/lo
-//     fp16 and store them as MFMA fragments (m = the MFMA K dimension);
+//   waves 8..15 (producers): one 16-column tile of dy or x per wave and task; a lane
+//     loads 8 rows of one column (a step ahead; branch-free buffer loads, rows past the
+//     workgroup's range and columns past K read zeros), which is exactly its MFMA
+//     fragment; it scales the column by a power of two from the column's running
+//     maximum over the rows seen so far, splits into hi/lo fp16 and stores the
+//     fragments;
 //   waves 0..7 (consumers): 2 n-tiles x one half of the k-tiles each, 3 MFMAs per
 //     fragment pair, accumulated in fp32 over the workgroup's rows.
+// The running maxima only grow, so a column's scale only shrinks (or leaves 1 when the
+// column had been all zero): when a step changes scales the producers publish the
+// ratios and the consumers rescale their accumulators exactly (powers of two, <= 1)
+// before adding the step; the last scales are undone on the partial.  No pass over
+// the operands beyond the one that feeds the MFMAs.
 // The conversion VALU of the producers runs beside the consumers' MFMAs on every SIMD.
 // ----------------------------------------------------------------------------
 struct WgradArgs {
     const float *dy;           // [M, N]
     const float *x;            // [M, K]
-    const uint32_t *cmax_dy;   // [N] float bits
-    const uint32_t *cmax_x;    // [K]
     float *part;               // [P][N][K]
     uint32_t M, N, K, rows;    // rows per workgroup (multiple of 32)
 };
@@ -414,73 +373,79 @@ __global__ void __launch_bounds__(kWgThreads) lin_wgrad_kernel(const WgradArgs a
     constexpr uint32_t NTn = 8;                             // n-tiles per workgroup
     constexpr uint32_t KH = (KT + 1) / 2;                   // k-tiles per consumer wave
     constexpr uint32_t kA = NTn * kTileF4, kB = KT * kTileF4;
-    constexpr uint32_t kTasks = (NTn + KT) * 16 * 4;        // (row group, column) per step
-    constexpr uint32_t kPer = ceil_div(kTasks, 512);        // per producer thread
+    constexpr uint32_t kCols = (NTn + KT) * 16;             // dy columns, then x columns
+    constexpr uint32_t kPer = ceil_div(NTn + KT, 8);        // tiles per producer wave
     __shared__ f4 As[2][kA];
     __shared__ f4 Bs[2][kB];
-    __shared__ float sd[NTn * 16], sx[KT * 16];
+    __shared__ float ratio[2][kCols];                       // scale change of the step
+    __shared__ float fin[kCols];                            // the last scales
+    __shared__ uint32_t chg[2][8];                          // per producer wave: any change
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t n0 = blockIdx.y * NTn * 16;
     const uint32_t m_begin = blockIdx.x * a.rows;
-    const uint32_t m_end = min(a.M, m_begin + a.rows);
-    for (uint32_t c = tid; c < NTn * 16; c += kWgThreads)
-        sd[c] = pow2_scale(__uint_as_float(a.cmax_dy[n0 + c]));
-    for (uint32_t c = tid; c < KT * 16; c += kWgThreads)
-        sx[c] = c < a.K ? pow2_scale(__uint_as_float(a.cmax_x[c])) : 1.0f;
-    __syncthreads();
-    const uint32_t nsteps = ceil_div(m_end > m_begin ? m_end - m_begin : 0, 32);
-    const bool producer = wave >= 8;
+    const uint32_t nrows = m_begin < a.M ? min(a.rows, a.M - m_begin) : 0;
+    const uint32_t nsteps = ceil_div(nrows, 32);
 
-    // ---- producer: task = (row group g8, column c), columns fastest
-    const uint32_t ptid = tid - 512;
-    auto task_of = [&](uint32_t task, bool &is_dy, uint32_t &c, uint32_t &g8) {
-        is_dy = task < NTn * 64;
-        const uint32_t tt = is_dy ? task : task - NTn * 64;
-        const uint32_t width = is_dy ? NTn * 16 : KT * 16;
-        g8 = tt / width;
-        c = tt - g8 * width;
-    };
-    float stv[kPer][8];
-    auto load = [&](uint32_t step) {
-        const uint32_t m0 = m_begin + 32 * step;
+    if (wave >= 8) {
+        // ---- producer wave pw: tiles pw, pw + 8, ... (tile < 8: dy columns n0 + 16 tile
+        // .., else x columns 16 (tile - 8) ..); lane = (column c = lane & 15, rows 8 g8 ..)
+        const uint32_t pw = wave - 8, c = lane & 15u, g8 = lane >> 4;
+        const __amdgpu_buffer_rsrc_t rdy = buf_rsrc(a.dy + (size_t)m_begin * a.N, nrows * a.N * 4u);
+        const __amdgpu_buffer_rsrc_t rx = buf_rsrc(a.x + (size_t)m_begin * a.K, nrows * a.K * 4u);
+        float stv[kPer][8];
+        float rmax[kPer], scl[kPer];
 #pragma unroll
         for (uint32_t i = 0; i < kPer; ++i) {
-            const uint32_t task = ptid + i * 512;
-            bool is_dy;
-            uint32_t c, g8;
-            task_of(task, is_dy, c, g8);
-            const bool tok = task < kTasks && (is_dy || c < a.K);
-            const float *src = is_dy ? a.dy + n0 + c : a.x + c;
-            const uint32_t C = is_dy ? a.N : a.K;
+            rmax[i] = 0.0f;
+            scl[i] = 1.0f;
+        }
+        auto load = [&](uint32_t step) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t m = m0 + 8 * g8 + j;
-                stv[i][j] = (tok && m < m_end) ? src[(size_t)m * C] : 0.0f;
+            for (uint32_t i = 0; i < kPer; ++i) {
+                const uint32_t tile = pw + 8 * i;
+                const bool is_dy = tile < NTn;              // (i == 0)
+                const uint32_t col = is_dy ? n0 + 16 * tile + c : 16 * (tile - NTn) + c;
+                const uint32_t C = is_dy ? a.N : a.K;
+                const bool ok = tile < NTn + KT && (is_dy || col < a.K);
+                const uint32_t r0 = 32 * step + 8 * g8;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t off = ok ? ((r0 + j) * C + col) * 4u : kOob;
+                    stv[i][j] = ld1(is_dy ? rdy : rx, off);
+                }
             }
-        }
-    };
-    auto store = [&](uint32_t slot) {
+        };
+        auto store = [&](uint32_t slot) {
+            bool any = false;
 #pragma unroll
-        for (uint32_t i = 0; i < kPer; ++i) {
-            const uint32_t task = ptid + i * 512;
-            if (task >= kTasks) continue;
-            bool is_dy;
-            uint32_t c, g8;
-            task_of(task, is_dy, c, g8);
-            const float sc = is_dy ? sd[c] : sx[c];
-            float v[8];
+            for (uint32_t i = 0; i < kPer; ++i) {
+                const uint32_t tile = pw + 8 * i;
+                if (tile >= NTn + KT) continue;             // wave-uniform
+                float mx = 0.0f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = __fmul_rn(stv[i][j], sc);
-            f4 hi, lo;
-            split8(v, hi, lo);
-            f4 *dst = (is_dy ? As[slot] : Bs[slot]) + (c >> 4) * kTileF4 + ((g8 << 4) | (c & 15u));
-            dst[0] = hi;
-            dst[64] = lo;
-        }
-    };
-
-    if (producer) {
+                for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(stv[i][j]));
+                mx = fmaxf(mx, __shfl_xor(mx, 16));
+                mx = fmaxf(mx, __shfl_xor(mx, 32));
+                rmax[i] = fmaxf(rmax[i], mx);
+                const float sn = pow2_scale(rmax[i]);
+                const float rt = sn / scl[i];               // powers of two: exact
+                any |= rt != 1.0f;
+                scl[i] = sn;
+                if (g8 == 0) ratio[slot][16 * tile + c] = rt;
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = __fmul_rn(stv[i][j], sn);
+                f4 hi, lo;
+                split8(v, hi, lo);
+                f4 *dst = (tile < NTn ? As[slot] + tile * kTileF4
+                                      : Bs[slot] + (tile - NTn) * kTileF4) + lane;
+                dst[0] = hi;
+                dst[64] = lo;
+            }
+            const uint32_t anyw = __builtin_amdgcn_readfirstlane(__any(any) ? 1u : 0u);
+            if (lane == 0) chg[slot][pw] = anyw;
+        };
         // (each role runs its own loop with the same barriers, one per step, so the
         // compiler never holds both roles' registers at once)
         if (nsteps > 0) {
@@ -496,6 +461,12 @@ __global__ void __launch_bounds__(kWgThreads) lin_wgrad_kernel(const WgradArgs a
             }
             __syncthreads();
         }
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint32_t tile = pw + 8 * i;
+            if (tile < NTn + KT && g8 == 0) fin[16 * tile + c] = scl[i];
+        }
+        __syncthreads();
         return;
     }
 
@@ -503,6 +474,7 @@ __global__ void __launch_bounds__(kWgThreads) lin_wgrad_kernel(const WgradArgs a
     const uint32_t np = wave & 3u, kh = (wave >> 2) & 1u;
     const uint32_t k_begin = kh * KH;
     const uint32_t k_count = KT - k_begin < KH ? KT - k_begin : KH;
+    const uint32_t kc = lane & 15u, g = lane >> 4;
     f4 acc[2][KH];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -511,6 +483,25 @@ __global__ void __launch_bounds__(kWgThreads) lin_wgrad_kernel(const WgradArgs a
     __syncthreads();
     for (uint32_t s = 0; s < nsteps; ++s) {
         const uint32_t slot = s & 1u;
+        const uint4 c0 = *reinterpret_cast<const uint4 *>(&chg[slot][0]);
+        const uint4 c1 = *reinterpret_cast<const uint4 *>(&chg[slot][4]);
+        if (s > 0 && (c0.x | c0.y | c0.z | c0.w | c1.x | c1.y | c1.z | c1.w)) {
+            // lane (kc, g) of (n-tile i, k-tile t) holds n = 16 (2 np + i) + 4 g + r,
+            // k = 16 (k_begin + t) + kc
+            f4 rn[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                rn[i] = *reinterpret_cast<const f4 *>(&ratio[slot][16 * (2 * np + i) + 4 * g]);
+#pragma unroll
+            for (uint32_t t = 0; t < KH; ++t) {
+                const float rk = t < k_count ? ratio[slot][NTn * 16 + 16 * (k_begin + t) + kc] : 1.0f;
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[i][t][r] = __fmul_rn(__fmul_rn(acc[i][t][r], rn[i][r]), rk);
+            }
+        }
         const f4 *A = As[slot] + (2 * np) * kTileF4 + lane;
         const f4 a0h = A[0], a0l = A[64], a1h = A[kTileF4], a1l = A[kTileF4 + 64];
         const f4 *Bp = Bs[slot] + k_begin * kTileF4 + lane;
@@ -528,23 +519,25 @@ __global__ void __launch_bounds__(kWgThreads) lin_wgrad_kernel(const WgradArgs a
         }
         __syncthreads();
     }
-    // lane (kc = lane & 15, g) of (n-tile i, k-tile t) holds n = 16 (2 np + i) + 4 g + r,
-    // k = 16 t + kc; unscale (exact) and store the partial
-    const uint32_t kc = lane & 15u, g = lane >> 4;
+    __syncthreads();                                   // fin[] written
+    // unscale (exact; one power of two at a time) and store the partial
     float *pp = a.part + (size_t)blockIdx.x * a.N * a.K;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t nb = 16 * (2 * np + i) + 4 * g;
+        const f4 sn = *reinterpret_cast<const f4 *>(&fin[nb]);
 #pragma unroll
         for (uint32_t t = 0; t < KH; ++t) {
             if (t >= k_count) continue;
             const uint32_t k = 16 * (k_begin + t) + kc;
             if (k >= a.K) continue;
+            const float sk = fin[NTn * 16 + k];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t nl = 16 * (2 * np + i) + 4 * g + r;
-                pp[(size_t)(n0 + nl) * a.K + k] = __fmul_rn(acc[i][t][r], 1.0f / (sd[nl] * sx[k]));
-            }
+            for (int r = 0; r < 4; ++r)
+                pp[(size_t)(n0 + nb + r) * a.K + k] =
+                    __fmul_rn(__fmul_rn(acc[i][t][r], 1.0f / sn[r]), 1.0f / sk);
         }
+    }
 }
 
 __global__ void __launch_bounds__(256) lin_reduce_kernel(const float *__restrict__ part, uint32_t P,
@@ -552,7 +545,15 @@ __global__ void __launch_bounds__(256) lin_reduce_kernel(const float *__restrict
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
     if (e >= count) return;
     float s = 0.0f;
-    for (uint32_t p = 0; p < P; ++p) s += part[(size_t)p * count + e];   // fixed order
+    uint32_t p = 0;
+    for (; p + 8 <= P; p += 8) {                       // loads in flight, sums in order
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = part[(size_t)(p + j) * count + e];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; p < P; ++p) s += part[(size_t)p * count + e];
     out[e] = s;
 }
 
@@ -620,8 +621,10 @@ int sdfr_film_linear_f16x3(float *out, float *y_save, const float *x, const void
         return fail(SDFR_EINVAL, "film_linear_f16x3: M must be a multiple of rows_per_face");
     if (K % 4 || N != 256 ||
         (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
-         reinterpret_cast<uintptr_t>(y_save)) % 16)
-        return fail(SDFR_EINVAL, "film_linear_f16x3: N = 256, K multiple of 4, 16-B aligned rows");
+         reinterpret_cast<uintptr_t>(y_save) | reinterpret_cast<uintptr_t>(bias) |
+         reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) % 16)
+        return fail(SDFR_EINVAL, "film_linear_f16x3: N = 256, K multiple of 4, 16-B aligned "
+                                 "x, out, y_save, bias, gamma, beta");
     LinArgs a;
     a.x = x;
     a.packed = static_cast<const f4 *>(packed);
@@ -677,8 +680,10 @@ int sdfr_linear_f16x3(float *out, const float *x, const void *packed, const floa
                       uint32_t M, uint32_t N, uint32_t K, void *stream) {
     if (M == 0) return SDFR_OK;
     if (!out || !x || !packed) return fail(SDFR_EINVAL, "linear_f16x3: null pointer");
-    if (K % 4 || N % 4 || (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) % 16)
-        return fail(SDFR_EINVAL, "linear_f16x3: K, N multiples of 4, 16-B aligned rows");
+    if (K % 4 || N % 4 ||
+        (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+         reinterpret_cast<uintptr_t>(bias)) % 16)
+        return fail(SDFR_EINVAL, "linear_f16x3: K, N multiples of 4, 16-B aligned x, out, bias");
     LinArgs a;
     a.x = x;
     a.packed = static_cast<const f4 *>(packed);
@@ -705,7 +710,7 @@ int sdfr_linear_f16x3(float *out, const float *x, const void *packed, const floa
 size_t sdfr_linear_wgrad_ws_bytes(uint32_t M, uint32_t N, uint32_t K) {
     if (M == 0 || N == 0 || K == 0) return 0;
     const uint32_t P = ceil_div(M, wgrad_rows(M));
-    return (size_t)(N + ceil_div(K, 16) * 16) * 4 + 256 + (size_t)P * N * K * 4;
+    return (size_t)P * N * K * 4;
 }
 
 int sdfr_linear_wgrad_f16x3(float *gw, const float *dy, const float *x, uint32_t M, uint32_t N,
@@ -714,8 +719,6 @@ int sdfr_linear_wgrad_f16x3(float *gw, const float *dy, const float *x, uint32_t
     if (N != 256 || K == 0 || K > 288 || K % 4)
         return fail(SDFR_EUNSUPPORTED,
                     "linear_wgrad_f16x3: N must be 256 and K <= 288 a multiple of 4");
-    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) % 16)
-        return fail(SDFR_EINVAL, "linear_wgrad_f16x3: 16-B aligned rows required");
     hipStream_t st = (hipStream_t)stream;
     if (M == 0) {
         if (hipMemsetAsync(gw, 0, (size_t)N * K * 4, st) != hipSuccess)
@@ -724,37 +727,23 @@ int sdfr_linear_wgrad_f16x3(float *gw, const float *dy, const float *x, uint32_t
     }
     if (!ws || ws_bytes < sdfr_linear_wgrad_ws_bytes(M, N, K))
         return fail(SDFR_EINVAL, "linear_wgrad_f16x3: workspace too small");
-    const uint32_t Kp = ceil_div(K, 16) * 16;
-    uint32_t *cmax = static_cast<uint32_t *>(ws);
-    float *part = reinterpret_cast<float *>(static_cast<char *>(ws) +
-                                            ((size_t)(N + Kp) * 4 + 255) / 256 * 256);
-    if (hipMemsetAsync(cmax, 0, (size_t)(N + Kp) * 4, st) != hipSuccess)
-        return fail(SDFR_ELAUNCH, "linear_wgrad_f16x3: memset");
-    const uint32_t rpb = ceil_div(ceil_div(M, 512), 8) * 8;     // ~512 blocks
-    hipLaunchKernelGGL(lin_colmax_kernel, dim3(ceil_div(M, rpb)), dim3(256), 0, st, dy, M, N, rpb,
-                       cmax);
-    hipLaunchKernelGGL(lin_colmax_kernel, dim3(ceil_div(M, rpb)), dim3(256), 0, st, x, M, K, rpb,
-                       cmax + N);
-    int rc = check_launch("linear_wgrad_f16x3: column max");
-    if (rc) return rc;
     WgradArgs a;
     a.dy = dy;
     a.x = x;
-    a.cmax_dy = cmax;
-    a.cmax_x = cmax + N;
-    a.part = part;
+    a.part = static_cast<float *>(ws);
     a.M = M;
     a.N = N;
     a.K = K;
     a.rows = wgrad_rows(M);
     const uint32_t P = ceil_div(M, a.rows);
     const uint32_t KT = ceil_div(K, 16);
+    int rc;
     if (KT <= 2) rc = launch_wgrad<2>(a, P, st);              // input_linear (K = 32)
     else if (KT <= 16) rc = launch_wgrad<16>(a, P, st);       // dense layers (K = 256)
     else if (KT <= 17) rc = launch_wgrad<17>(a, P, st);       // views (K = 272, 259)
     else rc = launch_wgrad<18>(a, P, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(lin_reduce_kernel, dim3(ceil_div(N * K, 256)), dim3(256), 0, st, part, P,
+    hipLaunchKernelGGL(lin_reduce_kernel, dim3(ceil_div(N * K, 256)), dim3(256), 0, st, a.part, P,
                        N * K, gw);
     return check_launch("linear_wgrad_f16x3: reduce");
 }

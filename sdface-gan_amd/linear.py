@@ -59,6 +59,14 @@ def _pack(w: torch.Tensor, transposed: bool) -> torch.Tensor:
     return buf
 
 
+def _a16(t):
+    """t, or a 16-B aligned copy (the kernels read bias / gamma / beta as 16-B vectors)."""
+    if t is None:
+        return None
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
 def _gemm(x2: torch.Tensor, packed: torch.Tensor, bias, N: int) -> torch.Tensor:
     M, K = x2.shape
     out = torch.empty(M, N, device=x2.device, dtype=torch.float32)
@@ -86,9 +94,9 @@ class _LinearF16x3(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         N, K = weight.shape
         lead = x.shape[:-1]
-        x2 = x.reshape(-1, K).contiguous()
+        x2 = _a16(x.reshape(-1, K))
         w = weight.contiguous()
-        out = _gemm(x2, _pack(w, False), bias.contiguous() if bias is not None else None, N)
+        out = _gemm(x2, _pack(w, False), _a16(bias), N)
         ctx.save_for_backward(x2, w)
         ctx.has_bias = bias is not None
         ctx.lead = lead
@@ -99,7 +107,7 @@ class _LinearF16x3(torch.autograd.Function):
     def backward(ctx, gy):
         x2, w = ctx.saved_tensors
         N, K = w.shape
-        gy2 = gy.reshape(-1, N).contiguous()
+        gy2 = _a16(gy.reshape(-1, N))
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = _gemm(gy2, _pack(w, True), None, K).view(*ctx.lead, K)
@@ -120,15 +128,15 @@ class _FiLMLinearF16x3(torch.autograd.Function):
         N, K = weight.shape
         F_ = gamma.shape[0]
         lead = x.shape[:-1]
-        x2 = x.reshape(-1, K).contiguous()
+        x2 = _a16(x.reshape(-1, K))
         M = x2.shape[0]
         w = weight.contiguous()
-        g2, b2 = gamma.reshape(F_, N).contiguous(), beta.reshape(F_, N).contiguous()
+        g2, b2 = _a16(gamma.reshape(F_, N)), _a16(beta.reshape(F_, N))
         out = torch.empty(M, N, device=x.device, dtype=torch.float32)
         y = torch.empty(M, N, device=x.device, dtype=torch.float32)
         _lib.check(_lib.lib().sdfr_film_linear_f16x3(
             _lib.ptr(out), _lib.ptr(y), _lib.ptr(x2), _lib.ptr(_pack(w, False)),
-            _lib.ptr(bias.contiguous() if bias is not None else None), _lib.ptr(g2),
+            _lib.ptr(_a16(bias)), _lib.ptr(g2),
             _lib.ptr(b2), M, N, K, M // F_, _lib.stream_of(x2)), "sdfr_film_linear_f16x3")
         ctx.save_for_backward(x2, w, y, g2, b2)
         ctx.meta = (lead, bias is not None, gamma.shape, beta.shape)
@@ -141,7 +149,7 @@ class _FiLMLinearF16x3(torch.autograd.Function):
         lead, has_bias, gshape, bshape = ctx.meta
         N, K = w.shape
         M, F_ = x2.shape[0], g2.shape[0]
-        ds2 = ds.reshape(-1, N).contiguous()
+        ds2 = _a16(ds.reshape(-1, N))
         L = _lib.lib()
         dy = torch.empty(M, N, device=ds.device, dtype=torch.float32)
         dg = torch.empty(F_, N, device=ds.device, dtype=torch.float32)
