@@ -314,6 +314,20 @@ int sdfr_film_backward(float *dy, float *dgamma, float *dbeta, float *dbf, const
                        uint32_t N, uint32_t rows_per_face, void *ws, size_t ws_bytes,
                        void *stream);
 
+/* The MLP's narrow output heads for training (sigma_linear 256 -> 1, rgb_linear
+ * 256 -> 3; LinearLayer, sdf_model.py:23-41, at :1586-1588), fp32 FMAs, J <= 4 outputs,
+ * K <= 256 inputs (a multiple of 4), 16-B aligned x, w, gx:
+ * sdfr_linear_head_forward: out [M,J] = x [M,K] . w [J,K]^T (+ bias [J], NULL = none).
+ * sdfr_linear_head_backward: gx [M,K] = gy [M,J] . w; gw [J,K] = gy^T . x; gb [J] =
+ *   column sums of gy -- each NULL to skip; gw / gb need ws >=
+ *   sdfr_linear_head_ws_bytes(M, J, K) (per-workgroup partials added in a fixed order). */
+int sdfr_linear_head_forward(float *out, const float *x, const float *w, const float *bias,
+                             uint32_t M, uint32_t J, uint32_t K, void *stream);
+size_t sdfr_linear_head_ws_bytes(uint32_t M, uint32_t J, uint32_t K);
+int sdfr_linear_head_backward(float *gx, float *gw, float *gb, const float *gy, const float *x,
+                              const float *w, uint32_t M, uint32_t J, uint32_t K, void *ws,
+                              size_t ws_bytes, void *stream);
+
 /* ---------------------------------------------------------------------------
  * StyleGAN2 decoder ops (im2scene/sdf/models/sdf_op.py).
  *

@@ -49,6 +49,7 @@ EXPORTS = (
     "sdfr_linear_pack_bytes", "sdfr_linear_pack", "sdfr_linear_f16x3",
     "sdfr_linear_wgrad_ws_bytes", "sdfr_linear_wgrad_f16x3",
     "sdfr_film_linear_f16x3", "sdfr_film_backward_ws_bytes", "sdfr_film_backward",
+    "sdfr_linear_head_forward", "sdfr_linear_head_ws_bytes", "sdfr_linear_head_backward",
 )
 
 
@@ -217,6 +218,10 @@ def lib():
     L.sdfr_film_backward_ws_bytes.argtypes = [_u32, _u32, _u32]
     L.sdfr_film_backward_ws_bytes.restype = ctypes.c_size_t
     L.sdfr_film_backward.argtypes = [_vp] * 8 + [_u32] * 3 + [_vp, ctypes.c_size_t, _vp]
+    L.sdfr_linear_head_forward.argtypes = [_vp] * 4 + [_u32] * 3 + [_vp]
+    L.sdfr_linear_head_ws_bytes.argtypes = [_u32, _u32, _u32]
+    L.sdfr_linear_head_ws_bytes.restype = ctypes.c_size_t
+    L.sdfr_linear_head_backward.argtypes = [_vp] * 6 + [_u32] * 3 + [_vp, ctypes.c_size_t, _vp]
     v = L.sdfr_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"libsdfr ABI {v} != expected {ABI_VERSION}; rebuild the library")

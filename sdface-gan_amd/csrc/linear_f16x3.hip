@@ -9,14 +9,15 @@
 //                            forward (B = W) and input gradient (B = W^T, no bias)
 //   sdfr_linear_wgrad_f16x3  gw[N,K] = sum_m dy[m,n] x[m,k]   (weight gradient)
 //
-// Forward / input gradient: a workgroup is 8 waves over 64 rows of x (16 per wave:
-// MFMA N = 16 columns = rows m of x; two waves per row group, one half of the output
-// tiles each); a lane loads its row's K values into registers up front, scales the
-// row by a power of two (max |x_m| into [0.5, 1): the fp16 lo parts stay normal at any
-// magnitude, activations and gradients alike) and splits them per k-step; the B
-// fragments (pre-split, row-scaled by su[n], packed in MFMA A-fragment order by
-// sdfr_linear_pack) stream through a two-slot LDS ring by LDS-DMA.  Outputs
-// accumulate in fp32 and are unscaled exactly.
+// Forward / input gradient: a workgroup is 8 waves over 128 rows of x (32 per wave:
+// two MFMA N = 16 columns = rows m of x; two waves per row group, one half of the
+// output tiles each); x tiles and the B fragments (pre-split, row-scaled by su[n],
+// packed in MFMA A-fragment order by sdfr_linear_pack) stream through a 3-slot LDS
+// ring by LDS-DMA; each row of x is scaled by a power of two from its running maximum
+// (max |x_m| into [0.5, 1): the fp16 lo parts stay normal at any magnitude,
+// activations and gradients alike; accumulators are rescaled exactly when a row's
+// scale shrinks) and split per k-step.  Outputs accumulate in fp32 and are unscaled
+// exactly.
 //
 // Weight gradient: the sum over m is split over workgroups (a contiguous range of
 // rows each), each accumulating an [N,K] partial in fp32; a second kernel adds the
@@ -27,7 +28,9 @@
 // fragments.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "f16x3.h"
 #include "render_ngp.h"
@@ -48,7 +51,7 @@ __device__ __forceinline__ float cos_hw(float x) {
 
 constexpr uint32_t kLinWaves = 8;
 constexpr uint32_t kLinThreads = kLinWaves * 64;
-constexpr uint32_t kLinRows = 64;                      // rows of x per forward workgroup
+constexpr uint32_t kLinRows = 256;                     // rows of x per forward block (32 per wave)
 constexpr uint32_t kTileF4 = 128;                      // one 16-row tile: [hi,lo][64 lanes]
 
 __host__ __device__ constexpr uint32_t ceil_div(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
@@ -127,129 +130,234 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 }
 constexpr uint32_t kOob = 0x80000000u;                  // a buffer offset that reads zeros
 
-__device__ __forceinline__ f4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
-}
 __device__ __forceinline__ float ld1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
 
+// output tiles per workgroup (the weights of one split stay resident in LDS) and splits
+template <int NT>
+constexpr int fwd_ntw() { return NT > 9 ? (NT + 1) / 2 : NT; }
+template <int NT>
+constexpr int fwd_nsplit() { return (NT + fwd_ntw<NT>() - 1) / fwd_ntw<NT>(); }
+// x prefetch depth in k-steps (divides KS, so every step's register slot is static;
+// 3 for KS = 9 spills)
+template <int KS>
+constexpr int fwd_pf() { return KS % 2 == 0 ? 2 : 1; }
+
 template <int NT, int KS, bool FILM>
-__global__ void __launch_bounds__(kLinThreads, 2) lin_fwd_kernel(const LinArgs a) {
-    // 8 waves: 4 row groups of 16 rows x 2 halves of the NT output tiles.  A lane holds
-    // its row's 8 K values of every k-step in registers, all loaded up front (branch-free
-    // buffer loads: rows past M and columns past K read zeros), so x is read from HBM
-    // once and the loads of one workgroup overlap the MFMAs of the other on the CU
-    constexpr int NTH = (NT + 1) / 2;
-    constexpr uint32_t kSliceF4 = NT * kTileF4;                 // one k-step of B
-    constexpr uint32_t kPieces = 2 * NT;                        // 1 KB LDS-DMA pieces
-    __shared__ f4 ring[2][kSliceF4];
+__global__ void __launch_bounds__(kLinThreads) lin_fwd_kernel(const LinArgs a) {
+    // Workgroup (split sp, row partition w): the split's NTW output tiles' B fragments
+    // (weights, pre-split and packed; <= 144 KB) are loaded into LDS once by LDS-DMA and
+    // stay resident; the workgroup then walks its blocks of 256 rows, each wave 32 rows
+    // (two MFMA B columns of 16) x all NTW tiles, so every A fragment read from LDS feeds
+    // 6 MFMAs.  No barriers in the main loop: a wave streams its rows' x through
+    // registers PF k-steps ahead (branch-free buffer loads; rows past M and columns past
+    // K read zeros), across block boundaries.  The two splits of a row range run on one
+    // XCD (workgroup ids 8 apart) and share its x in L2.  Each row is scaled by a power
+    // of two from its running maximum over the k-steps read so far (the fp16 lo parts
+    // stay normal at any magnitude); when a row's scale shrinks its accumulators are
+    // rescaled exactly.
+    constexpr int NTW = fwd_ntw<NT>();
+    constexpr int NSPLIT = fwd_nsplit<NT>();
+    constexpr int PF = fwd_pf<KS>();
+    __shared__ f4 wl[KS * NTW * kTileF4];                      // [ks][tile][hi 64 | lo 64]
+    __shared__ float cst[4][NTW * 16];                          // 1/su, bias, gamma, beta
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t rg = wave >> 1, nh = wave & 1u;
-    const uint32_t t_begin = nh * NTH;
-    const uint32_t t_count = NT - t_begin < (uint32_t)NTH ? NT - t_begin : NTH;
     const uint32_t n = lane & 15u, g = lane >> 4;
-    const uint32_t m_blk = blockIdx.x * kLinRows;
-    const uint32_t rows = a.M - m_blk < kLinRows ? a.M - m_blk : kLinRows;
-    const uint32_t r_in = rg * 16 + n;
-    const uint32_t m = m_blk + r_in;
+    // workgroup id -> (split, row partition): ids 8 apart share an XCD
+    const uint32_t id = blockIdx.x;
+    const uint32_t sp = NSPLIT == 1 ? 0 : (id >> 3) & 1u;
+    const uint32_t w = NSPLIT == 1 ? id : ((id >> 4) << 3) | (id & 7u);
+    const uint32_t G = gridDim.x / NSPLIT;
+    const uint32_t t0 = sp * NTW;                               // first output tile
+    const uint32_t t_count = NT - t0 < (uint32_t)NTW ? NT - t0 : NTW;
+    const uint32_t nblk = ceil_div(a.M, kLinRows);
+    const uint32_t b0 = (uint32_t)((uint64_t)w * nblk / G);
+    const uint32_t b1 = (uint32_t)((uint64_t)(w + 1) * nblk / G);
 
-    // the B fragments of a slice by LDS-DMA (no VGPRs): pieces wave, wave + 8, ...
-    const v4i rs = make_rsrc(a.packed, KS * kSliceF4 * 16u);
-    auto dma_slice = [&](int q, uint32_t slot) {
-        for (uint32_t p = wave; p < kPieces; p += kLinWaves)
-            dma16(rs, lane * 16u, (uint32_t)((q * kSliceF4 + p * 64) * 16),
-                  lds_addr(&ring[slot][p * 64]));
-    };
-    dma_slice(0, 0);
-
-    const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x + (size_t)m_blk * a.K, rows * a.K * 4u);
-    f4 xv[KS][2];
-#pragma unroll
-    for (int q = 0; q < KS; ++q) {
-        const uint32_t k0 = 32 * q + 8 * g;
-        const uint32_t off = (r_in * a.K + k0) * 4u;
-        xv[q][0] = ld4(xr, k0 + 4 <= a.K ? off : kOob);
-        xv[q][1] = ld4(xr, k0 + 8 <= a.K ? off + 16 : kOob);
-    }
-    // the row's power-of-two scale (max |x_m| into [0.5, 1): the fp16 lo parts stay
-    // normal at any magnitude; the row's 4 lane groups hold all of its K)
-    float mx = 0.0f;
-#pragma unroll
-    for (int q = 0; q < KS; ++q)
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) mx = fmaxf(mx, fabsf(xv[q][h][j]));
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float xs = pow2_scale(mx);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    f4 acc[NTH];
-#pragma unroll
-    for (int t = 0; t < NTH; ++t) acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int q = 0; q < KS; ++q) {
-        const uint32_t slot = q & 1;
-        if (q + 1 < KS) dma_slice(q + 1, slot ^ 1u);   // slot^1 was last read before the barrier
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            v[j] = __fmul_rn(xv[q][0][j], xs);
-            v[4 + j] = __fmul_rn(xv[q][1][j], xs);
+    {   // resident weights: pieces (ks, tile, hi/lo) of 1 KB, round-robin over the waves
+        const v4i rs = make_rsrc(a.packed, KS * NT * kTileF4 * 16u);
+        for (uint32_t p = wave; p < (uint32_t)(KS * NTW * 2); p += kLinWaves) {
+            const uint32_t ks = p / (NTW * 2), tl = (p / 2) % NTW, h = p & 1u;
+            if (tl >= t_count) continue;
+            dma16(rs, lane * 16u, ((ks * NT + t0 + tl) * kTileF4 + h * 64) * 16u,
+                  lds_addr(&wl[(ks * NTW + tl) * kTileF4 + h * 64]));
         }
-        f4 bh, bl;
-        split8(v, bh, bl);
-        const f4 *A = ring[slot] + t_begin * kTileF4 + lane;
+        for (uint32_t c = tid; c < NTW * 16u; c += kLinThreads) {
+            const uint32_t col = 16 * t0 + c;
+            cst[0][c] = col < a.N ? 1.0f / a.su[col] : 0.0f;      // powers of two: exact
+            cst[1][c] = (col < a.N && a.bias) ? a.bias[col] : 0.0f;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (b0 >= b1) return;
+
+    // this lane's 8 K values (k = 32 q + 8 g + j) of its two rows in block blk
+    // (rows = 0: an empty range, the loads read zeros -- branch-free past the last
+    // block); only the last k-step can run past K (KS = ceil(K / 32)), the others take
+    // compile-time offsets from the lane's row base
+    uint32_t xbase[2];
 #pragma unroll
-        for (int t = 0; t < NTH; ++t) {
-            if (t < (int)t_count) {
-                const f4 ah = A[t * kTileF4], al = A[t * kTileF4 + 64];
-                acc[t] = mfma16(al, bh, acc[t]);
-                acc[t] = mfma16(ah, bl, acc[t]);
-                acc[t] = mfma16(ah, bh, acc[t]);
+    for (int c = 0; c < 2; ++c) xbase[c] = ((wave * 32 + 16 * c + n) * a.K + 8 * g) * 4u;
+    auto load_x = [&](uint32_t blk, int q, f4 (&v)[2][2]) {
+        const uint32_t m0 = blk * kLinRows;
+        const uint32_t rows = blk >= b1 ? 0u : (a.M - m0 < kLinRows ? a.M - m0 : kLinRows);
+        const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x + (size_t)m0 * a.K, rows * a.K * 4u);
+        const uint32_t k0 = 32 * q + 8 * g;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                // the constant part as the instruction's scalar offset
+                const uint32_t voff = q + 1 < KS || k0 + 4 * h + 4 <= a.K ? xbase[c] : kOob;
+                v[c][h] = __builtin_bit_cast(
+                    f4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)voff, 128 * q + 16 * h, 0));
+            }
+    };
+    f4 xb[PF][2][2];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) load_x(b0, p, xb[p]);
+
+    uint32_t face = 0xffffffffu;
+    for (uint32_t blk = b0; blk < b1; ++blk) {
+        const uint32_t m_blk = blk * kLinRows;
+        const uint32_t rows = a.M - m_blk < kLinRows ? a.M - m_blk : kLinRows;
+        bool straddle = false;
+        if constexpr (FILM) {
+            // the face's gamma / beta into LDS when it changes (every wave walks the same
+            // blocks, so the barriers match; faces are ~98 K rows apart); a block that
+            // straddles two faces reads them per row from global memory instead
+            const uint32_t f0 = m_blk / a.rows_per_face, f1 = (m_blk + rows - 1) / a.rows_per_face;
+            straddle = f0 != f1;
+            if (!straddle && f0 != face) {
+                __syncthreads();                                 // the last epilogue is done
+                for (uint32_t c = tid; c < NTW * 16u; c += kLinThreads) {
+                    const uint32_t col = 16 * t0 + c;
+                    cst[2][c] = col < a.N ? a.gamma[(size_t)f0 * a.N + col] : 0.0f;
+                    cst[3][c] = col < a.N ? a.beta[(size_t)f0 * a.N + col] : 0.0f;
+                }
+                __syncthreads();
+                face = f0;
             }
         }
-        if (q + 1 < KS) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of q+1 landed
-            __syncthreads();                                     // everyone's; slot free
-        }
-    }
-    if (r_in >= rows) return;
-    // lane (n, g) of tile t holds output columns 16 t + 4 g + r of row m (N % 4 == 0,
-    // so a quad is wholly inside or outside N)
-    const float inv_xs = 1.0f / xs;                        // powers of two: exact
-    float *orow = a.out + (size_t)m * a.N;
-    const size_t frow = FILM ? (size_t)(m / a.rows_per_face) * a.N : 0;
+        float rmax[2] = {0.0f, 0.0f}, xs[2] = {1.0f, 1.0f};
+        f4 acc[2][NTW];
 #pragma unroll
-    for (int tt = 0; tt < NTH; ++tt) {
-        if (tt >= (int)t_count) continue;
-        const uint32_t c0 = 16 * (t_begin + tt) + 4 * g;
-        if (c0 >= a.N) continue;
-        const f4 s4 = *reinterpret_cast<const f4 *>(a.su + c0);
-        const f4 b4 = a.bias ? *reinterpret_cast<const f4 *>(a.bias + c0) : f4{0.0f, 0.0f, 0.0f, 0.0f};
-        f4 yv, v;
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float y = __fmul_rn(__fmul_rn(acc[tt][r], inv_xs), 1.0f / s4[r]);
-            if (a.bias) y = __fadd_rn(y, b4[r]);
-            yv[r] = y;
-        }
-        if constexpr (FILM) {
-            // FiLMSiren.forward (sdf_model.py:62-67): sin(gamma * out + beta), one
-            // rounding per op as the reference's separate elementwise ops
-            const f4 gm = *reinterpret_cast<const f4 *>(a.gamma + frow + c0);
-            const f4 bt = *reinterpret_cast<const f4 *>(a.beta + frow + c0);
+            for (int t = 0; t < NTW; ++t) acc[c][t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = sin_hw(__fadd_rn(__fmul_rn(gm[r], yv[r]), bt[r]));
-            *reinterpret_cast<f4 *>(a.y_save + (size_t)m * a.N + c0) = yv;
-        } else {
-            v = yv;
+        for (int q = 0; q < KS; ++q) {
+            f4 xa[2][2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) xa[c][h] = xb[q % PF][c][h];
+            // refill the slot with step q + PF (this block, or the next one's)
+            if (q + PF < KS) load_x(blk, q + PF, xb[q % PF]);
+            else load_x(blk + 1, q + PF - KS, xb[q % PF]);
+            // running row maxima -> scales; rescale the rows whose scale shrank
+            float ratio[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                float mx = 0.0f;
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) mx = fmaxf(mx, fabsf(xa[c][h][j]));
+                mx = fmaxf(mx, __shfl_xor(mx, 16));
+                mx = fmaxf(mx, __shfl_xor(mx, 32));
+                rmax[c] = fmaxf(rmax[c], mx);
+                const float sn = pow2_scale(rmax[c]);
+                ratio[c] = __builtin_amdgcn_ldexpf(1.0f, __builtin_amdgcn_frexp_expf(sn) -
+                                                             __builtin_amdgcn_frexp_expf(xs[c]));
+                xs[c] = sn;
+            }
+            if (q > 0 && __any(ratio[0] != 1.0f || ratio[1] != 1.0f)) {
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc[c][t][r] = __fmul_rn(acc[c][t][r], ratio[c]);
+            }
+            f4 bh[2], bl[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    v[j] = __fmul_rn(xa[c][0][j], xs[c]);
+                    v[4 + j] = __fmul_rn(xa[c][1][j], xs[c]);
+                }
+                split8(v, bh[c], bl[c]);
+            }
+            const f4 *A = wl + q * NTW * kTileF4 + lane;
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) {
+                if (t < (int)t_count) {
+                    const f4 ah = A[t * kTileF4], al = A[t * kTileF4 + 64];
+                    acc[0][t] = mfma16(al, bh[0], acc[0][t]);
+                    acc[1][t] = mfma16(al, bh[1], acc[1][t]);
+                    acc[0][t] = mfma16(ah, bl[0], acc[0][t]);
+                    acc[1][t] = mfma16(ah, bl[1], acc[1][t]);
+                    acc[0][t] = mfma16(ah, bh[0], acc[0][t]);
+                    acc[1][t] = mfma16(ah, bh[1], acc[1][t]);
+                }
+            }
         }
-        *reinterpret_cast<f4 *>(orow + c0) = v;
+        // lane (n, g) of tile t, column c holds output columns 16 (t0 + t) + 4 g + r of
+        // row m_blk + 32 wave + 16 c + n (N % 16 == 0).  FiLM's gamma / beta from LDS, or
+        // per row from global memory where the block straddles two faces (two copies of
+        // the epilogue, so the common one carries no load waits)
+        auto epilogue = [&](auto from_lds) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const uint32_t r_in = wave * 32 + 16 * c + n;
+                if (r_in >= rows) continue;
+                const uint32_t m = m_blk + r_in;
+                const float inv_xs = 1.0f / xs[c];             // powers of two: exact
+                float *orow = a.out + (size_t)m * a.N;
+                const size_t frow = FILM ? (size_t)(m / a.rows_per_face) * a.N : 0;
+#pragma unroll
+                for (int t = 0; t < NTW; ++t) {
+                    if (t >= (int)t_count) continue;
+                    const uint32_t cl = 16 * t + 4 * g, c0 = 16 * t0 + cl;
+                    const f4 is4 = *reinterpret_cast<const f4 *>(&cst[0][cl]);
+                    const f4 b4 = *reinterpret_cast<const f4 *>(&cst[1][cl]);
+                    f4 yv, v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float y = __fmul_rn(__fmul_rn(acc[c][t][r], inv_xs), is4[r]);
+                        if (a.bias) y = __fadd_rn(y, b4[r]);
+                        yv[r] = y;
+                    }
+                    if constexpr (FILM) {
+                        // FiLMSiren.forward (sdf_model.py:62-67): sin(gamma * out + beta),
+                        // one rounding per op as the reference's separate elementwise ops
+                        f4 gm, bt;
+                        if constexpr (decltype(from_lds)::value) {
+                            gm = *reinterpret_cast<const f4 *>(&cst[2][cl]);
+                            bt = *reinterpret_cast<const f4 *>(&cst[3][cl]);
+                        } else {
+                            gm = *reinterpret_cast<const f4 *>(a.gamma + frow + c0);
+                            bt = *reinterpret_cast<const f4 *>(a.beta + frow + c0);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            v[r] = sin_hw(__fadd_rn(__fmul_rn(gm[r], yv[r]), bt[r]));
+                        *reinterpret_cast<f4 *>(a.y_save + (size_t)m * a.N + c0) = yv;
+                    } else {
+                        v = yv;
+                    }
+                    *reinterpret_cast<f4 *>(orow + c0) = v;
+                }
+            }
+        };
+        if (!FILM || !straddle) epilogue(std::true_type{});
+        else epilogue(std::false_type{});
     }
 }
 
@@ -565,8 +673,14 @@ uint32_t wgrad_rows(uint32_t M) {
 
 template <int NT, int KS, bool FILM = false>
 int launch_fwd(const LinArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL((lin_fwd_kernel<NT, KS, FILM>), dim3(ceil_div(a.M, kLinRows)),
-                       dim3(kLinThreads), 0, st, a);
+    // persistent: one workgroup per CU (resident weights take up to 146 KB of LDS),
+    // NSPLIT of them per row partition; at most one partition per block of rows, and a
+    // multiple of 8 partitions when split (the splits' ids are 8 apart)
+    constexpr uint32_t ns = fwd_nsplit<NT>();
+    const uint32_t nblk = ceil_div(a.M, kLinRows);
+    uint32_t G = 256 / ns;
+    if (nblk < G) G = ns > 1 ? std::max<uint32_t>(8, ceil_div(nblk, 8) * 8) : nblk;
+    hipLaunchKernelGGL((lin_fwd_kernel<NT, KS, FILM>), dim3(G * ns), dim3(kLinThreads), 0, st, a);
     return check_launch("linear_f16x3");
 }
 
@@ -621,10 +735,10 @@ int sdfr_film_linear_f16x3(float *out, float *y_save, const float *x, const void
         return fail(SDFR_EINVAL, "film_linear_f16x3: M must be a multiple of rows_per_face");
     if (K % 4 || N != 256 ||
         (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
-         reinterpret_cast<uintptr_t>(y_save) | reinterpret_cast<uintptr_t>(bias) |
-         reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) % 16)
+         reinterpret_cast<uintptr_t>(y_save) | reinterpret_cast<uintptr_t>(gamma) |
+         reinterpret_cast<uintptr_t>(beta)) % 16)
         return fail(SDFR_EINVAL, "film_linear_f16x3: N = 256, K multiple of 4, 16-B aligned "
-                                 "x, out, y_save, bias, gamma, beta");
+                                 "x, out, y_save, gamma, beta");
     LinArgs a;
     a.x = x;
     a.packed = static_cast<const f4 *>(packed);
@@ -680,10 +794,9 @@ int sdfr_linear_f16x3(float *out, const float *x, const void *packed, const floa
                       uint32_t M, uint32_t N, uint32_t K, void *stream) {
     if (M == 0) return SDFR_OK;
     if (!out || !x || !packed) return fail(SDFR_EINVAL, "linear_f16x3: null pointer");
-    if (K % 4 || N % 4 ||
-        (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
-         reinterpret_cast<uintptr_t>(bias)) % 16)
-        return fail(SDFR_EINVAL, "linear_f16x3: K, N multiples of 4, 16-B aligned x, out, bias");
+    if (K % 4 || N % 16 ||
+        (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) % 16)
+        return fail(SDFR_EINVAL, "linear_f16x3: K a multiple of 4, N of 16, 16-B aligned x, out");
     LinArgs a;
     a.x = x;
     a.packed = static_cast<const f4 *>(packed);

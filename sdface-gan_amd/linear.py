@@ -13,11 +13,14 @@ fp32 accumulation, power-of-two row / column scaling: fp32-level accuracy):
   input gradient   gx  = gy W                  sdfr_linear_f16x3 (B = W^T)
   weight gradient  gW  = gy^T x                sdfr_linear_wgrad_f16x3
   bias gradient    gb  = gy.sum(0)             (torch reduction)
+  narrow heads     J <= 4 outputs (sigma 1, rgb 3): sdfr_linear_head_forward / _backward
+                   (HBM-streaming fp32 FMA kernels in place of rocBLAS's N = 1..3 GEMMs)
 
 Shapes the kernels take: out features 256 with in features 32 / 256 / 259..288
-(the networks' input_linear, dense and views layers).  Everything else (the
-3- and 1-wide heads, the per-face gamma / beta layers on the styles, CPU tensors,
-inference) stays on F.linear.  ``set_train_gemm("torch")`` turns the routing off.
+(the networks' input_linear, dense and views layers), and J <= 4 outputs with K <= 256
+(the 3- and 1-wide heads).  Everything else (the per-face gamma / beta layers on the
+styles, CPU tensors, inference) stays on F.linear.  ``set_train_gemm("torch")`` turns
+the routing off.
 
 The backward is first-order only (``once_differentiable``), so only the ngp network
 routes here (``NGPSIRENGenerator`` marks its layers ``train_kernels = True``): its
@@ -173,6 +176,47 @@ class _FiLMLinearF16x3(torch.autograd.Function):
         return gx, gw, gb, gg, gbt
 
 
+class _LinearHead(torch.autograd.Function):
+    """x W^T + b for the narrow heads (J <= 4 outputs): HBM-streaming HIP kernels."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        J, K = weight.shape
+        lead = x.shape[:-1]
+        x2 = _a16(x.reshape(-1, K))
+        w = _a16(weight)
+        M = x2.shape[0]
+        out = torch.empty(M, J, device=x.device, dtype=torch.float32)
+        _lib.check(_lib.lib().sdfr_linear_head_forward(
+            _lib.ptr(out), _lib.ptr(x2), _lib.ptr(w), _lib.ptr(bias.contiguous() if bias is not None
+                                                               else None),
+            M, J, K, _lib.stream_of(x2)), "sdfr_linear_head_forward")
+        ctx.save_for_backward(x2, w)
+        ctx.has_bias = bias is not None
+        ctx.lead = lead
+        return out.view(*lead, J)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        J, K = w.shape
+        M = x2.shape[0]
+        gy2 = gy.reshape(-1, J).contiguous()
+        L = _lib.lib()
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        gx = torch.empty(M, K, device=gy.device, dtype=torch.float32) if need_x else None
+        gw = torch.empty(J, K, device=gy.device, dtype=torch.float32) if need_w else None
+        gb = torch.empty(J, device=gy.device, dtype=torch.float32) if need_b else None
+        nws = L.sdfr_linear_head_ws_bytes(M, J, K) if (need_w or need_b) else 0
+        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=gy.device)
+        _lib.check(L.sdfr_linear_head_backward(
+            _lib.ptr(gx), _lib.ptr(gw), _lib.ptr(gb), _lib.ptr(gy2), _lib.ptr(x2), _lib.ptr(w),
+            M, J, K, _lib.ptr(ws), nws, _lib.stream_of(gy2)), "sdfr_linear_head_backward")
+        return (gx.view(*ctx.lead, K) if gx is not None else None), gw, gb
+
+
 def film_linear(x, weight, bias, gamma, beta, kernels=True):
     """FiLMSiren's ``sin(gamma * F.linear(x, weight, bias) + beta)`` (sdf_model.py:62-67),
     gamma / beta [F, 1, ..., 1, N] broadcast over each face's samples: fused on the HIP
@@ -197,9 +241,21 @@ def _routable(x: torch.Tensor, weight: torch.Tensor) -> bool:
     return x.numel() // K >= 1024            # the per-face gamma / beta layers stay on F.linear
 
 
+def _head_routable(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    if _MODE["gemm"] != "f16x3" or not x.is_cuda or not torch.is_grad_enabled():
+        return False
+    if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() < 2:
+        return False
+    J, K = weight.shape
+    return J <= 4 and K % 4 == 0 and K <= 256 and x.numel() // K >= 1024
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, kernels=True) -> torch.Tensor:
     """F.linear(x, weight, bias), on the split-fp16 MFMA kernels for the renderer MLP's
-    training shapes (module docstring) when ``kernels``, on F.linear otherwise."""
+    training shapes (module docstring) or the narrow-head kernels when ``kernels``, on
+    F.linear otherwise."""
     if kernels and _routable(x, weight):
         return _LinearF16x3.apply(x, weight, bias)
+    if kernels and _head_routable(x, weight):
+        return _LinearHead.apply(x, weight, bias)
     return F.linear(x, weight, bias)

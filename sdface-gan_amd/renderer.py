@@ -171,7 +171,8 @@ class NGPSIRENGenerator(nn.Module):
         self.sigma_linear = LinearLayer(W, 1, freq_init=True)
         # training GEMMs on the split-fp16 kernels (first-order backward suffices here:
         # the eikonal term leaves autograd in the grid encoder's backward, linear.py)
-        for m in [self.input_linear, *self.pts_linears, self.views_linears]:
+        for m in [self.input_linear, *self.pts_linears, self.views_linears, self.rgb_linear,
+                  self.sigma_linear]:
             m.train_kernels = True
 
     def forward(self, x, styles):
