@@ -6,7 +6,7 @@
 set -eu
 cd "$(dirname "$0")/../sdface-gan_amd"
 SRC=${VAR_SRC:-field_f16x3}
-ALL="encoders render_ngp field_f16x3 decoder conv_f16x3 mesh"
+ALL="encoders render_ngp field_f16x3 decoder conv_f16x3 mesh linear_f16x3 linear_head"
 FIXED=""
 for s in $ALL; do [ "$s" = "$SRC" ] || FIXED="$FIXED build/$s.o"; done
 make -s $FIXED

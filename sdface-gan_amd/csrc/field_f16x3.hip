@@ -37,6 +37,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "f16x3.h"
 #include "render_ngp.h"
@@ -220,6 +221,7 @@ __global__ void __launch_bounds__(256) xprep_kernel(const XPrepArgs a) {
 struct XFieldArgs {
     GeomArgs g;
     const float *enc;              // ngp: [L=16][S_total][2]; siren: unused
+    const float2 *zd;              // ngp: [S_total] (z, segment length) from the encode kernel
     const f4 *packed;              // [slices][1024]
     const float *film;             // [B][films][2][256], gamma pre-divided by su
     const float *su;               // [layers][256]
@@ -229,6 +231,7 @@ struct XFieldArgs {
     int force_background, with_sdf;
     float *rgb, *features, *sdf, *xyz, *mask;
     uint32_t nseg;                 // sample segments per ray (1: whole rays, no merge)
+    uint32_t rsplit;               // field_p_kernel: ray groups per workgroup split over 2 (1 / 2)
     float *part;                   // nseg > 1: [nseg][kPartQ][rays] segment partials
 };
 
@@ -847,6 +850,710 @@ __global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs
     }
 }
 
+// ----------------------------------------------------------------------------
+// field_p_kernel: wave pairs split the output rows.
+//
+// In field_x2_kernel every wave multiplies the WHOLE weight matrix into its own
+// 16-sample column, so each A fragment read from LDS feeds 3 MFMAs and the eight
+// waves of a CU read 8x the weight stream from LDS per pass (ablating those reads
+// alone took 30 % off the kernel).  Here the two waves of a SIMD (w, w + 4) form a
+// pair over 32 samples = 8 rays x 4 consecutive samples (two MFMA blocks of N = 16:
+// block c, lane n holds sample 4p + 2c + (n >= 8) of ray n & 7); wave h of the pair
+// owns output rows 128h .. 128h + 127 (half-slice h of every k-step), so each A
+// fragment feeds 6 MFMAs and LDS A reads halve.  A layer's input k-step q (rows
+// 32q .. 32q + 31 of the previous layer's output) is computed by wave q >> 2 of the
+// pair: that wave activates it one k-step ahead (FiLM in the MFMA shadow, as
+// field_x2_kernel), splits it and writes the (hi, lo) B fragments of both blocks to
+// a double-buffered 4 KB exchange slot; after the k-step barrier both waves read it
+// back.  Per k-step and wave: 48 MFMAs, 16 A + 4 B ds_read_b128 (field_x2_kernel:
+// 32 A reads per 48 MFMAs), 4 pieces of the LDS-DMA weight ring.  The pair chains
+// the sigma head across its halves (wave 0's per-lane partial after chunk 3 seeds
+// wave 1's), so sdf values are those of field_x2_kernel bit for bit; the colour
+// head's two half-sums are added (fp32-rounding-level difference).  Four samples of
+// a ray per pass halve the per-ray feature accumulators (4 KB per wave in LDS).
+// ----------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+constexpr int kPWaves = 8;
+constexpr int kPThreads = kPWaves * 64;
+constexpr uint32_t kPTiles = 2;          // 16-ray tiles per workgroup (4 pairs x 8 rays)
+constexpr uint32_t kPSamples = 4;        // samples of a ray per pass
+#ifndef PEARLY
+#define PEARLY 0
+#endif
+#ifndef PPIN
+#define PPIN 0
+#endif
+#ifndef PABL
+#define PABL 0
+#endif
+#ifndef PSTAG
+#define PSTAG 1
+#endif
+
+template <class Net>
+struct PNet {
+    static constexpr int kSteps = 1 + 8 * Net::kHidden + 9;   // k-steps per pass
+    static constexpr int kViews = 1 + 8 * Net::kHidden;        // first k-step of the views layer
+    static_assert(2 * kSteps == (int)Net::kSlices && kSteps % 2 == 0, "ring parity per pass");
+};
+
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+
+struct PRing {
+    f4 *lds;          // weight ring: 4 half-slice slots of kXSliceF4
+    f4 *xch;          // this pair's exchange: [2 slots][2 blocks][hi, lo][64 lanes]
+    v4i drsrc;
+    uint32_t tid, wave, h;
+    f4 na[4];         // the next k-step's group-0 A fragments (t0 hi, t0 lo, t1 hi, t1 lo)
+};
+
+__device__ __forceinline__ void p_dma(const PRing &R, uint32_t slice, uint32_t slot) {
+    const uint32_t sbase = R.wave * (kX2DmaPieces * 1024u);
+    const uint32_t lbase = lds_addr(R.lds) + sbase;
+#pragma unroll
+    for (int k = 0; k < kX2DmaPieces; ++k)
+        dma16x(R.drsrc, (R.tid & 63u) * 16u, sbase, slice * kXSliceF4 * 16u + k * 1024u, lbase,
+               slot * kXSliceF4 * 16u + k * 1024u);
+}
+
+// p_dma for the waves whose h == HSEL only.  The wave-uniform skip is a scalar branch
+// INSIDE the asm, so the compiler's view of the unrolled MFMA stream stays one basic
+// block (a C++ branch on h split it and spilled); offsets are immediates.
+template <uint32_t HSEL, uint32_t SLICE, uint32_t SLOT>
+__device__ __forceinline__ void p_dma_if(const PRing &R) {
+    const uint32_t sbase = R.wave * (kX2DmaPieces * 1024u);
+    const uint32_t lbase = lds_addr(R.lds) + sbase;
+    const uint32_t voff = (R.tid & 63u) * 16u;
+#pragma unroll
+    for (int k = 0; k < kX2DmaPieces; ++k) {
+        uint32_t keep, so;
+        asm volatile(
+            "s_cmp_lg_u32 %6, %7\n\ts_cbranch_scc1 1f\n\t"
+            "s_mov_b32 %0, m0\n\ts_add_u32 m0, %4, %8\n\ts_add_u32 %1, %5, %9\n\ts_nop 0\n\t"
+            "buffer_load_dwordx4 %2, %3, %1 offen lds\n\ts_mov_b32 m0, %0\n1:"
+            : "=&s"(keep), "=&s"(so)
+            : "v"(voff), "s"(R.drsrc), "s"(lbase), "s"(sbase), "s"(R.h), "i"(HSEL),
+              "i"(SLOT * kXSliceF4 * 16u + k * 1024u), "i"(SLICE * kXSliceF4 * 16u + k * 1024u)
+            : "memory", "scc");
+    }
+}
+
+// B fragments of exchange chunk q (both blocks): (hi0, lo0, hi1, lo1)
+__device__ __forceinline__ void p_read_chunk(const PRing &R, int q, f4 (&b)[4]) {
+    const f4 *s = R.xch + (q & 1) * 256 + (R.tid & 63u);
+    b[0] = s[0];
+    b[1] = s[64];
+    b[2] = s[128];
+    b[3] = s[192];
+}
+
+// One k-step of one wave: 8 own output tiles x 2 sample blocks x 3 split terms = 48
+// MFMAs in 4 groups of 2 tiles (a group's 12 MFMAs term-major, so an accumulator is
+// touched every 4th).  Own half-slice of k-step KS: ring slot 2 (KS & 1) + h.  The
+// next k-step's half-slices are DMA'd at entry into the previous k-step's slots; the
+// barrier (own DMA landed, own LDS traffic drained) sits ahead of group 3, behind it
+// the next k-step's group-0 A fragments and B fragments (next_b) are read, so their
+// latency hides under group 3.  side() runs after group 1.
+template <class Net, int KS, bool ZC, class NextB, class Side>
+__device__ __forceinline__ void pstep(PRing &R, f4 (&acc)[16], const f4 (&bf)[4], f4 (&bn)[4],
+                                      NextB &&next_b, Side &&side) {
+    constexpr f4 kZ = {0.0f, 0.0f, 0.0f, 0.0f};
+    constexpr int KN = (KS + 1) % PNet<Net>::kSteps, KN2 = (KS + 2) % PNet<Net>::kSteps;
+    const uint32_t lane = R.tid & 63u;
+    // The two waves of a SIMD issue their LDS-DMA pieces at different points (each
+    // piece holds the wave's issue for ~100 cycles): wave 1 here, for the next
+    // k-step; wave 0 behind this k-step's barrier, for the one after (both land
+    // in the slots the barrier before them closed).
+    if constexpr (PSTAG == 0) {
+        p_dma_if<0, 2 * KN, 2 * (KN & 1)>(R);
+        p_dma_if<0, 2 * KN + 1, 2 * (KN & 1) + 1>(R);
+        p_dma_if<1, 2 * KN, 2 * (KN & 1)>(R);
+        p_dma_if<1, 2 * KN + 1, 2 * (KN & 1) + 1>(R);
+    } else {
+        p_dma_if<1, 2 * KN, 2 * (KN & 1)>(R);
+        p_dma_if<1, 2 * KN + 1, 2 * (KN & 1) + 1>(R);
+    }
+    // local tile t = global tile 2t + h: half-slice t >> 2, position 2 (t & 3) + h
+    const f4 *A = R.lds + 2 * (KS & 1) * kXSliceF4 + R.h * 128 + lane;
+    const f4 *An = R.lds + 2 * (KN & 1) * kXSliceF4 + R.h * 128 + lane;
+    auto aoff = [](int t, int hl) { return (t >> 2) * (int)kXSliceF4 + (t & 3) * 256 + hl * 64; };
+    f4 a[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[0][i] = R.na[i];
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+        if (grp == 3) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        if (grp < 3) {
+            const int tn = 2 * (grp + 1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[grp + 1][i] = A[aoff(tn + (i >> 1), i & 1)];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) R.na[i] = An[aoff(i >> 1, i & 1)];
+            if constexpr (PEARLY) next_b(bn);
+            if constexpr (PSTAG != 0) {
+                p_dma_if<0, 2 * KN2, 2 * (KN2 & 1)>(R);
+                p_dma_if<0, 2 * KN2 + 1, 2 * (KN2 & 1) + 1>(R);
+            }
+        }
+        const int t0 = 2 * grp, t1 = t0 + 1;
+        const f4 *ag = a[grp];
+        // per accumulator: W_lo x_hi, W_hi x_lo, W_hi x_hi (field_x2_kernel's order)
+        // ZC: the layer's first k-step starts its accumulators from zero
+        acc[2 * t0] = mfma16(ag[1], bf[0], ZC ? kZ : acc[2 * t0]);
+        acc[2 * t0 + 1] = mfma16(ag[1], bf[2], ZC ? kZ : acc[2 * t0 + 1]);
+        acc[2 * t1] = mfma16(ag[3], bf[0], ZC ? kZ : acc[2 * t1]);
+        acc[2 * t1 + 1] = mfma16(ag[3], bf[2], ZC ? kZ : acc[2 * t1 + 1]);
+        acc[2 * t0] = mfma16(ag[0], bf[1], acc[2 * t0]);
+        acc[2 * t0 + 1] = mfma16(ag[0], bf[3], acc[2 * t0 + 1]);
+        acc[2 * t1] = mfma16(ag[2], bf[1], acc[2 * t1]);
+        acc[2 * t1 + 1] = mfma16(ag[2], bf[3], acc[2 * t1 + 1]);
+        acc[2 * t0] = mfma16(ag[0], bf[0], acc[2 * t0]);
+        acc[2 * t0 + 1] = mfma16(ag[0], bf[2], acc[2 * t0 + 1]);
+        acc[2 * t1] = mfma16(ag[2], bf[0], acc[2 * t1]);
+        acc[2 * t1 + 1] = mfma16(ag[2], bf[2], acc[2 * t1 + 1]);
+        // this group's and the previous group's A fragments stay allocated until the
+        // MFMAs have issued (no WAR hazard padding on their re-use)
+        asm volatile("" ::"v"(ag[0]), "v"(ag[1]), "v"(ag[2]), "v"(ag[3]));
+        if (PPIN && grp > 0)
+            asm volatile("" ::"v"(a[grp - 1][0]), "v"(a[grp - 1][1]), "v"(a[grp - 1][2]), "v"(a[grp - 1][3]));
+        __builtin_amdgcn_sched_barrier(0);
+        if (grp == 1) side();
+    }
+    if constexpr (!PEARLY) next_b(bn);
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// This wave's half of exchange chunk q (k-step q of the next layer = global tiles
+// 2q, 2q+1 of this layer's output; wave h holds tile 2q + h as local tile q):
+// activate local tile q of both blocks, split it and write the (hi, lo) dword pairs
+// to bytes 8h .. 8h + 7 of the chunk's 16-B B-fragment elements in slot q & 1.
+//   MODE 0: ngp input_linear, fma(x 2^-es, 1/su, b) (see feat_scale)
+//   MODE 1: FiLM sin_rev(fma(gamma'', x, beta''))
+//   MODE 2: FiLM + the sigma head's partial dot product (per lane over own tiles)
+template <int MODE>
+__device__ __forceinline__ void p_act(const PRing &R, f4 (&in)[16], int q, const float *gam,
+                                      const float *bet, const float *sw, float (&sdfp)[2],
+                                      uint32_t g, const int (&es)[2]) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const int f0 = 16 * (2 * q + (int)R.h) + 4 * (int)g;
+    const f4 gm = *reinterpret_cast<const f4 *>(gam + f0);
+    const f4 bt = *reinterpret_cast<const f4 *>(bet + f0);
+    f4 w4;
+    if constexpr (MODE == 2) w4 = *reinterpret_cast<const f4 *>(sw + f0);
+    char *dst = reinterpret_cast<char *>(R.xch + (q & 1) * 256 + (R.tid & 63u)) + 8 * R.h;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const f4 z = in[2 * q + c];
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if constexpr (MODE == 0) v[r] = __fmaf_rn(__builtin_ldexpf(z[r], -es[c]), gm[r], bt[r]);
+            else v[r] = sin_rev(__fmaf_rn(gm[r], z[r], bt[r]));
+        }
+        if constexpr (MODE == 2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sdfp[c] = __fmaf_rn(v[r], w4[r], sdfp[c]);
+        }
+        uint32_t hp[2], lp[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            h2 H;
+            H[0] = (_Float16)v[2 * j];
+            H[1] = (_Float16)v[2 * j + 1];
+            hp[j] = __builtin_bit_cast(uint32_t, H);
+            uint32_t l;
+            asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hp[j]), "v"(v[2 * j]));
+            asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                : "+v"(l) : "v"(hp[j]), "v"(v[2 * j + 1]));
+            lp[j] = l;
+        }
+        *reinterpret_cast<uint2 *>(dst + 128 * 16 * c) = make_uint2(hp[0], hp[1]);
+        *reinterpret_cast<uint2 *>(dst + 128 * 16 * c + 64 * 16) = make_uint2(lp[0], lp[1]);
+    }
+}
+
+template <class Net>
+__global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs a) {
+    constexpr int NF = Net::kFilmN;
+    constexpr int KV = PNet<Net>::kViews;
+    constexpr int NL = Net::kLayers;
+    __shared__ f4 ring_lds[kX2Slots * kXSliceF4];           // 64 KB weight ring
+    __shared__ f4 xch_lds[4][2 * 2 * 2 * 64];               // 32 KB: [pair][slot][block][hi,lo][lane]
+    __shared__ f4 facc_lds[kPWaves][8 * 4 * 8];             // 32 KB: [wave][tile][g][ray] feature sums
+    __shared__ float film_lds[NF * 2 * kW];                 // the workgroup's face
+    __shared__ float cst[6 * kW];                           // ngp layer-0 bias, 1/su0, sigma_w, rgb_w[3]
+    __shared__ float sdfx_lds[4][2][2][64];                 // [pair][wave][block][lane] sigma half-sums
+    __shared__ float pcol_lds[4][6][16];                    // wave 0's colour half-sums per column
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t h = __builtin_amdgcn_readfirstlane(wave >> 2), pair = wave & 3u;
+    const uint32_t n = lane & 15u, g = lane >> 4, r8 = n & 7u;
+    const bool colB = n >= 8u;
+    const GeomArgs &G = a.g;
+
+    // workgroup = 2 tiles; pair k: tile k >> 1, rays 8 (k & 1) .. +7
+    const uint32_t wg_per_face = (G.tiles_per_face + kPTiles - 1) / kPTiles;
+    const uint32_t seg = blockIdx.x % a.nseg, blk = blockIdx.x / a.nseg;
+    const uint32_t b = blk / wg_per_face;
+    const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
+    {
+        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * NF * 2 * kW);
+        f4 *dst = reinterpret_cast<f4 *>(film_lds);
+        for (uint32_t i = tid; i < NF * 2 * kW / 4; i += kPThreads) dst[i] = src[i];
+    }
+    PRing R;
+    R.lds = ring_lds;
+    R.xch = xch_lds[pair];
+    R.tid = tid;
+    R.wave = __builtin_amdgcn_readfirstlane(wave);
+    R.h = h;
+    R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
+    for (uint32_t i = tid; i < 6 * kW; i += kPThreads) {
+        float v;
+        if (i < kW) v = Net::kSiren ? 0.0f : a.bias_s[i];     // raw input_linear bias
+        else if (i < 2 * kW) v = __fdiv_rn(1.0f, a.su[i - kW]);
+        else if (i < 3 * kW) v = a.sigma_w[i - 2 * kW];
+        else v = a.rgb_w[i - 3 * kW];
+        cst[i] = v;
+    }
+    // prologue: k-step 0's half-slices -> slots 0, 1; wave 0 of each SIMD also k-step 1's
+    // (pstep: wave 1 issues the next k-step, wave 0 the one after)
+    p_dma(R, 0, 0);
+    p_dma(R, 1, 1);
+    if (PSTAG != 0 && h == 0) {
+        p_dma(R, 2, 2);
+        p_dma(R, 3, 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    f4 *facc = facc_lds[wave];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) R.na[i] = R.lds[h * 128 + (i >> 1) * 256 + (i & 1) * 64 + lane];
+
+    const float *bias0 = cst;
+    const float *inv_su0 = cst + kW;
+    const float *sig_w = cst + 2 * kW, *rgb_w = cst + 3 * kW;
+    auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
+    auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
+    const float sig_b = a.sigma_b[0];
+    const float rgb_b0 = a.rgb_b[0], rgb_b1 = a.rgb_b[1], rgb_b2 = a.rgb_b[2];
+    const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
+    const uint32_t npass = (G.N + kPSamples - 1) / kPSamples;
+    const uint32_t pps = (npass + a.nseg - 1) / a.nseg;
+    const uint32_t p_begin = seg * pps, p_end = min(npass, p_begin + pps);
+
+    uint32_t tile_local = (blk % wg_per_face) * kPTiles + (pair >> 1);
+    const bool tile_ok = tile_local < G.tiles_per_face;
+    if (!tile_ok) tile_local = G.tiles_per_face - 1;
+    const uint32_t tile = b * G.tiles_per_face + tile_local;
+    const uint32_t ray_in_tile = 8u * (pair & 1u) + r8;
+    uint32_t ray_local = tile_local * kTileRays + ray_in_tile;
+    const bool ray_ok = tile_ok && ray_local < G.H * G.W;
+    if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
+    const uint32_t py = ray_local / G.W, px = ray_local % G.W;
+    const uint32_t ray_index = (b * G.H + py) * G.W + px;
+
+    Ray ray;
+    make_ray(G.cam + (size_t)b * 12, G.focal[b], G.pix_x[px], G.pix_y[py], G.half_res, ray);
+    const float nr = G.near_[b], fr = G.far_[b];
+    const float span = __fsub_rn(fr, nr);
+    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
+    f4 vx[4];                                               // the views layer's extra k-step
+    {
+        const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
+        const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
+        const float v2 = G.static_viewdirs ? ray.dir[2] : ray.d[2];
+        const float vn = norm3_torch(v0, v1, v2);
+        const float ux = __fdiv_rn(v0, vn), uy = __fdiv_rn(v1, vn), uz = __fdiv_rn(v2, vn);
+        float v[8];
+        if constexpr (Net::kSiren) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = 0.0f;
+            if (g == 0) {
+                v[0] = ux;
+                v[1] = uy;
+                v[2] = uz;
+            }
+        } else {
+            const f4 qa = sh_quad(ux, uy, uz, (2 * g) & 3), qb = sh_quad(ux, uy, uz, (2 * g + 1) & 3);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = g < 2 ? qa[r] : 0.0f;
+                v[4 + r] = g < 2 ? qb[r] : 0.0f;
+            }
+        }
+        split8(v, vx[0], vx[1]);
+        vx[2] = vx[0];                                       // both blocks: the same ray
+        vx[3] = vx[1];
+    }
+    float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
+    float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) facc[t * 64 + lane] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    const size_t tile_sid = (size_t)(tile * G.N) * kTileRays + ray_in_tile;
+    float2 en[2][4];
+    auto load_inputs = [&](uint32_t p) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            uint32_t s = kPSamples * p + 2 * c + (colB ? 1u : 0u);
+            if (s >= G.N) s = G.N - 1;
+            if constexpr (Net::kSiren) {
+                const float z = sample_z(G.sc, nr, fr, ray_index, s);
+                float np_[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const float pp = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));
+                    np_[k] = G.z_normalize ? __fdiv_rn(__fmul_rn(pp, 2.0f), span) : pp;
+                }
+                const bool g0 = g == 0;
+                en[c][0] = make_float2(g0 ? np_[0] : 0.0f, g0 ? np_[1] : 0.0f);
+                en[c][1] = make_float2(g0 ? np_[2] : 0.0f, 0.0f);
+                en[c][2] = make_float2(0.0f, 0.0f);
+                en[c][3] = make_float2(0.0f, 0.0f);
+            } else {
+                const size_t sid = tile_sid + (size_t)s * kTileRays;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) en[c][k] = enc2[(4 * g + k) * (size_t)G.S_total + sid];
+            }
+        }
+    };
+    load_inputs(p_begin);
+
+    for (uint32_t p = p_begin; p < p_end; ++p) {
+        f4 X[16], Y[16];                                   // [2 local tile + block]
+        f4 e[4];                                           // layer-0 B fragments
+        int es[2] = {0, 0};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                v[2 * k] = en[c][k].x;
+                v[2 * k + 1] = en[c][k].y;
+            }
+            if constexpr (!Net::kSiren) es[c] = feat_scale(v);
+            split8(v, e[2 * c], e[2 * c + 1]);
+        }
+        float sdfp[2] = {0.0f, 0.0f};
+        // activation of layer l's output, chunk q, by its owner (wave q >> 2)
+        auto act_out = [&](auto L, f4 (&o)[16], int q) {
+            constexpr int l = decltype(L)::value;
+            if constexpr (l == 0 && !Net::kSiren) {
+                p_act<0>(R, o, q, inv_su0, bias0, nullptr, sdfp, g, es);
+            } else {
+                constexpr int f = Net::kSiren ? l : l - 1;
+                if constexpr (l == NL - 2) p_act<2>(R, o, q, fg(f), fb(f), sig_w, sdfp, g, es);
+                else p_act<1>(R, o, q, fg(f), fb(f), nullptr, sdfp, g, es);
+            }
+        };
+        auto chunk_b = [&](int q) { return [&, q](f4 (&bn)[4]) { p_read_chunk(R, q, bn); }; };
+        f4 bn[4];
+        // layer 0: one k-step on the encoded inputs; wave 0 activates chunk 0 of its output
+        pstep<Net, 0, true>(R, X, e, bn, chunk_b(0), [&] {
+            act_out(std::integral_constant<int, 0>{}, X, 0);
+        });
+        // hidden layers 1 .. kHidden (in -> out alternate between X and Y)
+        auto dense = [&](auto L, f4 (&in)[16], f4 (&out)[16]) {
+            constexpr int l = decltype(L)::value;
+            sfor<0, 8>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                constexpr int KS = 1 + 8 * (l - 1) + j;
+                f4 bc[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) bc[i] = bn[i];
+                pstep<Net, KS, j == 0>(R, out, bc, bn, chunk_b((j + 1) & 7), [&] {
+                    if constexpr (j < 7) act_out(std::integral_constant<int, l - 1>{}, in, j + 1);
+                    else act_out(std::integral_constant<int, l>{}, out, 0);
+                });
+            });
+        };
+        sfor<1, Net::kHidden + 1>([&](auto L) {
+            constexpr int l = decltype(L)::value;
+            if constexpr (l & 1) dense(L, X, Y);
+            else dense(L, Y, X);
+        });
+        // views layer: input chunks 0-7 (the last hidden layer's output, sigma head
+        // chained: wave 0 chunks 0-3, wave 1 continues from its per-lane partial), then
+        // the direction k-step; the compositing weights are formed at k-step 7
+        constexpr bool kInX = (Net::kHidden & 1) == 0;     // last hidden output array
+        f4 (&vin)[16] = kInX ? X : Y;
+        f4 (&vout)[16] = kInX ? Y : X;
+        const uint32_t s0 = kPSamples * p;
+        float z[2] = {0.0f, 0.0f}, wj[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float sdf[2] = {0.0f, 0.0f}, dist[2] = {0.0f, 0.0f};
+        sfor<0, 9>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            constexpr int KS = KV + j;
+            f4 bc[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bc[i] = bn[i];
+            if constexpr (j == 5 && !Net::kSiren) {
+                // the compositing inputs that do not depend on the network (sample depth,
+                // segment length) come from the encode kernel; waited at this barrier
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    uint32_t s = s0 + 2 * c + (colB ? 1u : 0u);
+                    if (s >= G.N) s = G.N - 1;
+                    const float2 v = a.zd[tile_sid + (size_t)s * kTileRays];
+                    z[c] = v.x;
+                    dist[c] = v.y;
+                }
+            }
+            if constexpr (j == 7) {
+                if (p + 1 < p_end) load_inputs(p + 1);
+            }
+            auto nb = [&](f4 (&o)[4]) {
+                if constexpr (j < 7) {
+                    p_read_chunk(R, j + 1, o);
+                } else if constexpr (j == 7) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[i] = vx[i];
+                }
+            };
+            pstep<Net, KS, j == 0>(R, vout, bc, bn, nb, [&] {
+                if constexpr (j < 7) {
+                    act_out(std::integral_constant<int, NL - 2>{}, vin, j + 1);
+                    if constexpr (j == 6) {
+                        // the pair's sigma half-sums, added in wave order after the barrier
+                        sdfx_lds[pair][h][0][lane] = group_sum(sdfp[0]);
+                        sdfx_lds[pair][h][1][lane] = group_sum(sdfp[1]);
+                    }
+                } else if constexpr (j == 7 && (PABL & 2)) {
+                    wj[0] = sdfx_lds[pair][0][0][lane];
+                    wj[1] = sdfx_lds[pair][1][0][lane];
+                } else if constexpr (j == 7) {
+                    // compositing weights of the pass's 4 samples, identically in both
+                    // lanes of a ray and both waves of the pair, front to back
+                    float al[2];
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        sdf[c] = __fadd_rn(__fadd_rn(sdfx_lds[pair][0][c][lane], sdfx_lds[pair][1][c][lane]),
+                                           sig_b);
+                        const uint32_t s = s0 + 2 * c + (colB ? 1u : 0u);
+                        const bool s_ok = s < G.N;
+                        const uint32_t sc_ = s_ok ? s : G.N - 1;
+                        if constexpr (Net::kSiren) {
+                            z[c] = sample_z(G.sc, nr, fr, ray_index, sc_);
+                            dist[c] = (sc_ + 1 < G.N)
+                                          ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), z[c]), dnorm)
+                                          : __fmul_rn(1e10f, dnorm);
+                        }
+                        float alpha;
+                        if (a.with_sdf) {
+                            const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf[c], beta_s)), beta_s);
+                            alpha = 1.0f - expf(-sig * dist[c]);
+                        } else {
+                            float raw = sdf[c];
+                            if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
+                            const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+                            alpha = 1.0f - expf(-sp * dist[c]);
+                        }
+                        al[c] = s_ok ? alpha : 0.0f;
+                    }
+                    const float o0 = ror8(al[0]), o1 = ror8(al[1]);
+                    const float aj[4] = {colB ? o0 : al[0], colB ? al[0] : o0, colB ? o1 : al[1],
+                                         colB ? al[1] : o1};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t s = s0 + k;
+                        if (s < G.N) {
+                            float w = aj[k] * T;
+                            if (a.force_background && s + 1 == G.N) w = 1.0f - wsum;
+                            T = T * ((1.0f - aj[k]) + 1e-10f);
+                            wsum += w;
+                            wj[k] = w;
+                        }
+                    }
+                }
+            });
+        });
+        // colour features f = sin(gamma_v x + beta_v) of the own rows, rgb half-sums.
+        // Packed fp32 over the two sample blocks (each half of a v_pk_fma_f32 is the
+        // scalar fma of its block, in the same order): this tail runs outside the MFMA
+        // stream, on both waves of the SIMD at once.
+        const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
+        f2 P[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};   // rgb half-sums (block 0, 1)
+        if constexpr (PABL & 1) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) P[t % 3][t & 1] += vout[t][0] + vout[t][3] * wj[0];
+        } else
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int f0 = 16 * (2 * t + (int)h) + 4 * (int)g;
+            const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
+            const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
+            const f4 w0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
+            const f4 w1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
+            const f4 w2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
+            f4 fa, fb_;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const f2 arg = pk_fma(f2{vout[2 * t][r], vout[2 * t + 1][r]}, f2{gm[r], gm[r]},
+                                      f2{bt[r], bt[r]});
+                const f2 fv = {sin_rev(arg.x), sin_rev(arg.y)};
+                P[0] = pk_fma(fv, f2{w0[r], w0[r]}, P[0]);
+                P[1] = pk_fma(fv, f2{w1[r], w1[r]}, P[1]);
+                P[2] = pk_fma(fv, f2{w2[r], w2[r]}, P[2]);
+                fa[r] = fv.x;
+                fb_[r] = fv.y;
+            }
+            vout[2 * t] = fa;
+            vout[2 * t + 1] = fb_;
+        }
+        float pc[2][3];
+#pragma unroll
+        for (int o = 0; o < 3; ++o) {
+            pc[0][o] = group_sum(P[o].x);
+            pc[1][o] = group_sum(P[o].y);
+        }
+        if (h == 0 && g == 0) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int o = 0; o < 3; ++o) pcol_lds[pair][3 * c + o][n] = pc[c][o];
+        }
+        if (a.features && !(PABL & 1)) {
+            // facc += w0 f0 + w1 f1 + w2 f2 + w3 f3 (in that order) by the lane of the
+            // ray's samples 0 and 2 (block 0 / 1, n < 8); row pairs packed
+            const f2 W0 = {wj[0], wj[0]}, W1 = {wj[1], wj[1]}, W2 = {wj[2], wj[2]}, W3 = {wj[3], wj[3]};
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                f4 o0, o1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    o0[r] = ror8(vout[2 * t][r]);
+                    o1[r] = ror8(vout[2 * t + 1][r]);
+                }
+                if (!colB) {
+                    f4 v = facc[(t * 4 + g) * 8 + r8];
+#pragma unroll
+                    for (int r = 0; r < 4; r += 2) {
+                        f2 u = {v[r], v[r + 1]};
+                        u = pk_fma(f2{vout[2 * t][r], vout[2 * t][r + 1]}, W0, u);
+                        u = pk_fma(f2{o0[r], o0[r + 1]}, W1, u);
+                        u = pk_fma(f2{vout[2 * t + 1][r], vout[2 * t + 1][r + 1]}, W2, u);
+                        u = pk_fma(f2{o1[r], o1[r + 1]}, W3, u);
+                        v[r] = u.x;
+                        v[r + 1] = u.y;
+                    }
+                    facc[(t * 4 + g) * 8 + r8] = v;
+                }
+            }
+        }
+        if (a.sdf && h == 0 && ray_ok && g == 0) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const uint32_t s = s0 + 2 * c + (colB ? 1u : 0u);
+                if (s < G.N) a.sdf[(size_t)ray_index * G.N + s] = sdf[c];
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (h == 1) {
+            float q[2][3];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                q[c][0] = sigmoidf_(__fadd_rn(__fadd_rn(pcol_lds[pair][3 * c][n], pc[c][0]), rgb_b0));
+                q[c][1] = sigmoidf_(__fadd_rn(__fadd_rn(pcol_lds[pair][3 * c + 1][n], pc[c][1]), rgb_b1));
+                q[c][2] = sigmoidf_(__fadd_rn(__fadd_rn(pcol_lds[pair][3 * c + 2][n], pc[c][2]), rgb_b2));
+            }
+            float racc[3] = {racc0, racc1, racc2};
+#pragma unroll
+            for (int o = 0; o < 3; ++o) {
+                const float e0 = ror8(q[0][o]), e1 = ror8(q[1][o]);
+                const float qj[4] = {colB ? e0 : q[0][o], colB ? q[0][o] : e0, colB ? e1 : q[1][o],
+                                     colB ? q[1][o] : e1};
+                float v = racc[o];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v = __fmaf_rn(wj[k], qj[k], v);
+                racc[o] = v;
+            }
+            racc0 = racc[0];
+            racc1 = racc[1];
+            racc2 = racc[2];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (s0 + k < G.N) w_last = wj[k];
+            if (a.xyz) {
+                const float e0 = ror8(z[0]), e1 = ror8(z[1]);
+                const float zj[4] = {colB ? e0 : z[0], colB ? z[0] : e0, colB ? e1 : z[1],
+                                     colB ? z[1] : e1};
+                float xa[3] = {xacc0, xacc1, xacc2};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int d = 0; d < 3; ++d)
+                        xa[d] = __fmaf_rn(wj[k], __fadd_rn(ray.o[d], __fmul_rn(ray.d[d], zj[k])), xa[d]);
+                xacc0 = xa[0];
+                xacc1 = xa[1];
+                xacc2 = xa[2];
+            }
+        }
+    }
+    // the ring runs ahead across passes: no LDS-DMA may land after the workgroup ends
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!ray_ok || colB) return;
+    if (a.nseg > 1) {
+        const size_t Rr = (size_t)G.total_tiles * kTileRays;
+        float *pp = a.part + (size_t)seg * kPartQ * Rr + (size_t)tile * kTileRays + ray_in_tile;
+        if (a.features) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const uint32_t jf = 16 * (2 * t + h) + 4 * g;
+                const f4 v = facc[(t * 4 + g) * 8 + r8];
+                pp[(size_t)(jf + 0) * Rr] = v.x;
+                pp[(size_t)(jf + 1) * Rr] = v.y;
+                pp[(size_t)(jf + 2) * Rr] = v.z;
+                pp[(size_t)(jf + 3) * Rr] = v.w;
+            }
+        }
+        if (h == 1 && g == 0) {
+            const float q[8] = {racc0, racc1, racc2, xacc0, xacc1, xacc2, T, w_last};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pp[(size_t)(kW + k) * Rr] = q[k];
+        }
+        return;
+    }
+    const size_t HW = (size_t)G.H * G.W;
+    const size_t pix = (size_t)py * G.W + px;
+    if (h == 1) {
+        if (g < 3) {
+            const float rc = g == 0 ? racc0 : (g == 1 ? racc1 : racc2);
+            a.rgb[((size_t)b * 3 + g) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, rc));
+            if (a.xyz) {
+                const float xc = g == 0 ? xacc0 : (g == 1 ? xacc1 : xacc2);
+                a.xyz[((size_t)b * 3 + g) * HW + pix] = xc;
+            }
+        } else if (a.mask) {
+            a.mask[(size_t)b * HW + pix] = w_last;
+        }
+    }
+    if (a.features) {
+        float *fbp = a.features + (size_t)b * kW * HW + pix;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t jf = 16 * (2 * t + h) + 4 * g;
+            const f4 v = facc[(t * 4 + g) * 8 + r8];
+            fbp[(size_t)(jf + 0) * HW] = v.x;
+            fbp[(size_t)(jf + 1) * HW] = v.y;
+            fbp[(size_t)(jf + 2) * HW] = v.z;
+            fbp[(size_t)(jf + 3) * HW] = v.w;
+        }
+    }
+}
+
 // Chains the nseg segment partials of every ray (see kPartQ): one thread per
 // (ray, quantity), quantities on grid.y.
 __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
@@ -899,8 +1606,39 @@ uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_b
     return nseg;
 }
 
+// field_p_kernel: 4 tiles (2 ray groups) per workgroup, 4 samples of a ray per pass.
+// Small batches first give each ray group its own workgroup (rsplit = 2), then split
+// the samples (nseg) while the grid stays under one workgroup per CU.
+static void field_p_split(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background,
+                          uint32_t max_seg, uint32_t *rsplit, uint32_t *nseg_out) {
+    if (max_seg == 0 || max_seg > kFieldSplitMax) max_seg = kFieldSplitMax;
+    const uint32_t wgs = B * ((tiles_per_face + kPTiles - 1) / kPTiles);
+    *rsplit = 1;
+    const uint32_t npass = (N + kPSamples - 1) / kPSamples;
+    uint32_t nseg = 1;
+    while (!force_background && wgs * nseg < 256 && 2 * nseg <= max_seg) {
+        const uint32_t c = 2 * nseg, pps = (npass + c - 1) / c;
+        if ((c - 1) * pps >= npass) break;            // no empty last segment
+        nseg = c;
+    }
+    *nseg_out = nseg;
+}
+
+uint32_t field_p_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background,
+                      uint32_t max_seg) {
+    uint32_t rs, ns;
+    field_p_split(B, tiles_per_face, N, force_background, max_seg, &rs, &ns);
+    return ns;
+}
+
+static bool field_pair() {
+    static const bool v = getenv("SDFR_FIELD_X2") == nullptr;
+    return v;
+}
+
 size_t field_part_bytes(uint32_t B, uint32_t tiles_per_face, uint32_t N) {
-    const uint32_t nseg = field_nseg(B, tiles_per_face, N, 0, kFieldSplitMax);
+    const uint32_t nseg = field_pair() ? field_p_nseg(B, tiles_per_face, N, 0, kFieldSplitMax)
+                                       : field_nseg(B, tiles_per_face, N, 0, kFieldSplitMax);
     return nseg > 1 ? (size_t)nseg * kPartQ * B * tiles_per_face * kTileRays * sizeof(float) : 0;
 }
 
@@ -980,10 +1718,11 @@ static int launch_xprep(const NetPtrs &P, const sdfr_ngp_render_args *a, char *x
 template <class Net>
 static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const GeomArgs &g,
                          const float *enc, char *xws, const float *film, hipStream_t st,
-                         float *part = nullptr) {
+                         float *part = nullptr, const float2 *zd = nullptr) {
     XFieldArgs f;
     f.g = g;
     f.enc = enc;
+    f.zd = zd;
     if (a->prepacked) xws = const_cast<char *>(reinterpret_cast<const char *>(a->prepacked));
     f.packed = reinterpret_cast<const f4 *>(xws);
     f.su = reinterpret_cast<const float *>(xws + (size_t)Net::kSlices * kXSliceF4 * sizeof(f4));
@@ -1002,9 +1741,23 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     f.sdf = a->sdf;
     f.xyz = a->xyz;
     f.mask = a->mask;
+    f.part = part;
+    f.rsplit = 1;
+    if (field_pair()) {
+        field_p_split(g.B, g.tiles_per_face, g.N, a->force_background, a->max_field_segments,
+                      &f.rsplit, &f.nseg);
+        if (!part) f.nseg = 1;
+        const uint32_t blocks =
+            g.B * ((g.tiles_per_face + kPTiles - 1) / kPTiles) * f.rsplit * f.nseg;
+        hipLaunchKernelGGL((field_p_kernel<Net>), dim3(blocks), dim3(kPThreads), 0, st, f);
+        int rc = check_launch("render: field (f16x3)");
+        if (rc || f.nseg == 1) return rc;
+        const uint32_t rays = g.total_tiles * kTileRays;
+        hipLaunchKernelGGL(field_merge_kernel, dim3((rays + 255) / 256, kPartQ), dim3(256), 0, st, f);
+        return check_launch("render: field segment merge");
+    }
     f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background,
                               a->max_field_segments) : 1;
-    f.part = part;
     const uint32_t blocks = g.B * ((g.tiles_per_face + kWaves - 1) / kWaves) * f.nseg;
     switch (field_variant()) {
 #ifdef SDFR_ABLATION
@@ -1063,8 +1816,8 @@ int launch_xprep_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, c
 
 int launch_xfield_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
                       const GeomArgs &g, const float *enc, char *xws, const float *film,
-                      hipStream_t st, float *part) {
-    return launch_xfield<NgpNet>(ngp_ptrs(w), a, g, enc, xws, film, st, part);
+                      hipStream_t st, float *part, const float2 *zd) {
+    return launch_xfield<NgpNet>(ngp_ptrs(w), a, g, enc, xws, film, st, part, zd);
 }
 
 // ----------------------------------------------------------------------------

@@ -135,7 +135,7 @@ int launch_xprep_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a, c
                      float *film, hipStream_t st);
 int launch_xfield_ngp(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
                       const GeomArgs &g, const float *enc, char *xws, const float *film,
-                      hipStream_t st, float *part);
+                      hipStream_t st, float *part, const float2 *zd);
 // sample-segment split of the f16x3 field kernel for small batches
 constexpr uint32_t kFieldSplitMax = 4;   // sample segments per ray at most
 uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background,

@@ -116,6 +116,7 @@ struct EncodeArgs {
     const float *emb;
     const int32_t *offsets;
     float *enc;                    // [L][S_total][2]
+    float2 *zd;                    // [S_total] (z, segment length) for the f16x3 field, or null
     LevelTable lt;
     int pair_ok;                   // table 16-B aligned (paired corner loads)
 };
@@ -252,6 +253,25 @@ __device__ __forceinline__ void level_interp_adj(const float *__restrict__ grid,
         for (uint32_t c = 0; c < 2; ++c) out[c] = __fmaf_rn(wts[idx], v[idx][c], out[c]);
 }
 
+// Depth z of sample `sid` and its segment length dist = (z_{s+1} - z_s) |d| (1e10 |d|
+// for the last sample), sdf_model.py:240-243 -- the compositing inputs that do not
+// depend on the network, handed to field_p_kernel with the features.
+__device__ __forceinline__ float2 sample_zd(const GeomArgs &g, uint32_t sid) {
+    const SampleId id = decode_sid(g, sid);
+    const uint32_t rl = id.ray_local < g.H * g.W ? id.ray_local : g.H * g.W - 1;
+    const uint32_t y = rl / g.W, x = rl % g.W;
+    const uint32_t ray_index = (id.b * g.H + y) * g.W + x;
+    Ray ray;
+    make_ray(g.cam + (size_t)id.b * 12, g.focal[id.b], g.pix_x[x], g.pix_y[y], g.half_res, ray);
+    const float nr = g.near_[id.b], fr = g.far_[id.b];
+    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
+    const float z = sample_z(g.sc, nr, fr, ray_index, id.s);
+    const float dist = (id.s + 1 < g.N)
+                           ? __fmul_rn(__fsub_rn(sample_z(g.sc, nr, fr, ray_index, id.s + 1), z), dnorm)
+                           : __fmul_rn(1e10f, dnorm);
+    return make_float2(z, dist);
+}
+
 // One thread: SPT samples (256 apart) x LPT levels {y, y + 16/LPT, ...}.
 // Branch-free: padding / out-of-box samples gather at u = 0.5 and store 0, so
 // every corner load of the thread can be in flight at once.
@@ -293,6 +313,11 @@ __global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
                 out[(size_t)level * a.g.S_total + sid[k]] =
                     in[k] ? make_float2(res[0], res[1]) : make_float2(0.0f, 0.0f);
         }
+    }
+    if (a.zd && blockIdx.y == 0) {
+#pragma unroll
+        for (uint32_t k = 0; k < SPT; ++k)
+            if (live[k]) a.zd[sid[k]] = sample_zd(a.g, sid[k]);
     }
 }
 
@@ -761,10 +786,11 @@ struct Workspace {
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-// enc [L][S][2] | packed fp32 fragments | film | split-fp16 region (field_f16x3.hip)
+// enc [L][S][2] | packed fp32 fragments | film | split-fp16 region (field_f16x3.hip) |
+// segment partials | zd [S] (z, segment length)
 static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t L,
                         size_t *o_packed, size_t *o_film, size_t *o_x = nullptr,
-                        size_t *o_part = nullptr) {
+                        size_t *o_part = nullptr, size_t *o_zd = nullptr) {
     const size_t tiles = (size_t)B * ((H * W + kTileRays - 1) / kTileRays);
     const size_t S = tiles * N * kTileRays;
     size_t off = align256(S * L * 2 * sizeof(float));
@@ -776,6 +802,8 @@ static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t
     off += align256(f16x3_ws_bytes(0));
     if (o_part) *o_part = off;
     off += align256(field_part_bytes(B, (H * W + kTileRays - 1) / kTileRays, N));
+    if (o_zd) *o_zd = off;
+    off += align256(S * 2 * sizeof(float));
     return off;
 }
 
@@ -917,12 +945,13 @@ static void launch_encode_mode(hipStream_t st, const EncodeArgs &e) {
 }
 
 static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
-                         const GeomArgs &g, float *enc, hipStream_t st) {
+                         const GeomArgs &g, float *enc, hipStream_t st, float2 *zd = nullptr) {
     EncodeArgs e;
     e.g = g;
     e.emb = w->embeddings;
     e.offsets = w->offsets;
     e.enc = enc;
+    e.zd = zd;
     e.pair_ok = (reinterpret_cast<uintptr_t>(w->embeddings) & 15u) == 0;
     make_level_table(16, w->log2_per_level_scale, w->base_resolution, e.lt);
 #ifdef SDFR_ABLATION
@@ -1020,8 +1049,8 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     int rc = validate(w, a);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    size_t o_packed, o_film, o_x, o_part;
-    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film, &o_x, &o_part);
+    size_t o_packed, o_film, o_x, o_part, o_zd;
+    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film, &o_x, &o_part, &o_zd);
     char *ws = reinterpret_cast<char *>(a->workspace);
     float *enc = reinterpret_cast<float *>(ws);
     f4 *packed = reinterpret_cast<f4 *>(ws + o_packed);
@@ -1033,10 +1062,11 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     if (a->field_precision == SDFR_FIELD_F16X3) {
         if ((rc = launch_xprep_ngp(w, a, ws + o_x, film, st))) return rc;
         record_event(a->stage_events[1], st);
-        if ((rc = launch_encode(w, a, g, enc, st))) return rc;
+        float2 *zd = reinterpret_cast<float2 *>(ws + o_zd);
+        if ((rc = launch_encode(w, a, g, enc, st, zd))) return rc;
         record_event(a->stage_events[2], st);
         float *part = reinterpret_cast<float *>(ws + o_part);
-        if ((rc = launch_xfield_ngp(w, a, g, enc, ws + o_x, film, st, part))) return rc;
+        if ((rc = launch_xfield_ngp(w, a, g, enc, ws + o_x, film, st, part, zd))) return rc;
         record_event(a->stage_events[3], st);
         return SDFR_OK;
     }

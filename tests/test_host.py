@@ -78,12 +78,17 @@ def test_workspace_size(sdfr):
     enc = 2 * 4096 * 24 * 16 * 2 * 4
     fixed = 67 * 1024 * 16 + 2 * 8 * 256 * 4          # fp32 fragments + FiLM vectors
     xfixed = 68 * 1024 * 16 + 2 * 5 * 256 * 4         # split-fp16 fragments, su, bias_s
-    # 2 faces = 128 workgroups: rays split in 2 sample segments, partials of
+    zd = 2 * 4096 * 24 * 2 * 4                         # per-sample (z, segment length)
+    # 2 faces = 256 workgroups of 2 tiles: no sample split, no partials
+    assert enc + fixed + xfixed + zd <= n <= enc + fixed + xfixed + zd + 1536
+    # 1 face = 128 workgroups: rays split in 2 sample segments, partials of
     # (256 features + rgb, xyz, T, w_last) per segment and ray
-    part = 2 * (256 + 8) * 2 * 4096 * 4
-    assert enc + fixed + xfixed + part <= n <= enc + fixed + xfixed + part + 1280
+    n1 = lib.sdfr_render_ngp_workspace_bytes(1, 64, 64, 24, 16)
+    part = 2 * (256 + 8) * 4096 * 4
+    base1 = enc // 2 + 67 * 1024 * 16 + 8 * 256 * 4 + xfixed + zd // 2
+    assert base1 + part <= n1 <= base1 + part + 1536
     n32 = lib.sdfr_render_ngp_workspace_bytes(32, 64, 64, 24, 16)   # >= 256 workgroups: no split
-    assert n32 <= 16 * enc + fixed + 32 * 8 * 256 * 4 + xfixed + 1280
+    assert n32 <= 16 * (enc + zd) + fixed + 32 * 8 * 256 * 4 + xfixed + 1536
     # the per-call sample-split bound is validated before anything is launched
     w, a = sdfr._lib.NgpWeights(), sdfr._lib.NgpRenderArgs()
     w.num_levels, a.B, a.H, a.W, a.N = 16, 1, 8, 8, 24
