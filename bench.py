@@ -267,8 +267,8 @@ def main():
     field_tflops = flop * samples / (field_ms * 1e-3) / 1e12
     gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9 if not siren else 0.0
     f16x3 = args.field_precision == "f16x3"
-    field_kernel = ("field_x2_kernel<0, sdfr::SirenNet>" if siren else
-                    "field_x2_kernel<0, sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
+    field_kernel = ("field_p_kernel<sdfr::SirenNet>" if siren else
+                    "field_p_kernel<sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
     def traffic_of(kernel):
         """HBM bytes per launch of `kernel` at this batch, from the committed
         rocprofv3 PMC passes (profiles/, scripts/summarize_profiles.py), or None."""

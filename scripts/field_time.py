@@ -40,13 +40,24 @@ print(f"out {h}  {med:.3f} ms  {550912 * B * 4096 * 24 / med / 1e9:.1f} TFLOP/s"
 
 def main():
     prec = os.environ.get("PREC", "f16x3")
-    for lib in sys.argv[1:]:
-        env = dict(os.environ, SDFR_LIB=str(REPO / lib) if not lib.startswith("/") else lib)
-        out = subprocess.run([sys.executable, "-c", CHILD, str(REPO), prec], env=env,
-                             capture_output=True, text=True, timeout=240)
-        res = out.stdout.strip().splitlines()[-1] if out.returncode == 0 else \
-            f"FAILED rc={out.returncode}: {out.stderr.strip().splitlines()[-1:]}"
-        print(f"{lib:50s} {res}", flush=True)
+    reps = int(os.environ.get("REPS", "3"))
+    libs = sys.argv[1:]
+    res = {lib: [] for lib in libs}
+    for _ in range(reps):                       # libs interleaved, each in its own process
+        for lib in libs:
+            env = dict(os.environ, SDFR_LIB=str(REPO / lib) if not lib.startswith("/") else lib)
+            out = subprocess.run([sys.executable, "-c", CHILD, str(REPO), prec], env=env,
+                                 capture_output=True, text=True, timeout=240)
+            if out.returncode:
+                print(f"{lib:50s} FAILED rc={out.returncode}: {out.stderr.strip().splitlines()[-1:]}")
+                continue
+            line = out.stdout.strip().splitlines()[-1]
+            res[lib].append(float(line.split()[2]))
+            print(f"{lib:50s} {line}", flush=True)
+    for lib, v in res.items():
+        if v:
+            print(f"SUMMARY {lib:50s} median {statistics.median(v):.3f} ms  min {min(v):.3f}  "
+                  f"n {len(v)}", flush=True)
 
 
 if __name__ == "__main__":

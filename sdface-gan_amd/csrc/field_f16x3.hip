@@ -9,8 +9,8 @@
 //             Points are formed in-kernel from the ray (bit-exact chain).
 //
 // followed by SDF->density and front-to-back alpha compositing
-// (volume_integration, :236-301), 16 rays per wave.  Every fp32 GEMM tile runs
-// as three v_mfma_f32_16x16x32_f16 on a hi/lo fp16 split of both operands:
+// (volume_integration, :236-301).  Every fp32 GEMM tile runs as three
+// v_mfma_f32_16x16x32_f16 on a hi/lo fp16 split of both operands:
 //
 //     W.x = W_hi.x_hi + W_hi.x_lo + W_lo.x_hi   (+ W_lo.x_lo, dropped: 2^-22 rel.)
 //
@@ -24,14 +24,14 @@
 // divided by su (gamma' x_scaled == gamma x, bit for bit), and NGP's identity
 // input layer multiplies by 1/su.
 //
-// Work unit (field_x2_kernel below): a workgroup of 8 waves, two per SIMD; a wave
-// owns one MFMA sample column of N = 16 = 8 rays x 2 samples, so each A fragment
-// read from LDS feeds 3 MFMAs, and the weight stream (1.1 MB ngp / 2.1 MB siren per
-// pass, shared by the 8 waves through a 4-slot LDS-DMA ring of 16 KB half-slices) is
-// amortised over 128 ray-samples.  The accumulator of layer l is the B operand of
-// layer l+1 with no lane movement:
-// after a pair of 16-row tiles (2q, 2q+1) is activated, its 8 values per lane
-// are split in place into (hi, lo) fp16x8, which is exactly the k-step q
+// Work unit (field_p_kernel below): a workgroup of 8 waves, two per SIMD, over 2
+// tiles of 16 rays; the two waves of a SIMD form a pair over 32 samples (8 rays x 4
+// consecutive samples) and split the 256 output rows of every layer between them
+// (wave h: global 16-row tiles 2t + h), so each A fragment read from LDS feeds 6
+// MFMAs.  The weight stream (1.1 MB ngp / 2.1 MB siren per pass) is shared by the 8
+// waves through a 4-slot LDS-DMA ring of 16 KB half-slices.  The accumulator of
+// layer l is the B operand of layer l+1 with no lane movement: a 16-row tile's 4
+// values per lane, activated, are half (one 8-byte half per wave) of the k-step
 // fragment (the packed weights permute K to match, xprep_kernel).
 #include <hip/hip_runtime.h>
 
@@ -231,7 +231,6 @@ struct XFieldArgs {
     int force_background, with_sdf;
     float *rgb, *features, *sdf, *xyz, *mask;
     uint32_t nseg;                 // sample segments per ray (1: whole rays, no merge)
-    uint32_t rsplit;               // field_p_kernel: ray groups per workgroup split over 2 (1 / 2)
     float *part;                   // nseg > 1: [nseg][kPartQ][rays] segment partials
 };
 
@@ -244,48 +243,6 @@ struct XFieldArgs {
 // differences; tests/test_gpu_render.py compares split and unsplit renders).
 // Partials per (segment, ray): 256 features, rgb[3], xyz[3], T, w_last.
 constexpr uint32_t kPartQ = kW + 8;
-
-// Activate tile pair (2q, 2q+1) of one sample column in place and split it
-// into the (hi, lo) B fragment of k-step q.
-//   MODE 0: identity layer, fma(x 2^-es, 1/su, b)  (ngp input_linear: the GEMM ran
-//           on features scaled by 2^es and accumulated from zero, see feat_scale)
-//   MODE 1: FiLM sin(gamma x + beta) = sin_rev(fma(gamma'', x_s, beta''))  (sdf_model.py:67;
-//           revolutions, see xprep_kernel)
-//   MODE 2: FiLM + partial sigma_linear dot product (the sdf head)
-template <int MODE, int V>
-__device__ __forceinline__ void act_pair(f4 &za, f4 &zb, int q, const float *gam,
-                                         const float *bet, const float *sw, float &sdfp,
-                                         uint32_t g, int es = 0) {
-    if constexpr ((V & 8) != 0) {
-        xpin(za);
-        xpin(zb);
-        return;
-    }
-    float v[8];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        const f4 z = half ? zb : za;
-        const int f0 = 16 * (2 * q + half) + 4 * (int)g;
-        const f4 gm = *reinterpret_cast<const f4 *>(gam + f0);
-        const f4 bt = *reinterpret_cast<const f4 *>(bet + f0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float x;
-            if constexpr (MODE == 0) x = __fmaf_rn(__builtin_ldexpf(z[r], -es), gm[r], bt[r]);
-            else x = sin_rev(__fmaf_rn(gm[r], z[r], bt[r]));
-            v[4 * half + r] = x;
-        }
-        if constexpr (MODE == 2) {
-            const f4 w4 = *reinterpret_cast<const f4 *>(sw + f0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sdfp = __fmaf_rn(v[4 * half + r], w4[r], sdfp);
-        }
-    }
-    split8(v, za, zb);
-    xpin(za);
-    xpin(zb);
-    if constexpr (MODE == 2) xpin(sdfp);
-}
 
 // ngp layer-0 inputs: the 32 hash-grid features of a sample span the 4 lane
 // groups of its column.  They are scaled by the power of two 2^es that brings the
@@ -307,590 +264,45 @@ __device__ __forceinline__ int feat_scale(float (&v)[8]) {
     return es;
 }
 
-__device__ __forceinline__ void zero_acc(f4 (&acc)[16]) {
-#pragma unroll
-    for (int t = 0; t < 16; ++t) acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-}
-
-
-// ----------------------------------------------------------------------------
-// field_x2_kernel: two waves per SIMD.
-//
-// field_x_kernel runs ONE wave per SIMD (472 VGPR+AGPR: two 16-ray sample
-// columns of accumulators in and out of a layer), so every LDS / barrier /
-// dependency latency of the wave is exposed and its VALU issues at the
-// single-wave rate (4 cycles per instruction).  Here a workgroup is 8 waves, two
-// per SIMD, each with ONE sample column of MFMA N = 16 = 8 rays x 2 samples
-// (lanes n < 8: sample 2p of ray n, lanes n >= 8: sample 2p+1 of ray n-8), half
-// the accumulators (<= 256 registers), so one wave's MFMAs run while its partner
-// waits or issues VALU.  Each A fragment now feeds 3 MFMAs instead of 6 (twice
-// the LDS read traffic per MFMA, 2 ds_read_b128 per 48 MFMA cycles per SIMD).
-// The two samples of a ray meet in the compositing through one DPP row rotation
-// (ror 8) per exchanged value; the transmittance chain, weights and sums are
-// formed in the same order in both lanes (sample 2p, then 2p+1), the feature
-// accumulator of a ray (8 KB per wave in LDS) is updated by the sample-2p lane.
-// The workgroup still covers 4 tiles of 16 rays of ONE face (wave w: tile w & 3,
-// rays 8 (w >> 2) .. +7), so the grid, the sample-segment split and the partial
-// layout are those of field_x_kernel.
-// ----------------------------------------------------------------------------
-constexpr int kWaves2 = 8;
-constexpr int kThreads2 = kWaves2 * 64;
-// The weight ring: 4 half-slice slots (16 KB each) filled by LDS-DMA (buffer_load
-// ... lds), DMA and barrier per whole k-step (two half-slices, the next k-step fetched
-// one k-step ahead: 34 barriers per ngp pass).  A fragments are prefetched one MFMA
-// group ahead across half-step and k-step boundaries: the k-step's barrier sits ahead
-// of its last group's MFMAs, and the next k-step's first group is read behind them.
-// The register work of a half-step (the next input pair's activation) is issued after
-// its MFMA group 1.  (Measured alternatives -- register staging through ds_write,
-// per-half-step barriers, staggered or interleaved side work, wave priorities -- are
-// in git history)
-constexpr int kX2Slots = 4;
-constexpr int kX2Side = 1;
-constexpr int kX2DmaPieces = 16 / kWaves2;          // 1 KB pieces per wave per half-slice
+constexpr int kRingSlots = 4;                        // weight ring: 4 half-slice slots (16 KB)
+constexpr int kDmaPieces = 2;                        // 1 KB LDS-DMA pieces per wave per half-slice
 
 __device__ __forceinline__ float ror8(float v) {   // lane n <- lane (n + 8) mod 16 of its row
     return __builtin_bit_cast(
         float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
 }
 
-struct XRing2 {
-    f4 *lds;
-    f4 nh[2], nl[2];      // the next half-step's first group of A fragments
-    v4i drsrc;            // the packed fragments for the LDS-DMA
-    uint32_t it, tid, wave;
-    uint32_t slot0;       // DMA ring slot of the pass's first half-slice (wave-uniform)
-};
-
-// ring slot of half-step it (0 <= it < kSlices) of the current pass
-template <class Net>
-__device__ __forceinline__ uint32_t x2_slot(const XRing2 &R, uint32_t it) {
-    constexpr uint32_t S = kX2Slots;
-    if constexpr (Net::kSlices % S == 0) return it % S;  // slot0 stays 0
-    return (R.slot0 + it) % S;
-}
-
-// One 1 KB LDS-DMA piece: source byte offset sbase + soff, LDS byte address lbase +
-// loff.  The two additions run inside the asm, so the compiler keeps only the
-// per-wave bases live (the constants are rematerialised at each use): with the
-// sums formed outside, the 68 distinct per-step addresses of an unrolled pass were
-// hoisted into SGPRs and spilled.
-__device__ __forceinline__ void dma16x(v4i rsrc, uint32_t voff, uint32_t sbase, uint32_t soff,
-                                       uint32_t lbase, uint32_t loff) {
-    uint32_t keep, so;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_add_u32 m0, %4, %5\n\ts_add_u32 %1, %6, %7\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %2, %3, %1 offen lds\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep), "=&s"(so)
-        : "v"(voff), "s"(rsrc), "s"(lbase), "s"(loff), "s"(sbase), "s"(soff)
-        : "memory", "scc");
-}
-
-// LDS-DMA of half-slice `slice` into ring slot `slot` (this wave's pieces)
-__device__ __forceinline__ void x2_dma(XRing2 &R, uint32_t slice, uint32_t slot) {
-    const uint32_t sbase = R.wave * (kX2DmaPieces * 1024u);
-    const uint32_t lbase = lds_addr(R.lds) + sbase;
-#pragma unroll
-    for (int k = 0; k < kX2DmaPieces; ++k)
-        dma16x(R.drsrc, (R.tid & 63u) * 16u, sbase, slice * kXSliceF4 * 16u + k * 1024u, lbase,
-               slot * kXSliceF4 * 16u + k * 1024u);
-}
-
-// One half k-step of one sample column: 8 output tiles x 3 split terms = 24
-// MFMAs, term-major so each accumulator is touched every 8th MFMA; then `side`,
-// the ring staging and the slice barrier (as xstep).
-template <int V, class Net, int H, class Side>
-__device__ __forceinline__ void xstep2(XRing2 &R, f4 (&acc)[16], const f4 bh, const f4 bl,
-                                       Side &&side) {
-    const uint32_t lane = R.tid & 63u;
-    if constexpr (H == 0 && (V & 4) == 0) {
-        // at its first half the next k-step's two half-slices go into the slots of the
-        // previous k-step (closed by its barrier)
-        x2_dma(R, (R.it + 2) % Net::kSlices, x2_slot<Net>(R, R.it + 2));
-        x2_dma(R, (R.it + 3) % Net::kSlices, x2_slot<Net>(R, R.it + 3));
-    }
-    // this half-slice and the next (H = 0: the same k-step's second half, already
-    // published; H = 1: the next k-step's first, published by this step's barrier)
-    const f4 *A = R.lds + x2_slot<Net>(R, R.it) * kXSliceF4 + lane;
-    const f4 *An = R.lds + x2_slot<Net>(R, R.it + 1) * kXSliceF4 + lane;
-    f4 ah[8], al[8];
-    auto rd = [&](const f4 *src, int t, f4 &h, f4 &l) {
-        if constexpr ((V & 2) != 0) {
-            h = bh * (float)(t + 1);
-            l = bl * (float)(t + 1);
-        } else {
-            h = src[(2 * t) * 64];
-            l = src[(2 * t + 1) * 64];
-        }
-    };
-    ah[0] = R.nh[0];
-    al[0] = R.nl[0];
-    ah[1] = R.nh[1];
-    al[1] = R.nl[1];
-#pragma unroll
-    for (int grp = 0; grp < 4; ++grp) {
-        const int gn = grp + 1;
-        if (H == 1 && gn == 4) {
-            // every read of this k-step's slots is issued: land own DMA pieces of the
-            // next k-step, drain the reads, publish / close at the barrier
-            if constexpr ((V & 4) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if constexpr ((V & 1) == 0) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-            }
-        }
-        if (gn < 4) {
-            rd(A, 2 * gn, ah[2 * gn], al[2 * gn]);
-            rd(A, 2 * gn + 1, ah[2 * gn + 1], al[2 * gn + 1]);
-        } else {
-            rd(An, 0, R.nh[0], R.nl[0]);
-            rd(An, 1, R.nh[1], R.nl[1]);
-        }
-        const int i0 = 2 * grp, i1 = 2 * grp + 1;
-        acc[8 * H + i0] = mfma16(al[i0], bh, acc[8 * H + i0]);
-        acc[8 * H + i1] = mfma16(al[i1], bh, acc[8 * H + i1]);
-        acc[8 * H + i0] = mfma16(ah[i0], bl, acc[8 * H + i0]);
-        acc[8 * H + i1] = mfma16(ah[i1], bl, acc[8 * H + i1]);
-        acc[8 * H + i0] = mfma16(ah[i0], bh, acc[8 * H + i0]);
-        acc[8 * H + i1] = mfma16(ah[i1], bh, acc[8 * H + i1]);
-        // keep this group's and the previous group's A fragments allocated until this
-        // group's MFMAs have issued: the allocator then cannot hand their registers to
-        // the next ds_read (or an MFMA result) while an in-flight MFMA still reads
-        // them, which cost s_nop hazard padding (506 -> 407 per pass, ~1 %)
-        asm volatile("" ::"v"(ah[i0]), "v"(ah[i1]), "v"(al[i0]), "v"(al[i1]));
-        if (grp > 0)
-            asm volatile("" ::"v"(ah[i0 - 2]), "v"(ah[i1 - 2]), "v"(al[i0 - 2]), "v"(al[i1 - 2]));
-        __builtin_amdgcn_sched_barrier(0);
-        if (grp == kX2Side) side();
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    ++R.it;
-}
-
-template <int V, class Net, class ActIn, class ActOut>
-__device__ __forceinline__ void dense_layer2(XRing2 &R, f4 (&in)[16], f4 (&out)[16],
-                                             ActIn &&act_in, ActOut &&act_out) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int qn = q < 7 ? q + 1 : 7;
-        xstep2<V, Net, 0>(R, out, in[2 * q], in[2 * q + 1], [&] {
-            if (q < 7) act_in(in[2 * qn], in[2 * qn + 1], qn);
-        });
-        xstep2<V, Net, 1>(R, out, in[2 * q], in[2 * q + 1], [&] {
-            if (q == 7) act_out(out[0], out[1], 0);
-        });
-    }
-}
-
-struct NoAct2 {
-    __device__ __forceinline__ void operator()(f4 &, f4 &, int) const {}
-};
-
-template <int V, class Net>
-__global__ void __launch_bounds__(kThreads2, 2) field_x2_kernel(const XFieldArgs a) {
-    constexpr int NF = Net::kFilmN;
-    __shared__ f4 ring_lds[kX2Slots * kXSliceF4];
-    __shared__ float cst[6 * kW];                          // ngp layer-0 bias, 1/su0, sigma_w, rgb_w[3]
-    __shared__ float film_lds[NF * 2 * kW];                // the workgroup's face
-    __shared__ f4 facc_lds[kWaves2][16 * 32];              // 64 KB: [tile][g][ray8] feature sums
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t n = lane & 15u, g = lane >> 4, r8 = n & 7u;
-    const bool colB = n >= 8u;                             // sample 2p+1 of the pair
-    const GeomArgs &G = a.g;
-
-    const uint32_t wg_per_face = (G.tiles_per_face + kWaves - 1) / kWaves;
-    const uint32_t seg = blockIdx.x % a.nseg, blk = blockIdx.x / a.nseg;
-    const uint32_t b = blk / wg_per_face;
-    uint32_t tile_local = (blk % wg_per_face) * kWaves + (wave & 3u);
-    const bool tile_ok = tile_local < G.tiles_per_face;
-    if (!tile_ok) tile_local = G.tiles_per_face - 1;
-    const uint32_t tile = b * G.tiles_per_face + tile_local;
-    const uint32_t ray_in_tile = 8u * (wave >> 2) + r8;
-    uint32_t ray_local = tile_local * kTileRays + ray_in_tile;
-    const bool ray_ok = tile_ok && ray_local < G.H * G.W;
-    if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
-    const uint32_t py = ray_local / G.W, px = ray_local % G.W;
-    const uint32_t ray_index = (b * G.H + py) * G.W + px;
-
-    Ray ray;
-    make_ray(G.cam + (size_t)b * 12, G.focal[b], G.pix_x[px], G.pix_y[py], G.half_res, ray);
-    const float nr = G.near_[b], fr = G.far_[b];
-    const float span = __fsub_rn(fr, nr);
-    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
-    f4 vxh, vxl;
-    {
-        const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
-        const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
-        const float v2 = G.static_viewdirs ? ray.dir[2] : ray.d[2];
-        const float vn = norm3_torch(v0, v1, v2);
-        const float ux = __fdiv_rn(v0, vn), uy = __fdiv_rn(v1, vn), uz = __fdiv_rn(v2, vn);
-        float v[8];
-        if constexpr (Net::kSiren) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = 0.0f;
-            if (g == 0) {
-                v[0] = ux;
-                v[1] = uy;
-                v[2] = uz;
-            }
-        } else {
-            const f4 qa = sh_quad(ux, uy, uz, (2 * g) & 3), qb = sh_quad(ux, uy, uz, (2 * g + 1) & 3);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[r] = g < 2 ? qa[r] : 0.0f;
-                v[4 + r] = g < 2 ? qb[r] : 0.0f;
-            }
-        }
-        split8(v, vxh, vxl);
-    }
-    const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
-    {
-        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * NF * 2 * kW);
-        f4 *dst = reinterpret_cast<f4 *>(film_lds);
-        for (uint32_t i = tid; i < NF * 2 * kW / 4; i += kThreads2) dst[i] = src[i];
-    }
-    XRing2 R;
-    R.lds = ring_lds;
-    R.tid = tid;
-    R.wave = __builtin_amdgcn_readfirstlane(wave);
-    R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
-    R.it = 0;
-    for (uint32_t i = tid; i < 6 * kW; i += kThreads2) {
-        float v;
-        if (i < kW) v = Net::kSiren ? 0.0f : a.bias_s[i];     // raw input_linear bias
-        else if (i < 2 * kW) v = __fdiv_rn(1.0f, a.su[i - kW]);
-        else if (i < 3 * kW) v = a.sigma_w[i - 2 * kW];
-        else v = a.rgb_w[i - 3 * kW];
-        cst[i] = v;
-    }
-    // prologue: half-slices 0, 1 (k-step 0) -> slots 0, 1 (the first step issues the next)
-    R.slot0 = 0;
-    for (uint32_t k = 0; k < 2u; ++k) x2_dma(R, k % Net::kSlices, k);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    f4 *facc = facc_lds[wave];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) facc[t * 64 + lane] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        R.nh[i] = R.lds[(2 * i) * 64 + lane];
-        R.nl[i] = R.lds[(2 * i + 1) * 64 + lane];
-    }
-
-    float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
-    float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
-    const float *bias0 = cst;
-    const float *inv_su0 = cst + kW;
-    const float *sig_w = cst + 2 * kW, *rgb_w = cst + 3 * kW;
-    auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
-    auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
-    const float sig_b = a.sigma_b[0];
-    const float rgb_b0 = a.rgb_b[0], rgb_b1 = a.rgb_b[1], rgb_b2 = a.rgb_b[2];
-
-    const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
-    const size_t tile_sid = (size_t)(tile * G.N) * kTileRays + ray_in_tile;
-    float2 en[4];
-    auto load_inputs = [&](uint32_t s0) {
-        uint32_t s = s0 + (colB ? 1u : 0u);
-        if (s >= G.N) s = G.N - 1;
-        if constexpr (Net::kSiren) {
-            const float z = sample_z(G.sc, nr, fr, ray_index, s);
-            float np_[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));
-                np_[k] = G.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;
-            }
-            const bool g0 = g == 0;
-            en[0] = make_float2(g0 ? np_[0] : 0.0f, g0 ? np_[1] : 0.0f);
-            en[1] = make_float2(g0 ? np_[2] : 0.0f, 0.0f);
-            en[2] = make_float2(0.0f, 0.0f);
-            en[3] = make_float2(0.0f, 0.0f);
-        } else {
-            const size_t sid = tile_sid + (size_t)s * kTileRays;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) en[c] = enc2[(4 * g + c) * (size_t)G.S_total + sid];
-        }
-    };
-    const uint32_t npass = (G.N + 1) / 2;
-    const uint32_t pps = (npass + a.nseg - 1) / a.nseg;
-    const uint32_t p_begin = seg * pps, p_end = min(npass, p_begin + pps);
-    load_inputs(2 * p_begin);
-
-    for (uint32_t p = p_begin; p < p_end; ++p) {
-        // a pass consumes exactly Net::kSlices half-slices (68 ngp, 132 siren):
-        // restarting the step counter makes every slice index a compile-time constant;
-        // the register rings' slot counts divide kSlices, the DMA ring carries its slot
-        // base across passes (x2_slot)
-        static_assert(Net::kSlices % 3 == (Net::kSiren ? 0 : 2) && Net::kSlices % 4 == 0,
-                      "ring slot cycle");
-        if (p != p_begin) R.slot0 = (R.slot0 + Net::kSlices) % (uint32_t)kX2Slots;
-        R.it = 0;
-        f4 X[16], Y[16];
-        f4 eh, el;
-        int es = 0;
-        {
-            float v[8];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                v[2 * c] = en[c].x;
-                v[2 * c + 1] = en[c].y;
-            }
-            if constexpr (!Net::kSiren) es = feat_scale(v);
-            split8(v, eh, el);
-        }
-        float sdfp = 0.0f;
-        auto act_film = [&](int f) {
-            return [&, f](f4 &za, f4 &zb, int q) {
-                float dummy = 0.0f;
-                act_pair<1, V>(za, zb, q, fg(f), fb(f), nullptr, dummy, g);
-            };
-        };
-        auto act_sdf = [&](int f) {
-            return [&, f](f4 &za, f4 &zb, int q) {
-                act_pair<2, V>(za, zb, q, fg(f), fb(f), sig_w, sdfp, g);
-            };
-        };
-        auto act_l0 = [&](f4 &za, f4 &zb, int q) {
-            if constexpr (Net::kSiren) {
-                act_film(0)(za, zb, q);
-            } else {
-                float dummy = 0.0f;
-                act_pair<0, V>(za, zb, q, inv_su0, bias0, nullptr, dummy, g, es);
-            }
-        };
-
-        // every layer accumulates from zero: ngp layer 0 adds its bias in act_pair<0>,
-        // the FiLM layers' biases are folded into beta'' (xprep_kernel)
-        zero_acc(X);
-        xstep2<V, Net, 0>(R, X, eh, el, [] {});
-        xstep2<V, Net, 1>(R, X, eh, el, [&] { act_l0(X[0], X[1], 0); });
-        if constexpr (Net::kSiren) {
-            zero_acc(Y);
-            dense_layer2<V, Net>(R, X, Y, act_l0, act_film(1));
-            for (int l = 2; l < 6; l += 2) {
-                zero_acc(X);
-                dense_layer2<V, Net>(R, Y, X, act_film(l - 1), act_film(l));
-                zero_acc(Y);
-                dense_layer2<V, Net>(R, X, Y, act_film(l), act_film(l + 1));
-            }
-            zero_acc(X);
-            dense_layer2<V, Net>(R, Y, X, act_film(5), act_film(6));
-            zero_acc(Y);
-            dense_layer2<V, Net>(R, X, Y, act_film(6), act_sdf(7));
-        } else {
-            zero_acc(Y);
-            dense_layer2<V, Net>(R, X, Y, act_l0, act_film(0));
-            zero_acc(X);
-            dense_layer2<V, Net>(R, Y, X, act_film(0), act_film(1));
-            zero_acc(Y);
-            dense_layer2<V, Net>(R, X, Y, act_film(1), act_sdf(2));
-        }
-        // compositing weights of the pass's two samples (this lane's s = 2p + colB),
-        // front to back: formed in the views layer's last k-step, in the MFMA shadow
-        // (the sigma head sdfp is complete once the layer's last input pair is
-        // activated)
-        const uint32_t s = 2 * p + (colB ? 1u : 0u);
-        const bool s_ok = s < G.N;
-        const uint32_t sc_ = s_ok ? s : G.N - 1;
-        float sdf = 0.0f, z = 0.0f, wA = 0.0f, wB = 0.0f;
-        auto weights = [&] {
-            sdf = __fadd_rn(group_sum(sdfp), sig_b);
-            z = sample_z(G.sc, nr, fr, ray_index, sc_);
-            const float dist = (sc_ + 1 < G.N)
-                                   ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), z),
-                                               dnorm)
-                                   : __fmul_rn(1e10f, dnorm);
-            float alpha;
-            if (a.with_sdf) {
-                const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf, beta_s)), beta_s);
-                alpha = 1.0f - expf(-sig * dist);
-            } else {
-                float raw = sdf;
-                if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
-                const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
-                alpha = 1.0f - expf(-sp * dist);
-            }
-            if (!s_ok) alpha = 0.0f;
-            // the pair's weights, identically in both lanes (sample 2p, then 2p+1)
-            const float alpha_o = ror8(alpha);
-            const float aA = colB ? alpha_o : alpha, aB = colB ? alpha : alpha_o;
-            const bool lastA = 2 * p + 1 == G.N, lastB = 2 * p + 2 == G.N;
-            wA = aA * T;
-            if (a.force_background && lastA) wA = 1.0f - wsum;
-            T = T * ((1.0f - aA) + 1e-10f);
-            wsum += wA;
-            wB = aB * T;
-            if (a.force_background && lastB) wB = 1.0f - wsum;
-            if (2 * p + 1 < G.N) {
-                T = T * ((1.0f - aB) + 1e-10f);
-                wsum += wB;
-            } else {
-                wB = 0.0f;
-            }
-        };
-        constexpr bool kComp = (V & 16) == 0;
-        zero_acc(X);
-        dense_layer2<V, Net>(R, Y, X, act_sdf(NF - 2), NoAct2{});
-        xstep2<V, Net, 0>(R, X, vxh, vxl, [&] {
-            if constexpr (kComp) weights();
-        });
-        xstep2<V, Net, 1>(R, X, vxh, vxl, [&] {
-            if (p + 1 < p_end) load_inputs(2 * p + 2);
-        });
-
-        if constexpr (!kComp) {
-#pragma unroll
-            for (int t = 0; t < 16; ++t) racc0 += (X[t][0] + X[t][1]) + (X[t][2] + X[t][3]);
-            racc0 += sdfp;
-            continue;
-        }
-        // colour features f = sin(gamma_v x + beta_v); rgb_linear
-        const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
-        float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const int f0 = 16 * t + 4 * (int)g;
-            const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
-            const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
-            const f4 w0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
-            const f4 w1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
-            const f4 w2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
-            f4 fv;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                fv[r] = sin_rev(__fmaf_rn(gm[r], X[t][r], bt[r]));
-                p0 = __fmaf_rn(fv[r], w0[r], p0);
-                p1 = __fmaf_rn(fv[r], w1[r], p1);
-                p2 = __fmaf_rn(fv[r], w2[r], p2);
-            }
-            X[t] = fv;
-        }
-        const float q0 = sigmoidf_(__fadd_rn(group_sum(p0), rgb_b0));
-        const float q1 = sigmoidf_(__fadd_rn(group_sum(p1), rgb_b1));
-        const float q2 = sigmoidf_(__fadd_rn(group_sum(p2), rgb_b2));
-        const float o0 = ror8(q0), o1 = ror8(q1), o2 = ror8(q2);
-        racc0 = __fmaf_rn(wB, colB ? q0 : o0, __fmaf_rn(wA, colB ? o0 : q0, racc0));
-        racc1 = __fmaf_rn(wB, colB ? q1 : o1, __fmaf_rn(wA, colB ? o1 : q1, racc1));
-        racc2 = __fmaf_rn(wB, colB ? q2 : o2, __fmaf_rn(wA, colB ? o2 : q2, racc2));
-        w_last = (2 * p + 1 < G.N) ? wB : wA;
-        if (a.xyz) {
-            const float zo = ror8(z);
-            const float zA = colB ? zo : z, zB = colB ? z : zo;
-            xacc0 = __fmaf_rn(wB, __fadd_rn(ray.o[0], __fmul_rn(ray.d[0], zB)),
-                              __fmaf_rn(wA, __fadd_rn(ray.o[0], __fmul_rn(ray.d[0], zA)), xacc0));
-            xacc1 = __fmaf_rn(wB, __fadd_rn(ray.o[1], __fmul_rn(ray.d[1], zB)),
-                              __fmaf_rn(wA, __fadd_rn(ray.o[1], __fmul_rn(ray.d[1], zA)), xacc1));
-            xacc2 = __fmaf_rn(wB, __fadd_rn(ray.o[2], __fmul_rn(ray.d[2], zB)),
-                              __fmaf_rn(wA, __fadd_rn(ray.o[2], __fmul_rn(ray.d[2], zA)), xacc2));
-        }
-        if (a.features) {
-            // facc += wA fA + wB fB (in that order) by the sample-2p lane of the ray
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                f4 ob;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) ob[r] = ror8(X[t][r]);
-                if (!colB) {
-                    f4 v = facc[(t * 4 + g) * 8 + r8];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = __fmaf_rn(wB, ob[r], __fmaf_rn(wA, X[t][r], v[r]));
-                    facc[(t * 4 + g) * 8 + r8] = v;
-                }
-            }
-        }
-        if (a.sdf && ray_ok && g == 0 && s_ok) a.sdf[(size_t)ray_index * G.N + s] = sdf;
-    }
-    // the ring runs ahead across passes: no LDS-DMA may land after the workgroup ends
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!ray_ok || colB) return;
-    if (a.nseg > 1) {
-        const size_t Rr = (size_t)G.total_tiles * kTileRays;
-        float *pp = a.part + (size_t)seg * kPartQ * Rr + (size_t)tile * kTileRays + ray_in_tile;
-        if (a.features) {
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const uint32_t jf = 16 * t + 4 * g;
-                const f4 v = facc[(t * 4 + g) * 8 + r8];
-                pp[(size_t)(jf + 0) * Rr] = v.x;
-                pp[(size_t)(jf + 1) * Rr] = v.y;
-                pp[(size_t)(jf + 2) * Rr] = v.z;
-                pp[(size_t)(jf + 3) * Rr] = v.w;
-            }
-        }
-        if (g == 0) {
-            const float q[8] = {racc0, racc1, racc2, xacc0, xacc1, xacc2, T, w_last};
-#pragma unroll
-            for (int k = 0; k < 8; ++k) pp[(size_t)(kW + k) * Rr] = q[k];
-        }
-        return;
-    }
-    const size_t HW = (size_t)G.H * G.W;
-    const size_t pix = (size_t)py * G.W + px;
-    if (g < 3) {
-        const float rc = g == 0 ? racc0 : (g == 1 ? racc1 : racc2);
-        a.rgb[((size_t)b * 3 + g) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, rc));
-        if (a.xyz) {
-            const float xc = g == 0 ? xacc0 : (g == 1 ? xacc1 : xacc2);
-            a.xyz[((size_t)b * 3 + g) * HW + pix] = xc;
-        }
-    } else if (a.mask) {
-        a.mask[(size_t)b * HW + pix] = w_last;
-    }
-    if (a.features) {
-        float *fbp = a.features + (size_t)b * kW * HW + pix;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const uint32_t jf = 16 * t + 4 * g;
-            const f4 v = facc[(t * 4 + g) * 8 + r8];
-            fbp[(size_t)(jf + 0) * HW] = v.x;
-            fbp[(size_t)(jf + 1) * HW] = v.y;
-            fbp[(size_t)(jf + 2) * HW] = v.z;
-            fbp[(size_t)(jf + 3) * HW] = v.w;
-        }
-    }
-}
-
 // ----------------------------------------------------------------------------
 // field_p_kernel: wave pairs split the output rows.
 //
-// In field_x2_kernel every wave multiplies the WHOLE weight matrix into its own
-// 16-sample column, so each A fragment read from LDS feeds 3 MFMAs and the eight
-// waves of a CU read 8x the weight stream from LDS per pass (ablating those reads
-// alone took 30 % off the kernel).  Here the two waves of a SIMD (w, w + 4) form a
-// pair over 32 samples = 8 rays x 4 consecutive samples (two MFMA blocks of N = 16:
-// block c, lane n holds sample 4p + 2c + (n >= 8) of ray n & 7); wave h of the pair
-// owns output rows 128h .. 128h + 127 (half-slice h of every k-step), so each A
-// fragment feeds 6 MFMAs and LDS A reads halve.  A layer's input k-step q (rows
-// 32q .. 32q + 31 of the previous layer's output) is computed by wave q >> 2 of the
-// pair: that wave activates it one k-step ahead (FiLM in the MFMA shadow, as
-// field_x2_kernel), splits it and writes the (hi, lo) B fragments of both blocks to
-// a double-buffered 4 KB exchange slot; after the k-step barrier both waves read it
-// back.  Per k-step and wave: 48 MFMAs, 16 A + 4 B ds_read_b128 (field_x2_kernel:
-// 32 A reads per 48 MFMAs), 4 pieces of the LDS-DMA weight ring.  The pair chains
-// the sigma head across its halves (wave 0's per-lane partial after chunk 3 seeds
-// wave 1's), so sdf values are those of field_x2_kernel bit for bit; the colour
-// head's two half-sums are added (fp32-rounding-level difference).  Four samples of
-// a ray per pass halve the per-ray feature accumulators (4 KB per wave in LDS).
-// ----------------------------------------------------------------------------
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-
+// The previous field kernel (field_x2_kernel, git history) gave every wave the WHOLE
+// weight matrix against its own 16-sample column, so each A fragment read from LDS fed
+// 3 MFMAs and the eight waves of a CU read 8x the weight stream from LDS per pass.
+// Here the two waves of a SIMD (w, w + 4) form a pair over 32 samples = 8 rays x 4
+// consecutive samples (two MFMA blocks of N = 16: block c, lane n holds sample
+// 4p + 2c + (n >= 8) of ray n & 7); wave h of the pair owns the 16-row output tiles
+// 2t + h (t = 0..7), so each A fragment feeds 6 MFMAs and LDS A reads halve.  A
+// layer's input k-step q (rows 32q .. 32q + 31 = tiles 2q, 2q+1 of the previous
+// layer's output) is half in each wave: both activate their tile one k-step ahead
+// (FiLM in the MFMA shadow) and write its (hi, lo) dword pairs to their 8-byte half of
+// a double-buffered 4 KB exchange slot; after the k-step barrier both read the whole
+// fragment back.  Per k-step and wave: 48 MFMAs, 16 A + 4 B ds_read_b128
+// (field_x2_kernel: 32 A reads per 48 MFMAs), 4 pieces of the LDS-DMA weight ring.
+// Balanced work matters: with one wave activating a whole k-step the other idled at
+// the barrier (measured).  The sigma head and the colour head are per-wave half-sums
+// over own rows, added in wave order (fp32-rounding-level differences to the previous
+// kernel, <= 5e-7); alpha is computed once per sample block by one wave of the pair.
+// Four samples of a ray per pass halve the per-ray feature accumulators (4 KB per wave
+// in LDS).  Measured alternatives (in git history): issuing the two waves' LDS-DMA at
+// different points (+-0), placing their activations after different groups (+5 %),
+// the next k-step's B fragments read ahead of the last group (+-0), a packed-fp32
+// colour head (raced: see below).
 constexpr int kPWaves = 8;
 constexpr int kPThreads = kPWaves * 64;
 constexpr uint32_t kPTiles = 2;          // 16-ray tiles per workgroup (4 pairs x 8 rays)
 constexpr uint32_t kPSamples = 4;        // samples of a ray per pass
-#ifndef PEARLY
-#define PEARLY 0
-#endif
-#ifndef PPIN
-#define PPIN 0
-#endif
-#ifndef PABL
-#define PABL 0
-#endif
-#ifndef PSTAG
-#define PSTAG 1
-#endif
+
+
 
 template <class Net>
 struct PNet {
@@ -915,32 +327,23 @@ struct PRing {
     f4 na[4];         // the next k-step's group-0 A fragments (t0 hi, t0 lo, t1 hi, t1 lo)
 };
 
-__device__ __forceinline__ void p_dma(const PRing &R, uint32_t slice, uint32_t slot) {
-    const uint32_t sbase = R.wave * (kX2DmaPieces * 1024u);
-    const uint32_t lbase = lds_addr(R.lds) + sbase;
-#pragma unroll
-    for (int k = 0; k < kX2DmaPieces; ++k)
-        dma16x(R.drsrc, (R.tid & 63u) * 16u, sbase, slice * kXSliceF4 * 16u + k * 1024u, lbase,
-               slot * kXSliceF4 * 16u + k * 1024u);
-}
-
-// p_dma for the waves whose h == HSEL only.  The wave-uniform skip is a scalar branch
-// INSIDE the asm, so the compiler's view of the unrolled MFMA stream stays one basic
-// block (a C++ branch on h split it and spilled); offsets are immediates.
-template <uint32_t HSEL, uint32_t SLICE, uint32_t SLOT>
-__device__ __forceinline__ void p_dma_if(const PRing &R) {
-    const uint32_t sbase = R.wave * (kX2DmaPieces * 1024u);
+// One LDS-DMA half-slice (this wave's pieces) with compile-time offsets as immediates
+// (with the offsets as SGPR operands the unrolled pass spilled).  Straight-line asm
+// only: a branch inside the asm would skip instructions the compiler counts as wait
+// states of MFMA -> VALU hazards (measured: nondeterministic colour features).
+template <uint32_t SLICE, uint32_t SLOT>
+__device__ __forceinline__ void p_dma_i(const PRing &R) {
+    const uint32_t sbase = R.wave * (kDmaPieces * 1024u);
     const uint32_t lbase = lds_addr(R.lds) + sbase;
     const uint32_t voff = (R.tid & 63u) * 16u;
 #pragma unroll
-    for (int k = 0; k < kX2DmaPieces; ++k) {
+    for (int k = 0; k < kDmaPieces; ++k) {
         uint32_t keep, so;
         asm volatile(
-            "s_cmp_lg_u32 %6, %7\n\ts_cbranch_scc1 1f\n\t"
-            "s_mov_b32 %0, m0\n\ts_add_u32 m0, %4, %8\n\ts_add_u32 %1, %5, %9\n\ts_nop 0\n\t"
-            "buffer_load_dwordx4 %2, %3, %1 offen lds\n\ts_mov_b32 m0, %0\n1:"
+            "s_mov_b32 %0, m0\n\ts_add_u32 m0, %4, %6\n\ts_add_u32 %1, %5, %7\n\ts_nop 0\n\t"
+            "buffer_load_dwordx4 %2, %3, %1 offen lds\n\ts_mov_b32 m0, %0"
             : "=&s"(keep), "=&s"(so)
-            : "v"(voff), "s"(R.drsrc), "s"(lbase), "s"(sbase), "s"(R.h), "i"(HSEL),
+            : "v"(voff), "s"(R.drsrc), "s"(lbase), "s"(sbase),
               "i"(SLOT * kXSliceF4 * 16u + k * 1024u), "i"(SLICE * kXSliceF4 * 16u + k * 1024u)
             : "memory", "scc");
     }
@@ -966,21 +369,12 @@ template <class Net, int KS, bool ZC, class NextB, class Side>
 __device__ __forceinline__ void pstep(PRing &R, f4 (&acc)[16], const f4 (&bf)[4], f4 (&bn)[4],
                                       NextB &&next_b, Side &&side) {
     constexpr f4 kZ = {0.0f, 0.0f, 0.0f, 0.0f};
-    constexpr int KN = (KS + 1) % PNet<Net>::kSteps, KN2 = (KS + 2) % PNet<Net>::kSteps;
+    constexpr int KN = (KS + 1) % PNet<Net>::kSteps;
     const uint32_t lane = R.tid & 63u;
-    // The two waves of a SIMD issue their LDS-DMA pieces at different points (each
-    // piece holds the wave's issue for ~100 cycles): wave 1 here, for the next
-    // k-step; wave 0 behind this k-step's barrier, for the one after (both land
-    // in the slots the barrier before them closed).
-    if constexpr (PSTAG == 0) {
-        p_dma_if<0, 2 * KN, 2 * (KN & 1)>(R);
-        p_dma_if<0, 2 * KN + 1, 2 * (KN & 1) + 1>(R);
-        p_dma_if<1, 2 * KN, 2 * (KN & 1)>(R);
-        p_dma_if<1, 2 * KN + 1, 2 * (KN & 1) + 1>(R);
-    } else {
-        p_dma_if<1, 2 * KN, 2 * (KN & 1)>(R);
-        p_dma_if<1, 2 * KN + 1, 2 * (KN & 1) + 1>(R);
-    }
+    // the next k-step's half-slices go into the slots of the previous k-step (closed by
+    // its barrier)
+    p_dma_i<2 * KN, 2 * (KN & 1)>(R);
+    p_dma_i<2 * KN + 1, 2 * (KN & 1) + 1>(R);
     // local tile t = global tile 2t + h: half-slice t >> 2, position 2 (t & 3) + h
     const f4 *A = R.lds + 2 * (KS & 1) * kXSliceF4 + R.h * 128 + lane;
     const f4 *An = R.lds + 2 * (KN & 1) * kXSliceF4 + R.h * 128 + lane;
@@ -1002,15 +396,10 @@ __device__ __forceinline__ void pstep(PRing &R, f4 (&acc)[16], const f4 (&bf)[4]
         } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i) R.na[i] = An[aoff(i >> 1, i & 1)];
-            if constexpr (PEARLY) next_b(bn);
-            if constexpr (PSTAG != 0) {
-                p_dma_if<0, 2 * KN2, 2 * (KN2 & 1)>(R);
-                p_dma_if<0, 2 * KN2 + 1, 2 * (KN2 & 1) + 1>(R);
-            }
         }
         const int t0 = 2 * grp, t1 = t0 + 1;
         const f4 *ag = a[grp];
-        // per accumulator: W_lo x_hi, W_hi x_lo, W_hi x_hi (field_x2_kernel's order)
+        // per accumulator: W_lo x_hi, W_hi x_lo, W_hi x_hi
         // ZC: the layer's first k-step starts its accumulators from zero
         acc[2 * t0] = mfma16(ag[1], bf[0], ZC ? kZ : acc[2 * t0]);
         acc[2 * t0 + 1] = mfma16(ag[1], bf[2], ZC ? kZ : acc[2 * t0 + 1]);
@@ -1024,15 +413,13 @@ __device__ __forceinline__ void pstep(PRing &R, f4 (&acc)[16], const f4 (&bf)[4]
         acc[2 * t0 + 1] = mfma16(ag[0], bf[2], acc[2 * t0 + 1]);
         acc[2 * t1] = mfma16(ag[2], bf[0], acc[2 * t1]);
         acc[2 * t1 + 1] = mfma16(ag[2], bf[2], acc[2 * t1 + 1]);
-        // this group's and the previous group's A fragments stay allocated until the
-        // MFMAs have issued (no WAR hazard padding on their re-use)
+        // this group's A fragments stay allocated until its MFMAs have issued (pinning
+        // the previous group's too measured 1.5 % slower)
         asm volatile("" ::"v"(ag[0]), "v"(ag[1]), "v"(ag[2]), "v"(ag[3]));
-        if (PPIN && grp > 0)
-            asm volatile("" ::"v"(a[grp - 1][0]), "v"(a[grp - 1][1]), "v"(a[grp - 1][2]), "v"(a[grp - 1][3]));
         __builtin_amdgcn_sched_barrier(0);
         if (grp == 1) side();
     }
-    if constexpr (!PEARLY) next_b(bn);
+    next_b(bn);
     __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -1090,13 +477,14 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
     constexpr int NF = Net::kFilmN;
     constexpr int KV = PNet<Net>::kViews;
     constexpr int NL = Net::kLayers;
-    __shared__ f4 ring_lds[kX2Slots * kXSliceF4];           // 64 KB weight ring
+    __shared__ f4 ring_lds[kRingSlots * kXSliceF4];           // 64 KB weight ring
     __shared__ f4 xch_lds[4][2 * 2 * 2 * 64];               // 32 KB: [pair][slot][block][hi,lo][lane]
     __shared__ f4 facc_lds[kPWaves][8 * 4 * 8];             // 32 KB: [wave][tile][g][ray] feature sums
     __shared__ float film_lds[NF * 2 * kW];                 // the workgroup's face
     __shared__ float cst[6 * kW];                           // ngp layer-0 bias, 1/su0, sigma_w, rgb_w[3]
     __shared__ float sdfx_lds[4][2][2][64];                 // [pair][wave][block][lane] sigma half-sums
     __shared__ float pcol_lds[4][6][16];                    // wave 0's colour half-sums per column
+    __shared__ float alx_lds[4][2][64];                     // [pair][block][lane] alpha
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t h = __builtin_amdgcn_readfirstlane(wave >> 2), pair = wave & 3u;
     const uint32_t n = lane & 15u, g = lane >> 4, r8 = n & 7u;
@@ -1128,14 +516,9 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
         else v = a.rgb_w[i - 3 * kW];
         cst[i] = v;
     }
-    // prologue: k-step 0's half-slices -> slots 0, 1; wave 0 of each SIMD also k-step 1's
-    // (pstep: wave 1 issues the next k-step, wave 0 the one after)
-    p_dma(R, 0, 0);
-    p_dma(R, 1, 1);
-    if (PSTAG != 0 && h == 0) {
-        p_dma(R, 2, 2);
-        p_dma(R, 3, 3);
-    }
+    // prologue: k-step 0's half-slices -> slots 0, 1 (each k-step issues the next)
+    p_dma_i<0, 0>(R);
+    p_dma_i<1, 1>(R);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     f4 *facc = facc_lds[wave];
     __syncthreads();
@@ -1292,7 +675,7 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
         f4 (&vout)[16] = kInX ? Y : X;
         const uint32_t s0 = kPSamples * p;
         float z[2] = {0.0f, 0.0f}, wj[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        float sdf[2] = {0.0f, 0.0f}, dist[2] = {0.0f, 0.0f};
+        float sdf_h = 0.0f, dist[2] = {0.0f, 0.0f};
         sfor<0, 9>([&](auto J) {
             constexpr int j = decltype(J)::value;
             constexpr int KS = KV + j;
@@ -1330,41 +713,44 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
                         sdfx_lds[pair][h][0][lane] = group_sum(sdfp[0]);
                         sdfx_lds[pair][h][1][lane] = group_sum(sdfp[1]);
                     }
-                } else if constexpr (j == 7 && (PABL & 2)) {
-                    wj[0] = sdfx_lds[pair][0][0][lane];
-                    wj[1] = sdfx_lds[pair][1][0][lane];
                 } else if constexpr (j == 7) {
+                    // alpha of this wave's sample block h (the pair's waves split the
+                    // blocks; exchanged through LDS across this k-step's barrier)
+                    sdf_h = __fadd_rn(__fadd_rn(sdfx_lds[pair][0][h][lane], sdfx_lds[pair][1][h][lane]),
+                                      sig_b);
+                    const uint32_t s = s0 + 2 * h + (colB ? 1u : 0u);
+                    const bool s_ok = s < G.N;
+                    const uint32_t sc_ = s_ok ? s : G.N - 1;
+                    if constexpr (Net::kSiren) {
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            const uint32_t sc = min(s0 + 2 * c + (colB ? 1u : 0u), G.N - 1);
+                            z[c] = sample_z(G.sc, nr, fr, ray_index, sc);
+                        }
+                        const float zh = h ? z[1] : z[0];
+                        dist[0] = dist[1] = (sc_ + 1 < G.N)
+                                      ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), zh), dnorm)
+                                      : __fmul_rn(1e10f, dnorm);
+                    }
+                    const float dh = h ? dist[1] : dist[0];
+                    float alpha;
+                    if (a.with_sdf) {
+                        const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf_h, beta_s)), beta_s);
+                        alpha = 1.0f - expf(-sig * dh);
+                    } else {
+                        float raw = sdf_h;
+                        if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
+                        const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+                        alpha = 1.0f - expf(-sp * dh);
+                    }
+                    alx_lds[pair][h][lane] = s_ok ? alpha : 0.0f;
+                } else {
                     // compositing weights of the pass's 4 samples, identically in both
                     // lanes of a ray and both waves of the pair, front to back
-                    float al[2];
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        sdf[c] = __fadd_rn(__fadd_rn(sdfx_lds[pair][0][c][lane], sdfx_lds[pair][1][c][lane]),
-                                           sig_b);
-                        const uint32_t s = s0 + 2 * c + (colB ? 1u : 0u);
-                        const bool s_ok = s < G.N;
-                        const uint32_t sc_ = s_ok ? s : G.N - 1;
-                        if constexpr (Net::kSiren) {
-                            z[c] = sample_z(G.sc, nr, fr, ray_index, sc_);
-                            dist[c] = (sc_ + 1 < G.N)
-                                          ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), z[c]), dnorm)
-                                          : __fmul_rn(1e10f, dnorm);
-                        }
-                        float alpha;
-                        if (a.with_sdf) {
-                            const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf[c], beta_s)), beta_s);
-                            alpha = 1.0f - expf(-sig * dist[c]);
-                        } else {
-                            float raw = sdf[c];
-                            if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
-                            const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
-                            alpha = 1.0f - expf(-sp * dist[c]);
-                        }
-                        al[c] = s_ok ? alpha : 0.0f;
-                    }
-                    const float o0 = ror8(al[0]), o1 = ror8(al[1]);
-                    const float aj[4] = {colB ? o0 : al[0], colB ? al[0] : o0, colB ? o1 : al[1],
-                                         colB ? al[1] : o1};
+                    const float al0 = alx_lds[pair][0][lane], al1 = alx_lds[pair][1][lane];
+                    const float o0 = ror8(al0), o1 = ror8(al1);
+                    const float aj[4] = {colB ? o0 : al0, colB ? al0 : o0, colB ? o1 : al1,
+                                         colB ? al1 : o1};
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
                         const uint32_t s = s0 + k;
@@ -1380,43 +766,39 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
             });
         });
         // colour features f = sin(gamma_v x + beta_v) of the own rows, rgb half-sums.
-        // Packed fp32 over the two sample blocks (each half of a v_pk_fma_f32 is the
-        // scalar fma of its block, in the same order): this tail runs outside the MFMA
-        // stream, on both waves of the SIMD at once.
+        // (Scalar fp32: a v_pk_fma_f32 form of this tail read some v_sin_f32 results
+        // before they were written -- nondeterministic colour features -- so there is no
+        // packed math in this kernel; tests/test_gpu_render.py::test_fused_render_deterministic.)
         const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
-        f2 P[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};   // rgb half-sums (block 0, 1)
-        if constexpr (PABL & 1) {
+        float P[3][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};   // [rgb][block] half-sums
+        {
 #pragma unroll
-            for (int t = 0; t < 16; ++t) P[t % 3][t & 1] += vout[t][0] + vout[t][3] * wj[0];
-        } else
+            for (int t = 0; t < 8; ++t) {
+                const int f0 = 16 * (2 * t + (int)h) + 4 * (int)g;
+                const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
+                const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
+                const f4 w0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
+                const f4 w1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
+                const f4 w2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int f0 = 16 * (2 * t + (int)h) + 4 * (int)g;
-            const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
-            const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
-            const f4 w0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
-            const f4 w1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
-            const f4 w2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
-            f4 fa, fb_;
+                for (int c = 0; c < 2; ++c) {
+                    f4 fv;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const f2 arg = pk_fma(f2{vout[2 * t][r], vout[2 * t + 1][r]}, f2{gm[r], gm[r]},
-                                      f2{bt[r], bt[r]});
-                const f2 fv = {sin_rev(arg.x), sin_rev(arg.y)};
-                P[0] = pk_fma(fv, f2{w0[r], w0[r]}, P[0]);
-                P[1] = pk_fma(fv, f2{w1[r], w1[r]}, P[1]);
-                P[2] = pk_fma(fv, f2{w2[r], w2[r]}, P[2]);
-                fa[r] = fv.x;
-                fb_[r] = fv.y;
+                    for (int r = 0; r < 4; ++r) {
+                        fv[r] = sin_rev(__fmaf_rn(gm[r], vout[2 * t + c][r], bt[r]));
+                        P[0][c] = __fmaf_rn(fv[r], w0[r], P[0][c]);
+                        P[1][c] = __fmaf_rn(fv[r], w1[r], P[1][c]);
+                        P[2][c] = __fmaf_rn(fv[r], w2[r], P[2][c]);
+                    }
+                    vout[2 * t + c] = fv;
+                }
             }
-            vout[2 * t] = fa;
-            vout[2 * t + 1] = fb_;
         }
         float pc[2][3];
 #pragma unroll
         for (int o = 0; o < 3; ++o) {
-            pc[0][o] = group_sum(P[o].x);
-            pc[1][o] = group_sum(P[o].y);
+            pc[0][o] = group_sum(P[o][0]);
+            pc[1][o] = group_sum(P[o][1]);
         }
         if (h == 0 && g == 0) {
 #pragma unroll
@@ -1424,10 +806,9 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
 #pragma unroll
                 for (int o = 0; o < 3; ++o) pcol_lds[pair][3 * c + o][n] = pc[c][o];
         }
-        if (a.features && !(PABL & 1)) {
+        if (a.features) {
             // facc += w0 f0 + w1 f1 + w2 f2 + w3 f3 (in that order) by the lane of the
-            // ray's samples 0 and 2 (block 0 / 1, n < 8); row pairs packed
-            const f2 W0 = {wj[0], wj[0]}, W1 = {wj[1], wj[1]}, W2 = {wj[2], wj[2]}, W3 = {wj[3], wj[3]};
+            // ray's samples 0 and 2 (block 0 / 1, n < 8)
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 f4 o0, o1;
@@ -1439,25 +820,16 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
                 if (!colB) {
                     f4 v = facc[(t * 4 + g) * 8 + r8];
 #pragma unroll
-                    for (int r = 0; r < 4; r += 2) {
-                        f2 u = {v[r], v[r + 1]};
-                        u = pk_fma(f2{vout[2 * t][r], vout[2 * t][r + 1]}, W0, u);
-                        u = pk_fma(f2{o0[r], o0[r + 1]}, W1, u);
-                        u = pk_fma(f2{vout[2 * t + 1][r], vout[2 * t + 1][r + 1]}, W2, u);
-                        u = pk_fma(f2{o1[r], o1[r + 1]}, W3, u);
-                        v[r] = u.x;
-                        v[r + 1] = u.y;
-                    }
+                    for (int r = 0; r < 4; ++r)
+                        v[r] = __fmaf_rn(wj[3], o1[r], __fmaf_rn(wj[2], vout[2 * t + 1][r],
+                                         __fmaf_rn(wj[1], o0[r], __fmaf_rn(wj[0], vout[2 * t][r], v[r]))));
                     facc[(t * 4 + g) * 8 + r8] = v;
                 }
             }
         }
-        if (a.sdf && h == 0 && ray_ok && g == 0) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const uint32_t s = s0 + 2 * c + (colB ? 1u : 0u);
-                if (s < G.N) a.sdf[(size_t)ray_index * G.N + s] = sdf[c];
-            }
+        if (a.sdf && ray_ok && g == 0) {
+            const uint32_t s = s0 + 2 * h + (colB ? 1u : 0u);   // this wave's block
+            if (s < G.N) a.sdf[(size_t)ray_index * G.N + s] = sdf_h;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -1588,15 +960,15 @@ __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
 // ----------------------------------------------------------------------------
 // host
 // ----------------------------------------------------------------------------
-// Segments per ray: enough workgroups for every CU (>= 256), at most max_seg (the
-// call's max_field_segments, 0 = kFieldSplitMax), at least one pass (two samples) in
-// every segment, and never with force_background (its last weight needs the whole
-// ray's sum).
+// Sample segments per ray: enough workgroups for every CU (>= 256), at most max_seg
+// (the call's max_field_segments, 0 = kFieldSplitMax), at least one pass (4 samples)
+// in every segment, and never with force_background (its last weight needs the
+// whole ray's sum).
 uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background,
                     uint32_t max_seg) {
     if (max_seg == 0 || max_seg > kFieldSplitMax) max_seg = kFieldSplitMax;
-    const uint32_t wgs = B * ((tiles_per_face + kWaves - 1) / kWaves);
-    const uint32_t npass = (N + 1) / 2;
+    const uint32_t wgs = B * ((tiles_per_face + kPTiles - 1) / kPTiles);
+    const uint32_t npass = (N + kPSamples - 1) / kPSamples;
     uint32_t nseg = 1;
     while (!force_background && wgs * nseg < 256 && 2 * nseg <= max_seg) {
         const uint32_t c = 2 * nseg, pps = (npass + c - 1) / c;
@@ -1606,39 +978,8 @@ uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_b
     return nseg;
 }
 
-// field_p_kernel: 4 tiles (2 ray groups) per workgroup, 4 samples of a ray per pass.
-// Small batches first give each ray group its own workgroup (rsplit = 2), then split
-// the samples (nseg) while the grid stays under one workgroup per CU.
-static void field_p_split(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background,
-                          uint32_t max_seg, uint32_t *rsplit, uint32_t *nseg_out) {
-    if (max_seg == 0 || max_seg > kFieldSplitMax) max_seg = kFieldSplitMax;
-    const uint32_t wgs = B * ((tiles_per_face + kPTiles - 1) / kPTiles);
-    *rsplit = 1;
-    const uint32_t npass = (N + kPSamples - 1) / kPSamples;
-    uint32_t nseg = 1;
-    while (!force_background && wgs * nseg < 256 && 2 * nseg <= max_seg) {
-        const uint32_t c = 2 * nseg, pps = (npass + c - 1) / c;
-        if ((c - 1) * pps >= npass) break;            // no empty last segment
-        nseg = c;
-    }
-    *nseg_out = nseg;
-}
-
-uint32_t field_p_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background,
-                      uint32_t max_seg) {
-    uint32_t rs, ns;
-    field_p_split(B, tiles_per_face, N, force_background, max_seg, &rs, &ns);
-    return ns;
-}
-
-static bool field_pair() {
-    static const bool v = getenv("SDFR_FIELD_X2") == nullptr;
-    return v;
-}
-
 size_t field_part_bytes(uint32_t B, uint32_t tiles_per_face, uint32_t N) {
-    const uint32_t nseg = field_pair() ? field_p_nseg(B, tiles_per_face, N, 0, kFieldSplitMax)
-                                       : field_nseg(B, tiles_per_face, N, 0, kFieldSplitMax);
+    const uint32_t nseg = field_nseg(B, tiles_per_face, N, 0, kFieldSplitMax);
     return nseg > 1 ? (size_t)nseg * kPartQ * B * tiles_per_face * kTileRays * sizeof(float) : 0;
 }
 
@@ -1742,40 +1083,10 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     f.xyz = a->xyz;
     f.mask = a->mask;
     f.part = part;
-    f.rsplit = 1;
-    if (field_pair()) {
-        field_p_split(g.B, g.tiles_per_face, g.N, a->force_background, a->max_field_segments,
-                      &f.rsplit, &f.nseg);
-        if (!part) f.nseg = 1;
-        const uint32_t blocks =
-            g.B * ((g.tiles_per_face + kPTiles - 1) / kPTiles) * f.rsplit * f.nseg;
-        hipLaunchKernelGGL((field_p_kernel<Net>), dim3(blocks), dim3(kPThreads), 0, st, f);
-        int rc = check_launch("render: field (f16x3)");
-        if (rc || f.nseg == 1) return rc;
-        const uint32_t rays = g.total_tiles * kTileRays;
-        hipLaunchKernelGGL(field_merge_kernel, dim3((rays + 255) / 256, kPartQ), dim3(256), 0, st, f);
-        return check_launch("render: field segment merge");
-    }
     f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background,
-                              a->max_field_segments) : 1;
-    const uint32_t blocks = g.B * ((g.tiles_per_face + kWaves - 1) / kWaves) * f.nseg;
-    switch (field_variant()) {
-#ifdef SDFR_ABLATION
-#define SDFR_X2FIELD_CASE(V)                                                                   \
-    case V:                                                                                    \
-        hipLaunchKernelGGL((field_x2_kernel<V, Net>), dim3(blocks), dim3(kThreads2), 0, st, f); \
-        break;
-        SDFR_X2FIELD_CASE(1)
-        SDFR_X2FIELD_CASE(2)
-        SDFR_X2FIELD_CASE(4)
-        SDFR_X2FIELD_CASE(8)
-        SDFR_X2FIELD_CASE(16)
-        SDFR_X2FIELD_CASE(31)
-#undef SDFR_X2FIELD_CASE
-#endif
-        default:
-            hipLaunchKernelGGL((field_x2_kernel<0, Net>), dim3(blocks), dim3(kThreads2), 0, st, f);
-    }
+                               a->max_field_segments) : 1;
+    const uint32_t blocks = g.B * ((g.tiles_per_face + kPTiles - 1) / kPTiles) * f.nseg;
+    hipLaunchKernelGGL((field_p_kernel<Net>), dim3(blocks), dim3(kPThreads), 0, st, f);
     int rc = check_launch("render: field (f16x3)");
     if (rc || f.nseg == 1) return rc;
     const uint32_t rays = g.total_tiles * kTileRays;

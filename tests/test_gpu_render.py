@@ -299,6 +299,29 @@ def siren_sd(golden_dir):
     return W.det_state_dict(W.golden_entries(golden_dir, siren=True), "renderer.")
 
 
+@pytest.mark.parametrize("net", ["ngp", "siren"])
+@pytest.mark.parametrize("B", [1, 4])
+def test_fused_render_deterministic(sdfr, renderer_sd, siren_sd, net, B):
+    """Repeated renders of the same inputs are bit-identical: every cross-wave hand-off
+    of the field kernel (weight ring, exchange slots, sigma / alpha / colour half-sums)
+    is ordered by its barriers.  (A scalar branch inside the LDS-DMA asm once let MFMA
+    results be read before they landed: colour-feature rows changed run to run.)"""
+    if net == "ngp":
+        ren = make_renderer(sdfr, renderer_sd, 64, 24, "f16x3", return_sdf=True, return_xyz=True)
+    else:
+        ren = make_siren(sdfr, siren_sd, 64, 24, return_sdf=True, return_xyz=True)
+    torch.manual_seed(11)
+    ext, focal, near, far, _ = sdfr.generate_camera_params(64, DEV, batch=B)
+    lat = torch.from_numpy(W.det_uniform((B, 256), -1, 1, 5)).to(DEV)
+    tr = torch.rand(B, 64, 64)
+    with torch.no_grad():
+        runs = [ren(ext, focal, near, far, styles=lat, t_rand=tr) for _ in range(3)]
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            if torch.is_tensor(a):
+                assert torch.equal(a, b)
+
+
 def make_siren(sdfr, sd, res, N, **flags):
     opt = sdfr.vol_render_opt(ngp=False)
     r = opt.rendering
