@@ -116,7 +116,6 @@ struct EncodeArgs {
     const float *emb;
     const int32_t *offsets;
     float *enc;                    // [L][S_total][2]
-    float2 *zd;                    // [S_total] (z, segment length) for the f16x3 field, or null
     LevelTable lt;
     int pair_ok;                   // table 16-B aligned (paired corner loads)
 };
@@ -253,25 +252,6 @@ __device__ __forceinline__ void level_interp_adj(const float *__restrict__ grid,
         for (uint32_t c = 0; c < 2; ++c) out[c] = __fmaf_rn(wts[idx], v[idx][c], out[c]);
 }
 
-// Depth z of sample `sid` and its segment length dist = (z_{s+1} - z_s) |d| (1e10 |d|
-// for the last sample), sdf_model.py:240-243 -- the compositing inputs that do not
-// depend on the network, handed to field_p_kernel with the features.
-__device__ __forceinline__ float2 sample_zd(const GeomArgs &g, uint32_t sid) {
-    const SampleId id = decode_sid(g, sid);
-    const uint32_t rl = id.ray_local < g.H * g.W ? id.ray_local : g.H * g.W - 1;
-    const uint32_t y = rl / g.W, x = rl % g.W;
-    const uint32_t ray_index = (id.b * g.H + y) * g.W + x;
-    Ray ray;
-    make_ray(g.cam + (size_t)id.b * 12, g.focal[id.b], g.pix_x[x], g.pix_y[y], g.half_res, ray);
-    const float nr = g.near_[id.b], fr = g.far_[id.b];
-    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
-    const float z = sample_z(g.sc, nr, fr, ray_index, id.s);
-    const float dist = (id.s + 1 < g.N)
-                           ? __fmul_rn(__fsub_rn(sample_z(g.sc, nr, fr, ray_index, id.s + 1), z), dnorm)
-                           : __fmul_rn(1e10f, dnorm);
-    return make_float2(z, dist);
-}
-
 // One thread: SPT samples (256 apart) x LPT levels {y, y + 16/LPT, ...}.
 // Branch-free: padding / out-of-box samples gather at u = 0.5 and store 0, so
 // every corner load of the thread can be in flight at once.
@@ -314,10 +294,32 @@ __global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
                     in[k] ? make_float2(res[0], res[1]) : make_float2(0.0f, 0.0f);
         }
     }
-    if (a.zd && blockIdx.y == 0) {
-#pragma unroll
-        for (uint32_t k = 0; k < SPT; ++k)
-            if (live[k]) a.zd[sid[k]] = sample_zd(a.g, sid[k]);
+}
+
+// Per sample depth z and segment length dist = (z_{s+1} - z_s) |d| (1e10 |d| for the
+// last sample), sdf_model.py:240-243 -- the compositing inputs that do not depend on
+// the network, for field_p_kernel (tile order, as the features).  One thread per ray
+// (each z computed once; the gather kernel stays a pure gather).
+__global__ void __launch_bounds__(256) sample_zd_kernel(const GeomArgs g, float2 *__restrict__ zd) {
+    const uint32_t rid = blockIdx.x * 256 + threadIdx.x;          // tile-order ray id
+    if (rid >= g.total_tiles * kTileRays) return;
+    const uint32_t tile = rid / kTileRays, n = rid % kTileRays;
+    const uint32_t b = tile / g.tiles_per_face;
+    uint32_t rl = (tile % g.tiles_per_face) * kTileRays + n;
+    if (rl >= g.H * g.W) rl = g.H * g.W - 1;                     // padding rays: any value
+    const uint32_t y = rl / g.W, x = rl % g.W;
+    const uint32_t ray_index = (b * g.H + y) * g.W + x;
+    Ray ray;
+    make_ray(g.cam + (size_t)b * 12, g.focal[b], g.pix_x[x], g.pix_y[y], g.half_res, ray);
+    const float nr = g.near_[b], fr = g.far_[b];
+    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
+    float2 *out = zd + (size_t)tile * g.N * kTileRays + n;
+    float z = sample_z(g.sc, nr, fr, ray_index, 0);
+    for (uint32_t s = 0; s < g.N; ++s) {
+        const float zn = s + 1 < g.N ? sample_z(g.sc, nr, fr, ray_index, s + 1) : 0.0f;
+        const float dist = s + 1 < g.N ? __fmul_rn(__fsub_rn(zn, z), dnorm) : __fmul_rn(1e10f, dnorm);
+        out[(size_t)s * kTileRays] = make_float2(z, dist);
+        z = zn;
     }
 }
 
@@ -945,13 +947,12 @@ static void launch_encode_mode(hipStream_t st, const EncodeArgs &e) {
 }
 
 static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
-                         const GeomArgs &g, float *enc, hipStream_t st, float2 *zd = nullptr) {
+                         const GeomArgs &g, float *enc, hipStream_t st) {
     EncodeArgs e;
     e.g = g;
     e.emb = w->embeddings;
     e.offsets = w->offsets;
     e.enc = enc;
-    e.zd = zd;
     e.pair_ok = (reinterpret_cast<uintptr_t>(w->embeddings) & 15u) == 0;
     make_level_table(16, w->log2_per_level_scale, w->base_resolution, e.lt);
 #ifdef SDFR_ABLATION
@@ -1061,9 +1062,12 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     record_event(a->stage_events[0], st);
     if (a->field_precision == SDFR_FIELD_F16X3) {
         if ((rc = launch_xprep_ngp(w, a, ws + o_x, film, st))) return rc;
-        record_event(a->stage_events[1], st);
         float2 *zd = reinterpret_cast<float2 *>(ws + o_zd);
-        if ((rc = launch_encode(w, a, g, enc, st, zd))) return rc;
+        hipLaunchKernelGGL(sample_zd_kernel, dim3((g.total_tiles * kTileRays + 255) / 256), dim3(256),
+                           0, st, g, zd);
+        if ((rc = check_launch("render_ngp: sample depths"))) return rc;
+        record_event(a->stage_events[1], st);                  // the encode stage is the gather alone
+        if ((rc = launch_encode(w, a, g, enc, st))) return rc;
         record_event(a->stage_events[2], st);
         float *part = reinterpret_cast<float *>(ws + o_part);
         if ((rc = launch_xfield_ngp(w, a, g, enc, ws + o_x, film, st, part, zd))) return rc;
