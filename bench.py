@@ -34,7 +34,11 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 METRIC = "rendered faces/sec/GPU at 256² (SDF+ngp path); 1/2/4/8-GPU scaling"
-FLOP_PER_SAMPLE = 550912          # renderer MLP, SURVEY.md §8(d) / BASELINE.md §2
+FLOP_PER_SAMPLE = 550912          # renderer MLP as the reference runs it, SURVEY.md §8(d)
+# what the fused split-fp16 kernel computes per sample: input_linear and pts_linears.0
+# composed into one 32 -> 256 map (no nonlinearity between them), so
+# one 256 x 256 GEMM (131,072 FLOP) less; the roofline counts THESE FLOPs
+FLOP_PER_SAMPLE_FUSED = 419840
 FLOP_PER_SAMPLE_SIREN = 1053696   # SirenGenerator MLP, SURVEY.md §8(d)
 GATHER_BYTES_PER_SAMPLE = 1024    # 16 levels x 8 corners x 2 x fp32
 MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
@@ -263,10 +267,10 @@ def main():
     field_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
     render_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args.steps
     samples = B * res * res * N
-    flop = FLOP_PER_SAMPLE_SIREN if siren else FLOP_PER_SAMPLE
+    f16x3 = args.field_precision == "f16x3"
+    flop = FLOP_PER_SAMPLE_SIREN if siren else (FLOP_PER_SAMPLE_FUSED if f16x3 else FLOP_PER_SAMPLE)
     field_tflops = flop * samples / (field_ms * 1e-3) / 1e12
     gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9 if not siren else 0.0
-    f16x3 = args.field_precision == "f16x3"
     field_kernel = ("field_p_kernel<sdfr::SirenNet>" if siren else
                     "field_p_kernel<sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
     def traffic_of(kernel):
@@ -300,6 +304,8 @@ def main():
                 "unit": "TFLOP/s", "frac": field_tflops / (MFMA_F16_PEAK_TFLOPS / 3),
                 "traffic": traffic, "mfma_dtype": "f16 (hi/lo split, fp32 accumulate)",
                 "mfma_issued_tflops": 3 * field_tflops, "mfma_peak_dtype": MFMA_F16_PEAK_TFLOPS,
+                "flop_per_sample": flop,
+                "reference_flop_per_sample": FLOP_PER_SAMPLE_SIREN if siren else FLOP_PER_SAMPLE,
                 "counters": counters_of(field_kernel.split("<")[0])}
         clk = (roof["counters"] or {}).get("effective_clock_GHz")
         if clk:

@@ -52,18 +52,24 @@ constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 t_out][hi,lo][64 l
 // ----------------------------------------------------------------------------
 struct NgpNet {
     static constexpr bool kSiren = false;
-    static constexpr bool kSlice2 = true;            // register ring: whole-K-step slots
-    static constexpr int kLayers = 5;          // input_linear, pts_linears.0-2, views
+    // input_linear (LinearLayer, affine: sdf_model.py:37-39) feeds pts_linears.0's
+    // linear with no nonlinearity between them (:1574-1577), so the two are ONE affine
+    // map W1 (W0 x + b0) + b1 = (W1 W0) x + (W1 b0 + b1), composed once per weight
+    // version in fp64 (compose_kernel): layer 0 is that 32 -> 256 map with
+    // pts_linears.0's FiLM, and the 256 x 256 GEMM of pts_linears.0 per sample is gone.
+    static constexpr bool kCompose = true;
+    static constexpr int kLayers = 4;          // composed 0, pts_linears.1-2, views
     static constexpr int kFilmN = 4;           // FiLM: pts_linears.0-2, views
-    static constexpr int kHidden = 3;          // dense layers after layer 0
-    static constexpr uint32_t kSlices = 2 + 16 * 3 + 18;
+    static constexpr int kHidden = 2;          // dense layers after layer 0
+    static constexpr uint32_t kSlices = 2 + 16 * 2 + 18;
     __host__ __device__ static constexpr uint32_t K(int l) {
-        return l == 0 ? kFeatIn : (l == 4 ? kViewsIn : kW);
+        return l == 0 ? kFeatIn : (l == 3 ? kViewsIn : kW);
     }
-    __host__ __device__ static constexpr int film_layer(int f) { return f + 1; }
+    __host__ __device__ static constexpr int film_layer(int f) { return f; }
 };
 struct SirenNet {
     static constexpr bool kSiren = true;
+    static constexpr bool kCompose = false;
     static constexpr bool kSlice2 = false;
     static constexpr int kLayers = 9;          // pts_linears.0-7, views
     static constexpr int kFilmN = 9;
@@ -130,6 +136,21 @@ __global__ void __launch_bounds__(256) xscale_kernel(const XScaleArgs a) {
     a.su[layer * kW + row] = su;
     a.bias_s[layer * kW + row] =
         (layer == 0 && a.raw_bias0) ? a.b[0][row] : __fmul_rn(a.b[layer][row], su);
+}
+
+// prep 0 (ngp): layer 0 = pts_linears.0 o input_linear, one row per block, fp64 sums
+// rounded once to fp32: wc = W1 W0 [256][32], bc = W1 b0 + b1 [256]
+__global__ void __launch_bounds__(64) compose_kernel(const float *w0, const float *b0,
+                                                     const float *w1, const float *b1,
+                                                     float *wc, float *bc) {
+    const uint32_t i = blockIdx.x, j = threadIdx.x;
+    if (j > kFeatIn) return;
+    const float *r1 = w1 + (size_t)i * kW;
+    double acc = j < kFeatIn ? 0.0 : (double)b1[i];
+    for (uint32_t k = 0; k < kW; ++k)
+        acc = fma((double)r1[k], j < kFeatIn ? (double)w0[(size_t)k * kFeatIn + j] : (double)b0[k], acc);
+    if (j < kFeatIn) wc[(size_t)i * kFeatIn + j] = (float)acc;
+    else bc[i] = (float)acc;
 }
 
 // ----------------------------------------------------------------------------
@@ -427,7 +448,7 @@ __device__ __forceinline__ void pstep(PRing &R, f4 (&acc)[16], const f4 (&bf)[4]
 // 2q, 2q+1 of this layer's output; wave h holds tile 2q + h as local tile q):
 // activate local tile q of both blocks, split it and write the (hi, lo) dword pairs
 // to bytes 8h .. 8h + 7 of the chunk's 16-B B-fragment elements in slot q & 1.
-//   MODE 0: ngp input_linear, fma(x 2^-es, 1/su, b) (see feat_scale)
+//   MODE 0: ngp layer 0, FiLM of x 2^-es (the features were scaled by 2^es, feat_scale)
 //   MODE 1: FiLM sin_rev(fma(gamma'', x, beta''))
 //   MODE 2: FiLM + the sigma head's partial dot product (per lane over own tiles)
 template <int MODE>
@@ -447,7 +468,7 @@ __device__ __forceinline__ void p_act(const PRing &R, f4 (&in)[16], int q, const
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            if constexpr (MODE == 0) v[r] = __fmaf_rn(__builtin_ldexpf(z[r], -es[c]), gm[r], bt[r]);
+            if constexpr (MODE == 0) v[r] = sin_rev(__fmaf_rn(gm[r], __builtin_ldexpf(z[r], -es[c]), bt[r]));
             else v[r] = sin_rev(__fmaf_rn(gm[r], z[r], bt[r]));
         }
         if constexpr (MODE == 2) {
@@ -481,7 +502,7 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
     __shared__ f4 xch_lds[4][2 * 2 * 2 * 64];               // 32 KB: [pair][slot][block][hi,lo][lane]
     __shared__ f4 facc_lds[kPWaves][8 * 4 * 8];             // 32 KB: [wave][tile][g][ray] feature sums
     __shared__ float film_lds[NF * 2 * kW];                 // the workgroup's face
-    __shared__ float cst[6 * kW];                           // ngp layer-0 bias, 1/su0, sigma_w, rgb_w[3]
+    __shared__ float cst[4 * kW];                           // sigma_w, rgb_w[3]
     __shared__ float sdfx_lds[4][2][2][64];                 // [pair][wave][block][lane] sigma half-sums
     __shared__ float pcol_lds[4][6][16];                    // wave 0's colour half-sums per column
     __shared__ float alx_lds[4][2][64];                     // [pair][block][lane] alpha
@@ -508,14 +529,8 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
     R.wave = __builtin_amdgcn_readfirstlane(wave);
     R.h = h;
     R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
-    for (uint32_t i = tid; i < 6 * kW; i += kPThreads) {
-        float v;
-        if (i < kW) v = Net::kSiren ? 0.0f : a.bias_s[i];     // raw input_linear bias
-        else if (i < 2 * kW) v = __fdiv_rn(1.0f, a.su[i - kW]);
-        else if (i < 3 * kW) v = a.sigma_w[i - 2 * kW];
-        else v = a.rgb_w[i - 3 * kW];
-        cst[i] = v;
-    }
+    for (uint32_t i = tid; i < 4 * kW; i += kPThreads)
+        cst[i] = i < kW ? a.sigma_w[i] : a.rgb_w[i - kW];
     // prologue: k-step 0's half-slices -> slots 0, 1 (each k-step issues the next)
     p_dma_i<0, 0>(R);
     p_dma_i<1, 1>(R);
@@ -525,9 +540,7 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
 #pragma unroll
     for (int i = 0; i < 4; ++i) R.na[i] = R.lds[h * 128 + (i >> 1) * 256 + (i & 1) * 64 + lane];
 
-    const float *bias0 = cst;
-    const float *inv_su0 = cst + kW;
-    const float *sig_w = cst + 2 * kW, *rgb_w = cst + 3 * kW;
+    const float *sig_w = cst, *rgb_w = cst + kW;
     auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
     auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
     const float sig_b = a.sigma_b[0];
@@ -633,13 +646,11 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
         // activation of layer l's output, chunk q, by its owner (wave q >> 2)
         auto act_out = [&](auto L, f4 (&o)[16], int q) {
             constexpr int l = decltype(L)::value;
-            if constexpr (l == 0 && !Net::kSiren) {
-                p_act<0>(R, o, q, inv_su0, bias0, nullptr, sdfp, g, es);
-            } else {
-                constexpr int f = Net::kSiren ? l : l - 1;
-                if constexpr (l == NL - 2) p_act<2>(R, o, q, fg(f), fb(f), sig_w, sdfp, g, es);
-                else p_act<1>(R, o, q, fg(f), fb(f), nullptr, sdfp, g, es);
-            }
+            constexpr int f = Net::film_layer(l) == l ? l : -1;   // layer l's FiLM
+            static_assert(f >= 0, "one FiLM per layer");
+            if constexpr (l == 0 && !Net::kSiren) p_act<0>(R, o, q, fg(f), fb(f), nullptr, sdfp, g, es);
+            else if constexpr (l == NL - 2) p_act<2>(R, o, q, fg(f), fb(f), sig_w, sdfp, g, es);
+            else p_act<1>(R, o, q, fg(f), fb(f), nullptr, sdfp, g, es);
         };
         auto chunk_b = [&](int q) { return [&, q](f4 (&bn)[4]) { p_read_chunk(R, q, bn); }; };
         f4 bn[4];
@@ -985,15 +996,26 @@ size_t field_part_bytes(uint32_t B, uint32_t tiles_per_face, uint32_t N) {
 
 template <class Net>
 static size_t xws_bytes() {
-    return (size_t)Net::kSlices * kXSliceF4 * sizeof(f4) + 2 * Net::kLayers * kW * sizeof(float);
+    return (size_t)Net::kSlices * kXSliceF4 * sizeof(f4) + 2 * Net::kLayers * kW * sizeof(float) +
+           (Net::kCompose ? (size_t)(kFeatIn + 1) * kW * sizeof(float) : 0);
+}
+
+// the composed ngp layer 0 inside the region: W [256][32] | b [256]
+template <class Net>
+static float *xws_composed(char *xws) {
+    return reinterpret_cast<float *>(xws + (size_t)Net::kSlices * kXSliceF4 * sizeof(f4)) +
+           2 * Net::kLayers * kW;
 }
 
 // workspace region of this path: packed [slices][1024] f4 | su [L][256] | bias_s [L][256]
+// (| composed layer 0, ngp)
 size_t f16x3_ws_bytes(int net) { return net ? xws_bytes<SirenNet>() : xws_bytes<NgpNet>(); }
 
-// The network's tensors in policy order (layer 0, dense layers, views; FiLM sets).
+// The network's tensors in policy order (layer 0, dense layers, views; FiLM sets); for
+// ngp also the two reference layers that make the composed layer 0 (xws_composed).
 struct NetPtrs {
     const float *w[kMaxLayers], *b[kMaxLayers];
+    const float *in_w, *in_b, *p0_w, *p0_b;
     const float *gw[kMaxLayers], *gb[kMaxLayers], *bw[kMaxLayers], *bb[kMaxLayers];
     const float *sigma_w, *sigma_b, *rgb_w, *rgb_b, *sigmoid_beta;
 };
@@ -1007,16 +1029,28 @@ static int launch_xpack(const NetPtrs &P, uint32_t B, const float *styles, char 
     f4 *packed = reinterpret_cast<f4 *>(xws);
     float *su = reinterpret_cast<float *>(xws + (size_t)Net::kSlices * kXSliceF4 * sizeof(f4));
     float *bias_s = su + Net::kLayers * kW;
+    NetPtrs Q = P;
+    if constexpr (Net::kCompose) {
+        float *wc = xws_composed<Net>(xws);
+        Q.w[0] = wc;
+        Q.b[0] = wc + kFeatIn * kW;
+        if (pack) {
+            hipLaunchKernelGGL(compose_kernel, dim3(kW), dim3(64), 0, st, P.in_w, P.in_b, P.p0_w,
+                               P.p0_b, wc, wc + kFeatIn * kW);
+            int rc = check_launch("render: compose layer 0");
+            if (rc) return rc;
+        }
+    }
     if (pack) {
         XScaleArgs sa;
         for (int l = 0; l < Net::kLayers; ++l) {
-            sa.w[l] = P.w[l];
-            sa.b[l] = P.b[l];
+            sa.w[l] = Q.w[l];
+            sa.b[l] = Q.b[l];
             sa.K[l] = Net::K(l);
         }
         sa.su = su;
         sa.bias_s = bias_s;
-        sa.raw_bias0 = !Net::kSiren;
+        sa.raw_bias0 = 0;
         hipLaunchKernelGGL(xscale_kernel, dim3(Net::kLayers, kW / 4), dim3(256), 0, st, sa);
         int rc = check_launch("render: xscale");
         if (rc) return rc;
@@ -1030,8 +1064,8 @@ static int launch_xpack(const NetPtrs &P, uint32_t B, const float *styles, char 
         p.bb[f] = P.bb[f];
     }
     for (int l = 0; l < Net::kLayers; ++l) {
-        p.w[l] = P.w[l];
-        p.lb[l] = P.b[l];
+        p.w[l] = Q.w[l];
+        p.lb[l] = Q.b[l];
     }
     p.su = su;
     p.film = film;
@@ -1096,18 +1130,22 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
 
 static NetPtrs ngp_ptrs(const sdfr_ngp_weights *w) {
     NetPtrs P{};
-    P.w[0] = w->input_w;
-    P.b[0] = w->input_b;
-    for (int l = 0; l < 3; ++l) {
-        P.w[1 + l] = w->pts_w[l];
-        P.b[1 + l] = w->pts_b[l];
-        P.gw[l] = w->pts_gw[l];
-        P.gb[l] = w->pts_gb[l];
-        P.bw[l] = w->pts_bw[l];
-        P.bb[l] = w->pts_bb[l];
+    P.in_w = w->input_w;                       // composed into layer 0 (launch_xpack)
+    P.in_b = w->input_b;
+    P.p0_w = w->pts_w[0];
+    P.p0_b = w->pts_b[0];
+    for (int l = 1; l < 3; ++l) {
+        P.w[l] = w->pts_w[l];
+        P.b[l] = w->pts_b[l];
     }
-    P.w[4] = w->views_w;
-    P.b[4] = w->views_b;
+    for (int f = 0; f < 3; ++f) {
+        P.gw[f] = w->pts_gw[f];
+        P.gb[f] = w->pts_gb[f];
+        P.bw[f] = w->pts_bw[f];
+        P.bb[f] = w->pts_bb[f];
+    }
+    P.w[3] = w->views_w;
+    P.b[3] = w->views_b;
     P.gw[3] = w->views_gw;
     P.gb[3] = w->views_gb;
     P.bw[3] = w->views_bw;

@@ -77,7 +77,9 @@ def test_workspace_size(sdfr):
     n = lib.sdfr_render_ngp_workspace_bytes(2, 64, 64, 24, 16)
     enc = 2 * 4096 * 24 * 16 * 2 * 4
     fixed = 67 * 1024 * 16 + 2 * 8 * 256 * 4          # fp32 fragments + FiLM vectors
-    xfixed = 68 * 1024 * 16 + 2 * 5 * 256 * 4         # split-fp16 fragments, su, bias_s
+    # split-fp16 fragments (52 half-slices: layer 0 = input_linear o pts_linears.0),
+    # su, bias_s, the composed layer 0 (W [256][32] | b [256])
+    xfixed = 52 * 1024 * 16 + 2 * 4 * 256 * 4 + 33 * 256 * 4
     zd = 2 * 4096 * 24 * 2 * 4                         # per-sample (z, segment length)
     # 2 faces = 256 workgroups of 2 tiles: no sample split, no partials
     assert enc + fixed + xfixed + zd <= n <= enc + fixed + xfixed + zd + 1536
