@@ -1,0 +1,68 @@
+"""Stage-1 training step under torch.profiler (profiling aid, not a test): which aten ops
+and which Python call sites issue the small elementwise kernels around the HIP ones.
+
+    python scripts/train_prof.py [--steps 2] [--out gpurun_out/train_prof.txt]"""
+import argparse
+import sys
+from pathlib import Path
+
+import torch
+from torch.profiler import ProfilerActivity, profile
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from sdfr_loader import load  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--steps", type=int, default=2)
+    p.add_argument("--out", default="gpurun_out/train_prof.txt")
+    a = p.parse_args()
+    dev = torch.device("cuda", 0)
+    sdfr = load()
+    from sdface_gan_amd.training import CoordConv2d, RendererTrainer
+    CoordConv2d.pad_to = 8
+    opt = sdfr.vol_render_opt(ngp=True, batch=8, chunk=2, train_renderer=True)
+    tr = RendererTrainer(opt, dev, seed=0)
+    tr.g_module.renderer.rng_device = "device"
+    tr.generator_test.renderer.rng_device = "device"
+    size = opt.training.renderer_output_size
+    torch.manual_seed(1000)
+    real = [torch.rand(8, 3, size, size, device=dev) * 2 - 1 for _ in range(4)]
+    for k in range(4):
+        tr.step(real[k % 4])
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        for k in range(a.steps):
+            tr.step(real[k % 4])
+        torch.cuda.synchronize()
+    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+    with open(a.out, "w") as f:
+        f.write(f"# {a.steps} stage-1 steps\n")
+        f.write(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=70,
+                                          max_name_column_width=70))
+        f.write("\n\n# by call site (5 frames)\n")
+        f.write(prof.key_averages(group_by_stack_n=5).table(
+            sort_by="self_cuda_time_total", row_limit=80, max_name_column_width=50,
+            max_src_column_width=120))
+        f.write("\n\n# call sites of the small torch ops (stack, repo frames only)\n")
+        rows = []
+        for ev in prof.key_averages(group_by_stack_n=12):
+            if not ev.key.startswith("aten::") or ev.key in ("aten::miopen_convolution",
+                                                             "aten::convolution_backward"):
+                continue
+            cuda = ev.self_device_time_total
+            if cuda <= 0:
+                continue
+            frames = [fr for fr in ev.stack if "sdface-gan_amd" in fr or "scripts/" in fr]
+            rows.append((cuda, ev.count, ev.key, frames[:4]))
+        rows.sort(key=lambda r: -r[0])
+        for cuda, cnt, key, frames in rows[:60]:
+            f.write(f"{cuda / 1e3 / a.steps:8.3f} ms/step {cnt / a.steps:7.1f} calls/step  {key}\n")
+            for fr in frames:
+                f.write(f"            {fr}\n")
+    print("wrote", a.out)
+
+
+if __name__ == "__main__":
+    main()
