@@ -30,6 +30,11 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from sdfr_loader import load  # noqa: E402
 
 
+class _NoCache(dict):
+    def __setitem__(self, k, v):
+        pass
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--stage", type=int, default=2, choices=[1, 2])
@@ -46,6 +51,8 @@ def main():
                         "rocBLAS fp32 (linear.py)")
     p.add_argument("--coord-pad", type=int, default=8,
                    help="stage-1 discriminator CoordConv channel padding (training.py; 1 = off)")
+    p.add_argument("--no-coord-cache", action="store_true",
+                   help="rebuild the CoordConv coordinate planes per call (A/B aid)")
     a = p.parse_args()
     torch.backends.cudnn.benchmark = a.miopen_find
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -61,6 +68,9 @@ def main():
     set_train_gemm(a.train_gemm)
     from sdface_gan_amd.training import CoordConv2d
     CoordConv2d.pad_to = a.coord_pad
+    if a.no_coord_cache:
+        import sdface_gan_amd.training as training_mod
+        training_mod._COORD_PLANES = _NoCache()
     opt = sdfr.vol_render_opt(ngp=a.net == "ngp", batch=a.batch, chunk=a.chunk,
                               train_renderer=a.stage == 1)
     if a.stage == 1:

@@ -409,18 +409,37 @@ class VolumeRenderDiscConv2d(nn.Module):
         return self.activation(out) if self.activate else out
 
 
+_COORD_PLANES = {}
+
+
+def coord_planes(dim_y, dim_x, device, pad=0):
+    """[1, 2 + pad, dim_y, dim_x]: the y and x coordinate planes exactly as
+    sdf_model.py:1252-1275 computes them (arange / (n - 1) * 2 - 1 in fp32), then
+    ``pad`` zero planes.  Built once per (size, device, pad): the discriminator runs
+    ten CoordConv layers per forward and a dozen forwards per training step, and
+    rebuilding the planes cost ~12 small launches each time."""
+    key = (dim_y, dim_x, str(device), pad)
+    t = _COORD_PLANES.get(key)
+    if t is None:
+        with torch.inference_mode(False), torch.no_grad():
+            xx = torch.arange(dim_x, dtype=torch.float32, device=device).repeat(1, 1, dim_y, 1)
+            yy = torch.arange(dim_y, dtype=torch.float32, device=device).repeat(1, 1, dim_x, 1)
+            yy = yy.transpose(2, 3)
+            xx = (xx / (dim_x - 1)) * 2 - 1
+            yy = (yy / (dim_y - 1)) * 2 - 1
+            z = torch.zeros(1, pad, dim_y, dim_x, dtype=torch.float32, device=device)
+            t = torch.cat([yy, xx, z], dim=1).contiguous()
+        _COORD_PLANES[key] = t
+    return t
+
+
 class AddCoords(nn.Module):
     """sdf_model.py:1252-1275: append the y, x pixel coordinates in [-1, 1]."""
 
-    def forward(self, input_tensor):
+    def forward(self, input_tensor, pad=0):
         b, _, dim_y, dim_x = input_tensor.shape
-        dev = input_tensor.device
-        xx = torch.arange(dim_x, dtype=torch.float32, device=dev).repeat(1, 1, dim_y, 1)
-        yy = torch.arange(dim_y, dtype=torch.float32, device=dev).repeat(1, 1, dim_x, 1)
-        yy = yy.transpose(2, 3)
-        xx = (xx / (dim_x - 1)) * 2 - 1
-        yy = (yy / (dim_y - 1)) * 2 - 1
-        return torch.cat([input_tensor, yy.repeat(b, 1, 1, 1), xx.repeat(b, 1, 1, 1)], dim=1)
+        planes = coord_planes(dim_y, dim_x, input_tensor.device, pad)
+        return torch.cat([input_tensor, planes.expand(b, -1, -1, -1)], dim=1)
 
 
 class CoordConv2d(nn.Module):
@@ -442,14 +461,13 @@ class CoordConv2d(nn.Module):
                               padding=padding, bias=bias)
 
     def forward(self, input_tensor):
-        x = self.addcoords(input_tensor)
-        c = x.shape[1]
-        pad = -c % self.pad_to
-        if not x.is_cuda or pad == 0:
-            return self.conv(x)
+        pad = -(input_tensor.shape[1] + 2) % self.pad_to
+        if not input_tensor.is_cuda or pad == 0:
+            return self.conv(self.addcoords(input_tensor))
+        # coordinates and zero channels appended by one concatenation
+        x = self.addcoords(input_tensor, pad)
         w = F.pad(self.conv.weight, (0, 0, 0, 0, 0, pad))
-        return F.conv2d(F.pad(x, (0, 0, 0, 0, 0, pad)), w, self.conv.bias,
-                        self.conv.stride, self.conv.padding)
+        return F.conv2d(x, w, self.conv.bias, self.conv.stride, self.conv.padding)
 
 
 class CoordConvLayer(nn.Module):

@@ -45,6 +45,27 @@ def test_volume_render_discriminator_shapes(sdfr):
     assert d.final_conv.conv.kernel_size == (2, 2)
 
 
+def test_add_coords_matches_reference_formula(sdfr):
+    """AddCoords with its cached planes == sdf_model.py:1252-1275 rebuilt per call,
+    bit for bit, with and without the zero channels CoordConv2d pads with; the
+    gradient reaches only the input channels."""
+    from sdface_gan_amd.training import AddCoords
+    torch.manual_seed(0)
+    for b, c, hh, ww in [(3, 5, 7, 9), (2, 128, 16, 16), (1, 1, 2, 2)]:
+        x = torch.randn(b, c, hh, ww, requires_grad=True)
+        xx = torch.arange(ww, dtype=torch.float32).repeat(1, 1, hh, 1)
+        yy = torch.arange(hh, dtype=torch.float32).repeat(1, 1, ww, 1).transpose(2, 3)
+        xx = (xx / (ww - 1)) * 2 - 1
+        yy = (yy / (hh - 1)) * 2 - 1
+        ref = torch.cat([x, yy.repeat(b, 1, 1, 1), xx.repeat(b, 1, 1, 1)], dim=1)
+        assert torch.equal(AddCoords()(x), ref)
+        out = AddCoords()(x, 3)
+        assert out.shape == (b, c + 5, hh, ww)
+        assert torch.equal(out[:, :c + 2], ref) and not out[:, c + 2:].any()
+        out.sum().backward()
+        assert torch.equal(x.grad, torch.ones_like(x))
+
+
 def test_eikonal_loss_known_answer(sdfr):
     from sdface_gan_amd.training import eikonal_loss
     g = torch.tensor([[3.0, 4.0, 0.0], [0.0, 0.0, 1.0]])          # norms 5, 1
