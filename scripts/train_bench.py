@@ -53,6 +53,8 @@ def main():
                    help="stage-1 discriminator CoordConv channel padding (training.py; 1 = off)")
     p.add_argument("--no-coord-cache", action="store_true",
                    help="rebuild the CoordConv coordinate planes per call (A/B aid)")
+    p.add_argument("--no-skip-identity", action="store_true",
+                   help="LinearLayer computes the literal 1 * y + 0 (A/B aid)")
     a = p.parse_args()
     torch.backends.cudnn.benchmark = a.miopen_find
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -68,6 +70,9 @@ def main():
     set_train_gemm(a.train_gemm)
     from sdface_gan_amd.training import CoordConv2d
     CoordConv2d.pad_to = a.coord_pad
+    if a.no_skip_identity:
+        from sdface_gan_amd.renderer import LinearLayer
+        LinearLayer.skip_identity = False
     if a.no_coord_cache:
         import sdface_gan_amd.training as training_mod
         training_mod._COORD_PLANES = _NoCache()

@@ -56,12 +56,19 @@ class LinearLayer(nn.Module):
 
     # the ngp network's layers take the training kernels (linear.py); others F.linear
     train_kernels = False
+    skip_identity = True          # False: the reference's literal 1 * y + 0 (A/B aid)
 
     def forward(self, input):
         # linear(): F.linear, or the split-fp16 MFMA kernels for the renderer MLP's
-        # training shapes (linear.py)
-        return self.std_init * linear(input, self.weight, self.bias,
-                                      self.train_kernels) + self.bias_init
+        # training shapes (linear.py).  The reference's ``1 * y + 0`` (the defaults) is
+        # the identity up to the sign of zero; skipping it saves two full passes over
+        # the [rays, samples, 256] activation forward and one backward.
+        y = linear(input, self.weight, self.bias, self.train_kernels)
+        if self.std_init != 1 or not self.skip_identity:
+            y = self.std_init * y
+        if self.bias_init != 0 or not self.skip_identity:
+            y = y + self.bias_init
+        return y
 
 
 class FiLMSiren(nn.Module):
