@@ -307,6 +307,13 @@ def main():
                 "flop_per_sample": flop,
                 "reference_flop_per_sample": FLOP_PER_SAMPLE_SIREN if siren else FLOP_PER_SAMPLE,
                 "counters": counters_of(field_kernel.split("<")[0])}
+        # the same time priced at SURVEY.md §8(d)'s per-sample figure (the reference's
+        # uncomposed network): the rate a user of the reference sees; `achieved` /
+        # `frac` above count only the FLOPs the kernel executes
+        ref_flop = roof["reference_flop_per_sample"]
+        ref_tflops = field_tflops * ref_flop / flop
+        roof["algorithmic"] = {"flop_per_sample": ref_flop, "achieved": ref_tflops,
+                               "frac": ref_tflops / (MFMA_F16_PEAK_TFLOPS / 3)}
         clk = (roof["counters"] or {}).get("effective_clock_GHz")
         if clk:
             # the same time against the peak at the clock the chip holds under this body
