@@ -32,7 +32,7 @@ def main():
     for k in range(4):
         tr.step(real[k % 4])
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True) as prof:
         for k in range(a.steps):
             tr.step(real[k % 4])
         torch.cuda.synchronize()
@@ -61,6 +61,16 @@ def main():
             f.write(f"{cuda / 1e3 / a.steps:8.3f} ms/step {cnt / a.steps:7.1f} calls/step  {key}\n")
             for fr in frames:
                 f.write(f"            {fr}\n")
+        f.write("\n\n# small torch ops by input shapes\n")
+        rows = []
+        for ev in prof.key_averages(group_by_input_shape=True):
+            if ev.key in ("aten::copy_", "aten::cat", "aten::mul", "aten::add", "aten::add_",
+                          "aten::sum", "aten::div", "aten::fill_", "aten::sub", "aten::mm") \
+                    and ev.self_device_time_total > 0:
+                rows.append((ev.self_device_time_total, ev.count, ev.key, ev.input_shapes))
+        rows.sort(key=lambda r: -r[0])
+        for cuda, cnt, key, shp in rows[:70]:
+            f.write(f"{cuda / 1e3 / a.steps:8.3f} ms/step {cnt / a.steps:7.1f}/step  {key:12s} {shp}\n")
     print("wrote", a.out)
 
 
