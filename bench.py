@@ -37,8 +37,8 @@ METRIC = "rendered faces/sec/GPU at 256² (SDF+ngp path); 1/2/4/8-GPU scaling"
 FLOP_PER_SAMPLE = 550912          # renderer MLP as the reference runs it, SURVEY.md §8(d)
 # what the fused split-fp16 kernel computes per sample: input_linear and pts_linears.0
 # composed into one 32 -> 256 map (no nonlinearity between them), so
-# one 256 x 256 GEMM (131,072 FLOP) less; roofline.executed counts these, roofline.achieved
-# the reference's (the algorithmic figure)
+# one 256 x 256 GEMM (131,072 FLOP) less; roofline.achieved / frac count these (what the
+# hardware runs), roofline.algorithmic_equivalent the reference's
 FLOP_PER_SAMPLE_FUSED = 419840
 FLOP_PER_SAMPLE_SIREN = 1053696   # SirenGenerator MLP, SURVEY.md §8(d)
 GATHER_BYTES_PER_SAMPLE = 1024    # 16 levels x 8 corners x 2 x fp32
@@ -290,7 +290,9 @@ def main():
         (SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x GRBM_GUI_ACTIVE / XCDs)), or None."""
         try:
             ks = json.loads(Path(args.counters_json).read_text())["kernels"]
-            k = next(v for n, v in ks.items() if kernel in n)
+            # the full templated name (field_p_kernel<sdfr::NgpNet> and <sdfr::SirenNet>
+            # are different kernels)
+            k = next(v for n, v in ks.items() if kernel in n.replace("sdfr::(anonymous namespace)::", ""))
             return {"mfma_busy_frac": k["mfma_busy_frac"],
                     "effective_clock_GHz": k["effective_clock_GHz"],
                     "source": str(Path(args.counters_json).relative_to(REPO))}
@@ -298,22 +300,24 @@ def main():
             return None
     if f16x3:
         # fp32-accurate GEMMs as 3 fp16 MFMA terms: the attainable fp32-equivalent
-        # peak is the dense fp16 MFMA peak / 3.  `achieved` is
-        # the ALGORITHMIC rate, SURVEY.md §8(d)'s per-sample FLOPs of the reference's
-        # network over the kernel's time; `executed` prices the same time at the FLOPs
-        # the kernel actually issues (the ngp network's first two layers composed)
+        # peak is the dense fp16 MFMA peak / 3.  `achieved` /
+        # `frac` count the FLOPs the kernel EXECUTES (ngp: input_linear and
+        # pts_linears.0 composed into one layer, 419,840 FLOP/sample) -- the hardware
+        # utilisation; `algorithmic_equivalent` prices the same time at SURVEY.md
+        # §8(d)'s per-sample FLOPs of the reference's network (550,912)
         ref_flop = FLOP_PER_SAMPLE_SIREN if siren else FLOP_PER_SAMPLE
         alg_tflops = field_tflops * ref_flop / flop
+        peak = MFMA_F16_PEAK_TFLOPS / 3
         roof = {"kernel": f"{field_kernel} (MLP as 3 split-fp16 v_mfma_f32_16x16x32_f16 "
                           "terms per fp32 tile + compositing)",
-                "bound": "mfma", "achieved": alg_tflops, "peak": MFMA_F16_PEAK_TFLOPS / 3,
-                "unit": "TFLOP/s", "frac": alg_tflops / (MFMA_F16_PEAK_TFLOPS / 3),
-                "traffic": traffic, "flop_per_sample": ref_flop,
-                "executed": {"flop_per_sample": flop, "achieved": field_tflops,
-                             "frac": field_tflops / (MFMA_F16_PEAK_TFLOPS / 3)},
+                "bound": "mfma", "achieved": field_tflops, "peak": peak,
+                "unit": "TFLOP/s", "frac": field_tflops / peak,
+                "traffic": traffic, "flop_per_sample": flop,
+                "algorithmic_equivalent": {"flop_per_sample": ref_flop, "achieved": alg_tflops,
+                                           "frac": alg_tflops / peak},
                 "mfma_dtype": "f16 (hi/lo split, fp32 accumulate)",
                 "mfma_issued_tflops": 3 * field_tflops, "mfma_peak_dtype": MFMA_F16_PEAK_TFLOPS,
-                "counters": counters_of(field_kernel.split("<")[0])}
+                "counters": counters_of(field_kernel)}
         clk = (roof["counters"] or {}).get("effective_clock_GHz")
         if clk:
             # the same time against the peak at the clock the chip holds under this body

@@ -100,7 +100,8 @@ int sdfr_grid_encode_backward_ws(const float *grad, const float *inputs,
 /* ---------------------------------------------------------------------------
  * Real spherical harmonics (shencoder.cu semantics), C = degree.
  *   inputs [B, D], D must be 3; outputs [B, C*C]; dy_dx [B, D*C*C] or NULL.
- *   Degrees 1..4 are implemented (SDFace uses 4); 5..8 -> SDFR_EUNSUPPORTED.
+ *   Degrees 1..8 are implemented (SDFace uses 4; 5..8 from the bands that
+ *   csrc/sh_gen.py generates); other degrees -> SDFR_EUNSUPPORTED.
  * ------------------------------------------------------------------------- */
 int sdfr_sh_encode_forward(const float *inputs, float *outputs, uint32_t B,
                            uint32_t D, uint32_t C, float *dy_dx, void *stream);

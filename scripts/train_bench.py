@@ -117,8 +117,9 @@ def main():
             "config": {"workload": f"train.py stage {a.stage}, {a.net} renderer, random-init G/D",
                        "batch_per_gpu": a.batch, "chunk": a.chunk, "size": size,
                        "miopen_find": a.miopen_find,
-                       "parallelism": f"ddp{world} (RCCL all-reduce of "
-                                      f"{'G' if a.stage == 1 else 'decoder'} + D grads)"},
+                       "parallelism": (f"ddp{world} ({dist.get_backend()} all-reduce of "
+                                       f"{'G' if a.stage == 1 else 'decoder'} + D grads)")
+                                      if world > 1 else "single process (no all-reduce)"},
             "losses": {k: float(v) for k, v in losses.items()}}), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -19,6 +19,7 @@ import torch.nn as nn
 from torch.autograd import Function
 
 from . import _lib
+from .linear import _edge, _wanted
 
 _gridtype_to_id = {"hash": 0, "tiled": 1}
 _interp_to_id = {"linear": 0, "smoothstep": 1}
@@ -27,25 +28,6 @@ _interp_to_id = {"linear": 0, "smoothstep": 1}
 def _check_cuda(t: torch.Tensor, name: str):
     if not t.is_cuda:
         raise RuntimeError(f"{name} must be a CUDA tensor")
-
-
-_INPUT_GRAD_ONLY = [False]
-
-
-class input_grad_only:
-    """Context for an autograd.grad call that asks for the grid encoder's INPUT
-    gradient only (VolumeFeatureRenderer.get_eikonal_term, sdf_model.py:224-229):
-    the reference's backward also computes the table gradient there, which
-    autograd.grad then discards; here it is not computed.  Process-wide while active
-    (the autograd engine may run the backward on its device thread)."""
-
-    def __enter__(self):
-        self.prev = _INPUT_GRAD_ONLY[0]
-        _INPUT_GRAD_ONLY[0] = True
-        return self
-
-    def __exit__(self, *exc):
-        _INPUT_GRAD_ONLY[0] = self.prev
 
 
 class _GridEncode(Function):
@@ -74,6 +56,7 @@ class _GridEncode(Function):
         outputs = outputs.permute(1, 0, 2).reshape(B, L * C)
         ctx.save_for_backward(inputs, embeddings, offsets, dy_dx)
         ctx.dims = (B, D, C, L, S, H, gridtype, interpolation, bool(align_corners))
+        ctx.table_edge = _edge(embeddings)
         return outputs
 
     @staticmethod
@@ -82,9 +65,10 @@ class _GridEncode(Function):
         B, D, C, L, S, H, gridtype, interpolation, align_corners = ctx.dims
         grad = grad.view(B, L, C).permute(1, 0, 2).contiguous()
         grad_inputs = torch.zeros_like(inputs, dtype=embeddings.dtype) if dy_dx is not None else None
-        # inside input_grad_only() (the eikonal term's autograd.grad, which returns the
-        # points' gradient only) the table gradient would be discarded: skip it
-        skip = _INPUT_GRAD_ONLY[0] and grad_inputs is not None
+        # a backward pass that does not use the table gradient (the eikonal term's
+        # autograd.grad, which returns the points' gradient only; linear._wanted, scoped to
+        # that graph task) would discard it: skip it
+        skip = grad_inputs is not None and not _wanted(ctx.needs_input_grad[1], ctx.table_edge)
         grad_embeddings = None if skip else torch.zeros_like(embeddings)
         # binned table gradient (csrc/encoders.hip) in a workspace from torch's allocator
         L_ = _lib.lib()

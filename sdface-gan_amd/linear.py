@@ -16,24 +16,28 @@ fp32 accumulation, power-of-two row / column scaling: fp32-level accuracy):
   narrow heads     J <= 4 outputs (sigma 1, rgb 3): sdfr_linear_head_forward / _backward
                    (HBM-streaming fp32 FMA kernels in place of rocBLAS's N = 1..3 GEMMs)
 
-Shapes the kernels take: out features 256 with in features 32 / 256 / 259..288
-(the networks' input_linear, dense and views layers), and J <= 4 outputs with K <= 256
-(the 3- and 1-wide heads).  Everything else (the per-face gamma / beta layers on the
-styles, CPU tensors, inference) stays on F.linear.  ``set_train_gemm("torch")`` turns
-the routing off.
+Shapes the kernels take: out features 256 with in features <= 32, 256 or 257..272
+(the networks' input / first layers, dense and views layers; in features padded with
+zero columns to a multiple of 4 and the input gradient's width to 32 / 256 / 272), and
+J <= 4 outputs with K <= 256 (the 3- and 1-wide heads).  Everything else (the per-face
+gamma / beta layers on the styles, CPU tensors, inference) stays on F.linear.
+``set_train_gemm("torch")`` turns the routing off.
 
-The backward is first-order only (``once_differentiable``), so only the ngp network
-routes here (``NGPSIRENGenerator`` marks its layers ``train_kernels = True``): its
-eikonal term leaves autograd inside the grid encoder's backward (grid.py:65-89) and
-carries no gradient (as in the reference), so nothing differentiates these ops twice.
-The SIREN network's eikonal loss does reach its weights through a double backward
-(the points feed the MLP directly), so SirenGenerator keeps F.linear.
+Both networks route here (their layers carry ``train_kernels = True``).  The SIREN
+network's eikonal term is an ``autograd.grad(..., create_graph=True)`` through the MLP
+(sdf_model.py:224-229), so its loss reaches the weights through a double backward: a
+backward that runs with grad enabled (create_graph) computes the same gradients as
+differentiable ops -- ``linear()`` of these kernels again, ``_WGradF16x3``, the FiLM
+elementwise part in torch ops around ``_LinearGiven`` (the saved pre-activation put
+on the graph without recomputing it) -- and a plain backward runs straight on the
+kernels.  A backward also skips the gradients the running backward pass does not use
+(``_wanted``: the eikonal pass wants d/d pts only), per graph task.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
-from torch.autograd.function import once_differentiable
+from torch.autograd.graph import get_gradient_edge
 
 from . import _lib
 
@@ -92,33 +96,187 @@ def _wgrad(gy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return gw
 
 
+def _film_fwd(x2, packed, bias, g2, b2, N):
+    """(sin(gamma[f] y + beta[f]), y = x2 . B^T + bias) over F = g2.shape[0] faces of
+    equal row count (sdfr_film_linear_f16x3)."""
+    M = x2.shape[0]
+    F_ = g2.shape[0]
+    out = torch.empty(M, N, device=x2.device, dtype=torch.float32)
+    y = torch.empty(M, N, device=x2.device, dtype=torch.float32)
+    _lib.check(_lib.lib().sdfr_film_linear_f16x3(
+        _lib.ptr(out), _lib.ptr(y), _lib.ptr(x2), _lib.ptr(packed), _lib.ptr(bias), _lib.ptr(g2),
+        _lib.ptr(b2), M, N, x2.shape[1], M // F_, _lib.stream_of(x2)), "sdfr_film_linear_f16x3")
+    return out, y
+
+
+def _film_bwd(ds2, y, g2, b2):
+    """The FiLM backward's elementwise part (sdfr_film_backward): dy [M,N] and the
+    per-face dgamma, dbeta, bias-gradient partials [F,N]."""
+    M, N = ds2.shape
+    F_ = g2.shape[0]
+    L = _lib.lib()
+    dy = torch.empty(M, N, device=ds2.device, dtype=torch.float32)
+    dg = torch.empty(F_, N, device=ds2.device, dtype=torch.float32)
+    db_ = torch.empty(F_, N, device=ds2.device, dtype=torch.float32)
+    dbf = torch.empty(F_, N, device=ds2.device, dtype=torch.float32)
+    nws = L.sdfr_film_backward_ws_bytes(M, N, M // F_)
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=ds2.device)
+    _lib.check(L.sdfr_film_backward(
+        _lib.ptr(dy), _lib.ptr(dg), _lib.ptr(db_), _lib.ptr(dbf), _lib.ptr(ds2), _lib.ptr(y),
+        _lib.ptr(g2), _lib.ptr(b2), M, N, M // F_, _lib.ptr(ws), nws, _lib.stream_of(ds2)),
+        "sdfr_film_backward")
+    return dy, dg, db_, dbf
+
+
+def _kp(K: int) -> int:
+    """In features padded to the GEMM's multiple of 4 (zero columns: the product is
+    unchanged)."""
+    return -(-K // 4) * 4
+
+
+def _np_t(K: int) -> int:
+    """Output width of the input-gradient GEMM (B = W^T [K, N]): the kernels take 32,
+    256 or 272 (a multiple of 16), so W^T gets zero rows up to that."""
+    return 32 if K <= 32 else (256 if K <= 256 else 272)
+
+
+def _xk(x: torch.Tensor, K: int) -> torch.Tensor:
+    """x [..., K] as a 16-B aligned [M, _kp(K)] matrix (zero-padded copy when K % 4)."""
+    x2 = x.reshape(-1, K)
+    Kp = _kp(K)
+    return F.pad(x2, (0, Kp - K)) if Kp != K else _a16(x2)
+
+
+def _wk(w: torch.Tensor) -> torch.Tensor:
+    N, K = w.shape
+    Kp = _kp(K)
+    return F.pad(w, (0, Kp - K)) if Kp != K else w.contiguous()
+
+
+def _gx(gy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """gy2 [M, N] . w [N, K] -> [M, K] on the split-fp16 GEMM (B = W^T, zero rows up to
+    _np_t(K))."""
+    K = w.shape[1]
+    Np = _np_t(K)
+    wp = F.pad(w, (0, Np - K)) if Np != K else w.contiguous()
+    out = _gemm(gy2, _pack(wp, True), None, Np)
+    return out[:, :K] if Np != K else out
+
+
+def _gw(gy2: torch.Tensor, x: torch.Tensor, K: int) -> torch.Tensor:
+    """Weight gradient gy2^T . x [N, K] (x [..., K] zero-padded to the kernel's K)."""
+    gw = _wgrad(gy2, _xk(x, K))
+    return gw[:, :K].contiguous() if gw.shape[1] != K else gw
+
+
+def _edge(t):
+    """The autograd node a gradient for t goes to (its AccumulateGrad for a leaf), or
+    None: kept by the forwards so a backward can tell which of its outputs the running
+    backward pass actually uses (_wanted)."""
+    if t is None or not t.requires_grad:
+        return None
+    return get_gradient_edge(t)
+
+
+def _wanted(need: bool, edge) -> bool:
+    """Whether the running backward pass uses this gradient: it may be an
+    autograd.grad over other inputs -- the eikonal term's d sdf / d pts -- whose graph
+    reaches a weight's node without running it (then the GEMM is skipped).  Scoped to
+    the one graph task, unlike a process-global switch."""
+    if not need or edge is None:
+        return need
+    try:
+        return bool(torch._C._will_engine_execute_node(edge.node))
+    except RuntimeError:                   # not inside a backward pass
+        return True
+
+
+def _linear_backward(gy, x, w, has_bias, needs, edges):
+    """Gradients of y = x W^T + b.  Inside a backward that builds a graph
+    (autograd.grad(..., create_graph=True): the SIREN eikonal term) as differentiable
+    ops -- linear() (these kernels again), _WGradF16x3, a sum -- so the eikonal loss
+    reaches the weights through a double backward; otherwise straight on the kernels."""
+    N, K = w.shape
+    lead = x.shape[:-1]
+    nx = needs[0]
+    nw = _wanted(needs[1], edges[0])
+    nb = has_bias and _wanted(needs[2], edges[1])
+    gx = gw = gb = None
+    if torch.is_grad_enabled():
+        gy2 = gy.reshape(-1, N)
+        if nx:
+            gx = linear(gy, w.t())
+        if nw:
+            gw = _WGradF16x3.apply(gy2, x.reshape(-1, K))
+        if nb:
+            gb = gy2.sum(0)
+        return gx, gw, gb
+    gy2 = _a16(gy.reshape(-1, N).contiguous())
+    if nx:
+        gx = _gx(gy2, w).reshape(*lead, K)
+    if nw:
+        gw = _gw(gy2, x, K)
+    if nb:
+        gb = gy2.sum(0)
+    return gx, gw, gb
+
+
 class _LinearF16x3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         N, K = weight.shape
         lead = x.shape[:-1]
-        x2 = _a16(x.reshape(-1, K))
-        w = weight.contiguous()
-        out = _gemm(x2, _pack(w, False), _a16(bias), N)
-        ctx.save_for_backward(x2, w)
+        out = _gemm(_xk(x, K), _pack(_wk(weight), False), _a16(bias), N)
+        ctx.save_for_backward(x, weight)        # the inputs themselves: double backward
         ctx.has_bias = bias is not None
-        ctx.lead = lead
+        ctx.edges = (_edge(weight), _edge(bias))
         return out.view(*lead, N)
 
     @staticmethod
-    @once_differentiable
     def backward(ctx, gy):
-        x2, w = ctx.saved_tensors
-        N, K = w.shape
-        gy2 = _a16(gy.reshape(-1, N))
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = _gemm(gy2, _pack(w, True), None, K).view(*ctx.lead, K)
-        if ctx.needs_input_grad[1]:
-            gw = _wgrad(gy2, x2)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = gy2.sum(0)
-        return gx, gw, gb
+        x, w = ctx.saved_tensors
+        return _linear_backward(gy, x, w, ctx.has_bias, ctx.needs_input_grad, ctx.edges)
+
+
+class _LinearGiven(torch.autograd.Function):
+    """y = x W^T + b whose value the caller already has (the fused FiLM forward saved
+    it): returns y, differentiates as the linear layer.  The FiLM double backward uses
+    it to put y on the graph without recomputing the GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, y):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        ctx.edges = (_edge(weight), _edge(bias))
+        return y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        return (*_linear_backward(gy, x, w, ctx.has_bias, ctx.needs_input_grad, ctx.edges), None)
+
+
+class _WGradF16x3(torch.autograd.Function):
+    """gw = gy^T x [N, K] (the weight gradient) as a differentiable op: its own
+    backward is two linear() products, so a graph built through a linear backward
+    (create_graph) can be differentiated again."""
+
+    @staticmethod
+    def forward(ctx, gy2, x2):
+        K = x2.shape[1]
+        ctx.save_for_backward(gy2, x2)
+        ctx.edges = (_edge(gy2), _edge(x2))
+        return _gw(_a16(gy2.contiguous()), x2, K)
+
+    @staticmethod
+    def backward(ctx, G):
+        gy2, x2 = ctx.saved_tensors
+        dgy = dx = None
+        if _wanted(ctx.needs_input_grad[0], ctx.edges[0]):
+            dgy = linear(x2, G)                 # d/dgy [m, n] = sum_k G[n, k] x[m, k]
+        if _wanted(ctx.needs_input_grad[1], ctx.edges[1]):
+            dx = linear(gy2, G.t())             # d/dx [m, k] = sum_n G[n, k] gy[m, n]
+        return dgy, dx
 
 
 class _FiLMLinearF16x3(torch.autograd.Function):
@@ -131,49 +289,77 @@ class _FiLMLinearF16x3(torch.autograd.Function):
         N, K = weight.shape
         F_ = gamma.shape[0]
         lead = x.shape[:-1]
-        x2 = _a16(x.reshape(-1, K))
-        M = x2.shape[0]
-        w = weight.contiguous()
         g2, b2 = _a16(gamma.reshape(F_, N)), _a16(beta.reshape(F_, N))
-        out = torch.empty(M, N, device=x.device, dtype=torch.float32)
-        y = torch.empty(M, N, device=x.device, dtype=torch.float32)
-        _lib.check(_lib.lib().sdfr_film_linear_f16x3(
-            _lib.ptr(out), _lib.ptr(y), _lib.ptr(x2), _lib.ptr(_pack(w, False)),
-            _lib.ptr(_a16(bias)), _lib.ptr(g2),
-            _lib.ptr(b2), M, N, K, M // F_, _lib.stream_of(x2)), "sdfr_film_linear_f16x3")
-        ctx.save_for_backward(x2, w, y, g2, b2)
-        ctx.meta = (lead, bias is not None, gamma.shape, beta.shape)
+        out, y = _film_fwd(_xk(x, K), _pack(_wk(weight), False), _a16(bias), g2, b2, N)
+        ctx.save_for_backward(x, weight, bias, gamma, beta, y)
+        ctx.meta = (lead, bias is not None)
+        ctx.edges = (_edge(weight), _edge(bias), _edge(gamma), _edge(beta))
         return out.view(*lead, N)
 
     @staticmethod
-    @once_differentiable
     def backward(ctx, ds):
-        x2, w, y, g2, b2 = ctx.saved_tensors
-        lead, has_bias, gshape, bshape = ctx.meta
+        x, w, bias, gamma, beta, y = ctx.saved_tensors
+        lead, has_bias = ctx.meta
         N, K = w.shape
-        M, F_ = x2.shape[0], g2.shape[0]
-        ds2 = _a16(ds.reshape(-1, N))
-        L = _lib.lib()
-        dy = torch.empty(M, N, device=ds.device, dtype=torch.float32)
-        dg = torch.empty(F_, N, device=ds.device, dtype=torch.float32)
-        db_ = torch.empty(F_, N, device=ds.device, dtype=torch.float32)
-        dbf = torch.empty(F_, N, device=ds.device, dtype=torch.float32)
-        nws = L.sdfr_film_backward_ws_bytes(M, N, M // F_)
-        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=ds.device)
-        _lib.check(L.sdfr_film_backward(
-            _lib.ptr(dy), _lib.ptr(dg), _lib.ptr(db_), _lib.ptr(dbf), _lib.ptr(ds2), _lib.ptr(y),
-            _lib.ptr(g2), _lib.ptr(b2), M, N, M // F_, _lib.ptr(ws), nws, _lib.stream_of(ds2)),
-            "sdfr_film_backward")
+        F_ = gamma.shape[0]
+        nx = ctx.needs_input_grad[0]
+        nw = _wanted(ctx.needs_input_grad[1], ctx.edges[0])
+        nb = has_bias and _wanted(ctx.needs_input_grad[2], ctx.edges[1])
+        ng = _wanted(ctx.needs_input_grad[3], ctx.edges[2])
+        nbe = _wanted(ctx.needs_input_grad[4], ctx.edges[3])
+        if torch.is_grad_enabled():
+            # create_graph (the SIREN eikonal term): the same gradients as differentiable
+            # ops, y put on the graph as the linear layer's output (_LinearGiven)
+            yl = _LinearGiven.apply(x, w, bias, y.view(*lead, N))
+            du = ds * torch.cos(gamma * yl + beta)
+            dyl = du * gamma
+            red = tuple(range(1, du.dim() - 1))
+            gx, gw, gb = _linear_backward(dyl, x, w, has_bias, (nx, nw, nb),
+                                          (None, None))
+            gg = (du * yl).sum(red, keepdim=True).view(gamma.shape) if ng else None
+            gbt = du.sum(red, keepdim=True).view(beta.shape) if nbe else None
+            return gx, gw, gb, gg, gbt
+        ds2 = _a16(ds.reshape(-1, N).contiguous())
+        g2, b2 = _a16(gamma.reshape(F_, N)), _a16(beta.reshape(F_, N))
+        dy, dg, db_, dbf = _film_bwd(ds2, y, g2, b2)
         gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = _gemm(dy, _pack(w, True), None, K).view(*lead, K)
-        if ctx.needs_input_grad[1]:
-            gw = _wgrad(dy, x2)
-        if has_bias and ctx.needs_input_grad[2]:
+        if nx:
+            gx = _gx(dy, w).reshape(*lead, K)
+        if nw:
+            gw = _gw(dy, x, K)
+        if nb:
             gb = dbf.sum(0)
-        gg = dg.view(gshape) if ctx.needs_input_grad[3] else None
-        gbt = db_.view(bshape) if ctx.needs_input_grad[4] else None
+        gg = dg.view(gamma.shape) if ng else None
+        gbt = db_.view(beta.shape) if nbe else None
         return gx, gw, gb, gg, gbt
+
+
+def _head_fwd(x2, w, bias):
+    """x2 [M,K] . w [J,K]^T (+ bias) on the narrow-head kernel."""
+    M, K = x2.shape
+    J = w.shape[0]
+    out = torch.empty(M, J, device=x2.device, dtype=torch.float32)
+    _lib.check(_lib.lib().sdfr_linear_head_forward(
+        _lib.ptr(out), _lib.ptr(x2), _lib.ptr(w), _lib.ptr(bias.contiguous() if bias is not None
+                                                           else None),
+        M, J, K, _lib.stream_of(x2)), "sdfr_linear_head_forward")
+    return out
+
+
+def _head_bwd(gy2, x2, w, need_x, need_w, need_b):
+    """(gx [M,K], gw [J,K], gb [J]) of the narrow head, each None unless needed."""
+    M, K = x2.shape
+    J = w.shape[0]
+    L = _lib.lib()
+    gx = torch.empty(M, K, device=gy2.device, dtype=torch.float32) if need_x else None
+    gw = torch.empty(J, K, device=gy2.device, dtype=torch.float32) if need_w else None
+    gb = torch.empty(J, device=gy2.device, dtype=torch.float32) if need_b else None
+    nws = L.sdfr_linear_head_ws_bytes(M, J, K) if (need_w or need_b) else 0
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=gy2.device)
+    _lib.check(L.sdfr_linear_head_backward(
+        _lib.ptr(gx), _lib.ptr(gw), _lib.ptr(gb), _lib.ptr(gy2), _lib.ptr(x2), _lib.ptr(w),
+        M, J, K, _lib.ptr(ws), nws, _lib.stream_of(gy2)), "sdfr_linear_head_backward")
+    return gx, gw, gb
 
 
 class _LinearHead(torch.autograd.Function):
@@ -183,38 +369,30 @@ class _LinearHead(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         J, K = weight.shape
         lead = x.shape[:-1]
-        x2 = _a16(x.reshape(-1, K))
-        w = _a16(weight)
-        M = x2.shape[0]
-        out = torch.empty(M, J, device=x.device, dtype=torch.float32)
-        _lib.check(_lib.lib().sdfr_linear_head_forward(
-            _lib.ptr(out), _lib.ptr(x2), _lib.ptr(w), _lib.ptr(bias.contiguous() if bias is not None
-                                                               else None),
-            M, J, K, _lib.stream_of(x2)), "sdfr_linear_head_forward")
-        ctx.save_for_backward(x2, w)
+        out = _head_fwd(_a16(x.reshape(-1, K)), _a16(weight), bias)
+        ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        ctx.lead = lead
+        ctx.edges = (_edge(weight), _edge(bias))
         return out.view(*lead, J)
 
     @staticmethod
-    @once_differentiable
     def backward(ctx, gy):
-        x2, w = ctx.saved_tensors
-        J, K = w.shape
-        M = x2.shape[0]
-        gy2 = gy.reshape(-1, J).contiguous()
-        L = _lib.lib()
-        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        need_b = ctx.has_bias and ctx.needs_input_grad[2]
-        gx = torch.empty(M, K, device=gy.device, dtype=torch.float32) if need_x else None
-        gw = torch.empty(J, K, device=gy.device, dtype=torch.float32) if need_w else None
-        gb = torch.empty(J, device=gy.device, dtype=torch.float32) if need_b else None
-        nws = L.sdfr_linear_head_ws_bytes(M, J, K) if (need_w or need_b) else 0
-        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=gy.device)
-        _lib.check(L.sdfr_linear_head_backward(
-            _lib.ptr(gx), _lib.ptr(gw), _lib.ptr(gb), _lib.ptr(gy2), _lib.ptr(x2), _lib.ptr(w),
-            M, J, K, _lib.ptr(ws), nws, _lib.stream_of(gy2)), "sdfr_linear_head_backward")
-        return (gx.view(*ctx.lead, K) if gx is not None else None), gw, gb
+        x, weight = ctx.saved_tensors
+        J, K = weight.shape
+        lead = x.shape[:-1]
+        need_x = ctx.needs_input_grad[0]
+        need_w = _wanted(ctx.needs_input_grad[1], ctx.edges[0])
+        need_b = ctx.has_bias and _wanted(ctx.needs_input_grad[2], ctx.edges[1])
+        if torch.is_grad_enabled():
+            # create_graph (the SIREN eikonal term runs through sigma_linear): differentiable
+            gy2 = gy.reshape(-1, J)
+            gx = linear(gy, weight.t()) if need_x else None
+            gw = gy2.t().mm(x.reshape(-1, K)) if need_w else None
+            gb = gy2.sum(0) if need_b else None
+            return gx, gw, gb
+        gx, gw, gb = _head_bwd(gy.reshape(-1, J).contiguous(), _a16(x.reshape(-1, K)),
+                               _a16(weight), need_x, need_w, need_b)
+        return (gx.view(*lead, K) if gx is not None else None), gw, gb
 
 
 def film_linear(x, weight, bias, gamma, beta, kernels=True):
@@ -230,19 +408,25 @@ def film_linear(x, weight, bias, gamma, beta, kernels=True):
     return torch.sin(gamma * linear(x, weight, bias, kernels) + beta)
 
 
+def _on_device(x: torch.Tensor) -> bool:
+    return x.is_cuda
+
+
 def _routable(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    if _MODE["gemm"] != "f16x3" or not x.is_cuda or not torch.is_grad_enabled():
+    if _MODE["gemm"] != "f16x3" or not _on_device(x) or not torch.is_grad_enabled():
         return False
     if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() < 2:
         return False
     N, K = weight.shape
-    if N != 256 or K % 4 or not (K <= 32 or K == 256 or 256 < K <= 288):
+    # in features padded to a multiple of 4 (forward) and the input gradient's output
+    # to 32 / 256 / 272 (_np_t): the shapes both directions take
+    if N != 256 or not (K <= 32 or K == 256 or 256 < K <= 272):
         return False
     return x.numel() // K >= 1024            # the per-face gamma / beta layers stay on F.linear
 
 
 def _head_routable(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    if _MODE["gemm"] != "f16x3" or not x.is_cuda or not torch.is_grad_enabled():
+    if _MODE["gemm"] != "f16x3" or not _on_device(x) or not torch.is_grad_enabled():
         return False
     if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() < 2:
         return False

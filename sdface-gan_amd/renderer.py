@@ -27,7 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .encoders import GridEncoder, SHEncoder, input_grad_only
+from .encoders import GridEncoder, SHEncoder
 from .linear import film_linear, linear
 
 
@@ -54,7 +54,7 @@ class LinearLayer(nn.Module):
         self.bias_init = bias_init
         self.std_init = std_init
 
-    # the ngp network's layers take the training kernels (linear.py); others F.linear
+    # the renderer networks' layers take the training kernels (linear.py); others F.linear
     train_kernels = False
     skip_identity = True          # False: the reference's literal 1 * y + 0 (A/B aid)
 
@@ -74,7 +74,7 @@ class LinearLayer(nn.Module):
 class FiLMSiren(nn.Module):
     """``sin(gamma(style) * (x W^T + b) + beta(style))`` (sdf_model.py:44-69)."""
 
-    train_kernels = False         # set by NGPSIRENGenerator (linear.py)
+    train_kernels = False         # set by NGPSIRENGenerator / SirenGenerator (linear.py)
 
     def __init__(self, in_channel, out_channel, style_dim, is_first=False):
         super().__init__()
@@ -121,6 +121,10 @@ class SirenGenerator(nn.Module):
         self.views_linears = FiLMSiren(input_ch_views + W, W, style_dim=style_dim)
         self.rgb_linear = LinearLayer(W, 3, freq_init=True)
         self.sigma_linear = LinearLayer(W, 1, freq_init=True)
+        # training GEMMs on the split-fp16 kernels, double-differentiable (the eikonal
+        # loss reaches these weights through autograd.grad(create_graph=True), linear.py)
+        for m in [*self.pts_linears, self.views_linears, self.rgb_linear, self.sigma_linear]:
+            m.train_kernels = True
 
     def forward(self, x, styles):
         pts, views = torch.split(x, [self.input_ch, self.input_ch_views], dim=-1)
@@ -351,10 +355,10 @@ class VolumeFeatureRenderer(nn.Module):
         return rays_o, rays_d, viewdirs
 
     def get_eikonal_term(self, pts, sdf):
-        # only d sdf / d pts is returned: the grid encoder skips its table gradient
-        with input_grad_only():
-            return autograd.grad(outputs=sdf, inputs=pts, grad_outputs=torch.ones_like(sdf),
-                                 create_graph=True)[0]
+        # only d sdf / d pts is returned: the grid encoder and the training GEMMs skip
+        # the gradients this pass does not use (linear._wanted)
+        return autograd.grad(outputs=sdf, inputs=pts, grad_outputs=torch.ones_like(sdf),
+                             create_graph=True)[0]
 
     def sdf_activation(self, input):
         return torch.sigmoid(input / self.sigmoid_beta) / self.sigmoid_beta

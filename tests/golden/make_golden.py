@@ -473,6 +473,43 @@ def case_eikonal(sdf_model, sdf_utils):
     print("eikonal.npz", tuple(eik.shape), "eik requires_grad:", eik.requires_grad)
 
 
+def case_eikonal_siren(sdf_model, sdf_utils):
+    """Stage-1 forward of the SIREN network (rendering.type 'sdf', configs[4]) with
+    return_eikonal: here the eikonal term d sdf / d pts (sdf_model.py:224-229) is an
+    autograd.grad(create_graph=True) through the FiLM MLP itself (:101-139), so the
+    eikonal loss reaches every pts_linears parameter through a double backward.  The
+    gradients of thumb + surface + eikonal loss (training_utils.py:396-451) are kept
+    for layers on every path: first, middle and last FiLM layers (weight, bias and
+    the gamma / beta style layers), the views layer and both heads."""
+    res, N, B = 8, 24, 2
+    g, opt = _stage1_generator(sdf_model, sdf_utils, res, N, type="sdf")
+    ext, focal, near, far, vp = _cams(sdf_utils, B, res, 191)
+    torch.manual_seed(192)
+    z = torch.randn(B, 256)
+    torch.manual_seed(193)
+    with _RandRecorder() as rr:
+        _, thumb, sdf, eik = g([z], ext, focal, near, far, return_sdf=True,
+                               return_eikonal=True)
+    eik_loss = ((eik.norm(dim=-1) - 1) ** 2).mean()
+    surf = torch.exp(-100 * torch.abs(sdf)).mean()
+    loss = thumb.mean() + surf + 0.1 * eik_loss
+    loss.backward()
+    net = g.renderer.network
+    grads = {}
+    for name, prm in net.named_parameters():
+        if any(name.startswith(p) for p in ("pts_linears.0.", "pts_linears.3.", "pts_linears.7.",
+                                            "views_linears.", "sigma_linear.", "rgb_linear.")):
+            grads["grad__" + name.replace(".", "__")] = _t2n(prm.grad)
+    np.savez_compressed(
+        OUT / "eikonal_siren.npz", z=_t2n(z), ext=_t2n(ext), focal=_t2n(focal), near=_t2n(near),
+        far=_t2n(far), t_rand=_t2n(rr.draws[0]), thumb=_t2n(thumb), sdf=_t2n(sdf),
+        eikonal=_t2n(eik), eik_requires_grad=np.bool_(eik.requires_grad),
+        eik_loss=np.float64(eik_loss.item()), grad_beta=_t2n(g.renderer.sigmoid_beta.grad),
+        res=np.int64(res), n_samples=np.int64(N), **grads)
+    print("eikonal_siren.npz", tuple(eik.shape), "eik requires_grad:", eik.requires_grad,
+          len(grads), "gradients")
+
+
 def case_init_pass(sdf_model, sdf_utils):
     """Sphere initialisation (training_utils.py:287-317): Generator.init_forward ->
     mlp_init_pass (sdf_model.py:380-409, 1156-1161) with its stratified torch.rand
@@ -588,6 +625,7 @@ def main():
     case_siren(sdf_model, sdf_utils)
     case_table_scales(sdf_model, sdf_utils)
     case_eikonal(sdf_model, sdf_utils)
+    case_eikonal_siren(sdf_model, sdf_utils)
     case_init_pass(sdf_model, sdf_utils)
     case_fc(sdf_model, sdf_utils)
 

@@ -52,7 +52,7 @@ def _stage1_generator(sdfr, golden_dir, g, kind="ngp"):
     gen = sdfr.Generator(opt.model, opt.rendering, full_pipeline=False)
     own = gen.state_dict()
     sd = W.det_state_dict(W.golden_entries(golden_dir, kind=kind), "",
-                          table_amp=float(g["table_amp"]))
+                          table_amp=float(g["table_amp"]) if "table_amp" in g.files else 1.0)
     sd = {k: v for k, v in sd.items() if k in own}
     assert set(sd) == set(own)
     gen.load_state_dict(sd, strict=True)
@@ -133,3 +133,43 @@ def test_fc_generator_vs_reference(sdfr, golden_dir):
                                            t_rand=torch.from_numpy(g["t_rand"]))
     for k, v in dict(rgb=rgb, features=feat, sdf=sdf, xyz=xyz, mask=mask).items():
         _rel(f"fc_{k}", v.cpu(), g[k], 2e-5)
+
+
+@pytest.mark.parametrize("gemm", ["f16x3", "torch"])
+def test_siren_eikonal_double_backward_vs_reference(sdfr, golden_dir, gemm):
+    """configs[4]'s stage 1 on the SIREN network (rendering.type 'sdf'): the eikonal term
+    is autograd.grad(sdf, pts, create_graph=True) through the FiLM MLP
+    (sdf_model.py:224-229, 101-139), so thumb + surface + eikonal loss reach every MLP
+    parameter, the eikonal part through a double backward.  gemm='f16x3': every MLP
+    GEMM on the HIP training kernels (linear.py: split-fp16 forward, input- and
+    weight-gradient GEMMs, fused FiLM, narrow heads, and their differentiable
+    restatements under create_graph); 'torch': the same module path on rocBLAS.
+    Fixture: the reference's own CPU computation (make_golden.case_eikonal_siren)."""
+    from sdface_gan_amd import linear
+    g = np.load(golden_dir / "eikonal_siren.npz")
+    prev = linear.train_gemm()
+    linear.set_train_gemm(gemm)
+    try:
+        gen = _stage1_generator(sdfr, golden_dir, g, kind="siren")
+        _, thumb, sdf, eik = gen([_t(g, "z")], _t(g, "ext"), _t(g, "focal"), _t(g, "near"),
+                                 _t(g, "far"), return_sdf=True, return_eikonal=True,
+                                 t_rand=torch.from_numpy(g["t_rand"]))
+        assert eik.requires_grad == bool(g["eik_requires_grad"]) is True
+        eik_loss = ((eik.norm(dim=-1) - 1) ** 2).mean()
+        loss = thumb.mean() + torch.exp(-100 * torch.abs(sdf)).mean() + 0.1 * eik_loss
+        loss.backward()
+    finally:
+        linear.set_train_gemm(prev)
+    tag = f"siren_eik_{gemm}"
+    _rel(f"{tag}_thumb", thumb.detach().cpu(), g["thumb"], 2e-5)
+    _rel(f"{tag}_sdf", sdf.detach().cpu(), g["sdf"], 2e-5)
+    _rel(f"{tag}_term", eik.detach().cpu(), g["eikonal"], 1e-4)
+    np.testing.assert_allclose(eik_loss.item(), float(g["eik_loss"]), rtol=1e-4)
+    net = gen.renderer.network
+    params = dict(net.named_parameters())
+    keys = [k for k in g.files if k.startswith("grad__")]
+    assert len(keys) == 28
+    for k in keys:
+        name = k[len("grad__"):].replace("__", ".")
+        _rel(f"{tag}_{name}", params[name].grad.cpu(), g[k], 2e-4)
+    _rel(f"{tag}_grad_beta", gen.renderer.sigmoid_beta.grad.cpu(), g["grad_beta"], 3e-4)

@@ -145,9 +145,9 @@ def test_bench_multi_rank_timing_world2():
 # one g_backward with perturb 0, every gradient equals a single process's on the
 # concatenated batch (discriminator: equal; generator: x 1/2, per-chunk losses summed
 # over 2x the chunks) -- training_utils.py:346-440, sdf_utils.py:344-379.
-def _ngp_stage1_opt(sdfr):
+def _ngp_stage1_opt(sdfr, ngp=True):
     from tests.test_train_renderer import stage1_opt
-    opt = stage1_opt(sdfr, ngp=True, res=16, samples=8, batch=2, chunk=1)
+    opt = stage1_opt(sdfr, ngp=ngp, res=16, samples=8, batch=2, chunk=1)
     opt.rendering.perturb = 0
     return opt
 
@@ -183,7 +183,7 @@ def _ngp_grads(tr, noise, cams, real, chunks):
     return d, g
 
 
-def _ngp_grad_worker(rank, world, port, out_dir):
+def _ngp_grad_worker(rank, world, port, out_dir, ngp=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -192,7 +192,7 @@ def _ngp_grad_worker(rank, world, port, out_dir):
     sdfr = load()
     from sdface_gan_amd.training import RendererTrainer
     from tests.test_train_renderer import _stage1_inputs
-    opt = _ngp_stage1_opt(sdfr)
+    opt = _ngp_stage1_opt(sdfr, ngp)
     tr = RendererTrainer(opt, DEV, seed=5)
     _chunk_seeded_smoothness()
     d, g = _ngp_grads(tr, *_stage1_inputs(sdfr, opt, rank))
@@ -200,11 +200,14 @@ def _ngp_grad_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_ngp_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path):
+@pytest.mark.parametrize("ngp", [True, False], ids=["ngp", "siren"])
+def test_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path, ngp):
+    """configs[2] (ngp) and configs[4] (SIREN, ngp=0: the eikonal loss reaches the MLP
+    through the double backward on the HIP training GEMMs)."""
     from sdface_gan_amd.training import RendererTrainer
     from tests.test_train_renderer import _stage1_inputs
-    mp.spawn(_ngp_grad_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    opt = _ngp_stage1_opt(sdfr)
+    mp.spawn(_ngp_grad_worker, args=(2, _free_port(), str(tmp_path), ngp), nprocs=2, join=True)
+    opt = _ngp_stage1_opt(sdfr, ngp)
     ins = [_stage1_inputs(sdfr, opt, r) for r in (0, 1)]
     noise = [torch.cat([ins[0][0][0], ins[1][0][0]])]
     cams = tuple(torch.cat([a, b]) for a, b in zip(ins[0][1], ins[1][1]))
@@ -219,7 +222,10 @@ def test_ngp_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path):
     finally:
         training.smoothness = orig
     table = "renderer.network.encoder.embeddings"
-    assert table in g and float(g[table].abs().max()) > 0
+    if ngp:
+        assert table in g and float(g[table].abs().max()) > 0
+    else:
+        assert float(g["renderer.network.pts_linears.3.weight"].abs().max()) > 0
     for rank in (0, 1):
         r = torch.load(tmp_path / f"ngp_grad{rank}.pt", weights_only=True)
         for what, got, ref, scale in (("discriminator", r["d"], d, 1.0),
@@ -232,6 +238,8 @@ def test_ngp_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path):
                 tol = 2e-5 * max(1e-6, float(want.abs().max()))
                 assert torch.allclose(v, want, rtol=2e-4, atol=tol), \
                     f"{what} {k}: max |diff| {float((v - want).abs().max()):.3e}"
+        if not ngp:
+            continue
         # the hashed levels (5-15) carry most of the table's gradient rows
         off = int(tr.g_module.renderer.network.encoder.offsets[5])
         hashed = r["g"][table][off:]
