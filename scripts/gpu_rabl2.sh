@@ -1,0 +1,16 @@
+#!/bin/bash
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$(pwd)
+V="rbase rnoaread rnoside rnotail rnodma rmfma"
+ARGS=""
+for v in $V; do ARGS="$ARGS sdface-gan_amd/lib_var/$v/libsdfr.so@r"; done
+REPS=3 timeout -k 10 500 python scripts/field_time.py $ARGS > gpurun_out/ft_rabl2.log 2>&1
+rc=$?; echo "ft rc=$rc"; grep SUMMARY gpurun_out/ft_rabl2.log
+[ $rc -eq 0 ] || exit $rc
+for v in $V; do
+  SDFR_FIELD_KERNEL=r SDFR_LIB=$R/sdface-gan_amd/lib_var/$v/libsdfr.so timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --kernel-include-regex "field_r_kernel" --output-format csv \
+      -d "$R/gpurun_out/pmc_abl2_$v" -o "c" -- python3 "$R/scripts/render_only.py" f16x3 > "gpurun_out/pmc_abl2_$v.log" 2>&1
+  rc=$?; echo "pmc $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done

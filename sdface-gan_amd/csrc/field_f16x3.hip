@@ -101,6 +101,48 @@ __device__ __forceinline__ int xperm_k(int l, uint32_t q, uint32_t g, uint32_t j
     return (int)(16 * (2 * q + (j >> 2)) + 4 * g + (j & 3));
 }
 
+constexpr int kRWaves = 4;
+constexpr int kRThreads = kRWaves * 64;
+constexpr uint32_t kRTiles = 4;          // 16-ray tiles per workgroup (one per wave)
+constexpr uint32_t kRSamples = 2;        // samples of a ray per pass
+constexpr uint32_t kRSliceF4 = 1024;     // 16 KB: one k-step's [8 tiles][hi, lo][64 lanes]
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f16v mfma32(f4 a, f4 b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(a), as_h8(b), c, 0, 0, 0);
+}
+
+template <class Net>
+struct RNet {
+    static constexpr int kL0 = Net::kSiren ? 1 : 2;                // layer-0 k-steps (K 3 / 32)
+    static constexpr int kSteps = kL0 + 16 * Net::kHidden + 17;    // k-steps (slices) per pass
+    static constexpr int kViews = kL0 + 16 * Net::kHidden;         // first views k-step
+    static_assert(kSteps <= (int)Net::kSlices, "R slices fit the packed region");
+};
+
+template <class Net>
+__host__ __device__ constexpr uint32_t rslice_base(int l) {
+    return l == 0 ? 0u
+                  : (uint32_t)RNet<Net>::kL0 + 16u * (l == Net::kLayers - 1 ? Net::kHidden : l - 1);
+}
+
+// K index (within layer l's input) of element j of lane half h in the layer's k-step s
+// (-1 = zero pad)
+template <class Net>
+__device__ __forceinline__ int rperm_k(int l, uint32_t s, uint32_t h, uint32_t j) {
+    const uint32_t e = 8 * h + j;
+    if (l == 0) {
+        if constexpr (Net::kSiren) return e < 3 ? (int)e : -1;   // xyz
+        return (int)(16 * s + e);                               // 32 grid features
+    }
+    if (l == Net::kLayers - 1 && s == 16) {
+        if constexpr (Net::kSiren) return e < 3 ? (int)(kW + e) : -1;   // viewdir
+        return (int)(kW + e);                                           // SH 0-15
+    }
+    return (int)(32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3));
+}
+
 __device__ __forceinline__ void xpin(f4 &x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void xpin(float &x) { asm volatile("" : "+v"(x)); }
 
@@ -165,7 +207,36 @@ struct XPrepArgs {
     float *film;                   // [B][films][2][256]
     f4 *packed;                    // [slices][8][2][64] fp16x8
     uint32_t B;
+    int rlayout;                   // 1: field_r_kernel's slices (32-row tiles, K steps of 16)
 };
+
+// field_r_kernel's packing (xprep_kernel with rlayout): slice = one k-step of 16 K,
+// [8 tiles of 32 rows][hi, lo][64 lanes], lane l holding W[32 T + (l & 31)][k] for
+// k = rperm_k(layer, s, l >> 5, 0..7)
+template <class Net>
+__device__ __forceinline__ void r_pack(const XPrepArgs &a, uint32_t e) {
+    const uint32_t slice = e / 512, rem = e % 512;
+    if (slice >= (uint32_t)RNet<Net>::kSteps) return;
+    const uint32_t t8 = rem >> 6, lane = rem & 63;
+    int layer = 0;
+    if (slice >= rslice_base<Net>(Net::kLayers - 1)) layer = Net::kLayers - 1;
+    else if (slice >= (uint32_t)RNet<Net>::kL0) layer = 1 + (slice - RNet<Net>::kL0) / 16;
+    const uint32_t s = slice - rslice_base<Net>(layer);
+    const uint32_t row = 32 * t8 + (lane & 31), h = lane >> 5;
+    const uint32_t K = Net::K(layer);
+    const float sc = a.su[layer * kW + row];
+    float v[8];
+#pragma unroll
+    for (uint32_t jj = 0; jj < 8; ++jj) {
+        const int k = rperm_k<Net>(layer, s, h, jj);
+        v[jj] = k < 0 ? 0.0f : __fmul_rn(a.w[layer][(size_t)row * K + k], sc);
+    }
+    f4 hi, lo;
+    split8(v, hi, lo);
+    f4 *dst = a.packed + (size_t)slice * kRSliceF4 + t8 * 128 + lane;
+    dst[0] = hi;
+    dst[64] = lo;
+}
 
 // blocks [0, B*films*2*256/4): FiLM rows, one wave per output row (lanes over K,
 // butterfly sum); then packing, one (slice, t8, lane) per thread
@@ -213,6 +284,10 @@ __global__ void __launch_bounds__(256) xprep_kernel(const XPrepArgs a) {
     }
     const uint32_t e = (blk - nfilm) * 256 + j;
     if (e >= Net::kSlices * 512) return;
+    if (a.rlayout) {
+        r_pack<Net>(a, e);
+        return;
+    }
     const uint32_t slice = e / 512, rem = e % 512;
     const uint32_t t8 = rem >> 6, lane = rem & 63;
     int layer = 0;
@@ -937,6 +1012,1207 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
     }
 }
 
+// ----------------------------------------------------------------------------
+// field_q_kernel: one wave per SIMD, every wave over all 256 output rows.
+//
+// field_p_kernel's wave pairs (two waves per SIMD, 256 VGPRs each) split the rows of
+// every layer, so each layer's input crossed between the waves through LDS (exchange
+// writes + B-fragment reads + a pair barrier per k-step) and the register budget left
+// the compiler no room to issue the A-fragment reads more than ~2 MFMAs ahead of their
+// use (the ablation that removed 3 of 4 A reads ran 41 % faster).  Here a workgroup is
+// 4 waves, one per SIMD (512 VGPRs), each over 32 samples (8 rays x 4 consecutive
+// samples, the pair's two MFMA blocks) and ALL 16 output tiles of a layer: the layer
+// output's accumulators are, activated and split in place, the next layer's B fragments
+// (no LDS exchange, no B reads), and the A fragments of a group of 2 tiles are read
+// two groups (24 MFMAs) ahead.  Per k-step and wave: 96 MFMAs, 32 A ds_read_b128, 8
+// LDS-DMA pieces of the weight ring (16 KB half-slices, 4 slots, one barrier per k-step
+// ahead of group 6 of 8).  The per-ray feature, colour and position sums are per-lane
+// partials over the lane's own two samples of each pass (lanes n and n+8 of a ray hold
+// samples {0,2} and {1,3}), added once per ray at the end.
+constexpr int kQWaves = 4;
+constexpr int kQThreads = kQWaves * 64;
+constexpr uint32_t kQDma = 4;            // 1 KB LDS-DMA pieces per wave per half-slice
+#ifndef SDFR_QVALU
+#define SDFR_QVALU 3
+#endif
+constexpr int kQValuPerMfma = SDFR_QVALU;  // VALU slots after each MFMA of a group
+#ifndef SDFR_RVALU
+#define SDFR_RVALU 5
+#endif
+constexpr int kRValuPerMfma = SDFR_RVALU;  // field_r_kernel: VALU slots after each MFMA
+#ifndef SDFR_RDS
+#define SDFR_RDS 2
+#endif
+constexpr int kRDsPerMfma = SDFR_RDS;      // field_r_kernel: LDS-read slots after each MFMA
+
+struct QRing {
+    f4 *lds;          // weight ring: 4 half-slice slots of kXSliceF4
+    v4i drsrc;
+    uint32_t tid, wave;
+    f4 na[2][4];      // the next k-step's groups 0 and 1 A fragments
+};
+
+// this wave's 4 pieces of half-slice SLICE -> ring slot SLOT: M0 and soffset set once, the
+// pieces at instruction offsets 0..3 KB (applied to the global and the LDS address alike)
+template <uint32_t SLICE, uint32_t SLOT>
+__device__ __forceinline__ void q_dma(const QRing &R) {
+    const uint32_t sbase = R.wave * (kQDma * 1024u);
+    const uint32_t lbase = lds_addr(R.lds) + sbase;
+    const uint32_t voff = (R.tid & 63u) * 16u;
+    uint32_t keep, so;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_add_u32 m0, %4, %6\n\ts_add_u32 %1, %5, %7\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %3, %1 offen lds\n\t"
+        "buffer_load_dwordx4 %2, %3, %1 offen offset:1024 lds\n\t"
+        "buffer_load_dwordx4 %2, %3, %1 offen offset:2048 lds\n\t"
+        "buffer_load_dwordx4 %2, %3, %1 offen offset:3072 lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep), "=&s"(so)
+        : "v"(voff), "s"(R.drsrc), "s"(lbase), "s"(sbase),
+          "i"(SLOT * kXSliceF4 * 16u), "i"(SLICE * kXSliceF4 * 16u)
+        : "memory", "scc");
+}
+
+// One k-step of one wave: 16 output tiles x 2 sample blocks x 3 split terms = 96 MFMAs in
+// 8 groups of 2 tiles.  Global tile T of k-step KS is at ring slot 2 (KS & 1) + (T >> 3),
+// position T & 7.  Group gi's A fragments were read during group gi - 2 (groups 0, 1: by
+// the previous k-step, R.na); this wave's 8 DMA pieces of the next k-step go out (4 per statement) in groups
+// 0 and 2 into the slots of the previous k-step (free since its barrier); the barrier (own
+// DMA landed, own A reads of this k-step done) sits ahead of group 6, behind it the next
+// k-step's groups 0, 1 A fragments are read.  side(gi) runs after group gi.
+template <class Net, int KS, bool ZC, class Side>
+__device__ __forceinline__ void qstep(QRing &R, f4 (&acc)[32], const f4 (&bf)[4], Side &&side) {
+    constexpr f4 kZ = {0.0f, 0.0f, 0.0f, 0.0f};
+    constexpr int KN = (KS + 1) % PNet<Net>::kSteps;
+    const uint32_t lane = R.tid & 63u;
+    const f4 *A = R.lds + 2 * (KS & 1) * kXSliceF4 + lane;
+    const f4 *An = R.lds + 2 * (KN & 1) * kXSliceF4 + lane;
+    auto aoff = [](int T, int hl) { return (T >> 3) * (int)kXSliceF4 + (T & 7) * 128 + hl * 64; };
+    f4 a[8][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        a[0][i] = R.na[0][i];
+        a[1][i] = R.na[1][i];
+    }
+    sfor<0, 8>([&](auto GI) {
+        constexpr int gi = decltype(GI)::value;
+        if constexpr (gi == 0 || gi == 2) {
+            constexpr uint32_t hs = gi >> 1;
+            q_dma<2 * KN + hs, 2 * (KN & 1) + hs>(R);
+        }
+        if constexpr (gi == 6) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (gi + 2 < 8) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[gi + 2][i] = A[aoff(2 * (gi + 2) + (i >> 1), i & 1)];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) R.na[gi - 6][i] = An[aoff(2 * (gi - 6) + (i >> 1), i & 1)];
+        }
+        // the side work (activations, compositing) goes between this group's MFMAs
+        side(GI);
+        constexpr int t0 = 2 * gi, t1 = t0 + 1;
+        const f4 *ag = a[gi];
+        // per accumulator: W_lo x_hi, W_hi x_lo, W_hi x_hi
+        acc[2 * t0] = mfma16(ag[1], bf[0], ZC ? kZ : acc[2 * t0]);
+        acc[2 * t0 + 1] = mfma16(ag[1], bf[2], ZC ? kZ : acc[2 * t0 + 1]);
+        acc[2 * t1] = mfma16(ag[3], bf[0], ZC ? kZ : acc[2 * t1]);
+        acc[2 * t1 + 1] = mfma16(ag[3], bf[2], ZC ? kZ : acc[2 * t1 + 1]);
+        acc[2 * t0] = mfma16(ag[0], bf[1], acc[2 * t0]);
+        acc[2 * t0 + 1] = mfma16(ag[0], bf[3], acc[2 * t0 + 1]);
+        acc[2 * t1] = mfma16(ag[2], bf[1], acc[2 * t1]);
+        acc[2 * t1 + 1] = mfma16(ag[2], bf[3], acc[2 * t1 + 1]);
+        acc[2 * t0] = mfma16(ag[0], bf[0], acc[2 * t0]);
+        acc[2 * t0 + 1] = mfma16(ag[0], bf[2], acc[2 * t0 + 1]);
+        acc[2 * t1] = mfma16(ag[2], bf[0], acc[2 * t1]);
+        acc[2 * t1 + 1] = mfma16(ag[2], bf[2], acc[2 * t1 + 1]);
+        asm volatile("" ::"v"(ag[0]), "v"(ag[1]), "v"(ag[2]), "v"(ag[3]));
+        // interleave: each MFMA followed by up to one LDS read (the first 6) and QV VALU
+        sfor<0, 12>([&](auto I) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if constexpr (decltype(I)::value < 6) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, kQValuPerMfma, 0);
+        });
+        __builtin_amdgcn_sched_barrier(0);
+    });
+}
+
+// FiLM activation of output tile T (both blocks) of a layer, in place into v[c][r]:
+//   MODE 0: ngp layer 0, FiLM of x 2^-es (the features were scaled by 2^es, feat_scale)
+//   MODE 1: FiLM sin_rev(fma(gamma'', x, beta''))
+//   MODE 2: FiLM + the sigma head's partial dot product (per lane over own rows)
+template <int MODE>
+__device__ __forceinline__ void q_act(const f4 (&in)[32], int T, const f4 &gm, const f4 &bt,
+                                      const f4 &w4, float (&sdfp)[2], const int (&es)[2],
+                                      float (&v)[2][4]) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const f4 z = in[2 * T + c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if constexpr (MODE == 0) v[c][r] = sin_rev(__fmaf_rn(gm[r], __builtin_ldexpf(z[r], -es[c]), bt[r]));
+            else v[c][r] = sin_rev(__fmaf_rn(gm[r], z[r], bt[r]));
+            if constexpr (MODE == 2) sdfp[c] = __fmaf_rn(v[c][r], w4[r], sdfp[c]);
+        }
+    }
+}
+
+// B fragments (hi0, lo0, hi1, lo1) of a k-step from its two activated tiles
+__device__ __forceinline__ void q_split(const float (&va)[2][4], const float (&vb)[2][4], f4 (&bn)[4]) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const float u[8] = {va[c][0], va[c][1], va[c][2], va[c][3],
+                            vb[c][0], vb[c][1], vb[c][2], vb[c][3]};
+        split8(u, bn[2 * c], bn[2 * c + 1]);
+    }
+}
+
+template <class Net>
+__global__ void __launch_bounds__(kQThreads, 1) field_q_kernel(const XFieldArgs a) {
+    constexpr int NF = Net::kFilmN;
+    constexpr int KV = PNet<Net>::kViews;
+    constexpr int NL = Net::kLayers;
+    __shared__ f4 ring_lds[kRingSlots * kXSliceF4];          // 64 KB weight ring
+    __shared__ f4 facc_lds[kQWaves][16][64];                // 64 KB: [wave][tile][lane] feature partials
+    __shared__ float film_lds[NF * 2 * kW];                 // the workgroup's face
+    __shared__ float cst[4 * kW];                           // sigma_w, rgb_w[3]
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t n = lane & 15u, g = lane >> 4, r8 = n & 7u;
+    const bool colB = n >= 8u;
+    const GeomArgs &G = a.g;
+
+    // workgroup = 2 tiles; wave k: tile k >> 1, rays 8 (k & 1) .. +7
+    const uint32_t wg_per_face = (G.tiles_per_face + kPTiles - 1) / kPTiles;
+    const uint32_t seg = blockIdx.x % a.nseg, blk = blockIdx.x / a.nseg;
+    const uint32_t b = blk / wg_per_face;
+    const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
+    {
+        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * NF * 2 * kW);
+        f4 *dst = reinterpret_cast<f4 *>(film_lds);
+        for (uint32_t i = tid; i < NF * 2 * kW / 4; i += kQThreads) dst[i] = src[i];
+    }
+    QRing R;
+    R.lds = ring_lds;
+    R.tid = tid;
+    R.wave = wave;
+    R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
+    for (uint32_t i = tid; i < 4 * kW; i += kQThreads)
+        cst[i] = i < kW ? a.sigma_w[i] : a.rgb_w[i - kW];
+    // prologue: k-step 0's half-slices -> slots 0, 1 (each k-step issues the next)
+    q_dma<0, 0>(R);
+    q_dma<1, 1>(R);
+    f4 *facc = &facc_lds[wave][0][lane];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) facc[t * 64] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        R.na[0][i] = R.lds[(i >> 1) * 128 + (i & 1) * 64 + lane];
+        R.na[1][i] = R.lds[(2 + (i >> 1)) * 128 + (i & 1) * 64 + lane];
+    }
+
+    const float *sig_w = cst, *rgb_w = cst + kW;
+    auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
+    auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
+    const float sig_b = a.sigma_b[0];
+    const float rgb_b0 = a.rgb_b[0], rgb_b1 = a.rgb_b[1], rgb_b2 = a.rgb_b[2];
+    const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
+    const uint32_t npass = (G.N + kPSamples - 1) / kPSamples;
+    const uint32_t pps = (npass + a.nseg - 1) / a.nseg;
+    const uint32_t p_begin = seg * pps, p_end = min(npass, p_begin + pps);
+
+    uint32_t tile_local = (blk % wg_per_face) * kPTiles + (wave >> 1);
+    const bool tile_ok = tile_local < G.tiles_per_face;
+    if (!tile_ok) tile_local = G.tiles_per_face - 1;
+    const uint32_t tile = b * G.tiles_per_face + tile_local;
+    const uint32_t ray_in_tile = 8u * (wave & 1u) + r8;
+    uint32_t ray_local = tile_local * kTileRays + ray_in_tile;
+    const bool ray_ok = tile_ok && ray_local < G.H * G.W;
+    if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
+    const uint32_t py = ray_local / G.W, px = ray_local % G.W;
+    const uint32_t ray_index = (b * G.H + py) * G.W + px;
+
+    Ray ray;
+    make_ray(G.cam + (size_t)b * 12, G.focal[b], G.pix_x[px], G.pix_y[py], G.half_res, ray);
+    const float nr = G.near_[b], fr = G.far_[b];
+    const float span = __fsub_rn(fr, nr);
+    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
+    f4 vx[4];                                               // the views layer's extra k-step
+    {
+        const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
+        const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
+        const float v2 = G.static_viewdirs ? ray.dir[2] : ray.d[2];
+        const float vn = norm3_torch(v0, v1, v2);
+        const float ux = __fdiv_rn(v0, vn), uy = __fdiv_rn(v1, vn), uz = __fdiv_rn(v2, vn);
+        float v[8];
+        if constexpr (Net::kSiren) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = 0.0f;
+            if (g == 0) {
+                v[0] = ux;
+                v[1] = uy;
+                v[2] = uz;
+            }
+        } else {
+            const f4 qa = sh_quad(ux, uy, uz, (2 * g) & 3), qb = sh_quad(ux, uy, uz, (2 * g + 1) & 3);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = g < 2 ? qa[r] : 0.0f;
+                v[4 + r] = g < 2 ? qb[r] : 0.0f;
+            }
+        }
+        split8(v, vx[0], vx[1]);
+        vx[2] = vx[0];                                       // both blocks: the same ray
+        vx[3] = vx[1];
+    }
+    // T, the weight sum and w_last run over all 4 samples of a pass identically in the two
+    // lanes of a ray; racc / xacc / facc are per-lane partials over the lane's own samples
+    float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
+    float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
+    const size_t tile_sid = (size_t)(tile * G.N) * kTileRays + ray_in_tile;
+    float2 en[2][4];
+    auto load_inputs = [&](uint32_t p) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            uint32_t s = kPSamples * p + 2 * c + (colB ? 1u : 0u);
+            if (s >= G.N) s = G.N - 1;
+            if constexpr (Net::kSiren) {
+                const float z = sample_z(G.sc, nr, fr, ray_index, s);
+                float np_[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const float pp = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));
+                    np_[k] = G.z_normalize ? __fdiv_rn(__fmul_rn(pp, 2.0f), span) : pp;
+                }
+                const bool g0 = g == 0;
+                en[c][0] = make_float2(g0 ? np_[0] : 0.0f, g0 ? np_[1] : 0.0f);
+                en[c][1] = make_float2(g0 ? np_[2] : 0.0f, 0.0f);
+                en[c][2] = make_float2(0.0f, 0.0f);
+                en[c][3] = make_float2(0.0f, 0.0f);
+            } else {
+                const size_t sid = tile_sid + (size_t)s * kTileRays;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) en[c][k] = enc2[(4 * g + k) * (size_t)G.S_total + sid];
+            }
+        }
+    };
+    load_inputs(p_begin);
+
+    for (uint32_t p = p_begin; p < p_end; ++p) {
+        f4 X[32], Y[32];                                   // [2 tile + block]
+        f4 bf[4];                                          // B fragments of the current k-step
+        int es[2] = {0, 0};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                v[2 * k] = en[c][k].x;
+                v[2 * k + 1] = en[c][k].y;
+            }
+            if constexpr (!Net::kSiren) es[c] = feat_scale(v);
+            split8(v, bf[2 * c], bf[2 * c + 1]);
+        }
+        float sdfp[2] = {0.0f, 0.0f};
+        f4 bn[4];
+        // the FiLM activation of chunk q (tiles 2q, 2q + 1) of layer l's output o into bn,
+        // spread over the groups of the k-step it runs beside: film vectors of tile 2q read
+        // after group G0, tile 2q activated after G0 + 1, tile 2q + 1's vectors after
+        // G0 + 2, activated and split after G0 + 3
+        struct ActState {
+            f4 gm, bt, w4;
+            float va[2][4], vb[2][4];
+        };
+        ActState as;
+        auto act_side = [&](auto L, f4 (&o)[32], int q, auto GI, auto G0) {
+            constexpr int l = decltype(L)::value;
+            constexpr int gi = decltype(GI)::value, g0 = decltype(G0)::value;
+            constexpr int MODE = (l == 0 && !Net::kSiren) ? 0 : (l == NL - 2 ? 2 : 1);
+            const int f = Net::film_layer(l);
+            if constexpr (gi == g0 || gi == g0 + 2) {
+                const int f0 = 16 * (2 * q + (gi == g0 ? 0 : 1)) + 4 * (int)g;
+                as.gm = *reinterpret_cast<const f4 *>(fg(f) + f0);
+                as.bt = *reinterpret_cast<const f4 *>(fb(f) + f0);
+                if constexpr (MODE == 2) as.w4 = *reinterpret_cast<const f4 *>(sig_w + f0);
+            } else if constexpr (gi == g0 + 1) {
+                q_act<MODE>(o, 2 * q, as.gm, as.bt, as.w4, sdfp, es, as.va);
+            } else if constexpr (gi == g0 + 3) {
+                q_act<MODE>(o, 2 * q + 1, as.gm, as.bt, as.w4, sdfp, es, as.vb);
+                q_split(as.va, as.vb, bn);
+            }
+        };
+        // layer 0: one k-step on the encoded inputs; chunk 0 of its output activated after
+        // groups 0-1 have accumulated tiles 0, 1 (side from group 2 on)
+        qstep<Net, 0, true>(R, X, bf, [&](auto GI) {
+            act_side(std::integral_constant<int, 0>{}, X, 0, GI, std::integral_constant<int, 2>{});
+        });
+        // hidden layers 1 .. kHidden (in -> out alternate between X and Y)
+        auto dense = [&](auto L, f4 (&in)[32], f4 (&out)[32]) {
+            constexpr int l = decltype(L)::value;
+            sfor<0, 8>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                constexpr int KS = 1 + 8 * (l - 1) + j;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) bf[i] = bn[i];
+                qstep<Net, KS, j == 0>(R, out, bf, [&](auto GI) {
+                    if constexpr (j < 7)
+                        act_side(std::integral_constant<int, l - 1>{}, in, j + 1, GI,
+                                 std::integral_constant<int, 0>{});
+                    else
+                        act_side(std::integral_constant<int, l>{}, out, 0, GI,
+                                 std::integral_constant<int, 2>{});
+                });
+            });
+        };
+        sfor<1, Net::kHidden + 1>([&](auto L) {
+            constexpr int l = decltype(L)::value;
+            if constexpr (l & 1) dense(L, X, Y);
+            else dense(L, Y, X);
+        });
+        // views layer: input chunks 0-7 (the last hidden layer's output, sigma head
+        // accumulated in the activation), then the direction k-step; alpha at k-step 7,
+        // the compositing weights at k-step 8
+        constexpr bool kInX = (Net::kHidden & 1) == 0;     // last hidden output array
+        f4 (&vin)[32] = kInX ? X : Y;
+        f4 (&vout)[32] = kInX ? Y : X;
+        const uint32_t s0 = kPSamples * p;
+        float z[2] = {0.0f, 0.0f}, wj[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float sdf_c[2] = {0.0f, 0.0f}, dist[2] = {0.0f, 0.0f}, al[2] = {0.0f, 0.0f};
+        sfor<0, 9>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            constexpr int KS = KV + j;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bf[i] = bn[i];
+            if constexpr (j == 5 && !Net::kSiren) {
+                // the compositing inputs that do not depend on the network (sample depth,
+                // segment length) come from the encode kernel
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    uint32_t s = s0 + 2 * c + (colB ? 1u : 0u);
+                    if (s >= G.N) s = G.N - 1;
+                    const float2 v = a.zd[tile_sid + (size_t)s * kTileRays];
+                    z[c] = v.x;
+                    dist[c] = v.y;
+                }
+            }
+            if constexpr (j == 7) {
+                if (p + 1 < p_end) load_inputs(p + 1);
+            }
+            qstep<Net, KS, j == 0>(R, vout, bf, [&](auto GI) {
+                constexpr int gi = decltype(GI)::value;
+                if constexpr (j < 7) {
+                    act_side(std::integral_constant<int, NL - 2>{}, vin, j + 1, GI,
+                             std::integral_constant<int, 0>{});
+                    if constexpr (j == 6 && gi == 5) {
+                        sdf_c[0] = __fadd_rn(group_sum(sdfp[0]), sig_b);
+                        sdf_c[1] = __fadd_rn(group_sum(sdfp[1]), sig_b);
+                    }
+                } else if constexpr (j == 7 && gi == 0) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) bn[i] = vx[i];   // k-step 8's B: the direction
+                } else if constexpr (j == 7 && gi == 1) {
+                    // alpha of this lane's two samples
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const uint32_t s = s0 + 2 * c + (colB ? 1u : 0u);
+                        const bool s_ok = s < G.N;
+                        const uint32_t sc_ = s_ok ? s : G.N - 1;
+                        if constexpr (Net::kSiren) {
+                            z[c] = sample_z(G.sc, nr, fr, ray_index, sc_);
+                            dist[c] = (sc_ + 1 < G.N)
+                                          ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), z[c]), dnorm)
+                                          : __fmul_rn(1e10f, dnorm);
+                        }
+                        float alpha;
+                        if (a.with_sdf) {
+                            const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf_c[c], beta_s)), beta_s);
+                            alpha = 1.0f - expf(-sig * dist[c]);
+                        } else {
+                            float raw = sdf_c[c];
+                            if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
+                            const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+                            alpha = 1.0f - expf(-sp * dist[c]);
+                        }
+                        al[c] = s_ok ? alpha : 0.0f;
+                    }
+                } else if constexpr (j == 8 && gi == 1) {
+                    // compositing weights of the pass's 4 samples, identically in both
+                    // lanes of a ray, front to back
+                    const float o0 = ror8(al[0]), o1 = ror8(al[1]);
+                    const float aj[4] = {colB ? o0 : al[0], colB ? al[0] : o0, colB ? o1 : al[1],
+                                         colB ? al[1] : o1};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t s = s0 + k;
+                        if (s < G.N) {
+                            float w = aj[k] * T;
+                            if (a.force_background && s + 1 == G.N) w = 1.0f - wsum;
+                            T = T * ((1.0f - aj[k]) + 1e-10f);
+                            wsum += w;
+                            wj[k] = w;
+                        }
+                    }
+                }
+            });
+        });
+        // colour features f = sin(gamma_v x + beta_v) of all 256 rows, rgb dot products,
+        // feature partials.  (Scalar fp32: a packed-fp32 form of this tail read some
+        // v_sin_f32 results before they were written in field_p_kernel.)
+        const float wo0 = colB ? wj[1] : wj[0], wo1 = colB ? wj[3] : wj[2];   // own samples
+        const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
+        float P[3][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};   // [rgb][block]
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int f0 = 16 * t + 4 * (int)g;
+            const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
+            const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
+            const f4 w0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
+            const f4 w1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
+            const f4 w2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
+            f4 fv[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    fv[c][r] = sin_rev(__fmaf_rn(gm[r], vout[2 * t + c][r], bt[r]));
+                    P[0][c] = __fmaf_rn(fv[c][r], w0[r], P[0][c]);
+                    P[1][c] = __fmaf_rn(fv[c][r], w1[r], P[1][c]);
+                    P[2][c] = __fmaf_rn(fv[c][r], w2[r], P[2][c]);
+                }
+            }
+            if (a.features) {
+                f4 v = facc[t * 64];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = __fmaf_rn(wo1, fv[1][r], __fmaf_rn(wo0, fv[0][r], v[r]));
+                facc[t * 64] = v;
+            }
+        }
+        if (a.sdf && ray_ok && g == 0) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const uint32_t s = s0 + 2 * c + (colB ? 1u : 0u);
+                if (s < G.N) a.sdf[(size_t)ray_index * G.N + s] = sdf_c[c];
+            }
+        }
+        {
+            const float q00 = sigmoidf_(__fadd_rn(group_sum(P[0][0]), rgb_b0));
+            const float q01 = sigmoidf_(__fadd_rn(group_sum(P[1][0]), rgb_b1));
+            const float q02 = sigmoidf_(__fadd_rn(group_sum(P[2][0]), rgb_b2));
+            const float q10 = sigmoidf_(__fadd_rn(group_sum(P[0][1]), rgb_b0));
+            const float q11 = sigmoidf_(__fadd_rn(group_sum(P[1][1]), rgb_b1));
+            const float q12 = sigmoidf_(__fadd_rn(group_sum(P[2][1]), rgb_b2));
+            racc0 = __fmaf_rn(wo1, q10, __fmaf_rn(wo0, q00, racc0));
+            racc1 = __fmaf_rn(wo1, q11, __fmaf_rn(wo0, q01, racc1));
+            racc2 = __fmaf_rn(wo1, q12, __fmaf_rn(wo0, q02, racc2));
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (s0 + k < G.N) w_last = wj[k];
+            if (a.xyz) {
+                float xa[3] = {xacc0, xacc1, xacc2};
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int d = 0; d < 3; ++d)
+                        xa[d] = __fmaf_rn(c ? wo1 : wo0, __fadd_rn(ray.o[d], __fmul_rn(ray.d[d], z[c])), xa[d]);
+                xacc0 = xa[0];
+                xacc1 = xa[1];
+                xacc2 = xa[2];
+            }
+        }
+    }
+    // the ring runs ahead across passes: no LDS-DMA may land after the workgroup ends
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the two lanes of a ray add their partials (a + b in one lane, b + a in the other:
+    // the same sum)
+    racc0 = __fadd_rn(racc0, ror8(racc0));
+    racc1 = __fadd_rn(racc1, ror8(racc1));
+    racc2 = __fadd_rn(racc2, ror8(racc2));
+    xacc0 = __fadd_rn(xacc0, ror8(xacc0));
+    xacc1 = __fadd_rn(xacc1, ror8(xacc1));
+    xacc2 = __fadd_rn(xacc2, ror8(xacc2));
+    // lanes n < 8 write tiles 0-7 of the ray's features, lanes n >= 8 tiles 8-15
+    f4 fs[8];
+    if (a.features) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const f4 v = facc[t * 64];
+            f4 s;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[r] = __fadd_rn(v[r], ror8(v[r]));
+            if (t < 8) {
+                if (!colB) fs[t] = s;
+            } else {
+                if (colB) fs[t - 8] = s;
+            }
+        }
+    }
+    if (!ray_ok) return;
+    const uint32_t tb = colB ? 8u : 0u;
+    if (a.nseg > 1) {
+        const size_t Rr = (size_t)G.total_tiles * kTileRays;
+        float *pp = a.part + (size_t)seg * kPartQ * Rr + (size_t)tile * kTileRays + ray_in_tile;
+        if (a.features) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const uint32_t jf = 16 * (tb + t) + 4 * g;
+                pp[(size_t)(jf + 0) * Rr] = fs[t].x;
+                pp[(size_t)(jf + 1) * Rr] = fs[t].y;
+                pp[(size_t)(jf + 2) * Rr] = fs[t].z;
+                pp[(size_t)(jf + 3) * Rr] = fs[t].w;
+            }
+        }
+        if (!colB && g == 0) {
+            const float q[8] = {racc0, racc1, racc2, xacc0, xacc1, xacc2, T, w_last};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pp[(size_t)(kW + k) * Rr] = q[k];
+        }
+        return;
+    }
+    const size_t HW = (size_t)G.H * G.W;
+    const size_t pix = (size_t)py * G.W + px;
+    if (!colB) {
+        if (g < 3) {
+            const float rc = g == 0 ? racc0 : (g == 1 ? racc1 : racc2);
+            a.rgb[((size_t)b * 3 + g) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, rc));
+            if (a.xyz) {
+                const float xc = g == 0 ? xacc0 : (g == 1 ? xacc1 : xacc2);
+                a.xyz[((size_t)b * 3 + g) * HW + pix] = xc;
+            }
+        } else if (a.mask) {
+            a.mask[(size_t)b * HW + pix] = w_last;
+        }
+    }
+    if (a.features) {
+        float *fbp = a.features + (size_t)b * kW * HW + pix;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t jf = 16 * (tb + t) + 4 * g;
+            fbp[(size_t)(jf + 0) * HW] = fs[t].x;
+            fbp[(size_t)(jf + 1) * HW] = fs[t].y;
+            fbp[(size_t)(jf + 2) * HW] = fs[t].z;
+            fbp[(size_t)(jf + 3) * HW] = fs[t].w;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// field_r_kernel: one wave per SIMD on v_mfma_f32_32x32x16_f16.
+//
+// field_q_kernel (one wave per SIMD, all 256 rows, 16x16x32) runs at field_p_kernel's
+// speed: with one wave a SIMD issues one instruction per 4 cycles, and a 16-cycle
+// 16x16x32 MFMA leaves it 2 slots for the k-step's activations, A reads, DMA and waits
+// (counters: 55 % MFMA busy, 34 % of wave cycles waiting on issue).  The 32x32x16 MFMA
+// takes 32 cycles for twice the FLOPs and holds the vector issue for 8 of them: the same
+// work per FLOP gets three times the free issue slots.
+//
+// Work unit: a workgroup of 4 waves (one per SIMD, 512 VGPRs) over 4 tiles of 16 rays;
+// wave w takes tile w, 2 samples of each of its 16 rays per pass: MFMA column
+// c = lane & 31 is ray c & 15, sample 2p + (c >> 4); lane half h = lane >> 5.  Output
+// tile T (32 rows of a 256-wide layer) is 16 accumulators per lane, register v holding
+// row 32 T + (v & 3) + 8 (v >> 2) + 4 h.  Registers 8 s' .. 8 s' + 7 (s' = 0, 1) of a tile,
+// activated and split, are the B fragment of k-step 2 T + s' of the next layer (element
+// j = row 32 T + 16 s' + 8 (j >> 2) + 4 h + (j & 3)); the packed weights permute K to match
+// (xprep_kernel, rperm_k).  Per k-step (16 K) and wave: 8 tiles x 3 split terms = 24
+// MFMAs (768 cycles), 16 A ds_read_b128, 4 LDS-DMA pieces of the 16 KB weight slice.
+struct RRing {
+    f4 *lds;          // weight ring: 4 slots of kRSliceF4
+    v4i drsrc;
+    uint32_t tid, wave;
+    uint32_t ubase;   // ring half of the pass's unit 0 (units per pass may be odd)
+    f4 na[3][2];      // the next k-step's groups 0-2 A fragments (hi, lo)
+};
+
+// this wave's 4 pieces of slice SLICE -> ring slot `slot` (instruction offsets 0..3 KB
+// move the global and the LDS address alike)
+template <uint32_t SLICE>
+__device__ __forceinline__ void r_dma(const RRing &R, uint32_t slot) {
+    const uint32_t sbase = R.wave * 4096u;
+    const uint32_t lbase = lds_addr(R.lds) + sbase + slot * (kRSliceF4 * 16u);
+    const uint32_t voff = (R.tid & 63u) * 16u;
+    uint32_t keep, so;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_add_u32 %1, %5, %6\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %3, %1 offen lds\n\t"
+        "buffer_load_dwordx4 %2, %3, %1 offen offset:1024 lds\n\t"
+        "buffer_load_dwordx4 %2, %3, %1 offen offset:2048 lds\n\t"
+        "buffer_load_dwordx4 %2, %3, %1 offen offset:3072 lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep), "=&s"(so)
+        : "v"(voff), "s"(R.drsrc), "s"(lbase), "s"(sbase), "i"(SLICE * kRSliceF4 * 16u)
+        : "memory", "scc");
+}
+
+// Ring units: k-steps (2u, 2u + 1) of a pass, the last k-step alone when a pass has an odd
+// count; unit U (counted over all passes) holds the ring half U & 1 (slots 2 (U & 1) +
+// 0, 1).  One barrier per unit, in its last k-step: behind it unit U + 2 is DMA'd into
+// unit U's half.
+template <class Net>
+__device__ __forceinline__ uint32_t r_slot(const RRing &R, int ks) {
+    return 2u * ((R.ubase + (uint32_t)(ks >> 1)) & 1u) + (uint32_t)(ks & 1);
+}
+
+// DMA of slice `piece` (0, 1) of in-pass unit V into ring half `half`
+template <class Net, int V, int PIECE>
+__device__ __forceinline__ void r_dma_unit(const RRing &R, uint32_t half) {
+    constexpr int NS = RNet<Net>::kSteps;
+    if constexpr (2 * V + PIECE < NS) r_dma<2 * V + PIECE>(R, 2u * half + PIECE);
+}
+
+// One k-step of one wave: 8 output tiles x 3 split terms = 24 MFMAs in 8 groups of one
+// tile.  Group gi's A fragments (hi, lo) were read during group gi - 3 (groups 0-2: by the
+// previous k-step, R.na).  In a unit's last k-step the barrier (this wave's DMA of the next
+// unit landed, its A reads of this unit done) sits ahead of group 5; behind it the unit
+// after next is DMA'd (one slice at group 5, one at group 6) into this unit's half, and the
+// next k-step's groups 0-2 A fragments are read.  side(gi) runs between group gi's MFMAs.
+template <class Net, int KS, bool ZC, class Side>
+__device__ __forceinline__ void rstep(RRing &R, f16v (&acc)[8], const f4 (&bf)[2], Side &&side) {
+    constexpr int NS = RNet<Net>::kSteps;
+    constexpr int UPP = (NS + 1) / 2;                       // units per pass
+    constexpr bool kBar = (KS & 1) || KS == NS - 1;         // the unit's last k-step
+#ifdef SDFR_RBAR1
+    constexpr bool kBarAll = true;                          // A/B: a barrier every k-step
+#else
+    constexpr bool kBarAll = kBar;
+#endif
+    constexpr int U = KS >> 1;
+    constexpr int VN = (U + 2) % UPP;                       // the unit DMA'd behind the barrier
+    const uint32_t lane = R.tid & 63u;
+    const f4 *A = R.lds + r_slot<Net>(R, KS) * kRSliceF4 + lane;
+    const f4 *An = R.lds + r_slot<Net>(R, KS + 1) * kRSliceF4 + lane;
+    const uint32_t half = (R.ubase + (uint32_t)U) & 1u;     // = the half of unit U + 2
+    f4 a[8][2];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        a[g][0] = R.na[g][0];
+        a[g][1] = R.na[g][1];
+    }
+    sfor<0, 8>([&](auto GI) {
+        constexpr int gi = decltype(GI)::value;
+        if constexpr (kBarAll && gi == 5) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (kBar && gi == 5) r_dma_unit<Net, VN, 0>(R, half);
+        if constexpr (kBar && gi == 6) r_dma_unit<Net, VN, 1>(R, half);
+        if constexpr (gi + 3 < 8) {
+            a[gi + 3][0] = A[(gi + 3) * 128];
+            a[gi + 3][1] = A[(gi + 3) * 128 + 64];
+        } else if constexpr (KS + 1 < NS) {
+            // (the next pass's first fragments are read after the pass tail, r_na)
+            R.na[gi - 5][0] = An[(gi - 5) * 128];
+            R.na[gi - 5][1] = An[(gi - 5) * 128 + 64];
+        }
+        side(GI);
+        constexpr f16v kZ = {};
+        // W_lo x_hi, W_hi x_lo, W_hi x_hi
+        acc[gi] = mfma32(a[gi][1], bf[0], ZC ? kZ : acc[gi]);
+        acc[gi] = mfma32(a[gi][0], bf[1], acc[gi]);
+        acc[gi] = mfma32(a[gi][0], bf[0], acc[gi]);
+        asm volatile("" ::"v"(a[gi][0]), "v"(a[gi][1]));
+        sfor<0, 3>([&](auto I) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, kRDsPerMfma, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, kRValuPerMfma, 0);
+        });
+        __builtin_amdgcn_sched_barrier(0);
+    });
+}
+
+// groups 0-2 A fragments of the k-step in ring slot `slot` (landed: behind its barrier)
+__device__ __forceinline__ void r_na(RRing &R, uint32_t slot) {
+    const f4 *A = R.lds + slot * kRSliceF4 + (R.tid & 63u);
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        R.na[g][0] = A[g * 128];
+        R.na[g][1] = A[g * 128 + 64];
+    }
+}
+
+// FiLM activation of registers 8 s' .. 8 s' + 7 of output tile T into v[8] (element j =
+// register 8 s' + j): film rows 32 T + 16 s' + 4 h + (0..3) (gm0, bt0, w0) and + 8 (gm1, ...)
+template <int MODE>
+__device__ __forceinline__ void r_act(const f16v &z, int sp, const f4 &gm0, const f4 &bt0,
+                                      const f4 &w0, const f4 &gm1, const f4 &bt1, const f4 &w1,
+                                      float &sdfp, int es, float (&v)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float zz = z[8 * sp + j];
+        const float g = j < 4 ? gm0[j & 3] : gm1[j & 3], b = j < 4 ? bt0[j & 3] : bt1[j & 3];
+        if constexpr (MODE == 0) v[j] = sin_rev(__fmaf_rn(g, __builtin_ldexpf(zz, -es), b));
+        else v[j] = sin_rev(__fmaf_rn(g, zz, b));
+        if constexpr (MODE == 2) sdfp = __fmaf_rn(v[j], j < 4 ? w0[j & 3] : w1[j & 3], sdfp);
+    }
+}
+
+// v_permlane16_swap of (pa, pb) between the two 16-lane rows of each pair: the even
+// row gets pa(even) + pa(odd), the odd row pb(even) + pb(odd).  The results pass through
+// an empty asm: on float values bit-cast to the builtin's operands, hipcc (ROCm 7.2)
+// returned the first result twice (checked on a probe kernel's ISA).
+__device__ __forceinline__ float row_pair_sum(float pa, float pb) {
+    const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, pa),
+                                                     __builtin_bit_cast(uint32_t, pb), false, false);
+    uint32_t r0 = sw[0], r1 = sw[1];
+    asm volatile("" : "+v"(r0), "+v"(r1));
+    return __fadd_rn(__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1));
+}
+
+template <class Net>
+__global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs a) {
+    constexpr int NF = Net::kFilmN;
+    constexpr int KV = RNet<Net>::kViews;
+    constexpr int KL0 = RNet<Net>::kL0;
+    constexpr int NS = RNet<Net>::kSteps;
+    constexpr int NL = Net::kLayers;
+    __shared__ f4 ring_lds[4 * kRSliceF4];                  // 64 KB weight ring
+    __shared__ f4 facc_lds[kRWaves][16][64];                // 64 KB: [wave][f4 of 64 features][lane]
+    __shared__ float film_lds[NF * 2 * kW];                 // the workgroup's face
+    __shared__ float cst[4 * kW];                           // sigma_w, rgb_w[3]
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t c = lane & 31u, h = lane >> 5, r16 = c & 15u;
+    const bool odd = c >= 16u;                              // sample 2p + 1 of the pass
+    const GeomArgs &G = a.g;
+
+    const uint32_t wg_per_face = (G.tiles_per_face + kRTiles - 1) / kRTiles;
+    const uint32_t seg = blockIdx.x % a.nseg, blk = blockIdx.x / a.nseg;
+    const uint32_t b = blk / wg_per_face;
+    const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
+    {
+        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * NF * 2 * kW);
+        f4 *dst = reinterpret_cast<f4 *>(film_lds);
+        for (uint32_t i = tid; i < NF * 2 * kW / 4; i += kRThreads) dst[i] = src[i];
+    }
+    RRing R;
+    R.lds = ring_lds;
+    R.tid = tid;
+    R.wave = wave;
+    R.ubase = 0;
+    R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
+    for (uint32_t i = tid; i < 4 * kW; i += kRThreads)
+        cst[i] = i < kW ? a.sigma_w[i] : a.rgb_w[i - kW];
+    // prologue: units 0, 1 (slices 0-3) -> slots 0-3 (unit U's barrier issues unit U + 2)
+    r_dma<0>(R, 0);
+    r_dma<1>(R, 1);
+    r_dma<2>(R, 2);
+    r_dma<3>(R, 3);
+    f4 *facc = &facc_lds[wave][0][lane];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) facc[t * 64] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const float *sig_w = cst, *rgb_w = cst + kW;
+    auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
+    auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
+    const float sig_b = a.sigma_b[0];
+    const float rgb_b0 = a.rgb_b[0], rgb_b1 = a.rgb_b[1], rgb_b2 = a.rgb_b[2];
+    const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
+    const uint32_t npass = (G.N + kRSamples - 1) / kRSamples;
+    const uint32_t pps = (npass + a.nseg - 1) / a.nseg;
+    const uint32_t p_begin = seg * pps, p_end = min(npass, p_begin + pps);
+
+    uint32_t tile_local = (blk % wg_per_face) * kRTiles + wave;
+    const bool tile_ok = tile_local < G.tiles_per_face;
+    if (!tile_ok) tile_local = G.tiles_per_face - 1;
+    const uint32_t tile = b * G.tiles_per_face + tile_local;
+    uint32_t ray_local = tile_local * kTileRays + r16;
+    const bool ray_ok = tile_ok && ray_local < G.H * G.W;
+    if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
+    const uint32_t py = ray_local / G.W, px = ray_local % G.W;
+    const uint32_t ray_index = (b * G.H + py) * G.W + px;
+
+    Ray ray;
+    make_ray(G.cam + (size_t)b * 12, G.focal[b], G.pix_x[px], G.pix_y[py], G.half_res, ray);
+    const float nr = G.near_[b], fr = G.far_[b];
+    const float span = __fsub_rn(fr, nr);
+    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
+    f4 vx[2];                                               // the views layer's k-step 16
+    {
+        const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
+        const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
+        const float v2 = G.static_viewdirs ? ray.dir[2] : ray.d[2];
+        const float vn = norm3_torch(v0, v1, v2);
+        const float ux = __fdiv_rn(v0, vn), uy = __fdiv_rn(v1, vn), uz = __fdiv_rn(v2, vn);
+        float v[8];
+        if constexpr (Net::kSiren) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = 0.0f;
+            if (h == 0) {
+                v[0] = ux;
+                v[1] = uy;
+                v[2] = uz;
+            }
+        } else {
+            const f4 qa = sh_quad(ux, uy, uz, 2 * h), qb = sh_quad(ux, uy, uz, 2 * h + 1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = qa[r];
+                v[4 + r] = qb[r];
+            }
+        }
+        split8(v, vx[0], vx[1]);
+    }
+    float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
+    float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
+    const size_t tile_sid = (size_t)(tile * G.N) * kTileRays + r16;
+    const __amdgpu_buffer_rsrc_t enc_r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(a.enc), (short)0, Net::kSiren ? 0 : (int)(16u * G.S_total * 8u), 0x00020000);
+    float2 en[2][4];                                        // [layer-0 k-step][level pair]
+    auto load_inputs = [&](uint32_t p) {
+        uint32_t s = kRSamples * p + (odd ? 1u : 0u);
+        if (s >= G.N) s = G.N - 1;
+        if constexpr (Net::kSiren) {
+            const float z = sample_z(G.sc, nr, fr, ray_index, s);
+            float np_[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float pp = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));
+                np_[k] = G.z_normalize ? __fdiv_rn(__fmul_rn(pp, 2.0f), span) : pp;
+            }
+            const bool h0 = h == 0;
+            en[0][0] = make_float2(h0 ? np_[0] : 0.0f, h0 ? np_[1] : 0.0f);
+            en[0][1] = make_float2(h0 ? np_[2] : 0.0f, 0.0f);
+            en[0][2] = en[0][3] = make_float2(0.0f, 0.0f);
+        } else {
+            // buffer loads: one 32-bit lane offset (level 4 h, sample), the level step as a
+            // wave-uniform offset (8 hoisted 64-bit addresses otherwise: VGPR pressure)
+            const uint32_t voff = ((uint32_t)(tile_sid + (size_t)s * kTileRays) + 4 * h * G.S_total) * 8u;
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    // (index the builtin's vector directly: a bit_cast of it to another vector
+                    // type made hipcc load one dword and use it twice, ROCm 7.2)
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(
+                        enc_r, (int)voff, (int)((8 * st + k) * G.S_total * 8u), 0);
+                    const uint32_t vx0 = v[0], vy0 = v[1];
+                    en[st][k] = make_float2(__builtin_bit_cast(float, vx0), __builtin_bit_cast(float, vy0));
+                }
+        }
+    };
+    load_inputs(p_begin);
+
+    for (uint32_t p = p_begin; p < p_end; ++p) {
+        R.ubase = __builtin_amdgcn_readfirstlane(((p - p_begin) * (uint32_t)((NS + 1) / 2)) & 1u);
+        r_na(R, r_slot<Net>(R, 0));
+        f16v X[8], Y[8];
+        f4 bf[2], e1[2];                                   // B fragments: current, layer-0 step 1
+        int es = 0;
+        {
+            float v[16];
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    v[8 * st + 2 * k] = en[st][k].x;
+                    v[8 * st + 2 * k + 1] = en[st][k].y;
+                }
+            if constexpr (!Net::kSiren) {
+                // the sample's 32 features over both lane halves -> 2^es into [0.5, 1)
+                float m = 0.0f;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) m = fmaxf(m, fabsf(v[j]));
+                m = fmaxf(m, __shfl_xor(m, 32));
+                if (m > 0.0f && m < 3.0e38f) {
+                    const int ex = __builtin_amdgcn_frexp_expf(m);
+                    es = ex < -100 ? 100 : -ex;
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) v[j] = __builtin_ldexpf(v[j], es);
+                }
+            }
+            float u0[8], u1[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                u0[j] = v[j];
+                u1[j] = v[8 + j];
+            }
+            split8(u0, bf[0], bf[1]);
+            split8(u1, e1[0], e1[1]);
+        }
+        float sdfp = 0.0f;
+        f4 bn[2];
+        struct ActState {
+            f4 gm0, bt0, w0, gm1, bt1, w1;
+            float v[8];
+        };
+        ActState as;
+        // activation of chunk q (registers 8 (q & 1) .. + 7 of tile q >> 1) of layer l's
+        // output o into bn: film vectors read beside group G0, activated beside G0 + 1,
+        // split beside G0 + 2
+        auto act_side = [&](auto L, f16v (&o)[8], int q, auto GI, auto G0) {
+            constexpr int l = decltype(L)::value;
+            constexpr int gi = decltype(GI)::value, g0 = decltype(G0)::value;
+            constexpr int MODE = (l == 0 && !Net::kSiren) ? 0 : (l == NL - 2 ? 2 : 1);
+            const int f = Net::film_layer(l);
+            const int r0 = 32 * (q >> 1) + 16 * (q & 1) + 4 * (int)h;
+            if constexpr (gi == g0) {
+                as.gm0 = *reinterpret_cast<const f4 *>(fg(f) + r0);
+                as.gm1 = *reinterpret_cast<const f4 *>(fg(f) + r0 + 8);
+                as.bt0 = *reinterpret_cast<const f4 *>(fb(f) + r0);
+                as.bt1 = *reinterpret_cast<const f4 *>(fb(f) + r0 + 8);
+                if constexpr (MODE == 2) {
+                    as.w0 = *reinterpret_cast<const f4 *>(sig_w + r0);
+                    as.w1 = *reinterpret_cast<const f4 *>(sig_w + r0 + 8);
+                }
+            } else if constexpr (gi == g0 + 1) {
+                r_act<MODE>(o[q >> 1], q & 1, as.gm0, as.bt0, as.w0, as.gm1, as.bt1, as.w1, sdfp, es,
+                            as.v);
+            } else if constexpr (gi == g0 + 2) {
+                split8(as.v, bn[0], bn[1]);
+            }
+        };
+        // layer 0: K = 32 (ngp, 2 k-steps) or 3 (siren, 1); chunk 0 of its output (tile 0
+        // registers 0-7, final after group 0 of the last layer-0 k-step) from group 1 on
+        sfor<0, KL0>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if constexpr (j == 1) {
+                bf[0] = e1[0];
+                bf[1] = e1[1];
+            }
+            rstep<Net, j, j == 0>(R, X, bf, [&](auto GI) {
+                if constexpr (j == KL0 - 1)
+                    act_side(std::integral_constant<int, 0>{}, X, 0, GI, std::integral_constant<int, 2>{});
+            });
+        });
+        // hidden layers 1 .. kHidden: 16 k-steps each (in -> out alternate X / Y)
+        auto dense = [&](auto L, f16v (&in)[8], f16v (&out)[8]) {
+            constexpr int l = decltype(L)::value;
+            sfor<0, 16>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                constexpr int KS = KL0 + 16 * (l - 1) + j;
+                bf[0] = bn[0];
+                bf[1] = bn[1];
+                rstep<Net, KS, j == 0>(R, out, bf, [&](auto GI) {
+                    if constexpr (j < 15)
+                        act_side(std::integral_constant<int, l - 1>{}, in, j + 1, GI,
+                                 std::integral_constant<int, 0>{});
+                    else
+                        act_side(std::integral_constant<int, l>{}, out, 0, GI,
+                                 std::integral_constant<int, 2>{});
+                });
+            });
+        };
+        sfor<1, Net::kHidden + 1>([&](auto L) {
+            constexpr int l = decltype(L)::value;
+            if constexpr (l & 1) dense(L, X, Y);
+            else dense(L, Y, X);
+        });
+        constexpr bool kInX = (Net::kHidden & 1) == 0;
+        f16v (&vin)[8] = kInX ? X : Y;
+        f16v (&vout)[8] = kInX ? Y : X;
+        const uint32_t s_own = kRSamples * p + (odd ? 1u : 0u);
+        const bool s_ok = s_own < G.N;
+        const uint32_t sc_ = s_ok ? s_own : G.N - 1;
+        float z = 0.0f, dist = 0.0f, al = 0.0f, sdf_c = 0.0f, w_own = 0.0f;
+        float wj[2] = {0.0f, 0.0f};
+        sfor<0, 17>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            constexpr int KS = KV + j;
+            bf[0] = bn[0];
+            bf[1] = bn[1];
+            if constexpr (j == 14 && !Net::kSiren) {
+                const float2 v = a.zd[tile_sid + (size_t)sc_ * kTileRays];
+                z = v.x;
+                dist = v.y;
+            }
+            if constexpr (j == 16) {
+                if (p + 1 < p_end) load_inputs(p + 1);
+            }
+            rstep<Net, KS, j == 0>(R, vout, bf, [&](auto GI) {
+                constexpr int gi = decltype(GI)::value;
+                if constexpr (j < 15) {
+                    act_side(std::integral_constant<int, NL - 2>{}, vin, j + 1, GI,
+                             std::integral_constant<int, 0>{});
+                } else if constexpr (j == 15 && gi == 0) {
+                    bn[0] = vx[0];                          // k-step 16's B: the direction
+                    bn[1] = vx[1];
+                    sdf_c = __fadd_rn(__fadd_rn(sdfp, __shfl_xor(sdfp, 32)), sig_b);
+                } else if constexpr (j == 15 && gi == 1) {
+                    if constexpr (Net::kSiren) {
+                        z = sample_z(G.sc, nr, fr, ray_index, sc_);
+                        dist = (sc_ + 1 < G.N)
+                                   ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), z), dnorm)
+                                   : __fmul_rn(1e10f, dnorm);
+                    }
+                    float alpha;
+                    if (a.with_sdf) {
+                        const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf_c, beta_s)), beta_s);
+                        alpha = 1.0f - expf(-sig * dist);
+                    } else {
+                        float raw = sdf_c;
+                        if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
+                        const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+                        alpha = 1.0f - expf(-sp * dist);
+                    }
+                    al = s_ok ? alpha : 0.0f;
+                } else if constexpr (j == 16 && gi == 1) {
+                    // the pass's two compositing weights, identically in both lanes of a ray
+                    const float ao = __shfl_xor(al, 16);
+                    const float aj[2] = {odd ? ao : al, odd ? al : ao};
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const uint32_t s = kRSamples * p + k;
+                        if (s < G.N) {
+                            float w = aj[k] * T;
+                            if (a.force_background && s + 1 == G.N) w = 1.0f - wsum;
+                            T = T * ((1.0f - aj[k]) + 1e-10f);
+                            wsum += w;
+                            wj[k] = w;
+                        }
+                    }
+                    w_own = odd ? wj[1] : wj[0];
+                }
+            });
+        });
+        // colour features f = sin(gamma_v x + beta_v), rgb dot products, and the ray's
+        // feature sums: w f of the two samples added across the lane rows by
+        // v_permlane16_swap (a tile-0..3 value to the even row, its tile-4..7 partner to
+        // the odd row), each row accumulating its half of the features
+        const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
+        // rgb dot products in 4 independent chains per channel (one per row r of a 4-row
+        // group), added at the end: no 128-long serial fma chain for the scheduler to wait on
+        float Pc[3][4] = {};
+        // 16 steps (tile t and its permlane partner t + 4, 4-row group bq), software
+        // pipelined: the next step's film / rgb vectors and feature partials are read
+        // (LDS) while this step's values are computed
+        struct TailIn {
+            f4 gm[2], bt[2], w0[2], w1[2], w2[2], fa;
+        };
+        auto tail_load = [&](int it, TailIn &T) {
+            const int t = it >> 2, bq = it & 3;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int r0 = 32 * (t + 4 * u) + 8 * bq + 4 * (int)h;
+                T.gm[u] = *reinterpret_cast<const f4 *>(f3g + r0);
+                T.bt[u] = *reinterpret_cast<const f4 *>(f3b + r0);
+                T.w0[u] = *reinterpret_cast<const f4 *>(rgb_w + r0);
+                T.w1[u] = *reinterpret_cast<const f4 *>(rgb_w + kW + r0);
+                T.w2[u] = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + r0);
+            }
+            T.fa = facc[(4 * t + bq) * 64];
+        };
+        TailIn tin[2];
+        tail_load(0, tin[0]);
+        sfor<0, 16>([&](auto IT) {
+            constexpr int it = decltype(IT)::value, t = it >> 2, bq = it & 3;
+            TailIn &T = tin[it & 1];
+            if constexpr (it + 1 < 16) tail_load(it + 1, tin[(it + 1) & 1]);
+            float fp[2][4];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float f = sin_rev(__fmaf_rn(T.gm[u][r], vout[t + 4 * u][4 * bq + r], T.bt[u][r]));
+                    Pc[0][r] = __fmaf_rn(f, T.w0[u][r], Pc[0][r]);
+                    Pc[1][r] = __fmaf_rn(f, T.w1[u][r], Pc[1][r]);
+                    Pc[2][r] = __fmaf_rn(f, T.w2[u][r], Pc[2][r]);
+                    fp[u][r] = f;
+                }
+            // (accumulated whether or not the call wants features: no branch here)
+            f4 acc4 = T.fa;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float pa = __fmul_rn(w_own, fp[0][r]);
+                const float pb = __fmul_rn(w_own, fp[1][r]);
+                acc4[r] = __fadd_rn(acc4[r], row_pair_sum(pa, pb));
+            }
+            facc[(4 * t + bq) * 64] = acc4;
+            // the dot-product partials are materialised here (IR sinking otherwise defers
+            // all 384 fmas past the loop and keeps every colour feature live: spills)
+#pragma unroll
+            for (int o = 0; o < 3; ++o)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xpin(Pc[o][r]);
+            __builtin_amdgcn_sched_barrier(0);     // one step of look-ahead (VGPRs)
+        });
+        float P0 = __fadd_rn(__fadd_rn(Pc[0][0], Pc[0][1]), __fadd_rn(Pc[0][2], Pc[0][3]));
+        float P1 = __fadd_rn(__fadd_rn(Pc[1][0], Pc[1][1]), __fadd_rn(Pc[1][2], Pc[1][3]));
+        float P2 = __fadd_rn(__fadd_rn(Pc[2][0], Pc[2][1]), __fadd_rn(Pc[2][2], Pc[2][3]));
+        if (a.sdf && ray_ok && h == 0 && s_ok) a.sdf[(size_t)ray_index * G.N + s_own] = sdf_c;
+        {
+            P0 = __fadd_rn(P0, __shfl_xor(P0, 32));
+            P1 = __fadd_rn(P1, __shfl_xor(P1, 32));
+            P2 = __fadd_rn(P2, __shfl_xor(P2, 32));
+            racc0 = __fmaf_rn(w_own, sigmoidf_(__fadd_rn(P0, rgb_b0)), racc0);
+            racc1 = __fmaf_rn(w_own, sigmoidf_(__fadd_rn(P1, rgb_b1)), racc1);
+            racc2 = __fmaf_rn(w_own, sigmoidf_(__fadd_rn(P2, rgb_b2)), racc2);
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (kRSamples * p + k < G.N) w_last = wj[k];
+            if (a.xyz) {
+                xacc0 = __fmaf_rn(w_own, __fadd_rn(ray.o[0], __fmul_rn(ray.d[0], z)), xacc0);
+                xacc1 = __fmaf_rn(w_own, __fadd_rn(ray.o[1], __fmul_rn(ray.d[1], z)), xacc1);
+                xacc2 = __fmaf_rn(w_own, __fadd_rn(ray.o[2], __fmul_rn(ray.d[2], z)), xacc2);
+            }
+        }
+    }
+    // the ring runs ahead across passes: no LDS-DMA may land after the workgroup ends
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the two lanes of a ray (samples 2p, 2p + 1) add their partials
+    racc0 = __fadd_rn(racc0, __shfl_xor(racc0, 16));
+    racc1 = __fadd_rn(racc1, __shfl_xor(racc1, 16));
+    racc2 = __fadd_rn(racc2, __shfl_xor(racc2, 16));
+    xacc0 = __fadd_rn(xacc0, __shfl_xor(xacc0, 16));
+    xacc1 = __fadd_rn(xacc1, __shfl_xor(xacc1, 16));
+    xacc2 = __fadd_rn(xacc2, __shfl_xor(xacc2, 16));
+    if (!ray_ok) return;
+    // this lane's features: tiles 4 odd .. 4 odd + 3, register v = 4 bq + r of tile t at row
+    // 32 t + 8 bq + 4 h + r
+    const uint32_t tb = odd ? 4u : 0u;
+    if (a.nseg > 1) {
+        const size_t Rr = (size_t)G.total_tiles * kTileRays;
+        float *pp = a.part + (size_t)seg * kPartQ * Rr + (size_t)tile * kTileRays + r16;
+        if (a.features) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int bq = 0; bq < 4; ++bq) {
+                    const f4 v = facc[(4 * t + bq) * 64];
+                    const uint32_t jf = 32 * (tb + t) + 8 * bq + 4 * h;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) pp[(size_t)(jf + r) * Rr] = v[r];
+                }
+        }
+        if (!odd && h == 0) {
+            const float q[8] = {racc0, racc1, racc2, xacc0, xacc1, xacc2, T, w_last};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pp[(size_t)(kW + k) * Rr] = q[k];
+        }
+        return;
+    }
+    const size_t HW = (size_t)G.H * G.W;
+    const size_t pix = (size_t)py * G.W + px;
+    if (!odd && h == 0) {
+        a.rgb[((size_t)b * 3 + 0) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, racc0));
+        a.rgb[((size_t)b * 3 + 1) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, racc1));
+        a.rgb[((size_t)b * 3 + 2) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, racc2));
+        if (a.xyz) {
+            a.xyz[((size_t)b * 3 + 0) * HW + pix] = xacc0;
+            a.xyz[((size_t)b * 3 + 1) * HW + pix] = xacc1;
+            a.xyz[((size_t)b * 3 + 2) * HW + pix] = xacc2;
+        }
+        if (a.mask) a.mask[(size_t)b * HW + pix] = w_last;
+    }
+    if (a.features) {
+        float *fbp = a.features + (size_t)b * kW * HW + pix;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int bq = 0; bq < 4; ++bq) {
+                const f4 v = facc[(4 * t + bq) * 64];
+                const uint32_t jf = 32 * (tb + t) + 8 * bq + 4 * h;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) fbp[(size_t)(jf + r) * HW] = v[r];
+            }
+    }
+}
+
 // Chains the nseg segment partials of every ray (see kPartQ): one thread per
 // (ray, quantity), quantities on grid.y.
 __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
@@ -971,6 +2247,16 @@ __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
 // ----------------------------------------------------------------------------
 // host
 // ----------------------------------------------------------------------------
+// field kernel variant (A/B while the one-wave-per-SIMD kernels are measured):
+// SDFR_FIELD_KERNEL = p (default) | q | r
+static char field_kernel_kind() {
+    static const char k = [] {
+        const char *e = getenv("SDFR_FIELD_KERNEL");
+        return (e && (e[0] == 'q' || e[0] == 'r')) ? e[0] : 'p';
+    }();
+    return k;
+}
+
 // Sample segments per ray: enough workgroups for every CU (>= 256), at most max_seg
 // (the call's max_field_segments, 0 = kFieldSplitMax), at least one pass (4 samples)
 // in every segment, and never with force_background (its last weight needs the
@@ -978,8 +2264,10 @@ __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
 uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_background,
                     uint32_t max_seg) {
     if (max_seg == 0 || max_seg > kFieldSplitMax) max_seg = kFieldSplitMax;
-    const uint32_t wgs = B * ((tiles_per_face + kPTiles - 1) / kPTiles);
-    const uint32_t npass = (N + kPSamples - 1) / kPSamples;
+    const bool r = field_kernel_kind() == 'r';
+    const uint32_t wg_tiles = r ? kRTiles : kPTiles, spp = r ? kRSamples : kPSamples;
+    const uint32_t wgs = B * ((tiles_per_face + wg_tiles - 1) / wg_tiles);
+    const uint32_t npass = (N + spp - 1) / spp;
     uint32_t nseg = 1;
     while (!force_background && wgs * nseg < 256 && 2 * nseg <= max_seg) {
         const uint32_t c = 2 * nseg, pps = (npass + c - 1) / c;
@@ -1071,6 +2359,7 @@ static int launch_xpack(const NetPtrs &P, uint32_t B, const float *styles, char 
     p.film = film;
     p.packed = packed;
     p.B = film ? B : 0;
+    p.rlayout = field_kernel_kind() == 'r';
     // blocks [0, B films x 2 x 256 / 4): FiLM rows; then (pack) the fragment packing
     const uint32_t nfilm = p.B * Net::kFilmN * 2 * kW / 4;
     const uint32_t blocks = nfilm + (pack ? (Net::kSlices * 512 + 255) / 256 : 0);
@@ -1119,8 +2408,12 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     f.part = part;
     f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background,
                                a->max_field_segments) : 1;
-    const uint32_t blocks = g.B * ((g.tiles_per_face + kPTiles - 1) / kPTiles) * f.nseg;
-    hipLaunchKernelGGL((field_p_kernel<Net>), dim3(blocks), dim3(kPThreads), 0, st, f);
+    const char kind = field_kernel_kind();
+    const uint32_t wg_tiles = kind == 'r' ? kRTiles : kPTiles;
+    const uint32_t blocks = g.B * ((g.tiles_per_face + wg_tiles - 1) / wg_tiles) * f.nseg;
+    if (kind == 'r') hipLaunchKernelGGL((field_r_kernel<Net>), dim3(blocks), dim3(kRThreads), 0, st, f);
+    else if (kind == 'q') hipLaunchKernelGGL((field_q_kernel<Net>), dim3(blocks), dim3(kQThreads), 0, st, f);
+    else hipLaunchKernelGGL((field_p_kernel<Net>), dim3(blocks), dim3(kPThreads), 0, st, f);
     int rc = check_launch("render: field (f16x3)");
     if (rc || f.nseg == 1) return rc;
     const uint32_t rays = g.total_tiles * kTileRays;
