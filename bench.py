@@ -37,9 +37,10 @@ METRIC = "rendered faces/sec/GPU at 256² (SDF+ngp path); 1/2/4/8-GPU scaling"
 FLOP_PER_SAMPLE = 550912          # renderer MLP as the reference runs it, SURVEY.md §8(d)
 # what the fused split-fp16 kernel computes per sample: input_linear and pts_linears.0
 # composed into one 32 -> 256 map (no nonlinearity between them), so
-# one 256 x 256 GEMM (131,072 FLOP) less; roofline.achieved / frac count these (what the
+# one 256 x 256 GEMM (131,072 FLOP) less, and the views layer at its 272 inputs
+# (32 + 256 + 256 + 272 rows of 256 x 2 FLOP); roofline.achieved / frac count these (what the
 # hardware runs), roofline.algorithmic_equivalent the reference's
-FLOP_PER_SAMPLE_FUSED = 419840
+FLOP_PER_SAMPLE_FUSED = 417792
 FLOP_PER_SAMPLE_SIREN = 1053696   # SirenGenerator MLP, SURVEY.md §8(d)
 GATHER_BYTES_PER_SAMPLE = 1024    # 16 levels x 8 corners x 2 x fp32
 MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
@@ -65,7 +66,7 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip the B=1/8 and host-copy measurements")
     p.add_argument("--traffic-json", default=str(REPO / "profiles" / "field_traffic.json"))
-    p.add_argument("--counters-json", default=str(REPO / "profiles" / "round3_counters.json"),
+    p.add_argument("--counters-json", default=str(REPO / "profiles" / "round4_counters.json"),
                    help="committed SQ counter summary (scripts/summarize_counters.py) quoted "
                         "as the field kernel's MFMA-busy fraction")
     return p.parse_args()
@@ -272,8 +273,8 @@ def main():
     flop = FLOP_PER_SAMPLE_SIREN if siren else (FLOP_PER_SAMPLE_FUSED if f16x3 else FLOP_PER_SAMPLE)
     field_tflops = flop * samples / (field_ms * 1e-3) / 1e12
     gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9 if not siren else 0.0
-    field_kernel = ("field_p_kernel<sdfr::SirenNet>" if siren else
-                    "field_p_kernel<sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
+    field_kernel = ("field_r_kernel<sdfr::SirenNet>" if siren else
+                    "field_r_kernel<sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
     def traffic_of(kernel):
         """HBM bytes per launch of `kernel` at this batch, from the committed
         rocprofv3 PMC passes (profiles/, scripts/summarize_profiles.py), or None."""
@@ -290,7 +291,7 @@ def main():
         (SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x GRBM_GUI_ACTIVE / XCDs)), or None."""
         try:
             ks = json.loads(Path(args.counters_json).read_text())["kernels"]
-            # the full templated name (field_p_kernel<sdfr::NgpNet> and <sdfr::SirenNet>
+            # the full templated name (field_r_kernel<sdfr::NgpNet> and <sdfr::SirenNet>
             # are different kernels)
             k = next(v for n, v in ks.items() if kernel in n.replace("sdfr::(anonymous namespace)::", ""))
             return {"mfma_busy_frac": k["mfma_busy_frac"],
@@ -302,13 +303,13 @@ def main():
         # fp32-accurate GEMMs as 3 fp16 MFMA terms: the attainable fp32-equivalent
         # peak is the dense fp16 MFMA peak / 3.  `achieved` /
         # `frac` count the FLOPs the kernel EXECUTES (ngp: input_linear and
-        # pts_linears.0 composed into one layer, 419,840 FLOP/sample) -- the hardware
+        # pts_linears.0 composed into one layer, 417,792 FLOP/sample) -- the hardware
         # utilisation; `algorithmic_equivalent` prices the same time at SURVEY.md
         # §8(d)'s per-sample FLOPs of the reference's network (550,912)
         ref_flop = FLOP_PER_SAMPLE_SIREN if siren else FLOP_PER_SAMPLE
         alg_tflops = field_tflops * ref_flop / flop
         peak = MFMA_F16_PEAK_TFLOPS / 3
-        roof = {"kernel": f"{field_kernel} (MLP as 3 split-fp16 v_mfma_f32_16x16x32_f16 "
+        roof = {"kernel": f"{field_kernel} (MLP as 3 split-fp16 v_mfma_f32_32x32x16_f16 "
                           "terms per fp32 tile + compositing)",
                 "bound": "mfma", "achieved": field_tflops, "peak": peak,
                 "unit": "TFLOP/s", "frac": field_tflops / peak,

@@ -76,7 +76,7 @@ def main(reps=5):
                           "field_ms": fms, "ms_per_mesh": mms,
                           "mesh_vertices": int(mesh.vertices.shape[0]),
                           "mesh_faces": int(mesh.faces.shape[0]),
-                          "field_tflops": 419840 * samples / fms / 1e9,
+                          "field_tflops": 417792 * samples / fms / 1e9,
                           "volume_shape": list(vol.shape)}), flush=True)
         del g, out, vol
         torch.cuda.empty_cache()

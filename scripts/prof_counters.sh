@@ -14,7 +14,7 @@ run() {   # name regex cmd...
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_WAIT_INST_LDS"
 P2="GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_LDS"
 FIELD=${FIELD_PREC:-f16x3}
-PMC=$P1 run field_sq1 field_p_kernel python3 "$R/scripts/render_only.py" $FIELD &&
-PMC=$P2 run field_sq2 field_p_kernel python3 "$R/scripts/render_only.py" $FIELD &&
+PMC=$P1 run field_sq1 field_r_kernel python3 "$R/scripts/render_only.py" $FIELD &&
+PMC=$P2 run field_sq2 field_r_kernel python3 "$R/scripts/render_only.py" $FIELD &&
 PMC=$P1 run conv_sq1 "conv_[xh]_kernel" python3 "$R/scripts/decoder_only.py" &&
 PMC=$P2 run conv_sq2 "conv_[xh]_kernel" python3 "$R/scripts/decoder_only.py"

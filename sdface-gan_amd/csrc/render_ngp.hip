@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
 
 // Per sample depth z and segment length dist = (z_{s+1} - z_s) |d| (1e10 |d| for the
 // last sample), sdf_model.py:240-243 -- the compositing inputs that do not depend on
-// the network, for field_p_kernel (tile order, as the features).  One thread per ray
+// the network, for field_r_kernel (tile order, as the features).  One thread per ray
 // (each z computed once; the gather kernel stays a pure gather).
 __global__ void __launch_bounds__(256) sample_zd_kernel(const GeomArgs g, float2 *__restrict__ zd) {
     const uint32_t rid = blockIdx.x * 256 + threadIdx.x;          // tile-order ray id

@@ -77,16 +77,17 @@ def test_workspace_size(sdfr):
     n = lib.sdfr_render_ngp_workspace_bytes(2, 64, 64, 24, 16)
     enc = 2 * 4096 * 24 * 16 * 2 * 4
     fixed = 67 * 1024 * 16 + 2 * 8 * 256 * 4          # fp32 fragments + FiLM vectors
-    # split-fp16 fragments (52 half-slices: layer 0 = input_linear o pts_linears.0),
-    # su, bias_s, the composed layer 0 (W [256][32] | b [256])
-    xfixed = 52 * 1024 * 16 + 2 * 4 * 256 * 4 + 33 * 256 * 4
+    # split-fp16 fragments (51 slices of one 16-K k-step: layer 0 = input_linear o
+    # pts_linears.0), su, bias_s, the composed layer 0 (W [256][32] | b [256])
+    xfixed = 51 * 1024 * 16 + 2 * 4 * 256 * 4 + 33 * 256 * 4
     zd = 2 * 4096 * 24 * 2 * 4                         # per-sample (z, segment length)
-    # 2 faces = 256 workgroups of 2 tiles: no sample split, no partials
-    assert enc + fixed + xfixed + zd <= n <= enc + fixed + xfixed + zd + 1536
-    # 1 face = 128 workgroups: rays split in 2 sample segments, partials of
+    # 2 faces = 128 workgroups of 4 tiles: rays split in 2 sample segments, partials of
     # (256 features + rgb, xyz, T, w_last) per segment and ray
+    part2 = 2 * (256 + 8) * 2 * 4096 * 4
+    assert enc + fixed + xfixed + zd + part2 <= n <= enc + fixed + xfixed + zd + part2 + 1536
+    # 1 face = 64 workgroups: 4 sample segments
     n1 = lib.sdfr_render_ngp_workspace_bytes(1, 64, 64, 24, 16)
-    part = 2 * (256 + 8) * 4096 * 4
+    part = 4 * (256 + 8) * 4096 * 4
     base1 = enc // 2 + 67 * 1024 * 16 + 8 * 256 * 4 + xfixed + zd // 2
     assert base1 + part <= n1 <= base1 + part + 1536
     n32 = lib.sdfr_render_ngp_workspace_bytes(32, 64, 64, 24, 16)   # >= 256 workgroups: no split
