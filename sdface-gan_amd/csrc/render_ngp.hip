@@ -115,6 +115,7 @@ struct EncodeArgs {
     GeomArgs g;
     const float *emb;
     const int32_t *offsets;
+    const f4 *gu;                  // [S_total] grid coordinate u (x, y, z) | inside [0,1]^3
     float *enc;                    // [L][S_total][2]
     LevelTable lt;
     int pair_ok;                   // table 16-B aligned (paired corner loads)
@@ -188,30 +189,6 @@ __device__ __forceinline__ void level_interp_pair(const float *__restrict__ grid
         for (uint32_t c = 0; c < 2; ++c) out[c] = __fmaf_rn(wts[idx], v[idx][c], out[c]);
 }
 
-// Normalised grid coordinate u of sample `sid` (grid.py:149 on the reference's
-// pts/normalisation chain, sdf_model.py:343-349); false for tile padding and for
-// samples outside [0,1]^3, whose features are 0 (gridencoder.cu:104-111).
-__device__ __forceinline__ bool sample_u(const GeomArgs &g, uint32_t sid, float (&u)[3]) {
-    const SampleId id = decode_sid(g, sid);
-    if (!id.valid) return false;
-    const uint32_t y = id.ray_local / g.W, x = id.ray_local % g.W;
-    const uint32_t ray_index = (id.b * g.H + y) * g.W + x;
-    Ray ray;
-    make_ray(g.cam + (size_t)id.b * 12, g.focal[id.b], g.pix_x[x], g.pix_y[y], g.half_res, ray);
-    const float nr = g.near_[id.b], fr = g.far_[id.b];
-    const float z = sample_z(g.sc, nr, fr, ray_index, id.s);
-    const float span = __fsub_rn(fr, nr);
-    bool in = true;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));            // :343
-        const float np_ = g.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;  // :349
-        u[k] = __fdiv_rn(__fadd_rn(np_, g.bound), __fmul_rn(2.0f, g.bound));     // grid.py:149
-        if (u[k] < 0 || u[k] > 1) in = false;
-    }
-    return in;
-}
-
 // One thread: SPT samples (256 apart) x LPT levels ({y, y+16/LPT, ...}, or
 // {LPT y, LPT y + 1, ...} with ADJ).  Branch-free: padding / out-of-box samples
 // gather at u = 0.5 and store 0, so every corner load of the thread can be in
@@ -265,8 +242,14 @@ __global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
     for (uint32_t k = 0; k < SPT; ++k) {
         sid[k] = (blockIdx.x * SPT + k) * 256 + threadIdx.x;
         live[k] = sid[k] < a.g.S_total;
-        in[k] = live[k] && sample_u(a.g, sid[k], u[k]);
-        if (!in[k]) u[k][0] = u[k][1] = u[k][2] = 0.5f;
+        // the sample's grid coordinate, computed once per sample by sample_geom_kernel
+        // (the per-level recomputation cost ~25 vector loads per wave on the texture
+        // addresser that the gather is bound by)
+        const f4 gv = a.gu[live[k] ? sid[k] : 0];
+        in[k] = live[k] && gv.w != 0.0f;
+        u[k][0] = in[k] ? gv.x : 0.5f;
+        u[k][1] = in[k] ? gv.y : 0.5f;
+        u[k][2] = in[k] ? gv.z : 0.5f;
     }
 #pragma unroll
     for (uint32_t j = 0; j < LPT; ++j) {
@@ -296,29 +279,49 @@ __global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
     }
 }
 
-// Per sample depth z and segment length dist = (z_{s+1} - z_s) |d| (1e10 |d| for the
-// last sample), sdf_model.py:240-243 -- the compositing inputs that do not depend on
-// the network, for field_r_kernel (tile order, as the features).  One thread per ray
-// (each z computed once; the gather kernel stays a pure gather).
-__global__ void __launch_bounds__(256) sample_zd_kernel(const GeomArgs g, float2 *__restrict__ zd) {
+// Per-sample geometry, one thread per ray (each z computed once), in tile order:
+//   gu [S]  the grid coordinate u = ((o + d z) (2 / (far - near)) + bound) / (2 bound)
+//           (sdf_model.py:343-349, grid.py:149; the same rounded ops as sample_u), w = 1
+//           when u lies in [0,1]^3 (the gather's zero-feature test, gridencoder.cu:104-111),
+//           0 for that and for tile-padding rays;
+//   zd [S]  depth z and segment length dist = (z_{s+1} - z_s) |d| (1e10 |d| for the last
+//           sample), sdf_model.py:240-243 -- the compositing inputs field_r_kernel reads
+//           (null: not wanted).
+__global__ void __launch_bounds__(256) sample_geom_kernel(const GeomArgs g, float2 *__restrict__ zd,
+                                                          f4 *__restrict__ gu) {
     const uint32_t rid = blockIdx.x * 256 + threadIdx.x;          // tile-order ray id
     if (rid >= g.total_tiles * kTileRays) return;
     const uint32_t tile = rid / kTileRays, n = rid % kTileRays;
     const uint32_t b = tile / g.tiles_per_face;
     uint32_t rl = (tile % g.tiles_per_face) * kTileRays + n;
-    if (rl >= g.H * g.W) rl = g.H * g.W - 1;                     // padding rays: any value
+    const bool ray_ok = rl < g.H * g.W;
+    if (!ray_ok) rl = g.H * g.W - 1;                             // padding rays: any value
     const uint32_t y = rl / g.W, x = rl % g.W;
     const uint32_t ray_index = (b * g.H + y) * g.W + x;
     Ray ray;
     make_ray(g.cam + (size_t)b * 12, g.focal[b], g.pix_x[x], g.pix_y[y], g.half_res, ray);
     const float nr = g.near_[b], fr = g.far_[b];
+    const float span = __fsub_rn(fr, nr);
     const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
-    float2 *out = zd + (size_t)tile * g.N * kTileRays + n;
+    const size_t base = (size_t)tile * g.N * kTileRays + n;
     float z = sample_z(g.sc, nr, fr, ray_index, 0);
     for (uint32_t s = 0; s < g.N; ++s) {
         const float zn = s + 1 < g.N ? sample_z(g.sc, nr, fr, ray_index, s + 1) : 0.0f;
-        const float dist = s + 1 < g.N ? __fmul_rn(__fsub_rn(zn, z), dnorm) : __fmul_rn(1e10f, dnorm);
-        out[(size_t)s * kTileRays] = make_float2(z, dist);
+        if (zd) {
+            const float dist = s + 1 < g.N ? __fmul_rn(__fsub_rn(zn, z), dnorm) : __fmul_rn(1e10f, dnorm);
+            zd[base + (size_t)s * kTileRays] = make_float2(z, dist);
+        }
+        f4 u;
+        bool in = ray_ok;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float p = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));            // :343
+            const float np_ = g.z_normalize ? __fdiv_rn(__fmul_rn(p, 2.0f), span) : p;  // :349
+            u[k] = __fdiv_rn(__fadd_rn(np_, g.bound), __fmul_rn(2.0f, g.bound));     // grid.py:149
+            if (u[k] < 0 || u[k] > 1) in = false;
+        }
+        u[3] = in ? 1.0f : 0.0f;
+        gu[base + (size_t)s * kTileRays] = u;
         z = zn;
     }
 }
@@ -789,10 +792,11 @@ struct Workspace {
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 // enc [L][S][2] | packed fp32 fragments | film | split-fp16 region (field_f16x3.hip) |
-// segment partials | zd [S] (z, segment length)
+// segment partials | zd [S] (z, segment length) | gu [S] (grid coordinate, inside flag)
 static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t L,
                         size_t *o_packed, size_t *o_film, size_t *o_x = nullptr,
-                        size_t *o_part = nullptr, size_t *o_zd = nullptr) {
+                        size_t *o_part = nullptr, size_t *o_zd = nullptr,
+                        size_t *o_gu = nullptr) {
     const size_t tiles = (size_t)B * ((H * W + kTileRays - 1) / kTileRays);
     const size_t S = tiles * N * kTileRays;
     size_t off = align256(S * L * 2 * sizeof(float));
@@ -806,6 +810,8 @@ static size_t ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, uint32_t
     off += align256(field_part_bytes(B, (H * W + kTileRays - 1) / kTileRays, N));
     if (o_zd) *o_zd = off;
     off += align256(S * 2 * sizeof(float));
+    if (o_gu) *o_gu = off;
+    off += align256(S * 4 * sizeof(float));
     return off;
 }
 
@@ -946,12 +952,20 @@ static void launch_encode_mode(hipStream_t st, const EncodeArgs &e) {
                        dim3(256), 0, st, e);
 }
 
+// the per-sample geometry (sample_geom_kernel: gu always, zd when wanted)
+static int launch_geom(const GeomArgs &g, float2 *zd, f4 *gu, hipStream_t st) {
+    hipLaunchKernelGGL(sample_geom_kernel, dim3((g.total_tiles * kTileRays + 255) / 256), dim3(256),
+                       0, st, g, zd, gu);
+    return check_launch("render_ngp: sample geometry");
+}
+
 static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
-                         const GeomArgs &g, float *enc, hipStream_t st) {
+                         const GeomArgs &g, float *enc, const f4 *gu, hipStream_t st) {
     EncodeArgs e;
     e.g = g;
     e.emb = w->embeddings;
     e.offsets = w->offsets;
+    e.gu = gu;
     e.enc = enc;
     e.pair_ok = (reinterpret_cast<uintptr_t>(w->embeddings) & 15u) == 0;
     make_level_table(16, w->log2_per_level_scale, w->base_resolution, e.lt);
@@ -1042,7 +1056,13 @@ int sdfr_render_ngp_encode_only(const sdfr_ngp_weights *w, const sdfr_ngp_render
     if (rc) return rc;
     GeomArgs g;
     fill_geom(w, a, g);
-    return launch_encode(w, a, g, reinterpret_cast<float *>(a->workspace), (hipStream_t)stream);
+    size_t o_packed, o_film, o_x, o_part, o_zd, o_gu;
+    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film, &o_x, &o_part, &o_zd, &o_gu);
+    char *ws = reinterpret_cast<char *>(a->workspace);
+    f4 *gu = reinterpret_cast<f4 *>(ws + o_gu);
+    hipStream_t st = (hipStream_t)stream;
+    if ((rc = launch_geom(g, nullptr, gu, st))) return rc;
+    return launch_encode(w, a, g, reinterpret_cast<float *>(ws), gu, st);
 }
 
 int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a,
@@ -1050,12 +1070,13 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     int rc = validate(w, a);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    size_t o_packed, o_film, o_x, o_part, o_zd;
-    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film, &o_x, &o_part, &o_zd);
+    size_t o_packed, o_film, o_x, o_part, o_zd, o_gu;
+    ws_layout(a->B, a->H, a->W, a->N, 16, &o_packed, &o_film, &o_x, &o_part, &o_zd, &o_gu);
     char *ws = reinterpret_cast<char *>(a->workspace);
     float *enc = reinterpret_cast<float *>(ws);
     f4 *packed = reinterpret_cast<f4 *>(ws + o_packed);
     float *film = reinterpret_cast<float *>(ws + o_film);
+    f4 *gu = reinterpret_cast<f4 *>(ws + o_gu);
 
     GeomArgs g;
     fill_geom(w, a, g);
@@ -1063,11 +1084,9 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     if (a->field_precision == SDFR_FIELD_F16X3) {
         if ((rc = launch_xprep_ngp(w, a, ws + o_x, film, st))) return rc;
         float2 *zd = reinterpret_cast<float2 *>(ws + o_zd);
-        hipLaunchKernelGGL(sample_zd_kernel, dim3((g.total_tiles * kTileRays + 255) / 256), dim3(256),
-                           0, st, g, zd);
-        if ((rc = check_launch("render_ngp: sample depths"))) return rc;
+        if ((rc = launch_geom(g, zd, gu, st))) return rc;
         record_event(a->stage_events[1], st);                  // the encode stage is the gather alone
-        if ((rc = launch_encode(w, a, g, enc, st))) return rc;
+        if ((rc = launch_encode(w, a, g, enc, gu, st))) return rc;
         record_event(a->stage_events[2], st);
         float *part = reinterpret_cast<float *>(ws + o_part);
         if ((rc = launch_xfield_ngp(w, a, g, enc, ws + o_x, film, st, part, zd))) return rc;
@@ -1075,8 +1094,9 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
         return SDFR_OK;
     }
     if ((rc = launch_prep(w, a, packed, film, st))) return rc;
+    if ((rc = launch_geom(g, nullptr, gu, st))) return rc;
     record_event(a->stage_events[1], st);
-    if ((rc = launch_encode(w, a, g, enc, st))) return rc;
+    if ((rc = launch_encode(w, a, g, enc, gu, st))) return rc;
     record_event(a->stage_events[2], st);
 
     FieldArgs f;

@@ -80,7 +80,7 @@ def test_workspace_size(sdfr):
     # split-fp16 fragments (51 slices of one 16-K k-step: layer 0 = input_linear o
     # pts_linears.0), su, bias_s, the composed layer 0 (W [256][32] | b [256])
     xfixed = 51 * 1024 * 16 + 2 * 4 * 256 * 4 + 33 * 256 * 4
-    zd = 2 * 4096 * 24 * 2 * 4                         # per-sample (z, segment length)
+    zd = 2 * 4096 * 24 * (2 + 4) * 4                   # per-sample (z, segment length), (u, inside)
     # 2 faces = 128 workgroups of 4 tiles: rays split in 2 sample segments, partials of
     # (256 features + rgb, xyz, T, w_last) per segment and ray
     part2 = 2 * (256 + 8) * 2 * 4096 * 4
