@@ -17,12 +17,13 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--out", default="gpurun_out/train_prof.txt")
+    p.add_argument("--net", default="ngp", choices=["ngp", "siren"])
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     sdfr = load()
     from sdface_gan_amd.training import CoordConv2d, RendererTrainer
     CoordConv2d.pad_to = 8
-    opt = sdfr.vol_render_opt(ngp=True, batch=8, chunk=2, train_renderer=True)
+    opt = sdfr.vol_render_opt(ngp=a.net == "ngp", batch=8, chunk=2, train_renderer=True)
     tr = RendererTrainer(opt, dev, seed=0)
     tr.g_module.renderer.rng_device = "device"
     tr.generator_test.renderer.rng_device = "device"

@@ -25,13 +25,15 @@ gamma / beta layers on the styles, CPU tensors, inference) stays on F.linear.
 
 Both networks route here (their layers carry ``train_kernels = True``).  The SIREN
 network's eikonal term is an ``autograd.grad(..., create_graph=True)`` through the MLP
-(sdf_model.py:224-229), so its loss reaches the weights through a double backward: a
-backward that runs with grad enabled (create_graph) computes the same gradients as
-differentiable ops -- ``linear()`` of these kernels again, ``_WGradF16x3``, the FiLM
-elementwise part in torch ops around ``_LinearGiven`` (the saved pre-activation put
-on the graph without recomputing it) -- and a plain backward runs straight on the
-kernels.  A backward also skips the gradients the running backward pass does not use
-(``_wanted``: the eikonal pass wants d/d pts only), per graph task.
+(sdf_model.py:224-229), so its loss reaches the weights through a double backward: its
+layers also carry ``double_backward = True``, and their backward, when it runs with grad
+enabled (create_graph), computes the same gradients as differentiable ops -- ``linear()``
+of these kernels again, ``_WGradF16x3``, the FiLM elementwise part in torch ops around
+``_LinearGiven`` (the saved pre-activation put on the graph without recomputing it).
+Every other backward (and the ngp network's, whose eikonal term leaves autograd in the
+grid encoder, grid.py:65-89) runs straight on the kernels.  A backward also skips the
+gradients the running backward pass does not use (``_wanted``: the eikonal pass wants
+d/d pts only), per graph task.
 """
 from __future__ import annotations
 
@@ -191,7 +193,7 @@ def _wanted(need: bool, edge) -> bool:
         return True
 
 
-def _linear_backward(gy, x, w, has_bias, needs, edges):
+def _linear_backward(gy, x, w, has_bias, needs, edges, twice=True):
     """Gradients of y = x W^T + b.  Inside a backward that builds a graph
     (autograd.grad(..., create_graph=True): the SIREN eikonal term) as differentiable
     ops -- linear() (these kernels again), _WGradF16x3, a sum -- so the eikonal loss
@@ -202,10 +204,10 @@ def _linear_backward(gy, x, w, has_bias, needs, edges):
     nw = _wanted(needs[1], edges[0])
     nb = has_bias and _wanted(needs[2], edges[1])
     gx = gw = gb = None
-    if torch.is_grad_enabled():
+    if twice and torch.is_grad_enabled():
         gy2 = gy.reshape(-1, N)
         if nx:
-            gx = linear(gy, w.t())
+            gx = linear(gy, w.t(), twice=True)
         if nw:
             gw = _WGradF16x3.apply(gy2, x.reshape(-1, K))
         if nb:
@@ -223,19 +225,21 @@ def _linear_backward(gy, x, w, has_bias, needs, edges):
 
 class _LinearF16x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, twice):
         N, K = weight.shape
         lead = x.shape[:-1]
         out = _gemm(_xk(x, K), _pack(_wk(weight), False), _a16(bias), N)
         ctx.save_for_backward(x, weight)        # the inputs themselves: double backward
         ctx.has_bias = bias is not None
         ctx.edges = (_edge(weight), _edge(bias))
+        ctx.twice = twice
         return out.view(*lead, N)
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        return _linear_backward(gy, x, w, ctx.has_bias, ctx.needs_input_grad, ctx.edges)
+        return (*_linear_backward(gy, x, w, ctx.has_bias, ctx.needs_input_grad, ctx.edges,
+                                  ctx.twice), None)
 
 
 class _LinearGiven(torch.autograd.Function):
@@ -273,9 +277,9 @@ class _WGradF16x3(torch.autograd.Function):
         gy2, x2 = ctx.saved_tensors
         dgy = dx = None
         if _wanted(ctx.needs_input_grad[0], ctx.edges[0]):
-            dgy = linear(x2, G)                 # d/dgy [m, n] = sum_k G[n, k] x[m, k]
+            dgy = linear(x2, G, twice=True)     # d/dgy [m, n] = sum_k G[n, k] x[m, k]
         if _wanted(ctx.needs_input_grad[1], ctx.edges[1]):
-            dx = linear(gy2, G.t())             # d/dx [m, k] = sum_n G[n, k] gy[m, n]
+            dx = linear(gy2, G.t(), twice=True)  # d/dx [m, k] = sum_n G[n, k] gy[m, n]
         return dgy, dx
 
 
@@ -285,7 +289,7 @@ class _FiLMLinearF16x3(torch.autograd.Function):
     elementwise part is one HIP kernel (dy, dgamma, dbeta, db) before the two GEMMs."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, gamma, beta):
+    def forward(ctx, x, weight, bias, gamma, beta, twice):
         N, K = weight.shape
         F_ = gamma.shape[0]
         lead = x.shape[:-1]
@@ -294,6 +298,7 @@ class _FiLMLinearF16x3(torch.autograd.Function):
         ctx.save_for_backward(x, weight, bias, gamma, beta, y)
         ctx.meta = (lead, bias is not None)
         ctx.edges = (_edge(weight), _edge(bias), _edge(gamma), _edge(beta))
+        ctx.twice = twice
         return out.view(*lead, N)
 
     @staticmethod
@@ -307,7 +312,7 @@ class _FiLMLinearF16x3(torch.autograd.Function):
         nb = has_bias and _wanted(ctx.needs_input_grad[2], ctx.edges[1])
         ng = _wanted(ctx.needs_input_grad[3], ctx.edges[2])
         nbe = _wanted(ctx.needs_input_grad[4], ctx.edges[3])
-        if torch.is_grad_enabled():
+        if ctx.twice and torch.is_grad_enabled():
             # create_graph (the SIREN eikonal term): the same gradients as differentiable
             # ops, y put on the graph as the linear layer's output (_LinearGiven)
             yl = _LinearGiven.apply(x, w, bias, y.view(*lead, N))
@@ -318,7 +323,7 @@ class _FiLMLinearF16x3(torch.autograd.Function):
                                           (None, None))
             gg = (du * yl).sum(red, keepdim=True).view(gamma.shape) if ng else None
             gbt = du.sum(red, keepdim=True).view(beta.shape) if nbe else None
-            return gx, gw, gb, gg, gbt
+            return gx, gw, gb, gg, gbt, None
         ds2 = _a16(ds.reshape(-1, N).contiguous())
         g2, b2 = _a16(gamma.reshape(F_, N)), _a16(beta.reshape(F_, N))
         dy, dg, db_, dbf = _film_bwd(ds2, y, g2, b2)
@@ -331,7 +336,7 @@ class _FiLMLinearF16x3(torch.autograd.Function):
             gb = dbf.sum(0)
         gg = dg.view(gamma.shape) if ng else None
         gbt = db_.view(beta.shape) if nbe else None
-        return gx, gw, gb, gg, gbt
+        return gx, gw, gb, gg, gbt, None
 
 
 def _head_fwd(x2, w, bias):
@@ -366,13 +371,14 @@ class _LinearHead(torch.autograd.Function):
     """x W^T + b for the narrow heads (J <= 4 outputs): HBM-streaming HIP kernels."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, twice):
         J, K = weight.shape
         lead = x.shape[:-1]
         out = _head_fwd(_a16(x.reshape(-1, K)), _a16(weight), bias)
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.edges = (_edge(weight), _edge(bias))
+        ctx.twice = twice
         return out.view(*lead, J)
 
     @staticmethod
@@ -383,19 +389,19 @@ class _LinearHead(torch.autograd.Function):
         need_x = ctx.needs_input_grad[0]
         need_w = _wanted(ctx.needs_input_grad[1], ctx.edges[0])
         need_b = ctx.has_bias and _wanted(ctx.needs_input_grad[2], ctx.edges[1])
-        if torch.is_grad_enabled():
+        if ctx.twice and torch.is_grad_enabled():
             # create_graph (the SIREN eikonal term runs through sigma_linear): differentiable
             gy2 = gy.reshape(-1, J)
-            gx = linear(gy, weight.t()) if need_x else None
+            gx = linear(gy, weight.t(), twice=True) if need_x else None
             gw = gy2.t().mm(x.reshape(-1, K)) if need_w else None
             gb = gy2.sum(0) if need_b else None
-            return gx, gw, gb
+            return gx, gw, gb, None
         gx, gw, gb = _head_bwd(gy.reshape(-1, J).contiguous(), _a16(x.reshape(-1, K)),
                                _a16(weight), need_x, need_w, need_b)
-        return (gx.view(*lead, K) if gx is not None else None), gw, gb
+        return (gx.view(*lead, K) if gx is not None else None), gw, gb, None
 
 
-def film_linear(x, weight, bias, gamma, beta, kernels=True):
+def film_linear(x, weight, bias, gamma, beta, kernels=True, twice=False):
     """FiLMSiren's ``sin(gamma * F.linear(x, weight, bias) + beta)`` (sdf_model.py:62-67),
     gamma / beta [F, 1, ..., 1, N] broadcast over each face's samples: fused on the HIP
     kernels for the renderer MLP's training shapes (and ``kernels``), the reference's
@@ -404,8 +410,8 @@ def film_linear(x, weight, bias, gamma, beta, kernels=True):
     if (kernels and _routable(x, weight) and x.shape[0] == F_ and gamma.shape[-1] == weight.shape[0]
             and gamma.numel() == F_ * weight.shape[0] and beta.shape == gamma.shape
             and weight.shape[1] > 32):
-        return _FiLMLinearF16x3.apply(x, weight, bias, gamma, beta)
-    return torch.sin(gamma * linear(x, weight, bias, kernels) + beta)
+        return _FiLMLinearF16x3.apply(x, weight, bias, gamma, beta, twice)
+    return torch.sin(gamma * linear(x, weight, bias, kernels, twice) + beta)
 
 
 def _on_device(x: torch.Tensor) -> bool:
@@ -434,12 +440,15 @@ def _head_routable(x: torch.Tensor, weight: torch.Tensor) -> bool:
     return J <= 4 and K % 4 == 0 and K <= 256 and x.numel() // K >= 1024
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, kernels=True) -> torch.Tensor:
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, kernels=True,
+           twice=False) -> torch.Tensor:
     """F.linear(x, weight, bias), on the split-fp16 MFMA kernels for the renderer MLP's
     training shapes (module docstring) or the narrow-head kernels when ``kernels``, on
-    F.linear otherwise."""
+    F.linear otherwise.  ``twice``: the backward may itself be differentiated (a graph
+    built by autograd.grad(create_graph=True) through this layer must reach its
+    parameters: the SIREN eikonal term); otherwise it runs straight on the kernels."""
     if kernels and _routable(x, weight):
-        return _LinearF16x3.apply(x, weight, bias)
+        return _LinearF16x3.apply(x, weight, bias, twice)
     if kernels and _head_routable(x, weight):
-        return _LinearHead.apply(x, weight, bias)
+        return _LinearHead.apply(x, weight, bias, twice)
     return F.linear(x, weight, bias)

@@ -56,6 +56,7 @@ class LinearLayer(nn.Module):
 
     # the renderer networks' layers take the training kernels (linear.py); others F.linear
     train_kernels = False
+    double_backward = False       # set by SirenGenerator (its eikonal loss, linear.py)
     skip_identity = True          # False: the reference's literal 1 * y + 0 (A/B aid)
 
     def forward(self, input):
@@ -63,7 +64,7 @@ class LinearLayer(nn.Module):
         # training shapes (linear.py).  The reference's ``1 * y + 0`` (the defaults) is
         # the identity up to the sign of zero; skipping it saves two full passes over
         # the [rays, samples, 256] activation forward and one backward.
-        y = linear(input, self.weight, self.bias, self.train_kernels)
+        y = linear(input, self.weight, self.bias, self.train_kernels, self.double_backward)
         if self.std_init != 1 or not self.skip_identity:
             y = self.std_init * y
         if self.bias_init != 0 or not self.skip_identity:
@@ -75,6 +76,7 @@ class FiLMSiren(nn.Module):
     """``sin(gamma(style) * (x W^T + b) + beta(style))`` (sdf_model.py:44-69)."""
 
     train_kernels = False         # set by NGPSIRENGenerator / SirenGenerator (linear.py)
+    double_backward = False       # set by SirenGenerator (its eikonal loss, linear.py)
 
     def __init__(self, in_channel, out_channel, style_dim, is_first=False):
         super().__init__()
@@ -99,7 +101,8 @@ class FiLMSiren(nn.Module):
         beta = self.beta(style).view(shape)
         # film_linear(): the reference's ops, or for the MLP's training shapes the GEMM
         # with the activation fused on the HIP kernels (linear.py, ngp network only)
-        return film_linear(input, self.weight, self.bias, gamma, beta, self.train_kernels)
+        return film_linear(input, self.weight, self.bias, gamma, beta, self.train_kernels,
+                           self.double_backward)
 
 
 # ---------------------------------------------------------------------------
@@ -125,6 +128,7 @@ class SirenGenerator(nn.Module):
         # loss reaches these weights through autograd.grad(create_graph=True), linear.py)
         for m in [*self.pts_linears, self.views_linears, self.rgb_linear, self.sigma_linear]:
             m.train_kernels = True
+            m.double_backward = True
 
     def forward(self, x, styles):
         pts, views = torch.split(x, [self.input_ch, self.input_ch_views], dim=-1)

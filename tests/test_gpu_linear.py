@@ -41,7 +41,7 @@ def test_linear_forward_and_backward_vs_float64(sdfr, M, N, K, mag):
     w = (_rand((N, K), "unit", 2) * 0.05).to(DEV).requires_grad_(True)
     b = (_rand((N,), "unit", 3) * 0.1).to(DEV).requires_grad_(True)
     gy = _rand((M, N), mag, 4).to(DEV)
-    y = _LinearF16x3.apply(x, w, b)
+    y = _LinearF16x3.apply(x, w, b, False)
     y.backward(gy)
     torch.cuda.synchronize()
     xd, wd, bd, gyd = (t.detach().double().cpu() for t in (x, w, b, gy))
@@ -75,6 +75,15 @@ def test_linear_routing_and_deterministic(sdfr):
         assert lin.linear(x, w).grad_fn is None             # inference: F.linear
     s = torch.randn(8, 256, device=DEV)
     assert "LinearF16x3" not in type(lin.linear(s.requires_grad_(), w).grad_fn).__name__
+    # in features up to 272 take both directions (padded); 276 would need a 288-wide input
+    # gradient, which the kernels do not take: F.linear
+    for K, routed in ((259, True), (272, True), (276, False)):
+        xk = torch.randn(4096, K, device=DEV, requires_grad=True)
+        wk = torch.randn(256, K, device=DEV, requires_grad=True)
+        yk = lin.linear(xk, wk)
+        assert ("LinearF16x3" in type(yk.grad_fn).__name__) == routed, K
+        yk.square().sum().backward()
+        assert xk.grad.shape == xk.shape and wk.grad.shape == wk.shape
     grads = []
     for _ in range(2):
         w.grad = None
@@ -156,7 +165,7 @@ def test_film_linear_vs_float64(sdfr, F_, R, K):
     gam = (30 + 15 * _rand((F_, 1, N), "unit", 8) * 0.2).to(DEV).requires_grad_(True)
     bet = (0.25 * _rand((F_, 1, N), "unit", 9)).to(DEV).requires_grad_(True)
     ds = _rand((F_, R, N), "unit", 10).to(DEV)
-    s = _FiLMLinearF16x3.apply(x, w, b, gam, bet)
+    s = _FiLMLinearF16x3.apply(x, w, b, gam, bet, False)
     s.backward(ds)
     torch.cuda.synchronize()
     xd, wd, bd, gd, btd = (t.detach().double().cpu().requires_grad_(True)
@@ -199,5 +208,5 @@ def test_linear_head_vs_float64(sdfr, J, K):
         _bound_check(name, got, exact, scale, c=64.0)
     g0 = w.grad.clone()
     w.grad = None
-    _LinearHead.apply(x, w, b).backward(gy)
+    _LinearHead.apply(x, w, b, False).backward(gy)
     assert torch.equal(g0, w.grad)
