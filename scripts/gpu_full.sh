@@ -1,11 +1,15 @@
 #!/bin/bash
-# Full GPU session: parity suite (parity record), smoke, then the bench line.
+# All GPU tests, then N short bench runs (no CPU baseline / extras)
 set -u
-R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
-bash scripts/gpu_tests.sh; rc=$?
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stop: pytest rc=$rc"; exit $rc; fi
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-src=$?; echo "smoke rc=$src"; tail -2 gpurun_out/smoke.log; [ $src -eq 0 ] || exit $src
-timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
-brc=$?; echo "bench rc=$brc"; tail -1 gpurun_out/bench.log | cut -c1-400
-exit $((rc > brc ? rc : brc))
+mkdir -p gpurun_out
+export SDFR_PARITY_JSON=gpurun_out/parity_full.json
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 \
+    --timeout-method thread > gpurun_out/pytest_full.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_full.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+for i in $(seq 1 ${NBENCH:-2}); do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras > gpurun_out/bench_full_$i.log 2>&1 || exit $?
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/bench_full_$i.log').read().strip().splitlines()[-1])
+print('bench', round(d['value'],1), 'ms', round(d['ms_per_step'],3), {k: round(v,3) for k, v in d.get('stage_ms_per_step', {}).items()})"
+done

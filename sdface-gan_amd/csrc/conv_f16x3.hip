@@ -42,6 +42,7 @@ constexpr int kCT = 128;        // output channels per workgroup
 constexpr int kPT = 256;        // output pixels per workgroup
 constexpr int kStepF4 = 1024;   // f4 of weight fragments per K-step (16 KB)
 constexpr int kStages = 3;   // LDS-DMA ring depth (kStages - 1 K-steps in flight)
+constexpr uint32_t kCusPerXcd = 32;   // MI355X: 256 CUs in 8 XCDs (persistent grids)
 
 __device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a),
@@ -574,11 +575,24 @@ __global__ void __launch_bounds__(512, 1) conv_splitk_kernel(const ConvArgs a) {
 // mid-step barrier / next-step fragment schedule are conv_x_kernel's;
 // the nine taps of a channel group are unrolled (stage = tap % 3), two groups per
 // loop iteration so the register sets alternate.
+//
+// Persistent: one workgroup per CU (LDS 155 KB) walks a strided share of its XCD's
+// contiguous tile run.  After the last K-step's barrier every LDS buffer is free, so
+// the NEXT tile's prologue (halo of channel group 0, weights of its first three
+// K-steps) is issued there and lands under the last MFMAs and this tile's epilogue,
+// instead of behind a workgroup exit + dispatch + cold prologue.  The epilogue's
+// per-channel operands (demod, bias, s_next, ToRGB weights) and the block's noise
+// arrive in LDS by six more DMA pieces during the tile's second K-step, so the
+// epilogue issues no global load that would have to wait (in-order vmcnt) behind the
+// next tile's DMAs.
 // ----------------------------------------------------------------------------
 constexpr uint32_t kHaloW = 18;
 constexpr uint32_t kHaloPx = kHaloW * kHaloW;          // 324
 constexpr uint32_t kHaloPieces = 48;                  // 6 per wave; 41 carry pixels
 constexpr uint32_t kHaloF4 = kHaloPieces * 64;        // 48 KB per buffer
+// epilogue operand pieces (1 KB, one per wave 0..5): demod, bias, s_next (128
+// channels in lanes 0-31 each), ToRGB weights o = 0 | 1, o = 2, noise (16 rows x 16)
+constexpr uint32_t kEpPieces = 6;
 
 __device__ __forceinline__ uint32_t halo_swz(uint32_t hx) { return (hx & 4u) | ((hx >> 1) & 1u); }
 
@@ -587,9 +601,81 @@ __device__ __forceinline__ f4 lds_f4(uint32_t byte_addr) {   // LDS byte address
     return *(const lds_f4_t *)(size_t)byte_addr;
 }
 
+// conv_epilogue<true> for a 16 x 16 block whose epilogue operands sit in LDS (Ep):
+// same arithmetic in the same order; lane (n, g) of tile (i, j) holds channels
+// 16 (4 wm + i) + 4 g .. +3 of block pixel (row 4 wn + j, column n).
+__device__ __forceinline__ void conv_h_epilogue(const ConvArgs &a, f4 (&acc)[4][4], const f4 *Ep,
+                                                uint32_t lane, uint32_t wm, uint32_t wn,
+                                                uint32_t cb, uint32_t pix0, uint32_t b) {
+    __shared__ float red[4][4][16][3];          // [wn][j][n][o] from the wm = 1 waves
+    // opaque copies: nothing of the epilogue's address arithmetic is hoisted out of
+    // conv_h_kernel's tile loop (it would stay live through the K loop and spill)
+    asm volatile("" : "+v"(lane), "+s"(wm), "+s"(wn));
+    uint32_t W = a.Win, HW = a.Hin * a.Win;
+    asm volatile("" : "+s"(W), "+s"(HW));
+    const uint32_t n = lane & 15u, g = lane >> 4;
+    const ActEpi &e = a.e;
+    const float nw = e.noise ? *e.noise_weight : 0.0f;
+    const float *epn = reinterpret_cast<const float *>(Ep + 5 * 64);
+    float part[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[j][0] = part[j][1] = part[j][2] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t lq = (4 * wm + i) * 4 + g;     // f4 index of the channel quad
+        const uint32_t ch = cb * kCT + 4 * lq;
+        const f4 dm = Ep[lq], bs = Ep[64 + lq];
+        const f4 sn = e.s_next ? Ep[128 + lq] : f4{1.0f, 1.0f, 1.0f, 1.0f};
+        const f4 rw[3] = {Ep[192 + lq], Ep[224 + lq], Ep[256 + lq]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t r = 4 * wn + j;
+            const uint32_t P = pix0 + r * W + n;
+            const float nz = e.noise ? nw * epn[r * 16 + n] : 0.0f;
+            f4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = act1(acc[i][j][q], dm[q], nz, bs[q], e.slope, e.scale);
+            if (e.ys) store_split8_pair(e.ys, (size_t)P * a.Cout + (ch & ~7u), v * sn, g);
+#pragma unroll
+            for (int o = 0; o < 3; ++o)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) part[j][o] = fmaf(v[q], rw[o][q], part[j][o]);
+        }
+    }
+    if (e.rgb_w) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int o = 0; o < 3; ++o) {
+                part[j][o] += __shfl_xor(part[j][o], 16, 64);
+                part[j][o] += __shfl_xor(part[j][o], 32, 64);
+            }
+        if (wm == 1 && g == 0)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int o = 0; o < 3; ++o) red[wn][j][n][o] = part[j][o];
+        // raw barrier: the LDS writes above are all it orders (a __syncthreads fence
+        // could add a vmcnt wait on the next tile's DMAs)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (wm == 0 && g < 3) {                 // lane (n, g = o) stores channel o
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t P = pix0 + (4 * wn + j) * W + n;
+                const float s = (g == 0 ? part[j][0] : g == 1 ? part[j][1] : part[j][2]) +
+                                red[wn][j][n][g];
+                e.rgbp[(((size_t)cb * a.B + b) * 3 + g) * HW + (P - b * HW)] = s;
+            }
+        }
+        // red is rewritten by the next tile's epilogue only after that tile's barriers
+    }
+}
+
 __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     __shared__ f4 As[3][kStepF4];        // weight ring [mt 8][hi,lo][64]
     __shared__ f4 Hs[2][kHaloF4];        // halo images, by channel-group parity
+    __shared__ f4 Ep[kEpPieces * 64];    // epilogue operands of the current tile
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t wm = wave & 1u, wn = wave >> 1;
@@ -598,23 +684,28 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     const uint32_t nbx = W / 16, nby = H / 16;
     const v4i rw = make_rsrc(a.wpk, 9u * nC * nB * kStepF4 * 16u);
     const v4i rx = make_rsrc(a.xs, a.B * H * W * a.Cin * 4);
-    // tile -> Cout block cb, first pixel pix0 and this wave's halo pieces k = wave + 8 i
-    // (per-lane source offsets at channel group 0; the group moves the buffer's
-    // soffset by 128 B)
-    uint32_t cb = 0, pix0 = 0, hoff[6];
+    // tile -> Cout block cb, first pixel pix0 (image b, block origin y0, x0) and this
+    // wave's halo pieces k = wave + 8 i (per-lane source offsets at channel group 0;
+    // the group moves the buffer's soffset by 128 B)
+    uint32_t cb = 0, pix0 = 0, bimg = 0, y0 = 0, x0 = 0, hoff[6];
     auto setup = [&](uint32_t tile) {
+        uint32_t ln = lane, wv = wave;        // opaque: computed here, not hoisted
+        asm volatile("" : "+v"(ln), "+s"(wv));
         cb = tile % nB;
         uint32_t blk = tile / nB;
         const uint32_t bx = blk % nbx;
         blk /= nbx;
         const uint32_t by = blk % nby, b = blk / nby;
-        pix0 = (b * H + by * 16) * W + bx * 16;
+        bimg = b;
+        y0 = by * 16;
+        x0 = bx * 16;
+        pix0 = (b * H + y0) * W + x0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            const uint32_t h = 8u * (wave + 8u * i) + (lane >> 3);
+            const uint32_t h = 8u * (wv + 8u * i) + (ln >> 3);
             const uint32_t hy = h / kHaloW, hx = h - hy * kHaloW;
-            const uint32_t q = (lane & 7u) ^ halo_swz(hx);
-            const int y = (int)(by * 16 + hy) - 1, x = (int)(bx * 16 + hx) - 1;
+            const uint32_t q = (ln & 7u) ^ halo_swz(hx);
+            const int y = (int)(y0 + hy) - 1, x = (int)(x0 + hx) - 1;
             const bool ok = h < kHaloPx && y >= 0 && y < (int)H && x >= 0 && x < (int)W;
             hoff[i] = ok ? (((b * H + (uint32_t)y) * W + (uint32_t)x) * a.Cin * 4u + q * 16u)
                          : 0x7FFFFFF0u;
@@ -645,6 +736,37 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     auto fire_h = [&](int buf, int i) {
         set_m0(lds_addr(&Hs[buf][(wave + 8u * i) * 64]));
         dma16<0>(uni(rx), hoff[i], __builtin_amdgcn_readfirstlane(hsoff));
+    };
+    // the current tile's epilogue operands -> Ep (wave w moves piece w; null tensors
+    // and the idle lanes read past num_records = zeros)
+    auto fire_ep = [&] {
+        if (wave >= kEpPieces) return;
+        uint32_t lane = tid & 63u;            // opaque: computed here, not hoisted
+        asm volatile("" : "+v"(lane));
+        const ActEpi &e = a.e;
+        const uint32_t OOB = 0x7FFFFFF0u;
+        const uint32_t ch = cb * kCT + 4u * (lane & 31u), lo = lane < 32;
+        const uint32_t bc = a.B * a.Cout * 4u;
+        const float *base;
+        uint32_t bytes, off;
+        if (wave == 0) {
+            base = e.demod; bytes = bc; off = lo ? (bimg * a.Cout + ch) * 4u : OOB;
+        } else if (wave == 1) {
+            base = e.bias; bytes = a.Cout * 4u; off = lo ? ch * 4u : OOB;
+        } else if (wave == 2) {
+            base = e.s_next; bytes = e.s_next ? bc : 0u; off = lo ? (bimg * a.Cout + ch) * 4u : OOB;
+        } else if (wave == 3) {
+            base = e.rgb_w; bytes = e.rgb_w ? 3u * bc : 0u;
+            off = ((bimg * 3u + (lane >> 5)) * a.Cout + ch) * 4u;
+        } else if (wave == 4) {
+            base = e.rgb_w; bytes = e.rgb_w ? 3u * bc : 0u;
+            off = lo ? ((bimg * 3u + 2u) * a.Cout + ch) * 4u : OOB;
+        } else {
+            base = e.noise; bytes = e.noise ? a.B * H * W * 4u : 0u;
+            off = ((bimg * H + y0 + (lane >> 2)) * W + x0 + 4u * (lane & 3u)) * 4u;
+        }
+        set_m0(lds_addr(&Ep[wave * 64]));
+        dma16<0>(uni(make_rsrc(base, bytes)), off, 0u);
     };
 
     f4 acc[4][4];
@@ -679,35 +801,12 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         }
     };
 
-    // K-step (c, T): MFMAs of rows 0-1; wait for step (c, T)+1 (in flight may stay only
-    // what step (c, T)-1 fired); barrier; fire step +3's weights (into stage T % 3) and,
-    // at taps 0-5, halo piece T of group c + 1 (into the buffer group c - 1 used, whose
-    // last fragment reads were before the barrier of (c - 1, 8)); read step +1's
-    // fragments; MFMAs of rows 2-3.
-    // P: parity of group c (its halo buffer), compile-time in the unrolled loop
-    auto step = [&](uint32_t c, auto tapc, auto parc, const f4 (&R)[16], f4 (&Rn)[16]) {
-        constexpr int T = decltype(tapc)::value;
-        constexpr int P = decltype(parc)::value;
-        const uint32_t s = c * 9 + T, nk = nC * 9;
-        const bool prev_w = s + 2 < nk;                     // step s-1 fired weights
-        const bool prev_h = T != 0 && T - 1 <= 5 && c + 1 < nC;   // ... and a halo piece
-        mfma_rows(R, 0, 2);
-        if (prev_w && prev_h) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
-        else if (prev_w) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (s + 3 < nk) {
-            constexpr uint32_t T3 = (T + 3) % 9;
-            fire_w(c + (T + 3) / 9, T3, T % 3);
-        }
-        if constexpr (T <= 5) {
-            if (c + 1 < nC) fire_h(1 - P, T);
-        }
-        if (s + 1 < nk) {
-            if constexpr (T == 8) read_frags(Rn, std::integral_constant<int, 0>{}, P ? hs0 : hs1);
-            else read_frags(Rn, std::integral_constant<int, T + 1>{}, P ? hs1 : hs0);
-        }
-        mfma_rows(R, 2, 2);
+    // split term t (0: lo.hi, 1: hi.lo, 2: hi.hi; mfma_rows' order) of row i
+    auto mfma_quad = [&](const f4 (&R)[16], int i, int t) {
+        const f4 &ra = t == 0 ? R[4 + i] : R[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc[i][j] = mfma16(ra, t == 1 ? R[12 + j] : R[8 + j], acc[i][j]);
     };
 
     // prologue of a tile: halo of group 0, weights of steps 0-2 (every LDS buffer is
@@ -721,59 +820,146 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         fire_w(0, 1, 1);
         fire_w(0, 2, 2);
     };
-    // XCD-aware tile order (slot_tile's, one class)
-    const uint32_t ntiles = a.cls[0].ntiles, per_xcd = (ntiles + 7) >> 3;
-    const uint32_t slot = blockIdx.x;
-    const uint32_t tile = __builtin_amdgcn_readfirstlane((slot & 7u) * per_xcd + (slot >> 3));
-    if (tile >= ntiles) return;    // padding slot (whole workgroup)
+
+    // persistent schedule: XCD x owns tiles [x per, (x + 1) per) (Cout block fastest,
+    // as slot_tile); its workgroups take them with stride nwg, so the ones running
+    // together share halos and weights in the XCD's L2
+    const uint32_t ntiles = a.cls[0].ntiles, per = (ntiles + 7) >> 3;
+    const uint32_t xcd = blockIdx.x & 7u, nwg = gridDim.x >> 3;
+    const uint32_t tend = min(xcd * per + per, ntiles);
+    uint32_t tile = __builtin_amdgcn_readfirstlane(xcd * per + (blockIdx.x >> 3));
+    if (tile >= tend) return;    // idle workgroup (whole)
+    uint32_t next = tile + nwg;
+    bool has_next = next < tend;
+
+    // K-step (c, T): MFMAs of rows 0-1; wait for step (c, T)+1 (in flight may stay only
+    // what step (c, T)-1 fired); barrier; fire step +3's weights (into stage T % 3) and,
+    // at taps 0-5, halo piece T of group c + 1 (into the buffer group c - 1 used, whose
+    // last fragment reads were before the barrier of (c - 1, 8)); read step +1's
+    // fragments; MFMAs of rows 2-3.  The tile's second step also fires the epilogue
+    // operands (older than everything step 3 waits for); the last one fires the next
+    // tile's prologue.
+    // P: parity of group c (its halo buffer), compile-time in the unrolled loop
+    auto step = [&](uint32_t c, auto tapc, auto parc, const f4 (&R)[16], f4 (&Rn)[16]) {
+        constexpr int T = decltype(tapc)::value;
+        constexpr int P = decltype(parc)::value;
+        const uint32_t s = c * 9 + T, nk = nC * 9;
+        const bool prev_w = s + 2 < nk;                     // step s-1 fired weights
+        const bool prev_h = T != 0 && T - 1 <= 5 && c + 1 < nC;   // ... and a halo piece
+        mfma_rows(R, 0, 2);
+        if (prev_w && prev_h) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+        else if (prev_w) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if constexpr (T == 1) {
+            if (c == 0) fire_ep();
+        }
+        // Issue order after the barrier, pinned by scheduling fences (left to itself
+        // the compiler clumps all DMAs and reads in front of the MFMAs, and an LDS-DMA
+        // issued in such a clump costs the wave several times its price between
+        // MFMAs; measured -3.7 % conv time): the next step's 16 fragment reads one per
+        // MFMA of row 2 (after the last step they read stale data nobody uses), then
+        // the weight pair and the halo piece (and after the last step the next tile's
+        // prologue) between the three MFMA quads of row 3.
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (T == 8) read_frags(Rn, std::integral_constant<int, 0>{}, P ? hs0 : hs1);
+        else read_frags(Rn, std::integral_constant<int, T + 1>{}, P ? hs1 : hs0);
+        mfma_rows(R, 2, 1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_quad(R, 3, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 3 < nk) {
+            constexpr uint32_t T3 = (T + 3) % 9;
+            fire_w(c + (T + 3) / 9, T3, T % 3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_quad(R, 3, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (T <= 5) {
+            if (c + 1 < nC) fire_h(1 - P, T);
+        }
+        if constexpr (T == 8) {
+            if (s + 1 == nk && has_next) {
+                setup(next);
+                prologue();
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_quad(R, 3, 2);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
     setup(tile);
     prologue();
+    bool first = true;
+    for (;;) {
+        const uint32_t ecb = cb, epix0 = pix0, eb = bimg;    // this tile (setup moves on)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    // everything but step 2's weights has landed
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    f4 R0[16], R1[16];
-    read_frags(R0, std::integral_constant<int, 0>{}, hs0);
-    // two channel groups per iteration: 18 steps alternate R0 / R1
-    uint32_t c = 0;
-    for (; c + 1 < nC; c += 2) {
-        step(c, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, R0, R1);
-        step(c, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}, R1, R0);
-        step(c, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{}, R0, R1);
-        step(c, std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{}, R1, R0);
-        step(c, std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{}, R0, R1);
-        step(c, std::integral_constant<int, 5>{}, std::integral_constant<int, 0>{}, R1, R0);
-        hsoff += 128u;
-        step(c, std::integral_constant<int, 6>{}, std::integral_constant<int, 0>{}, R0, R1);
-        step(c, std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, R1, R0);
-        step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
-        step(c + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, R1, R0);
-        step(c + 1, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, R0, R1);
-        step(c + 1, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{}, R1, R0);
-        step(c + 1, std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{}, R0, R1);
-        step(c + 1, std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, R1, R0);
-        step(c + 1, std::integral_constant<int, 5>{}, std::integral_constant<int, 1>{}, R0, R1);
-        hsoff += 128u;
-        step(c + 1, std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{}, R1, R0);
-        step(c + 1, std::integral_constant<int, 7>{}, std::integral_constant<int, 1>{}, R0, R1);
-        step(c + 1, std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{}, R1, R0);
+            for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        // everything but step 2's weights has landed (after the first tile: everything,
+        // the previous epilogue's stores included); the previous epilogue's LDS reads
+        // are done everywhere after the barrier
+        if (first) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        f4 R0[16], R1[16];
+        read_frags(R0, std::integral_constant<int, 0>{}, hs0);
+        // two channel groups per iteration: 18 steps alternate R0 / R1
+        uint32_t c = 0;
+        for (; c + 1 < nC; c += 2) {
+            step(c, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, R0, R1);
+            step(c, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}, R1, R0);
+            step(c, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{}, R0, R1);
+            step(c, std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{}, R1, R0);
+            step(c, std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{}, R0, R1);
+            step(c, std::integral_constant<int, 5>{}, std::integral_constant<int, 0>{}, R1, R0);
+            hsoff += 128u;
+            step(c, std::integral_constant<int, 6>{}, std::integral_constant<int, 0>{}, R0, R1);
+            step(c, std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, R1, R0);
+            step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
+            step(c + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, R1, R0);
+            step(c + 1, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, R0, R1);
+            step(c + 1, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{}, R1, R0);
+            step(c + 1, std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{}, R0, R1);
+            step(c + 1, std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, R1, R0);
+            step(c + 1, std::integral_constant<int, 5>{}, std::integral_constant<int, 1>{}, R0, R1);
+            hsoff += 128u;
+            step(c + 1, std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{}, R1, R0);
+            step(c + 1, std::integral_constant<int, 7>{}, std::integral_constant<int, 1>{}, R0, R1);
+            step(c + 1, std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{}, R1, R0);
+        }
+        if (c < nC) {
+            step(c, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, R0, R1);
+            step(c, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}, R1, R0);
+            step(c, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{}, R0, R1);
+            step(c, std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{}, R1, R0);
+            step(c, std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{}, R0, R1);
+            step(c, std::integral_constant<int, 5>{}, std::integral_constant<int, 0>{}, R1, R0);
+            step(c, std::integral_constant<int, 6>{}, std::integral_constant<int, 0>{}, R0, R1);
+            step(c, std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, R1, R0);
+            step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
+        }
+        conv_h_epilogue(a, acc, Ep, lane, wm, wn, ecb, epix0, eb);
+        if (!has_next) break;
+        tile = next;
+        next = tile + nwg;
+        has_next = next < tend;
+        first = false;
     }
-    if (c < nC) {
-        step(c, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, R0, R1);
-        step(c, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}, R1, R0);
-        step(c, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{}, R0, R1);
-        step(c, std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{}, R1, R0);
-        step(c, std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{}, R0, R1);
-        step(c, std::integral_constant<int, 5>{}, std::integral_constant<int, 0>{}, R1, R0);
-        step(c, std::integral_constant<int, 6>{}, std::integral_constant<int, 0>{}, R0, R1);
-        step(c, std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, R1, R0);
-        step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
-    }
-    // the epilogue's LDS reduction buffer is its own; no DMA is left in flight
-    conv_epilogue<true>(a, acc, lane, wm, wn, cb, pix0, a.B * H * W, H, W, 0, 0, W);
+}
+
+// conv_h_kernel's grid: up to one workgroup per CU, a multiple of 8 (XCD count)
+uint32_t conv_h_grid(uint32_t ntiles) {
+    const uint32_t per = (ntiles + 7) >> 3;
+    return 8u * (per < kCusPerXcd ? per : kCusPerXcd);
 }
 
 
@@ -905,7 +1091,7 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
         a.partial = reinterpret_cast<f4 *>(ws);
     }
     if (act && !transposed && a.ksplit == 1 && H % 16 == 0 && W % 16 == 0)
-        hipLaunchKernelGGL(conv_h_kernel, dim3(grid), dim3(512), 0, st, a);
+        hipLaunchKernelGGL(conv_h_kernel, dim3(conv_h_grid(a.cls[0].ntiles)), dim3(512), 0, st, a);
     else if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     if (a.ksplit > 1) {

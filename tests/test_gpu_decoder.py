@@ -256,6 +256,9 @@ def test_conv3x3_f16x3_vs_fp64(ops, B, Cin, Cout, H, W, transposed):
     (1, 32, 256, 16, 16, False, False, True),   # y only
     (2, 96, 128, 32, 48, True, True, True),     # halo kernel: odd channel-group count, 2x3 blocks
     (1, 256, 256, 64, 64, True, False, True),   # halo kernel: decoder-sized layer
+    (3, 32, 256, 128, 128, True, False, True),  # persistent halo kernel: 384 tiles (2 per
+                                                # workgroup on half the CUs), one group
+    (2, 64, 128, 256, 256, True, True, False),  # ... 512 tiles (2 per workgroup), rgb only
 ])
 def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, store_y):
     """sdfr_conv3x3_f16x3_act (+ sdfr_rgb_finish) against sdfr_conv3x3_f16x3 followed by
