@@ -22,7 +22,8 @@ extraction and the stage-2 start copy only the size-matching ``g_ema`` entries
 train.py:69-89: stage 1 runs while ``vol_renderer.pt`` is missing, stage 2 while
 ``full_pipeline.pt`` is missing (``--wod``: stage 2 only, from the sphere init).
 
-Checkpoints are written by rank 0 only; every rank reads them.  Loading uses
+Checkpoints are written by rank 0 only; every rank reads them; decisions taken from
+the directory's contents are rank 0's, broadcast (``agree``).  Loading uses
 ``torch.load(weights_only=True)``: state dicts, optimizer states and numbers only.
 """
 from __future__ import annotations
@@ -41,6 +42,19 @@ SPHERE_INIT = "sdf_init_models.pt"
 def _rank():
     import torch.distributed as dist
     return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def agree(value):
+    """Rank 0's ``value`` on every rank.  The file-system decisions that gate a
+    collective (resume point, sphere-init present, stages left; save() is a barrier
+    and every training step an all-reduce) are taken by rank 0 alone, so a rank with
+    a lagging view of a shared directory cannot skip a collective the others enter."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return value
+    box = [value]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
 
 
 def exp_dir(checkpoints_dir, expname) -> Path:
@@ -116,7 +130,7 @@ def resume(trainer, checkpoints_dir, expname, stage):
     """Load the stage's newest periodic checkpoint if there is one; returns the
     iteration to start from (that checkpoint's + 1, or 0)."""
     folder = exp_dir(checkpoints_dir, expname) / STAGE_DIRS[stage]
-    last = get_ckpt_nums(folder)
+    last = agree(get_ckpt_nums(folder))
     if last is None:
         return 0
     load_into(trainer, load_file(folder / f"models_{last.zfill(7)}.pt"))
@@ -141,7 +155,7 @@ def stage_plan(checkpoints_dir, expname, wod=False):
     need_full = not (d / STAGE_FINAL[2]).exists()
     if wod:
         need_vol, need_full = False, True
-    return need_vol, need_full
+    return agree((need_vol, need_full))
 
 
 def save_final(trainer, checkpoints_dir, expname, stage):

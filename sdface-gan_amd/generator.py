@@ -341,18 +341,20 @@ class Decoder(nn.Module):
                 inject_index=None, truncation=1, truncation_latent=None, input_is_latent=False,
                 noise=None, randomize_noise=True, mesh_path=None, prepared=None):
         if prepared is not None:         # prepare_fused() ran earlier (Generator.forward)
+            latent, noise, sty = prepared
             if self._fused_ok(features, rgbd_in, transform):
-                latent, noise_f, sty = prepared
-                return (self._fused_forward(features, latent, noise_f, sty),
+                return (self._fused_forward(features, latent, noise, sty),
                         (latent if return_latents else None))
             # the features turned out to need the autograd path (they require grad):
-            # drop the prep and run the module path below, so no gradient is lost
-            prepared = None
-        latent, noise = self.styles_and_noise_forward(styles, noise, inject_index, truncation,
-                                                      truncation_latent, input_is_latent,
-                                                      randomize_noise)
-        if self._fused_ok(features, rgbd_in, transform):
-            return self._fused_forward(features, latent, noise), (latent if return_latents else None)
+            # run the module path below on the prep's latent and noise maps -- drawing
+            # them again would shift the RNG streams against the reference's order
+        else:
+            latent, noise = self.styles_and_noise_forward(styles, noise, inject_index,
+                                                          truncation, truncation_latent,
+                                                          input_is_latent, randomize_noise)
+            if self._fused_ok(features, rgbd_in, transform):
+                return (self._fused_forward(features, latent, noise),
+                        (latent if return_latents else None))
         out = self.conv1(features, latent[:, 0], noise=noise[0], transform=transform,
                          mesh_path=mesh_path)
         skip = self.to_rgb1(out, latent[:, 1], skip=rgbd_in)

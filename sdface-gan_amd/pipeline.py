@@ -33,7 +33,7 @@ def train_vol_render(opt, expname, loader, device, checkpoints_dir, iters=10000,
     init_path = ck.exp_dir(checkpoints_dir, expname) / ck.SPHERE_INIT
     with_sdf = getattr(t, "with_sdf", True)
     if start == 0 and with_sdf and not getattr(t, "no_sphere_init", False):
-        if init_path.exists():
+        if ck.agree(init_path.exists()):
             ck.load_into(tr, ck.load_file(init_path))
             tr.iteration = 0
         else:

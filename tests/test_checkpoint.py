@@ -1,10 +1,14 @@
 """Checkpoint layout, resume and stage gating (training_utils.py:197-226, 318-324,
 526-547, 555-606, 858-879; sdf_utils.py:382-401; train.py:69-89; eval.py:73-77),
 on CPU with the SIREN network (configs[4]'s renderer; the ngp encoders need the GPU)."""
+import os
 import random
+import socket
 
 import pytest
 import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
 
 
 def _stage2_opt(sdfr):
@@ -120,3 +124,50 @@ def test_two_stage_pipeline_gating_and_files(sdfr, tmp_path):
     t1b = pipeline.train_vol_render(o1, "exp", _loader(8, 1), cpu, tmp_path, iters=1,
                                     sphere_init_iters=1)
     assert t1b.iteration == 2
+
+
+def _stage1_worker(rank, world, port, root):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    from sdfr_loader import load
+    sdfr = load()
+    from sdface_gan_amd import checkpoint as ck
+    from sdface_gan_amd import pipeline
+    # rank 1 looks at a directory whose contents disagree with rank 0's (a lagging
+    # view of a shared file system, exaggerated): a bogus sphere-init file and a
+    # bogus periodic checkpoint.  Following its own view it would skip the sphere
+    # init and its save() barrier, or resume elsewhere -- and hang the job.
+    ckdir = os.path.join(root, f"r{rank}")
+    if rank == 1:
+        os.makedirs(os.path.join(ckdir, "exp", "volume_renderer"), exist_ok=True)
+        open(os.path.join(ckdir, "exp", ck.SPHERE_INIT), "wb").close()
+        open(os.path.join(ckdir, "exp", "volume_renderer", "models_0000500.pt"), "wb").close()
+    plan = ck.stage_plan(ckdir, "exp")
+    tr = pipeline.train_vol_render(_stage1_opt(sdfr), "exp", _loader(8, 1 + rank),
+                                   torch.device("cpu"), ckdir, iters=2, sphere_init_iters=1)
+    torch.save({"plan": plan, "it": tr.iteration, "g": tr.g_module.state_dict()},
+               os.path.join(root, f"rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_stage1_ranks_follow_rank0_file_decisions(sdfr, tmp_path):
+    """World of 2 gloo ranks through train_vol_render's sphere init, periodic
+    checkpoint and save_final (each save a barrier): every branch taken from the
+    checkpoint directory is rank 0's (checkpoint.agree), so the ranks enter the same
+    collectives and finish with identical weights; only rank 0 writes."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_stage1_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    assert tuple(r0["plan"]) == tuple(r1["plan"]) == (True, True)
+    assert r0["it"] == r1["it"] == 2
+    for k, v in r0["g"].items():
+        assert torch.equal(v, r1["g"][k]), k
+    d0, d1 = tmp_path / "r0" / "exp", tmp_path / "r1" / "exp"
+    assert (d0 / "sdf_init_models.pt").exists() and (d0 / "vol_renderer.pt").exists()
+    assert not (d1 / "vol_renderer.pt").exists()          # rank 1 never writes

@@ -316,6 +316,31 @@ def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, 
                1e-5 * scale, 1e-6 * scale)
 
 
+def test_prepared_fallback_draws_nothing_twice(sdfr):
+    """Decoder.forward(prepared=...) falling back to the module path (features that
+    require grad) runs on the prep's latent and noise maps: no second draw of the
+    injection index or of the noise, so the RNG streams stay where the reference
+    leaves them."""
+    import random
+    opt = sdfr.vol_render_opt()
+    torch.manual_seed(3)
+    dec = sdfr.Generator(opt.model, opt.rendering).to(DEV).decoder.eval()
+    feats = (torch.randn(2, 256, 64, 64, device=DEV) * 0.3).requires_grad_()
+    styles = [torch.randn(2, 256, device=DEV), torch.randn(2, 256, device=DEV)]  # mixing
+    random.seed(5)
+    torch.manual_seed(7)
+    with torch.no_grad():
+        prep = dec.prepare_fused(styles, 2, torch.device(DEV))
+    py_state, t_state = random.getstate(), torch.cuda.get_rng_state()
+    img, lat = dec(feats, styles, prepared=prep, return_latents=True)
+    assert img.requires_grad                                  # the autograd path ran
+    assert random.getstate() == py_state                      # no second inject_index
+    assert torch.equal(torch.cuda.get_rng_state(), t_state)   # no second noise draw
+    ref, _ = dec(feats, [prep[0]], input_is_latent=True, noise=prep[1])
+    assert torch.equal(lat, prep[0])
+    torch.testing.assert_close(img, ref, rtol=0, atol=1e-6)
+
+
 @pytest.mark.parametrize("conv_impl,fuse", [("f16x3", True), ("f16x3", False), ("miopen", False)])
 def test_decoder_fused_equals_module_path(sdfr, conv_impl, fuse):
     """Same weights, latents and noise: HIP-epilogue decoder == op-by-op decoder."""
