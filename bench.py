@@ -273,8 +273,9 @@ def main():
     flop = FLOP_PER_SAMPLE_SIREN if siren else (FLOP_PER_SAMPLE_FUSED if f16x3 else FLOP_PER_SAMPLE)
     field_tflops = flop * samples / (field_ms * 1e-3) / 1e12
     gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9 if not siren else 0.0
-    field_kernel = ("field_r_kernel<sdfr::SirenNet>" if siren else
+    field_kernel = ("field_p_kernel<sdfr::SirenNet>" if siren else
                     "field_r_kernel<sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
+    field_mfma = "v_mfma_f32_16x16x32_f16" if siren else "v_mfma_f32_32x32x16_f16"
     def traffic_of(kernel):
         """HBM bytes per launch of `kernel` at this batch, from the committed
         rocprofv3 PMC passes (profiles/, scripts/summarize_profiles.py), or None."""
@@ -291,8 +292,8 @@ def main():
         (SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x GRBM_GUI_ACTIVE / XCDs)), or None."""
         try:
             ks = json.loads(Path(args.counters_json).read_text())["kernels"]
-            # the full templated name (field_r_kernel<sdfr::NgpNet> and <sdfr::SirenNet>
-            # are different kernels)
+            # the full templated name (field_r_kernel<sdfr::NgpNet> and
+            # field_p_kernel<sdfr::SirenNet> are different kernels)
             k = next(v for n, v in ks.items() if kernel in n.replace("sdfr::(anonymous namespace)::", ""))
             return {"mfma_busy_frac": k["mfma_busy_frac"],
                     "effective_clock_GHz": k["effective_clock_GHz"],
@@ -309,7 +310,7 @@ def main():
         ref_flop = FLOP_PER_SAMPLE_SIREN if siren else FLOP_PER_SAMPLE
         alg_tflops = field_tflops * ref_flop / flop
         peak = MFMA_F16_PEAK_TFLOPS / 3
-        roof = {"kernel": f"{field_kernel} (MLP as 3 split-fp16 v_mfma_f32_32x32x16_f16 "
+        roof = {"kernel": f"{field_kernel} (MLP as 3 split-fp16 {field_mfma} "
                           "terms per fp32 tile + compositing)",
                 "bound": "mfma", "achieved": field_tflops, "peak": peak,
                 "unit": "TFLOP/s", "frac": field_tflops / peak,

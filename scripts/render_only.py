@@ -1,5 +1,6 @@
 """Run only the fused renderer (B faces, 64^2 x 24) K times: a short, clean target
-for rocprofv3 counter passes on the field kernel (profiling aid, not a test)."""
+for rocprofv3 counter passes on the field kernel (profiling aid, not a test).
+    python scripts/render_only.py [f16x3|fp32] [ngp|siren]"""
 import sys
 from pathlib import Path
 
@@ -9,10 +10,10 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from sdfr_loader import load  # noqa: E402
 
 
-def main(B=32, K=3, precision="f16x3"):
+def main(B=32, K=3, precision="f16x3", net="ngp"):
     sdfr = load()
     dev = "cuda:0"
-    opt = sdfr.vol_render_opt()
+    opt = sdfr.vol_render_opt(ngp=net == "ngp")
     torch.manual_seed(0)
     g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
     ren = g.renderer
@@ -28,4 +29,5 @@ def main(B=32, K=3, precision="f16x3"):
 
 
 if __name__ == "__main__":
-    main(precision=sys.argv[1] if len(sys.argv) > 1 else "f16x3")
+    main(precision=sys.argv[1] if len(sys.argv) > 1 else "f16x3",
+         net=sys.argv[2] if len(sys.argv) > 2 else "ngp")

@@ -25,7 +25,7 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 # fp32 ngp / f16x3 ngp / f16x3 siren field kernels
-FIELDS = ("ngp_field_kernel", "field_r_kernel<sdfr::NgpNet>", "field_r_kernel<sdfr::SirenNet>",
+FIELDS = ("ngp_field_kernel", "field_r_kernel<sdfr::NgpNet>", "field_p_kernel<sdfr::SirenNet>",
           "field_x_kernel<0, sdfr::NgpNet>", "field_x_kernel<0, sdfr::SirenNet>")
 ENCODE = "ngp_encode_kernel"
 

@@ -9,8 +9,9 @@
 //             Points are formed in-kernel from the ray (bit-exact chain).
 //
 // followed by SDF->density and front-to-back alpha compositing
-// (volume_integration, :236-301).  Every fp32 GEMM tile runs as three
-// v_mfma_f32_32x32x16_f16 on a hi/lo fp16 split of both operands:
+// (volume_integration, :236-301).  Every fp32 GEMM tile runs as three fp16 MFMAs
+// (v_mfma_f32_32x32x16_f16 for ngp, v_mfma_f32_16x16x32_f16 for siren) on a hi/lo
+// fp16 split of both operands:
 //
 //     W.x = W_hi.x_hi + W_hi.x_lo + W_lo.x_hi   (+ W_lo.x_lo, dropped: 2^-22 rel.)
 //
@@ -27,9 +28,12 @@
 // VGPRs), over 4 tiles of 16 rays; each wave computes ALL 256 output rows of every
 // layer for 32 samples (16 rays x 2 consecutive samples), so a layer's accumulators,
 // activated and split in place, are the next layer's B fragments (no LDS hand-off).
-// The weight stream (0.8 MB ngp / 2.1 MB siren per pass) is shared by the 4 waves
-// through a 4-slot LDS-DMA ring of 16 KB slices (one per k-step of 16 K), with the
-// packed weights' K permuted to match the accumulator layout (xprep_kernel).
+// The weight stream (0.8 MB per pass) is shared by the 4 waves through a 4-slot
+// LDS-DMA ring of 16 KB slices (one per k-step of 16 K), with the packed weights' K
+// permuted to match the accumulator layout (xprep_kernel).  The SIREN net runs on
+// field_p_kernel (two waves per SIMD splitting each layer's rows, its own packing:
+// 16 KB half-slices per k-step of 32 K), which is 6 % faster on its nine FiLM layers
+// -- the one-wave kernel's 32x32 MFMAs hold a lower clock there (1.64 GHz, counters).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -50,6 +54,7 @@ constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 tiles][hi,lo][64 l
 // ----------------------------------------------------------------------------
 struct NgpNet {
     static constexpr bool kSiren = false;
+    static constexpr bool kFieldR = true;      // field_r_kernel (else field_p_kernel)
     // input_linear (LinearLayer, affine: sdf_model.py:37-39) feeds pts_linears.0's
     // linear with no nonlinearity between them (:1574-1577), so the two are ONE affine
     // map W1 (W0 x + b0) + b1 = (W1 W0) x + (W1 b0 + b1), composed once per weight
@@ -67,18 +72,41 @@ struct NgpNet {
 };
 struct SirenNet {
     static constexpr bool kSiren = true;
+    static constexpr bool kFieldR = false;
     static constexpr bool kCompose = false;
     static constexpr bool kSlice2 = false;
     static constexpr int kLayers = 9;          // pts_linears.0-7, views
     static constexpr int kFilmN = 9;
     static constexpr int kHidden = 7;
-    static constexpr uint32_t kSlices = 1 + 16 * 7 + 17;
+    static constexpr uint32_t kSlices = 2 + 16 * 7 + 18;     // field_p_kernel's half-slices
     __host__ __device__ static constexpr uint32_t K(int l) {
         return l == 0 ? 3u : (l == 8 ? kW + 3 : kW);
     }
     __host__ __device__ static constexpr int film_layer(int f) { return f; }
 };
 constexpr int kMaxLayers = 9;
+
+// field_p_kernel's packing (SirenNet): slices = 2 per k-step of 32 input features
+// (8 output tiles of 16 rows each); layer 0 one k-step, dense layers 8, views 9.
+template <class Net>
+__host__ __device__ constexpr uint32_t xslice_base(int l) {
+    return l == 0 ? 0u : (l == Net::kLayers - 1 ? 2u + 16u * Net::kHidden : 2u + 16u * (l - 1));
+}
+
+// K index of element j of lane group g in field_p_kernel's k-step q of layer l
+// (-1 = zero pad).
+template <class Net>
+__device__ __forceinline__ int xperm_k(int l, uint32_t q, uint32_t g, uint32_t j) {
+    if (l == 0) {
+        if constexpr (Net::kSiren) return (g == 0 && j < 3) ? (int)j : -1;   // xyz
+        return (int)(8 * g + j);                                           // 32 features
+    }
+    if (l == Net::kLayers - 1 && q == 8) {
+        if constexpr (Net::kSiren) return (g == 0 && j < 3) ? (int)(kW + j) : -1;   // viewdir
+        return g < 2 ? (int)(kW + 8 * g + j) : -1;                                // SH 0-15
+    }
+    return (int)(16 * (2 * q + (j >> 2)) + 4 * g + (j & 3));
+}
 
 constexpr int kRWaves = 4;
 constexpr int kRThreads = kRWaves * 64;
@@ -97,7 +125,7 @@ struct RNet {
     static constexpr int kL0 = Net::kSiren ? 1 : 2;                // layer-0 k-steps (K 3 / 32)
     static constexpr int kSteps = kL0 + 16 * Net::kHidden + 17;    // k-steps (slices) per pass
     static constexpr int kViews = kL0 + 16 * Net::kHidden;         // first views k-step
-    static_assert(kSteps == (int)Net::kSlices, "one packed slice per k-step");
+    static_assert(!Net::kFieldR || kSteps == (int)Net::kSlices, "one packed slice per k-step");
 };
 
 template <class Net>
@@ -262,7 +290,32 @@ __global__ void __launch_bounds__(256) xprep_kernel(const XPrepArgs a) {
     }
     const uint32_t e = (blk - nfilm) * 256 + j;
     if (e >= Net::kSlices * 512) return;
-    r_pack<Net>(a, e);
+    if constexpr (Net::kFieldR) {
+        r_pack<Net>(a, e);
+        return;
+    }
+    // field_p_kernel's half-slices
+    const uint32_t slice = e / 512, rem = e % 512;
+    const uint32_t t8 = rem >> 6, lane = rem & 63;
+    int layer = 0;
+    if (slice >= xslice_base<Net>(Net::kLayers - 1)) layer = Net::kLayers - 1;
+    else if (slice >= 2) layer = 1 + (slice - 2) / 16;
+    const uint32_t local = slice - xslice_base<Net>(layer);
+    const uint32_t q = local >> 1, h = local & 1;
+    const uint32_t row = 16 * (8 * h + t8) + (lane & 15), g = lane >> 4;
+    const uint32_t K = Net::K(layer);
+    const float s = a.su[layer * kW + row];
+    float v[8];
+#pragma unroll
+    for (uint32_t jj = 0; jj < 8; ++jj) {
+        const int k = xperm_k<Net>(layer, q, g, jj);
+        v[jj] = k < 0 ? 0.0f : __fmul_rn(a.w[layer][(size_t)row * K + k], s);
+    }
+    f4 hi, lo;
+    split8(v, hi, lo);
+    f4 *dst = a.packed + (size_t)slice * kXSliceF4 + t8 * 128 + lane;
+    dst[0] = hi;
+    dst[64] = lo;
 }
 
 // ----------------------------------------------------------------------------
@@ -310,6 +363,670 @@ constexpr int kRValuPerMfma = SDFR_RVALU;  // field_r_kernel: VALU slots after e
 #define SDFR_RDS 2
 #endif
 constexpr int kRDsPerMfma = SDFR_RDS;      // field_r_kernel: LDS-read slots after each MFMA
+
+// ngp layer-0 inputs: the 32 hash-grid features of a sample span the 4 lane
+// groups of its column.  They are scaled by the power of two 2^es that brings the
+// sample's max |x| into [0.5, 1) before the hi/lo split, so neither fp16 part
+// goes subnormal at any table scale (the reference initialises the table to
+// U(-1e-4, 1e-4), grid.py:138-140, where unscaled features would lose their lo
+// parts); the scaling is exact and undone exactly in act_pair<0>.
+__device__ __forceinline__ int feat_scale(float (&v)[8]) {
+    float m = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    if (!(m > 0.0f && m < 3.0e38f)) return 0;          // zeros (out of bounds) / non-finite
+    int ex = __builtin_amdgcn_frexp_expf(m);          // m = f 2^ex, f in [0.5, 1)
+    const int es = ex < -100 ? 100 : -ex;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = __builtin_ldexpf(v[j], es);
+    return es;
+}
+
+constexpr int kRingSlots = 4;                        // weight ring: 4 half-slice slots (16 KB)
+constexpr int kDmaPieces = 2;                        // 1 KB LDS-DMA pieces per wave per half-slice
+
+__device__ __forceinline__ float ror8(float v) {   // lane n <- lane (n + 8) mod 16 of its row
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+}
+
+// ----------------------------------------------------------------------------
+// field_p_kernel: wave pairs split the output rows.
+//
+// The previous field kernel (field_x2_kernel, git history) gave every wave the WHOLE
+// weight matrix against its own 16-sample column, so each A fragment read from LDS fed
+// 3 MFMAs and the eight waves of a CU read 8x the weight stream from LDS per pass.
+// Here the two waves of a SIMD (w, w + 4) form a pair over 32 samples = 8 rays x 4
+// consecutive samples (two MFMA blocks of N = 16: block c, lane n holds sample
+// 4p + 2c + (n >= 8) of ray n & 7); wave h of the pair owns the 16-row output tiles
+// 2t + h (t = 0..7), so each A fragment feeds 6 MFMAs and LDS A reads halve.  A
+// layer's input k-step q (rows 32q .. 32q + 31 = tiles 2q, 2q+1 of the previous
+// layer's output) is half in each wave: both activate their tile one k-step ahead
+// (FiLM in the MFMA shadow) and write its (hi, lo) dword pairs to their 8-byte half of
+// a double-buffered 4 KB exchange slot; after the k-step barrier both read the whole
+// fragment back.  Per k-step and wave: 48 MFMAs, 16 A + 4 B ds_read_b128
+// (field_x2_kernel: 32 A reads per 48 MFMAs), 4 pieces of the LDS-DMA weight ring.
+// Balanced work matters: with one wave activating a whole k-step the other idled at
+// the barrier (measured).  The sigma head and the colour head are per-wave half-sums
+// over own rows, added in wave order (fp32-rounding-level differences to the previous
+// kernel, <= 5e-7); alpha is computed once per sample block by one wave of the pair.
+// Four samples of a ray per pass halve the per-ray feature accumulators (4 KB per wave
+// in LDS).  Measured alternatives (in git history): issuing the two waves' LDS-DMA at
+// different points (+-0), placing their activations after different groups (+5 %),
+// the next k-step's B fragments read ahead of the last group (+-0), a packed-fp32
+// colour head (raced: see below).
+constexpr int kPWaves = 8;
+constexpr int kPThreads = kPWaves * 64;
+constexpr uint32_t kPTiles = 2;          // 16-ray tiles per workgroup (4 pairs x 8 rays)
+constexpr uint32_t kPSamples = 4;        // samples of a ray per pass
+
+
+
+template <class Net>
+struct PNet {
+    static constexpr int kSteps = 1 + 8 * Net::kHidden + 9;   // k-steps per pass
+    static constexpr int kViews = 1 + 8 * Net::kHidden;        // first k-step of the views layer
+    static_assert(2 * kSteps == (int)Net::kSlices && kSteps % 2 == 0, "ring parity per pass");
+};
+
+struct PRing {
+    f4 *lds;          // weight ring: 4 half-slice slots of kXSliceF4
+    f4 *xch;          // this pair's exchange: [2 slots][2 blocks][hi, lo][64 lanes]
+    v4i drsrc;
+    uint32_t tid, wave, h;
+    f4 na[4];         // the next k-step's group-0 A fragments (t0 hi, t0 lo, t1 hi, t1 lo)
+};
+
+// One LDS-DMA half-slice (this wave's pieces) with compile-time offsets as immediates
+// (with the offsets as SGPR operands the unrolled pass spilled).  Straight-line asm
+// only: a branch inside the asm would skip instructions the compiler counts as wait
+// states of MFMA -> VALU hazards (measured: nondeterministic colour features).
+template <uint32_t SLICE, uint32_t SLOT>
+__device__ __forceinline__ void p_dma_i(const PRing &R) {
+    const uint32_t sbase = R.wave * (kDmaPieces * 1024u);
+    const uint32_t lbase = lds_addr(R.lds) + sbase;
+    const uint32_t voff = (R.tid & 63u) * 16u;
+#pragma unroll
+    for (int k = 0; k < kDmaPieces; ++k) {
+        uint32_t keep, so;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_add_u32 m0, %4, %6\n\ts_add_u32 %1, %5, %7\n\ts_nop 0\n\t"
+            "buffer_load_dwordx4 %2, %3, %1 offen lds\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep), "=&s"(so)
+            : "v"(voff), "s"(R.drsrc), "s"(lbase), "s"(sbase),
+              "i"(SLOT * kXSliceF4 * 16u + k * 1024u), "i"(SLICE * kXSliceF4 * 16u + k * 1024u)
+            : "memory", "scc");
+    }
+}
+
+// B fragments of exchange chunk q (both blocks): (hi0, lo0, hi1, lo1)
+__device__ __forceinline__ void p_read_chunk(const PRing &R, int q, f4 (&b)[4]) {
+    const f4 *s = R.xch + (q & 1) * 256 + (R.tid & 63u);
+    b[0] = s[0];
+    b[1] = s[64];
+    b[2] = s[128];
+    b[3] = s[192];
+}
+
+// One k-step of one wave: 8 own output tiles x 2 sample blocks x 3 split terms = 48
+// MFMAs in 4 groups of 2 tiles (a group's 12 MFMAs term-major, so an accumulator is
+// touched every 4th).  Own half-slice of k-step KS: ring slot 2 (KS & 1) + h.  The
+// next k-step's half-slices are DMA'd at entry into the previous k-step's slots; the
+// barrier (own DMA landed, own LDS traffic drained) sits ahead of group 3, behind it
+// the next k-step's group-0 A fragments and B fragments (next_b) are read, so their
+// latency hides under group 3.  side() runs after group 1.
+template <class Net, int KS, bool ZC, class NextB, class Side>
+__device__ __forceinline__ void pstep(PRing &R, f4 (&acc)[16], const f4 (&bf)[4], f4 (&bn)[4],
+                                      NextB &&next_b, Side &&side) {
+    constexpr f4 kZ = {0.0f, 0.0f, 0.0f, 0.0f};
+    constexpr int KN = (KS + 1) % PNet<Net>::kSteps;
+    const uint32_t lane = R.tid & 63u;
+    // the next k-step's half-slices go into the slots of the previous k-step (closed by
+    // its barrier)
+    p_dma_i<2 * KN, 2 * (KN & 1)>(R);
+    p_dma_i<2 * KN + 1, 2 * (KN & 1) + 1>(R);
+    // local tile t = global tile 2t + h: half-slice t >> 2, position 2 (t & 3) + h
+    const f4 *A = R.lds + 2 * (KS & 1) * kXSliceF4 + R.h * 128 + lane;
+    const f4 *An = R.lds + 2 * (KN & 1) * kXSliceF4 + R.h * 128 + lane;
+    auto aoff = [](int t, int hl) { return (t >> 2) * (int)kXSliceF4 + (t & 3) * 256 + hl * 64; };
+    f4 a[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[0][i] = R.na[i];
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+        if (grp == 3) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        if (grp < 3) {
+            const int tn = 2 * (grp + 1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[grp + 1][i] = A[aoff(tn + (i >> 1), i & 1)];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) R.na[i] = An[aoff(i >> 1, i & 1)];
+        }
+        const int t0 = 2 * grp, t1 = t0 + 1;
+        const f4 *ag = a[grp];
+        // per accumulator: W_lo x_hi, W_hi x_lo, W_hi x_hi
+        // ZC: the layer's first k-step starts its accumulators from zero
+        acc[2 * t0] = mfma16(ag[1], bf[0], ZC ? kZ : acc[2 * t0]);
+        acc[2 * t0 + 1] = mfma16(ag[1], bf[2], ZC ? kZ : acc[2 * t0 + 1]);
+        acc[2 * t1] = mfma16(ag[3], bf[0], ZC ? kZ : acc[2 * t1]);
+        acc[2 * t1 + 1] = mfma16(ag[3], bf[2], ZC ? kZ : acc[2 * t1 + 1]);
+        acc[2 * t0] = mfma16(ag[0], bf[1], acc[2 * t0]);
+        acc[2 * t0 + 1] = mfma16(ag[0], bf[3], acc[2 * t0 + 1]);
+        acc[2 * t1] = mfma16(ag[2], bf[1], acc[2 * t1]);
+        acc[2 * t1 + 1] = mfma16(ag[2], bf[3], acc[2 * t1 + 1]);
+        acc[2 * t0] = mfma16(ag[0], bf[0], acc[2 * t0]);
+        acc[2 * t0 + 1] = mfma16(ag[0], bf[2], acc[2 * t0 + 1]);
+        acc[2 * t1] = mfma16(ag[2], bf[0], acc[2 * t1]);
+        acc[2 * t1 + 1] = mfma16(ag[2], bf[2], acc[2 * t1 + 1]);
+        // this group's A fragments stay allocated until its MFMAs have issued (pinning
+        // the previous group's too measured 1.5 % slower)
+        asm volatile("" ::"v"(ag[0]), "v"(ag[1]), "v"(ag[2]), "v"(ag[3]));
+        __builtin_amdgcn_sched_barrier(0);
+        if (grp == 1) side();
+    }
+    next_b(bn);
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// This wave's half of exchange chunk q (k-step q of the next layer = global tiles
+// 2q, 2q+1 of this layer's output; wave h holds tile 2q + h as local tile q):
+// activate local tile q of both blocks, split it and write the (hi, lo) dword pairs
+// to bytes 8h .. 8h + 7 of the chunk's 16-B B-fragment elements in slot q & 1.
+//   MODE 0: ngp layer 0, FiLM of x 2^-es (the features were scaled by 2^es, feat_scale)
+//   MODE 1: FiLM sin_rev(fma(gamma'', x, beta''))
+//   MODE 2: FiLM + the sigma head's partial dot product (per lane over own tiles)
+template <int MODE>
+__device__ __forceinline__ void p_act(const PRing &R, f4 (&in)[16], int q, const float *gam,
+                                      const float *bet, const float *sw, float (&sdfp)[2],
+                                      uint32_t g, const int (&es)[2]) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const int f0 = 16 * (2 * q + (int)R.h) + 4 * (int)g;
+    const f4 gm = *reinterpret_cast<const f4 *>(gam + f0);
+    const f4 bt = *reinterpret_cast<const f4 *>(bet + f0);
+    f4 w4;
+    if constexpr (MODE == 2) w4 = *reinterpret_cast<const f4 *>(sw + f0);
+    char *dst = reinterpret_cast<char *>(R.xch + (q & 1) * 256 + (R.tid & 63u)) + 8 * R.h;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const f4 z = in[2 * q + c];
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if constexpr (MODE == 0) v[r] = sin_rev(__fmaf_rn(gm[r], __builtin_ldexpf(z[r], -es[c]), bt[r]));
+            else v[r] = sin_rev(__fmaf_rn(gm[r], z[r], bt[r]));
+        }
+        if constexpr (MODE == 2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sdfp[c] = __fmaf_rn(v[r], w4[r], sdfp[c]);
+        }
+        uint32_t hp[2], lp[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            h2 H;
+            H[0] = (_Float16)v[2 * j];
+            H[1] = (_Float16)v[2 * j + 1];
+            hp[j] = __builtin_bit_cast(uint32_t, H);
+            uint32_t l;
+            asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hp[j]), "v"(v[2 * j]));
+            asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                : "+v"(l) : "v"(hp[j]), "v"(v[2 * j + 1]));
+            lp[j] = l;
+        }
+        *reinterpret_cast<uint2 *>(dst + 128 * 16 * c) = make_uint2(hp[0], hp[1]);
+        *reinterpret_cast<uint2 *>(dst + 128 * 16 * c + 64 * 16) = make_uint2(lp[0], lp[1]);
+    }
+}
+
+template <class Net>
+__global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs a) {
+    constexpr int NF = Net::kFilmN;
+    constexpr int KV = PNet<Net>::kViews;
+    constexpr int NL = Net::kLayers;
+    __shared__ f4 ring_lds[kRingSlots * kXSliceF4];           // 64 KB weight ring
+    __shared__ f4 xch_lds[4][2 * 2 * 2 * 64];               // 32 KB: [pair][slot][block][hi,lo][lane]
+    __shared__ f4 facc_lds[kPWaves][8 * 4 * 8];             // 32 KB: [wave][tile][g][ray] feature sums
+    __shared__ float film_lds[NF * 2 * kW];                 // the workgroup's face
+    __shared__ float cst[4 * kW];                           // sigma_w, rgb_w[3]
+    __shared__ float sdfx_lds[4][2][2][64];                 // [pair][wave][block][lane] sigma half-sums
+    __shared__ float pcol_lds[4][6][16];                    // wave 0's colour half-sums per column
+    __shared__ float alx_lds[4][2][64];                     // [pair][block][lane] alpha
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t h = __builtin_amdgcn_readfirstlane(wave >> 2), pair = wave & 3u;
+    const uint32_t n = lane & 15u, g = lane >> 4, r8 = n & 7u;
+    const bool colB = n >= 8u;
+    const GeomArgs &G = a.g;
+
+    // workgroup = 2 tiles; pair k: tile k >> 1, rays 8 (k & 1) .. +7
+    const uint32_t wg_per_face = (G.tiles_per_face + kPTiles - 1) / kPTiles;
+    const uint32_t seg = blockIdx.x % a.nseg, blk = blockIdx.x / a.nseg;
+    const uint32_t b = blk / wg_per_face;
+    const float beta_s = a.with_sdf ? a.sigmoid_beta[0] : 1.0f;
+    {
+        const f4 *src = reinterpret_cast<const f4 *>(a.film + (size_t)b * NF * 2 * kW);
+        f4 *dst = reinterpret_cast<f4 *>(film_lds);
+        for (uint32_t i = tid; i < NF * 2 * kW / 4; i += kPThreads) dst[i] = src[i];
+    }
+    PRing R;
+    R.lds = ring_lds;
+    R.xch = xch_lds[pair];
+    R.tid = tid;
+    R.wave = __builtin_amdgcn_readfirstlane(wave);
+    R.h = h;
+    R.drsrc = make_rsrc(a.packed, Net::kSlices * kXSliceF4 * sizeof(f4));
+    for (uint32_t i = tid; i < 4 * kW; i += kPThreads)
+        cst[i] = i < kW ? a.sigma_w[i] : a.rgb_w[i - kW];
+    // prologue: k-step 0's half-slices -> slots 0, 1 (each k-step issues the next)
+    p_dma_i<0, 0>(R);
+    p_dma_i<1, 1>(R);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    f4 *facc = facc_lds[wave];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) R.na[i] = R.lds[h * 128 + (i >> 1) * 256 + (i & 1) * 64 + lane];
+
+    const float *sig_w = cst, *rgb_w = cst + kW;
+    auto fg = [&](int f) { return (const float *)film_lds + f * 2 * kW; };
+    auto fb = [&](int f) { return (const float *)film_lds + f * 2 * kW + kW; };
+    const float sig_b = a.sigma_b[0];
+    const float rgb_b0 = a.rgb_b[0], rgb_b1 = a.rgb_b[1], rgb_b2 = a.rgb_b[2];
+    const float2 *enc2 = reinterpret_cast<const float2 *>(a.enc);
+    const uint32_t npass = (G.N + kPSamples - 1) / kPSamples;
+    const uint32_t pps = (npass + a.nseg - 1) / a.nseg;
+    const uint32_t p_begin = seg * pps, p_end = min(npass, p_begin + pps);
+
+    uint32_t tile_local = (blk % wg_per_face) * kPTiles + (pair >> 1);
+    const bool tile_ok = tile_local < G.tiles_per_face;
+    if (!tile_ok) tile_local = G.tiles_per_face - 1;
+    const uint32_t tile = b * G.tiles_per_face + tile_local;
+    const uint32_t ray_in_tile = 8u * (pair & 1u) + r8;
+    uint32_t ray_local = tile_local * kTileRays + ray_in_tile;
+    const bool ray_ok = tile_ok && ray_local < G.H * G.W;
+    if (ray_local >= G.H * G.W) ray_local = G.H * G.W - 1;
+    const uint32_t py = ray_local / G.W, px = ray_local % G.W;
+    const uint32_t ray_index = (b * G.H + py) * G.W + px;
+
+    Ray ray;
+    make_ray(G.cam + (size_t)b * 12, G.focal[b], G.pix_x[px], G.pix_y[py], G.half_res, ray);
+    const float nr = G.near_[b], fr = G.far_[b];
+    const float span = __fsub_rn(fr, nr);
+    const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
+    f4 vx[4];                                               // the views layer's extra k-step
+    {
+        const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
+        const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
+        const float v2 = G.static_viewdirs ? ray.dir[2] : ray.d[2];
+        const float vn = norm3_torch(v0, v1, v2);
+        const float ux = __fdiv_rn(v0, vn), uy = __fdiv_rn(v1, vn), uz = __fdiv_rn(v2, vn);
+        float v[8];
+        if constexpr (Net::kSiren) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = 0.0f;
+            if (g == 0) {
+                v[0] = ux;
+                v[1] = uy;
+                v[2] = uz;
+            }
+        } else {
+            const f4 qa = sh_quad(ux, uy, uz, (2 * g) & 3), qb = sh_quad(ux, uy, uz, (2 * g + 1) & 3);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = g < 2 ? qa[r] : 0.0f;
+                v[4 + r] = g < 2 ? qb[r] : 0.0f;
+            }
+        }
+        split8(v, vx[0], vx[1]);
+        vx[2] = vx[0];                                       // both blocks: the same ray
+        vx[3] = vx[1];
+    }
+    float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
+    float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) facc[t * 64 + lane] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    const size_t tile_sid = (size_t)(tile * G.N) * kTileRays + ray_in_tile;
+    float2 en[2][4];
+    auto load_inputs = [&](uint32_t p) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            uint32_t s = kPSamples * p + 2 * c + (colB ? 1u : 0u);
+            if (s >= G.N) s = G.N - 1;
+            if constexpr (Net::kSiren) {
+                const float z = sample_z(G.sc, nr, fr, ray_index, s);
+                float np_[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const float pp = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));
+                    np_[k] = G.z_normalize ? __fdiv_rn(__fmul_rn(pp, 2.0f), span) : pp;
+                }
+                const bool g0 = g == 0;
+                en[c][0] = make_float2(g0 ? np_[0] : 0.0f, g0 ? np_[1] : 0.0f);
+                en[c][1] = make_float2(g0 ? np_[2] : 0.0f, 0.0f);
+                en[c][2] = make_float2(0.0f, 0.0f);
+                en[c][3] = make_float2(0.0f, 0.0f);
+            } else {
+                const size_t sid = tile_sid + (size_t)s * kTileRays;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) en[c][k] = enc2[(4 * g + k) * (size_t)G.S_total + sid];
+            }
+        }
+    };
+    load_inputs(p_begin);
+
+    for (uint32_t p = p_begin; p < p_end; ++p) {
+        f4 X[16], Y[16];                                   // [2 local tile + block]
+        f4 e[4];                                           // layer-0 B fragments
+        int es[2] = {0, 0};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                v[2 * k] = en[c][k].x;
+                v[2 * k + 1] = en[c][k].y;
+            }
+            if constexpr (!Net::kSiren) es[c] = feat_scale(v);
+            split8(v, e[2 * c], e[2 * c + 1]);
+        }
+        float sdfp[2] = {0.0f, 0.0f};
+        // activation of layer l's output, chunk q, by its owner (wave q >> 2)
+        auto act_out = [&](auto L, f4 (&o)[16], int q) {
+            constexpr int l = decltype(L)::value;
+            constexpr int f = Net::film_layer(l) == l ? l : -1;   // layer l's FiLM
+            static_assert(f >= 0, "one FiLM per layer");
+            if constexpr (l == 0 && !Net::kSiren) p_act<0>(R, o, q, fg(f), fb(f), nullptr, sdfp, g, es);
+            else if constexpr (l == NL - 2) p_act<2>(R, o, q, fg(f), fb(f), sig_w, sdfp, g, es);
+            else p_act<1>(R, o, q, fg(f), fb(f), nullptr, sdfp, g, es);
+        };
+        auto chunk_b = [&](int q) { return [&, q](f4 (&bn)[4]) { p_read_chunk(R, q, bn); }; };
+        f4 bn[4];
+        // layer 0: one k-step on the encoded inputs; wave 0 activates chunk 0 of its output
+        pstep<Net, 0, true>(R, X, e, bn, chunk_b(0), [&] {
+            act_out(std::integral_constant<int, 0>{}, X, 0);
+        });
+        // hidden layers 1 .. kHidden (in -> out alternate between X and Y)
+        auto dense = [&](auto L, f4 (&in)[16], f4 (&out)[16]) {
+            constexpr int l = decltype(L)::value;
+            sfor<0, 8>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                constexpr int KS = 1 + 8 * (l - 1) + j;
+                f4 bc[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) bc[i] = bn[i];
+                pstep<Net, KS, j == 0>(R, out, bc, bn, chunk_b((j + 1) & 7), [&] {
+                    if constexpr (j < 7) act_out(std::integral_constant<int, l - 1>{}, in, j + 1);
+                    else act_out(std::integral_constant<int, l>{}, out, 0);
+                });
+            });
+        };
+        sfor<1, Net::kHidden + 1>([&](auto L) {
+            constexpr int l = decltype(L)::value;
+            if constexpr (l & 1) dense(L, X, Y);
+            else dense(L, Y, X);
+        });
+        // views layer: input chunks 0-7 (the last hidden layer's output, sigma head
+        // chained: wave 0 chunks 0-3, wave 1 continues from its per-lane partial), then
+        // the direction k-step; the compositing weights are formed at k-step 7
+        constexpr bool kInX = (Net::kHidden & 1) == 0;     // last hidden output array
+        f4 (&vin)[16] = kInX ? X : Y;
+        f4 (&vout)[16] = kInX ? Y : X;
+        const uint32_t s0 = kPSamples * p;
+        float z[2] = {0.0f, 0.0f}, wj[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float sdf_h = 0.0f, dist[2] = {0.0f, 0.0f};
+        sfor<0, 9>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            constexpr int KS = KV + j;
+            f4 bc[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bc[i] = bn[i];
+            if constexpr (j == 5 && !Net::kSiren) {
+                // the compositing inputs that do not depend on the network (sample depth,
+                // segment length) come from the encode kernel; waited at this barrier
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    uint32_t s = s0 + 2 * c + (colB ? 1u : 0u);
+                    if (s >= G.N) s = G.N - 1;
+                    const float2 v = a.zd[tile_sid + (size_t)s * kTileRays];
+                    z[c] = v.x;
+                    dist[c] = v.y;
+                }
+            }
+            if constexpr (j == 7) {
+                if (p + 1 < p_end) load_inputs(p + 1);
+            }
+            auto nb = [&](f4 (&o)[4]) {
+                if constexpr (j < 7) {
+                    p_read_chunk(R, j + 1, o);
+                } else if constexpr (j == 7) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[i] = vx[i];
+                }
+            };
+            pstep<Net, KS, j == 0>(R, vout, bc, bn, nb, [&] {
+                if constexpr (j < 7) {
+                    act_out(std::integral_constant<int, NL - 2>{}, vin, j + 1);
+                    if constexpr (j == 6) {
+                        // the pair's sigma half-sums, added in wave order after the barrier
+                        sdfx_lds[pair][h][0][lane] = group_sum(sdfp[0]);
+                        sdfx_lds[pair][h][1][lane] = group_sum(sdfp[1]);
+                    }
+                } else if constexpr (j == 7) {
+                    // alpha of this wave's sample block h (the pair's waves split the
+                    // blocks; exchanged through LDS across this k-step's barrier)
+                    sdf_h = __fadd_rn(__fadd_rn(sdfx_lds[pair][0][h][lane], sdfx_lds[pair][1][h][lane]),
+                                      sig_b);
+                    const uint32_t s = s0 + 2 * h + (colB ? 1u : 0u);
+                    const bool s_ok = s < G.N;
+                    const uint32_t sc_ = s_ok ? s : G.N - 1;
+                    if constexpr (Net::kSiren) {
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            const uint32_t sc = min(s0 + 2 * c + (colB ? 1u : 0u), G.N - 1);
+                            z[c] = sample_z(G.sc, nr, fr, ray_index, sc);
+                        }
+                        const float zh = h ? z[1] : z[0];
+                        dist[0] = dist[1] = (sc_ + 1 < G.N)
+                                      ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), zh), dnorm)
+                                      : __fmul_rn(1e10f, dnorm);
+                    }
+                    const float dh = h ? dist[1] : dist[0];
+                    float alpha;
+                    if (a.with_sdf) {
+                        const float sig = __fdiv_rn(sigmoidf_(__fdiv_rn(-sdf_h, beta_s)), beta_s);
+                        alpha = 1.0f - expf(-sig * dh);
+                    } else {
+                        float raw = sdf_h;
+                        if (a.sigma_noise) raw += a.sigma_noise[(size_t)ray_index * G.N + sc_];
+                        const float sp = raw > 20.0f ? raw : log1pf(expf(raw));
+                        alpha = 1.0f - expf(-sp * dh);
+                    }
+                    alx_lds[pair][h][lane] = s_ok ? alpha : 0.0f;
+                } else {
+                    // compositing weights of the pass's 4 samples, identically in both
+                    // lanes of a ray and both waves of the pair, front to back
+                    const float al0 = alx_lds[pair][0][lane], al1 = alx_lds[pair][1][lane];
+                    const float o0 = ror8(al0), o1 = ror8(al1);
+                    const float aj[4] = {colB ? o0 : al0, colB ? al0 : o0, colB ? o1 : al1,
+                                         colB ? al1 : o1};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t s = s0 + k;
+                        if (s < G.N) {
+                            float w = aj[k] * T;
+                            if (a.force_background && s + 1 == G.N) w = 1.0f - wsum;
+                            T = T * ((1.0f - aj[k]) + 1e-10f);
+                            wsum += w;
+                            wj[k] = w;
+                        }
+                    }
+                }
+            });
+        });
+        // colour features f = sin(gamma_v x + beta_v) of the own rows, rgb half-sums.
+        // (Scalar fp32: a v_pk_fma_f32 form of this tail read some v_sin_f32 results
+        // before they were written -- nondeterministic colour features -- so there is no
+        // packed math in this kernel; tests/test_gpu_render.py::test_fused_render_deterministic.)
+        const float *f3g = fg(NF - 1), *f3b = fb(NF - 1);
+        float P[3][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};   // [rgb][block] half-sums
+        {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int f0 = 16 * (2 * t + (int)h) + 4 * (int)g;
+                const f4 gm = *reinterpret_cast<const f4 *>(f3g + f0);
+                const f4 bt = *reinterpret_cast<const f4 *>(f3b + f0);
+                const f4 w0 = *reinterpret_cast<const f4 *>(rgb_w + f0);
+                const f4 w1 = *reinterpret_cast<const f4 *>(rgb_w + kW + f0);
+                const f4 w2 = *reinterpret_cast<const f4 *>(rgb_w + 2 * kW + f0);
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    f4 fv;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        fv[r] = sin_rev(__fmaf_rn(gm[r], vout[2 * t + c][r], bt[r]));
+                        P[0][c] = __fmaf_rn(fv[r], w0[r], P[0][c]);
+                        P[1][c] = __fmaf_rn(fv[r], w1[r], P[1][c]);
+                        P[2][c] = __fmaf_rn(fv[r], w2[r], P[2][c]);
+                    }
+                    vout[2 * t + c] = fv;
+                }
+            }
+        }
+        float pc[2][3];
+#pragma unroll
+        for (int o = 0; o < 3; ++o) {
+            pc[0][o] = group_sum(P[o][0]);
+            pc[1][o] = group_sum(P[o][1]);
+        }
+        if (h == 0 && g == 0) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int o = 0; o < 3; ++o) pcol_lds[pair][3 * c + o][n] = pc[c][o];
+        }
+        if (a.features) {
+            // facc += w0 f0 + w1 f1 + w2 f2 + w3 f3 (in that order) by the lane of the
+            // ray's samples 0 and 2 (block 0 / 1, n < 8)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                f4 o0, o1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    o0[r] = ror8(vout[2 * t][r]);
+                    o1[r] = ror8(vout[2 * t + 1][r]);
+                }
+                if (!colB) {
+                    f4 v = facc[(t * 4 + g) * 8 + r8];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        v[r] = __fmaf_rn(wj[3], o1[r], __fmaf_rn(wj[2], vout[2 * t + 1][r],
+                                         __fmaf_rn(wj[1], o0[r], __fmaf_rn(wj[0], vout[2 * t][r], v[r]))));
+                    facc[(t * 4 + g) * 8 + r8] = v;
+                }
+            }
+        }
+        if (a.sdf && ray_ok && g == 0) {
+            const uint32_t s = s0 + 2 * h + (colB ? 1u : 0u);   // this wave's block
+            if (s < G.N) a.sdf[(size_t)ray_index * G.N + s] = sdf_h;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (h == 1) {
+            float q[2][3];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                q[c][0] = sigmoidf_(__fadd_rn(__fadd_rn(pcol_lds[pair][3 * c][n], pc[c][0]), rgb_b0));
+                q[c][1] = sigmoidf_(__fadd_rn(__fadd_rn(pcol_lds[pair][3 * c + 1][n], pc[c][1]), rgb_b1));
+                q[c][2] = sigmoidf_(__fadd_rn(__fadd_rn(pcol_lds[pair][3 * c + 2][n], pc[c][2]), rgb_b2));
+            }
+            float racc[3] = {racc0, racc1, racc2};
+#pragma unroll
+            for (int o = 0; o < 3; ++o) {
+                const float e0 = ror8(q[0][o]), e1 = ror8(q[1][o]);
+                const float qj[4] = {colB ? e0 : q[0][o], colB ? q[0][o] : e0, colB ? e1 : q[1][o],
+                                     colB ? q[1][o] : e1};
+                float v = racc[o];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v = __fmaf_rn(wj[k], qj[k], v);
+                racc[o] = v;
+            }
+            racc0 = racc[0];
+            racc1 = racc[1];
+            racc2 = racc[2];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (s0 + k < G.N) w_last = wj[k];
+            if (a.xyz) {
+                const float e0 = ror8(z[0]), e1 = ror8(z[1]);
+                const float zj[4] = {colB ? e0 : z[0], colB ? z[0] : e0, colB ? e1 : z[1],
+                                     colB ? z[1] : e1};
+                float xa[3] = {xacc0, xacc1, xacc2};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int d = 0; d < 3; ++d)
+                        xa[d] = __fmaf_rn(wj[k], __fadd_rn(ray.o[d], __fmul_rn(ray.d[d], zj[k])), xa[d]);
+                xacc0 = xa[0];
+                xacc1 = xa[1];
+                xacc2 = xa[2];
+            }
+        }
+    }
+    // the ring runs ahead across passes: no LDS-DMA may land after the workgroup ends
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!ray_ok || colB) return;
+    if (a.nseg > 1) {
+        const size_t Rr = (size_t)G.total_tiles * kTileRays;
+        float *pp = a.part + (size_t)seg * kPartQ * Rr + (size_t)tile * kTileRays + ray_in_tile;
+        if (a.features) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const uint32_t jf = 16 * (2 * t + h) + 4 * g;
+                const f4 v = facc[(t * 4 + g) * 8 + r8];
+                pp[(size_t)(jf + 0) * Rr] = v.x;
+                pp[(size_t)(jf + 1) * Rr] = v.y;
+                pp[(size_t)(jf + 2) * Rr] = v.z;
+                pp[(size_t)(jf + 3) * Rr] = v.w;
+            }
+        }
+        if (h == 1 && g == 0) {
+            const float q[8] = {racc0, racc1, racc2, xacc0, xacc1, xacc2, T, w_last};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pp[(size_t)(kW + k) * Rr] = q[k];
+        }
+        return;
+    }
+    const size_t HW = (size_t)G.H * G.W;
+    const size_t pix = (size_t)py * G.W + px;
+    if (h == 1) {
+        if (g < 3) {
+            const float rc = g == 0 ? racc0 : (g == 1 ? racc1 : racc2);
+            a.rgb[((size_t)b * 3 + g) * HW + pix] = __fadd_rn(-1.0f, __fmul_rn(2.0f, rc));
+            if (a.xyz) {
+                const float xc = g == 0 ? xacc0 : (g == 1 ? xacc1 : xacc2);
+                a.xyz[((size_t)b * 3 + g) * HW + pix] = xc;
+            }
+        } else if (a.mask) {
+            a.mask[(size_t)b * HW + pix] = w_last;
+        }
+    }
+    if (a.features) {
+        float *fbp = a.features + (size_t)b * kW * HW + pix;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t jf = 16 * (2 * t + h) + 4 * g;
+            const f4 v = facc[(t * 4 + g) * 8 + r8];
+            fbp[(size_t)(jf + 0) * HW] = v.x;
+            fbp[(size_t)(jf + 1) * HW] = v.y;
+            fbp[(size_t)(jf + 2) * HW] = v.z;
+            fbp[(size_t)(jf + 3) * HW] = v.w;
+        }
+    }
+}
 
 // ----------------------------------------------------------------------------
 // field_r_kernel: one wave per SIMD on v_mfma_f32_32x32x16_f16.
@@ -1103,10 +1820,20 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     f.xyz = a->xyz;
     f.mask = a->mask;
     f.part = part;
-    f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background,
-                               a->max_field_segments) : 1;
-    const uint32_t blocks = g.B * ((g.tiles_per_face + kRTiles - 1) / kRTiles) * f.nseg;
-    hipLaunchKernelGGL((field_r_kernel<Net>), dim3(blocks), dim3(kRThreads), 0, st, f);
+    // field_r_kernel for ngp; the SIREN net (nine FiLM layers, no encode stage, no
+    // sample-segment split) keeps field_p_kernel, 6 % faster on it (7.76 vs 8.25 ms per
+    // 32 faces, interleaved A/B on one box; field_r_kernel is 3.5 % faster on ngp)
+    if constexpr (Net::kFieldR) {
+        f.nseg = part ? field_nseg(g.B, g.tiles_per_face, g.N, a->force_background,
+                                   a->max_field_segments) : 1;
+        const uint32_t blocks = g.B * ((g.tiles_per_face + kRTiles - 1) / kRTiles) * f.nseg;
+        hipLaunchKernelGGL((field_r_kernel<Net>), dim3(blocks), dim3(kRThreads), 0, st, f);
+    } else {
+        if (part) return fail(SDFR_EUNSUPPORTED, "render: field_p_kernel has no segment split");
+        f.nseg = 1;
+        const uint32_t blocks = g.B * ((g.tiles_per_face + kPTiles - 1) / kPTiles);
+        hipLaunchKernelGGL((field_p_kernel<Net>), dim3(blocks), dim3(kPThreads), 0, st, f);
+    }
     int rc = check_launch("render: field (f16x3)");
     if (rc || f.nseg == 1) return rc;
     const uint32_t rays = g.total_tiles * kTileRays;
