@@ -134,6 +134,10 @@ struct EncodeArgs {
 //           slower, 1.17 ms, with four levels' tables live in each L2).
 //  +32      SPT = 2 samples per thread, 256 apart: twice the corner loads in
 //           flight per wave.                                    -> 289 0.77 ms
+//           Since the per-sample coordinate comes precomputed (sample_geom_kernel)
+//           one sample per thread is faster again: 257 0.787 vs 289 0.803 ms (and
+//           258, two levels per thread, 0.824), interleaved on one box, geom
+//           kernel included.
 // The gather is bound by L1 tag lookups (one 128-B line per lane per load
 // instruction, ~54 cycles per wave-load measured): the wins above all cut
 // load instructions per sample-level (6 -> ~4.9).  Measured and dropped:
@@ -141,7 +145,7 @@ struct EncodeArgs {
 // sc1 (L2-dropping) output stores (+-1%), adjacent level pairs {2y, 2y+1}
 // (1.09 ms), whole image rows per wave (0.86 ms), 4 samples per thread (0.78 ms),
 // nontemporal table loads (2.1 ms: the table no longer stays in L2).
-constexpr uint32_t kEncDefault = 256 | 32 | 1;
+constexpr uint32_t kEncDefault = 256 | 1;
 
 // level_interp<3,2> with paired x-corner loads: the same corner weights
 // (x factor first, then y, z) and the same fma order over corners 0..7, so the
@@ -976,12 +980,14 @@ static int launch_encode(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *
         case 2: launch_encode_mode<true, false, 2, 1>(st, e); break;
         case 32 | 1: launch_encode_mode<true, false, 1, 2>(st, e); break;
         case 256 | 1: launch_encode_mode<true, true, 1, 1>(st, e); break;
+        case 256 | 2: launch_encode_mode<true, true, 2, 1>(st, e); break;
         case 256 | 32 | 2: launch_encode_mode<true, true, 2, 2>(st, e); break;
-        default: launch_encode_mode<true, true, 1, 2>(st, e); break;   // 289
+        case 256 | 32 | 1: launch_encode_mode<true, true, 1, 2>(st, e); break;
+        default: launch_encode_mode<true, true, 1, 1>(st, e); break;   // 257
     }
 #else
-    static_assert(kEncDefault == (256 | 32 | 1), "product gather: A8, 1 level, 2 samples");
-    launch_encode_mode<true, true, 1, 2>(st, e);
+    static_assert(kEncDefault == (256 | 1), "product gather: A8, 1 level, 1 sample per thread");
+    launch_encode_mode<true, true, 1, 1>(st, e);
 #endif
     return check_launch("render_ngp: encode");
 }
@@ -1022,7 +1028,7 @@ int sdfr_camera_extrinsics(const float *azim, const float *elev, uint32_t B, flo
 #ifdef SDFR_ABLATION
 // profiling hooks (make ABLATION=1 builds only; process-global)
 int sdfr_debug_set_encode_mode(int mode) {
-    const int ok[] = {1, 2, 9, 33, 257, 289, 290};
+    const int ok[] = {1, 2, 9, 33, 257, 258, 289, 290};
     bool found = false;
     for (int m : ok) found |= m == mode;
     if (!found)
