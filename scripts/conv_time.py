@@ -16,7 +16,8 @@ sys.path.insert(0, sys.argv[1])
 from sdfr_loader import load
 sdfr = load()
 from sdface_gan_amd import decoder_ops as ops
-dev = "cuda:0"; B = 32
+import os
+dev = "cuda:0"; B = int(os.environ.get("B", "32"))
 # (Cin, Cout, H_in, transposed): conv1, up 64->128, conv 128, up 128->256, conv 256
 LAYERS = [(256, 512, 64, False), (512, 256, 64, True), (256, 256, 128, False),
           (256, 128, 128, True), (128, 128, 256, False)]
@@ -32,7 +33,7 @@ for Cin, Cout, H, tr in LAYERS:
     ts = []
     for r in range(reps + 2):
         ev[0].record()
-        ops.conv3x3_f16x3(xs, packed, Cout, transposed=tr)
+        ops.conv3x3_f16x3(xs, packed, Cout, transposed=tr, split_k=True)
         ev[1].record()
         torch.cuda.synchronize()
         if r >= 2: ts.append(ev[0].elapsed_time(ev[1]))
