@@ -260,11 +260,29 @@ def main():
             e.record()              # materialise the event handles before the timed loop
     torch.cuda.synchronize()
 
-    def set_events(k):
-        g.renderer.stage_events = evs[k]
-    elapsed = timed_steps(step, args.steps, world, device, before_step=set_events)
-    g.renderer.stage_events = None
+    # and around the decoder's fused regular convolutions (conv_h_kernel), on the
+    # decoder's stream
+    dev_evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(8)] for _ in range(args.steps)]
+    for pairs in dev_evs:
+        for a_, b_ in pairs:
+            a_.record()
+            b_.record()
+    torch.cuda.synchronize()
+    conv_flops = []
 
+    def set_events(k):
+        if k > 0:
+            conv_flops.append(g.decoder.conv_flops)
+        g.renderer.stage_events = evs[k]
+        g.decoder.profile_convs(dev_evs[k])
+    elapsed = timed_steps(step, args.steps, world, device, before_step=set_events)
+    conv_flops.append(g.decoder.conv_flops)
+    n_conv = g.decoder._conv_ev
+    g.renderer.stage_events = None
+    g.decoder.profile_convs(None)
+
+    conv_ms = sum(a_.elapsed_time(b_) for pairs in dev_evs for a_, b_ in pairs[:n_conv]) / args.steps
     enc_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     field_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
     render_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args.steps
@@ -286,6 +304,23 @@ def main():
             return None
 
     traffic = traffic_of(field_kernel)
+
+    def decoder_roofline():
+        """The decoder's fused regular convolutions (conv_h_kernel, now the largest
+        kernel of the step): their fp32-equivalent FLOPs (2 B H W 9 Cin Cout per layer)
+        over their HIP-event time, against the same fp32-accurate split-fp16 bound."""
+        if not conv_ms or not conv_flops or n_conv == 0:
+            return None
+        flops = sum(conv_flops) / len(conv_flops)
+        tf = flops / (conv_ms * 1e-3) / 1e12
+        peak = MFMA_F16_PEAK_TFLOPS / 3
+        per_launch = traffic_of("conv_h_kernel")
+        return {"kernel": "conv_h_kernel (3x3 convs + styled epilogue + ToRGB partials, "
+                          "3 split-fp16 v_mfma_f32_16x16x32_f16 terms per fp32 tile)",
+                "bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
+                "frac": tf / peak, "launches_per_step": n_conv, "flop_per_step": flops,
+                "traffic": None if per_launch is None else per_launch * n_conv,
+                "counters": counters_of("conv_h_kernel")}
 
     def counters_of(kernel):
         """MFMA-busy fraction of `kernel` from the committed SQ counter passes
@@ -357,8 +392,9 @@ def main():
             "bound": "hbm", "achieved": gather_gbps, "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": gather_gbps / HBM_PEAK_GBPS,
             "traffic": traffic_of("ngp_encode_kernel")},
+        "roofline_decoder": decoder_roofline(),
         "stage_ms_per_step": {"renderer_total": render_ms, "hash_grid": enc_ms,
-                              "field": field_ms},
+                              "field": field_ms, "decoder_regular_convs": conv_ms},
         "cpu_baseline": None,
     }
     if not args.no_extras:

@@ -24,9 +24,10 @@ from collections import defaultdict
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
-# fp32 ngp / f16x3 ngp / f16x3 siren field kernels
+# fp32 ngp / f16x3 ngp / f16x3 siren field kernels, the decoder's regular convs
 FIELDS = ("ngp_field_kernel", "field_r_kernel<sdfr::NgpNet>", "field_p_kernel<sdfr::SirenNet>",
-          "field_x_kernel<0, sdfr::NgpNet>", "field_x_kernel<0, sdfr::SirenNet>")
+          "field_x_kernel<0, sdfr::NgpNet>", "field_x_kernel<0, sdfr::SirenNet>",
+          "conv_h_kernel")                  # (and the decoder's largest kernel)
 ENCODE = "ngp_encode_kernel"
 
 

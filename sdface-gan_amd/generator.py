@@ -303,6 +303,12 @@ class Decoder(nn.Module):
         # regular f16x3 convs with the styled epilogue fused into the conv kernel
         # (sdfr_conv3x3_f16x3_act + sdfr_rgb_finish) instead of a separate pass
         self.fuse_conv_act = True
+        # profiling: (start, end) HIP event pairs recorded on the current stream around
+        # the fused regular convolutions (conv_h_kernel) of the next forward, in order,
+        # and their fp32-equivalent FLOPs (bench.py's decoder roofline)
+        self.conv_events = None
+        self.conv_flops = 0
+        self._conv_ev = 0
         self._fir = None
         self._packs = {}
         self._mod_stack = None
@@ -591,6 +597,11 @@ class Decoder(nn.Module):
             tc._sdfr_base = cache
         return cache[1]
 
+    def profile_convs(self, events):
+        """Record `events[k] = (start, end)` around the k-th fused regular convolution of
+        the next forward (None: stop); `conv_flops` counts their fp32-equivalent FLOPs."""
+        self.conv_events, self._conv_ev, self.conv_flops = events, 0, 0
+
     def _fused_forward(self, features, latent, noise, sty=None):
         """Same computation as the module path: per layer one split-fp16 convolution
         (or MIOpen's) plus one sdfr_styled_epilogue on NHWC activations -- for the
@@ -626,10 +637,17 @@ class Decoder(nn.Module):
                     tc = to_rgb.conv
                     s_rgb = rgb_mods[i // 2]
                     rgb_w = self._rgb_base(tc)[None] * s_rgb[:, None, :]
+                ev = self.conv_events
+                if ev is not None:
+                    ev[self._conv_ev][0].record()
                 x, part = conv3x3_f16x3_act(
                     x, packed, cout, demod=demod_su, bias=sc.activate.bias,
                     noise_weight=sc.noise.weight, noise=n,
                     s_next=None if last else mods[i + 1], store_y=not last, rgb_w=rgb_w)
+                if ev is not None:
+                    ev[self._conv_ev][1].record()
+                    self._conv_ev += 1
+                    self.conv_flops += 2 * B * H * W * 9 * mc.weight.shape[2] * cout
                 if part is not None:
                     rgb = rgb_finish(part, to_rgb.bias, skip=rgb if i else None, fir=self._fir)
                 continue
