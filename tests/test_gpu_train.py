@@ -234,10 +234,14 @@ def test_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path, ngp):
             for k, v in got.items():
                 want = ref[k] * scale
                 # fp32 sums in a different order (atomics / binned table gradient,
-                # the all-reduce): relative to the tensor's largest entry
-                tol = 2e-5 * max(1e-6, float(want.abs().max()))
+                # the all-reduce): relative to the tensor's largest entry, with an
+                # absolute floor of 1e-9 -- a scalar gradient that is a cancelling sum
+                # over every sample (renderer.sigmoid_beta, |g| ~ 1e-6) carries ~1e-10 of
+                # that reordering noise (seen once in ~10 runs)
+                tol = max(2e-5 * float(want.abs().max()), 1e-9)
                 assert torch.allclose(v, want, rtol=2e-4, atol=tol), \
-                    f"{what} {k}: max |diff| {float((v - want).abs().max()):.3e}"
+                    (f"{what} {k}: max |diff| {float((v - want).abs().max()):.3e} "
+                     f"(max |ref| {float(want.abs().max()):.3e})")
         if not ngp:
             continue
         # the hashed levels (5-15) carry most of the table's gradient rows
