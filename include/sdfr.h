@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 7
+#define SDFR_ABI_VERSION 8
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -314,6 +314,22 @@ int sdfr_film_backward(float *dy, float *dgamma, float *dbeta, float *dbf, const
                        const float *y, const float *gamma, const float *beta, uint32_t M,
                        uint32_t N, uint32_t rows_per_face, void *ws, size_t ws_bytes,
                        void *stream);
+
+/* sdfr_film_backward_grad: the derivative of sdfr_film_backward's (dy, dgamma, dbeta)
+ * w.r.t. (ds, y, gamma, beta) -- the second-order step of a FiLM layer whose backward
+ * was built with create_graph (the SIREN eikonal term, sdf_model.py:224-229, then
+ * differentiated by the loss).  Given the upstream gradients g_dy [M,N], g_dgamma,
+ * g_dbeta [F,N] (each may be NULL = 0), with u = gamma[f] y + beta[f] and
+ * H = g_dy gamma[f] + g_dgamma[f] y + g_dbeta[f]:
+ *   d_ds = H cos u, d_y = -H ds sin u gamma[f] + g_dgamma[f] ds cos u  [M,N],
+ *   d_gamma[f] = sum (-H ds sin u y + g_dy ds cos u), d_beta[f] = sum -H ds sin u  [F,N];
+ * sums in a fixed order; ws >= sdfr_film_backward_grad_ws_bytes(M, N, rows_per_face). */
+size_t sdfr_film_backward_grad_ws_bytes(uint32_t M, uint32_t N, uint32_t rows_per_face);
+int sdfr_film_backward_grad(float *d_ds, float *d_y, float *d_gamma, float *d_beta,
+                            const float *ds, const float *y, const float *gamma,
+                            const float *beta, const float *g_dy, const float *g_dgamma,
+                            const float *g_dbeta, uint32_t M, uint32_t N, uint32_t rows_per_face,
+                            void *ws, size_t ws_bytes, void *stream);
 
 /* The MLP's narrow output heads for training (sigma_linear 256 -> 1, rgb_linear
  * 256 -> 3; LinearLayer, sdf_model.py:23-41, at :1586-1588), fp32 FMAs, J <= 4 outputs,

@@ -23,7 +23,7 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 7
+ABI_VERSION = 8
 FIELD_F16X3 = 0
 FIELD_FP32 = 1
 
@@ -49,6 +49,7 @@ EXPORTS = (
     "sdfr_linear_pack_bytes", "sdfr_linear_pack", "sdfr_linear_f16x3",
     "sdfr_linear_wgrad_ws_bytes", "sdfr_linear_wgrad_f16x3",
     "sdfr_film_linear_f16x3", "sdfr_film_backward_ws_bytes", "sdfr_film_backward",
+    "sdfr_film_backward_grad_ws_bytes", "sdfr_film_backward_grad",
     "sdfr_linear_head_forward", "sdfr_linear_head_ws_bytes", "sdfr_linear_head_backward",
 )
 
@@ -218,6 +219,9 @@ def lib():
     L.sdfr_film_backward_ws_bytes.argtypes = [_u32, _u32, _u32]
     L.sdfr_film_backward_ws_bytes.restype = ctypes.c_size_t
     L.sdfr_film_backward.argtypes = [_vp] * 8 + [_u32] * 3 + [_vp, ctypes.c_size_t, _vp]
+    L.sdfr_film_backward_grad_ws_bytes.argtypes = [_u32, _u32, _u32]
+    L.sdfr_film_backward_grad_ws_bytes.restype = ctypes.c_size_t
+    L.sdfr_film_backward_grad.argtypes = [_vp] * 11 + [_u32] * 3 + [_vp, ctypes.c_size_t, _vp]
     L.sdfr_linear_head_forward.argtypes = [_vp] * 4 + [_u32] * 3 + [_vp]
     L.sdfr_linear_head_ws_bytes.argtypes = [_u32, _u32, _u32]
     L.sdfr_linear_head_ws_bytes.restype = ctypes.c_size_t

@@ -448,6 +448,47 @@ __global__ void __launch_bounds__(256) film_bwd_reduce_kernel(const float *__res
     }
 }
 
+// Second order (sdfr_film_backward_grad): the derivative of film_bwd_kernel's outputs
+// (dy, dgamma, dbeta) w.r.t. its inputs, for a graph built with create_graph (the
+// SIREN eikonal term, differentiated again by the loss).  Per element, with u = gm y +
+// bt recomputed as film_bwd_kernel does and H = G_dy gm + G_dgamma y + G_dbeta:
+//   d_ds = H cos u;  dU = -H ds sin u;  d_y = dU gm + G_dgamma ds cos u;
+// per (face, column): d_gamma = sum (dU y + G_dy ds cos u), d_beta = sum dU.  One thread
+// per column over a block of rows (film_bwd_kernel's layout); partials reduced by
+// film_bwd_reduce_kernel (third sum unused).  The composite torch form (autograd of
+// du = ds cos(gamma y + beta), dy = du gamma, the two row sums) launched ~18
+// elementwise / reduction passes per layer.
+__global__ void __launch_bounds__(256) film_bwd2_kernel(
+    const float *__restrict__ ds, const float *__restrict__ y, const float *__restrict__ gamma,
+    const float *__restrict__ beta, const float *__restrict__ gdy, const float *__restrict__ gdg,
+    const float *__restrict__ gdb, float *__restrict__ d_ds, float *__restrict__ d_y, uint32_t N,
+    uint32_t rows_per_face, uint32_t rpb, float *__restrict__ part) {
+    const uint32_t f = blockIdx.y, j = blockIdx.x, c = threadIdx.x;
+    const uint32_t r0 = j * rpb, r1 = min(rows_per_face, r0 + rpb);
+    const size_t fc = (size_t)f * N + c;
+    const float gm = gamma[fc], bt = beta[fc];
+    const float gg = gdg ? gdg[fc] : 0.0f, gb = gdb ? gdb[fc] : 0.0f;
+    float sg = 0.0f, sb = 0.0f;
+    const size_t base = (size_t)f * rows_per_face;
+    for (uint32_t r = r0; r < r1; ++r) {
+        const size_t e = (base + r) * N + c;
+        const float dsv = ds[e], yv = y[e], gd = gdy ? gdy[e] : 0.0f;
+        const float u = __fadd_rn(__fmul_rn(gm, yv), bt);
+        const float cu = cos_hw(u), su = sin_hw(u);
+        const float h = __fadd_rn(__fadd_rn(__fmul_rn(gd, gm), __fmul_rn(gg, yv)), gb);
+        const float dsc = __fmul_rn(dsv, cu);
+        const float du_ = -__fmul_rn(__fmul_rn(h, dsv), su);
+        d_ds[e] = __fmul_rn(h, cu);
+        d_y[e] = __fadd_rn(__fmul_rn(du_, gm), __fmul_rn(gg, dsc));
+        sg = __fadd_rn(sg, __fadd_rn(__fmul_rn(du_, yv), __fmul_rn(gd, dsc)));
+        sb = __fadd_rn(sb, du_);
+    }
+    float *p = part + ((size_t)f * gridDim.x + j) * 3 * N;
+    p[c] = sg;
+    p[N + c] = sb;
+    p[2 * N + c] = 0.0f;
+}
+
 // ----------------------------------------------------------------------------
 // weight gradient partials: part[p][n][k] = sum over workgroup p's rows of
 // dy[m, n] x[m, k] (N = 256; blockIdx.y = which 128 of the n).  16 waves in two roles
@@ -788,6 +829,37 @@ int sdfr_film_backward(float *dy, float *dgamma, float *dbeta, float *dbf, const
     hipLaunchKernelGGL(film_bwd_reduce_kernel, dim3(N / 32, F), dim3(256), 0, st, part, nb, N,
                        dgamma, dbeta, dbf);
     return check_launch("film_backward: reduce");
+}
+
+int sdfr_film_backward_grad(float *d_ds, float *d_y, float *d_gamma, float *d_beta,
+                            const float *ds, const float *y, const float *gamma,
+                            const float *beta, const float *g_dy, const float *g_dgamma,
+                            const float *g_dbeta, uint32_t M, uint32_t N, uint32_t rows_per_face,
+                            void *ws, size_t ws_bytes, void *stream) {
+    if (M == 0) return SDFR_OK;
+    if (!d_ds || !d_y || !d_gamma || !d_beta || !ds || !y || !gamma || !beta)
+        return fail(SDFR_EINVAL, "film_backward_grad: null pointer");
+    if (N != 256 || rows_per_face == 0 || M % rows_per_face)
+        return fail(SDFR_EINVAL, "film_backward_grad: N = 256, M a multiple of rows_per_face");
+    if (!ws || ws_bytes < sdfr_film_backward_ws_bytes(M, N, rows_per_face) + (size_t)(M / rows_per_face) * N * 4)
+        return fail(SDFR_EINVAL, "film_backward_grad: workspace too small");
+    const uint32_t F = M / rows_per_face, nb = film_blocks_per_face(F, rows_per_face);
+    const uint32_t rpb = ceil_div(rows_per_face, nb);
+    hipStream_t st = (hipStream_t)stream;
+    float *part = static_cast<float *>(ws);
+    float *unused = part + (size_t)F * nb * 3 * N;          // the reduce's third sum
+    hipLaunchKernelGGL(film_bwd2_kernel, dim3(nb, F), dim3(256), 0, st, ds, y, gamma, beta, g_dy,
+                       g_dgamma, g_dbeta, d_ds, d_y, N, rows_per_face, rpb, part);
+    int rc = check_launch("film_backward_grad");
+    if (rc) return rc;
+    hipLaunchKernelGGL(film_bwd_reduce_kernel, dim3(N / 32, F), dim3(256), 0, st, part, nb, N,
+                       d_gamma, d_beta, unused);
+    return check_launch("film_backward_grad: reduce");
+}
+
+size_t sdfr_film_backward_grad_ws_bytes(uint32_t M, uint32_t N, uint32_t rows_per_face) {
+    if (M == 0 || rows_per_face == 0) return 0;
+    return sdfr_film_backward_ws_bytes(M, N, rows_per_face) + (size_t)(M / rows_per_face) * N * 4;
 }
 
 int sdfr_linear_f16x3(float *out, const float *x, const void *packed, const float *bias,

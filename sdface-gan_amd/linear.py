@@ -130,6 +130,58 @@ def _film_bwd(ds2, y, g2, b2):
     return dy, dg, db_, dbf
 
 
+def _film_bwd2(ds2, y, g2, b2, gdy, gdg, gdb):
+    """The derivative of _film_bwd's (dy, dgamma, dbeta) w.r.t. (ds, y, gamma, beta)
+    given their upstream gradients (each may be None) (sdfr_film_backward_grad)."""
+    M, N = ds2.shape
+    F_ = g2.shape[0]
+    L = _lib.lib()
+    d_ds = torch.empty(M, N, device=ds2.device, dtype=torch.float32)
+    d_y = torch.empty(M, N, device=ds2.device, dtype=torch.float32)
+    d_g = torch.empty(F_, N, device=ds2.device, dtype=torch.float32)
+    d_b = torch.empty(F_, N, device=ds2.device, dtype=torch.float32)
+    nws = L.sdfr_film_backward_grad_ws_bytes(M, N, M // F_)
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=ds2.device)
+    opt = [None if t is None else _a16(t.contiguous()) for t in (gdy, gdg, gdb)]
+    _lib.check(L.sdfr_film_backward_grad(
+        _lib.ptr(d_ds), _lib.ptr(d_y), _lib.ptr(d_g), _lib.ptr(d_b), _lib.ptr(ds2), _lib.ptr(y),
+        _lib.ptr(g2), _lib.ptr(b2), *[None if t is None else _lib.ptr(t) for t in opt],
+        M, N, M // F_, _lib.ptr(ws), nws, _lib.stream_of(ds2)), "sdfr_film_backward_grad")
+    return d_ds, d_y, d_g, d_b
+
+
+class _FiLMGrad(torch.autograd.Function):
+    """The FiLM backward's elementwise part as ONE differentiable op, for graphs built
+    with create_graph (the SIREN eikonal term): forward = sdfr_film_backward
+    (du = ds cos(gamma y + beta); dy = du gamma, dgamma = sum du y, dbeta = sum du),
+    backward = sdfr_film_backward_grad.  Autograd of the same math as torch ops ran
+    ~18 elementwise / reduction passes over the [rows, 256] activation per layer (the
+    SIREN stage-1 step's largest cost).  Not differentiable a third time."""
+
+    @staticmethod
+    def forward(ctx, ds, y, gamma, beta):
+        N = y.shape[-1]
+        F_ = gamma.shape[0]
+        ds2 = _a16(ds.reshape(-1, N).contiguous())
+        y2 = _a16(y.reshape(-1, N).contiguous())
+        g2, b2 = _a16(gamma.reshape(F_, N).contiguous()), _a16(beta.reshape(F_, N).contiguous())
+        dy, dg, db_, _ = _film_bwd(ds2, y2, g2, b2)
+        ctx.save_for_backward(ds2, y2, g2, b2)
+        ctx.shapes = (ds.shape, y.shape, gamma.shape, beta.shape)
+        return dy.view(y.shape), dg.view(gamma.shape), db_.view(beta.shape)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gdy, gdg, gdb):
+        ds2, y2, g2, b2 = ctx.saved_tensors
+        sh_ds, sh_y, sh_g, sh_b = ctx.shapes
+        N, F_ = y2.shape[1], g2.shape[0]
+        d_ds, d_y, d_g, d_b = _film_bwd2(
+            ds2, y2, g2, b2, None if gdy is None else gdy.reshape(-1, N),
+            None if gdg is None else gdg.reshape(F_, N), None if gdb is None else gdb.reshape(F_, N))
+        return d_ds.view(sh_ds), d_y.view(sh_y), d_g.view(sh_g), d_b.view(sh_b)
+
+
 def _kp(K: int) -> int:
     """In features padded to the GEMM's multiple of 4 (zero columns: the product is
     unchanged)."""
@@ -316,14 +368,10 @@ class _FiLMLinearF16x3(torch.autograd.Function):
             # create_graph (the SIREN eikonal term): the same gradients as differentiable
             # ops, y put on the graph as the linear layer's output (_LinearGiven)
             yl = _LinearGiven.apply(x, w, bias, y.view(*lead, N))
-            du = ds * torch.cos(gamma * yl + beta)
-            dyl = du * gamma
-            red = tuple(range(1, du.dim() - 1))
+            dyl, gg, gbt = _FiLMGrad.apply(ds, yl, gamma, beta)
             gx, gw, gb = _linear_backward(dyl, x, w, has_bias, (nx, nw, nb),
                                           (None, None))
-            gg = (du * yl).sum(red, keepdim=True).view(gamma.shape) if ng else None
-            gbt = du.sum(red, keepdim=True).view(beta.shape) if nbe else None
-            return gx, gw, gb, gg, gbt, None
+            return gx, gw, gb, (gg if ng else None), (gbt if nbe else None), None
         ds2 = _a16(ds.reshape(-1, N).contiguous())
         g2, b2 = _a16(gamma.reshape(F_, N)), _a16(beta.reshape(F_, N))
         dy, dg, db_, dbf = _film_bwd(ds2, y, g2, b2)

@@ -19,7 +19,7 @@ lin = importlib.import_module(sdfr.__name__ + ".linear")
 @pytest.fixture()
 def cpu_kernels(monkeypatch):
     L = lin
-    calls = {"wgrad": 0, "gemm": 0, "film_fwd": 0, "film_bwd": 0, "head_bwd": 0}
+    calls = {"wgrad": 0, "gemm": 0, "film_fwd": 0, "film_bwd": 0, "film_bwd2": 0, "head_bwd": 0}
 
     def pack(w, transposed):
         return (w.t() if transposed else w).contiguous()      # B [N, K]
@@ -51,6 +51,25 @@ def cpu_kernels(monkeypatch):
         dy = du * g2[:, None]
         return dy.reshape(-1, N), (du * yf).sum(1), du.sum(1), dy.sum(1)
 
+    def film_bwd2(ds2, y, g2, b2, gdy, gdg, gdb):
+        # sdfr_film_backward_grad's formulas (include/sdfr.h), checked here against
+        # autograd of the reference's ops through the whole double backward
+        calls["film_bwd2"] += 1
+        F_, N = g2.shape
+        dsf, yf = ds2.view(F_, -1, N), y.view(F_, -1, N)
+        gm, bt = g2[:, None], b2[:, None]
+        u = gm * yf + bt
+        cu, su = torch.cos(u), torch.sin(u)
+        gd = gdy.view(F_, -1, N) if gdy is not None else torch.zeros_like(dsf)
+        gg = gdg[:, None] if gdg is not None else torch.zeros_like(gm)
+        gb = gdb[:, None] if gdb is not None else torch.zeros_like(gm)
+        h = gd * gm + gg * yf + gb
+        dU = -h * dsf * su
+        d_ds = h * cu
+        d_y = dU * gm + gg * dsf * cu
+        return (d_ds.reshape(-1, N), d_y.reshape(-1, N), (dU * yf + gd * dsf * cu).sum(1),
+                dU.sum(1))
+
     def head_fwd(x2, w, bias):
         out = x2 @ w.t()
         return out + bias if bias is not None else out
@@ -61,7 +80,8 @@ def cpu_kernels(monkeypatch):
                 gy2.sum(0) if nb else None)
 
     for k, v in dict(_pack=pack, _gemm=gemm, _wgrad=wgrad, _film_fwd=film_fwd, _film_bwd=film_bwd,
-                     _head_fwd=head_fwd, _head_bwd=head_bwd, _on_device=lambda x: True).items():
+                     _film_bwd2=film_bwd2, _head_fwd=head_fwd, _head_bwd=head_bwd,
+                     _on_device=lambda x: True).items():
         monkeypatch.setattr(L, k, v)
     return calls
 
@@ -100,6 +120,7 @@ def test_siren_double_backward_matches_reference_ops(cpu_kernels):
     torch.testing.assert_close(ea, eb, rtol=1e-4, atol=1e-5)
     la.backward()
     lb.backward()
+    assert cpu_kernels["film_bwd2"] > 0                      # the second-order FiLM op ran
     torch.testing.assert_close(la, lb, rtol=1e-5, atol=1e-6)
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         assert pa.grad is not None, n
