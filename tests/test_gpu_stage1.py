@@ -135,6 +135,46 @@ def test_fc_generator_vs_reference(sdfr, golden_dir):
         _rel(f"fc_{k}", v.cpu(), g[k], 2e-5)
 
 
+def test_fc_generator_hip_gemms_vs_torch(sdfr):
+    """FCGenerator's 256 -> 256 layers and heads on the split-fp16 training GEMMs (shapes
+    routed: >= 1024 rows) against the same module on F.linear: forward, and an
+    eikonal-style double backward (create_graph through the ReLU MLP) to every weight."""
+    import torch.nn.functional as F
+    torch.manual_seed(11)
+    net = sdfr.FCGenerator().to(DEV)
+    x = torch.rand(2, 16, 64, 6, device=DEV) * 2 - 1                # 2048 rows per layer
+    styles = torch.randn(2, 256, device=DEV)
+
+    def ref_forward(x):                      # sdf_model.py:1640-1670 on F.linear
+        pts, views = torch.split(x, [3, 3], dim=-1)
+        pts, views = net.transform_points(pts), net.transform_points(views, True)
+        h = F.linear(pts, net.x_in.weight, net.x_in.bias)
+        s = F.linear(styles, net.style_in.weight, net.style_in.bias)[:, None, None]
+        h = F.relu(h + s)
+        for layer in net.pts_linears:
+            h = F.relu(F.linear(h, layer.weight, layer.bias))
+        sdf = F.linear(h, net.sigma_linear.weight, net.sigma_linear.bias)
+        feat = F.linear(torch.cat([h, views], -1), net.views_linears.weight, net.views_linears.bias)
+        rgb = F.linear(feat, net.rgb_linear.weight, net.rgb_linear.bias)
+        return torch.cat([rgb, sdf, feat], -1)
+
+    def run(fwd):
+        net.zero_grad(set_to_none=True)
+        xx = x.clone().requires_grad_(True)
+        out = fwd(xx)
+        sdf = out[..., 3:4]
+        eik = torch.autograd.grad(sdf, xx, torch.ones_like(sdf), create_graph=True)[0][..., :3]
+        loss = out[..., :3].mean() + ((eik.norm(dim=-1) - 1) ** 2).mean()
+        loss.backward()
+        return out.detach(), {n: p.grad.clone() for n, p in net.named_parameters()}
+
+    out_a, g_a = run(lambda xx: net(xx, styles))
+    out_b, g_b = run(ref_forward)
+    _rel("fc_hip_out", out_a.cpu(), out_b.cpu().numpy(), 1e-5)
+    for n in g_b:
+        _rel(f"fc_hip_grad_{n}", g_a[n].cpu(), g_b[n].cpu().numpy(), 2e-4)
+
+
 @pytest.mark.parametrize("gemm", ["f16x3", "torch"])
 def test_siren_eikonal_double_backward_vs_reference(sdfr, golden_dir, gemm):
     """configs[4]'s stage 1 on the SIREN network (rendering.type 'sdf'): the eikonal term
