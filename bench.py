@@ -76,13 +76,14 @@ def setup_dist(args=None):
     """One process per GPU (torchrun's RANK / LOCAL_RANK / WORLD_SIZE): backend "nccl"
     (RCCL over xGMI).  SDFR_BENCH_BACKEND=gloo with SDFR_BENCH_SAME_DEVICE=1 runs the
     same multi-rank path with every rank on cuda:0 (the world-2 test on a one-GPU
-    box, tests/test_gpu_train.py)."""
+    box, tests/test_gpu_train.py); SDFR_BENCH_DIST=1 forms the process group at world
+    size 1 too (RCCL init, barriers and the MAX all-reduce on a one-GPU box)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("SDFR_BENCH_SAME_DEVICE") == "1":
         local = 0
-    if world > 1:
+    if world > 1 or os.environ.get("SDFR_BENCH_DIST") == "1":
         torch.cuda.set_device(local)
         backend = os.environ.get("SDFR_BENCH_BACKEND", "nccl")
         kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
@@ -93,7 +94,8 @@ def setup_dist(args=None):
 def timed_steps(step, steps, world, device, before_step=None):
     """The timed region: barrier + synchronize on both sides of exactly `steps`
     steps; returns the MAX over ranks of the wall time (seconds)."""
-    if world > 1:
+    grouped = dist.is_available() and dist.is_initialized()
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -102,10 +104,10 @@ def timed_steps(step, steps, world, device, before_step=None):
             before_step(k)
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if grouped:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -262,8 +264,9 @@ def main():
 
     # and around the decoder's fused regular convolutions (conv_h_kernel), on the
     # decoder's stream
+    n_pairs = 1 + len(g.decoder.convs)        # at most one pair per regular convolution
     dev_evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                for _ in range(8)] for _ in range(args.steps)]
+                for _ in range(n_pairs)] for _ in range(args.steps)]
     for pairs in dev_evs:
         for a_, b_ in pairs:
             a_.record()
@@ -424,15 +427,18 @@ def main():
             g.renderer.stage_events = None
             g.renderer.field_precision = args.field_precision
             f32_ms = ev[2].elapsed_time(ev[3])
+            # ngp_field_kernel runs the uncomposed network (input_linear, then
+            # pts_linears.0): the reference's 550,912 FLOP/sample
             line["extras"]["fp32_field"] = {
                 "kernel": "ngp_field_kernel (v_mfma_f32_16x16x4_f32)", "faces_per_s": B / dt,
-                "field_ms": f32_ms, "field_tflops": flop * samples / (f32_ms * 1e-3) / 1e12,
+                "field_ms": f32_ms, "flop_per_sample": FLOP_PER_SAMPLE,
+                "field_tflops": FLOP_PER_SAMPLE * samples / (f32_ms * 1e-3) / 1e12,
                 "peak_tflops": MFMA_F32_PEAK_TFLOPS}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, siren)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -1,4 +1,4 @@
-"""Outputs of the fused renderer under SDFR_FIELD_KERNEL=<kind> vs the reference fixture
+"""Outputs of the fused renderer (the libsdfr.so SDFR_LIB names) vs the reference fixture
 (render_face64 / render_small, with sdf/xyz when present): max |diff| per output, split
 into segments or not (profiling aid for the field-kernel variants, not a test)."""
 import sys

@@ -49,10 +49,7 @@ def main():
     res = {lib: [] for lib in libs}
     for _ in range(reps):                       # libs interleaved, each in its own process
         for lib in libs:
-            path, _, kern = lib.partition("@")       # lib.so@q: SDFR_FIELD_KERNEL=q
-            env = dict(os.environ, SDFR_LIB=str(REPO / path) if not path.startswith("/") else path)
-            if kern:
-                env["SDFR_FIELD_KERNEL"] = kern
+            env = dict(os.environ, SDFR_LIB=str(REPO / lib) if not lib.startswith("/") else lib)
             out = subprocess.run([sys.executable, "-c", CHILD, str(REPO), prec], env=env,
                                  capture_output=True, text=True, timeout=240)
             if out.returncode:

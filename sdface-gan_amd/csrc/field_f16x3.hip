@@ -363,6 +363,13 @@ constexpr int kRValuPerMfma = SDFR_RVALU;  // field_r_kernel: VALU slots after e
 #define SDFR_RDS 2
 #endif
 constexpr int kRDsPerMfma = SDFR_RDS;      // field_r_kernel: LDS-read slots after each MFMA
+// profiling-only ablations of field_r_kernel (wrong results by construction; bit flags:
+// 1 no barrier, 2 no weight DMA after the prologue, 4 no FiLM/sin in the layer
+// activations, 8 trivial colour tail, 16 no vmcnt wait before the barrier)
+#ifndef SDFR_FABL
+#define SDFR_FABL 0
+#endif
+constexpr int kFAbl = SDFR_FABL;
 
 // ngp layer-0 inputs: the 32 hash-grid features of a sample span the 4 lane
 // groups of its column.  They are scaled by the power of two 2^es that brings the
@@ -1122,12 +1129,12 @@ __device__ __forceinline__ void rstep(RRing &R, f16v (&acc)[8], const f4 (&bf)[2
     sfor<0, 8>([&](auto GI) {
         constexpr int gi = decltype(GI)::value;
         if constexpr (kBar && gi == 5) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (!(kFAbl & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
+            if constexpr (!(kFAbl & 1)) __builtin_amdgcn_s_barrier();
         }
-        if constexpr (kBar && gi == 5) r_dma_unit<Net, VN, 0>(R, half);
-        if constexpr (kBar && gi == 6) r_dma_unit<Net, VN, 1>(R, half);
+        if constexpr (kBar && gi == 5 && !(kFAbl & 2)) r_dma_unit<Net, VN, 0>(R, half);
+        if constexpr (kBar && gi == 6 && !(kFAbl & 2)) r_dma_unit<Net, VN, 1>(R, half);
         if constexpr (gi + 3 < 8) {
             a[gi + 3][0] = A[(gi + 3) * 128];
             a[gi + 3][1] = A[(gi + 3) * 128 + 64];
@@ -1172,7 +1179,8 @@ __device__ __forceinline__ void r_act(const f16v &z, int sp, const f4 &gm0, cons
     for (int j = 0; j < 8; ++j) {
         const float zz = z[8 * sp + j];
         const float g = j < 4 ? gm0[j & 3] : gm1[j & 3], b = j < 4 ? bt0[j & 3] : bt1[j & 3];
-        if constexpr (MODE == 0) v[j] = sin_rev(__fmaf_rn(g, __builtin_ldexpf(zz, -es), b));
+        if constexpr (kFAbl & 4) v[j] = zz;
+        else if constexpr (MODE == 0) v[j] = sin_rev(__fmaf_rn(g, __builtin_ldexpf(zz, -es), b));
         else v[j] = sin_rev(__fmaf_rn(g, zz, b));
         if constexpr (MODE == 2) sdfp = __fmaf_rn(v[j], j < 4 ? w0[j & 3] : w1[j & 3], sdfp);
     }
@@ -1531,6 +1539,14 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
             TailIn &T = tin[it & 1];
             if constexpr (it + 1 < 16) tail_load(it + 1, tin[(it + 1) & 1]);
             float fp[2][4];
+            if constexpr (kFAbl & 8) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) Pc[0][r] = __fadd_rn(Pc[0][r], vout[t + 4 * u][4 * bq + r]);
+                __builtin_amdgcn_sched_barrier(0);
+                return;
+            }
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll

@@ -637,7 +637,9 @@ class Decoder(nn.Module):
                     tc = to_rgb.conv
                     s_rgb = rgb_mods[i // 2]
                     rgb_w = self._rgb_base(tc)[None] * s_rgb[:, None, :]
-                ev = self.conv_events
+                # (events run out: later convolutions go unrecorded, not an IndexError)
+                ev = self.conv_events if (self.conv_events is not None
+                                          and self._conv_ev < len(self.conv_events)) else None
                 if ev is not None:
                     ev[self._conv_ev][0].record()
                 x, part = conv3x3_f16x3_act(

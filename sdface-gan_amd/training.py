@@ -178,8 +178,14 @@ def mixing_noise(batch, latent_dim, prob, device):
     return [make_noise(batch, latent_dim, 1, device)]
 
 
+def _dist_on():
+    """A process group exists: the collectives and DDP run (at any world size, so a
+    world-1 RCCL group exercises the same calls as eight ranks)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def _world():
-    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    return dist.get_world_size() if _dist_on() else 1
 
 
 def reduce_loss_dict(loss_dict):
@@ -188,7 +194,7 @@ def reduce_loss_dict(loss_dict):
     if not keys:
         return {}
     vals = torch.stack([loss_dict[k].detach().float().reshape(()) for k in keys])
-    if _world() > 1:
+    if _dist_on():
         dist.all_reduce(vals)
         vals /= _world()
     return dict(zip(keys, vals))
@@ -201,7 +207,7 @@ def allreduce_grads(params):
     reference's replicas drift apart there)."""
     world = _world()
     grads = [p.grad for p in params if p.grad is not None]
-    if world == 1 or not grads:
+    if not _dist_on() or not grads:
         return
     flat = torch.cat([g.reshape(-1) for g in grads])
     dist.all_reduce(flat)
@@ -224,6 +230,7 @@ class FullPipelineTrainer:
     def __init__(self, opt, device, seed=0):
         self.opt, self.t, self.device = opt, opt.training, device
         self.world = _world()
+        self.dist = _dist_on()
         torch.manual_seed(seed)                   # identical initial replicas on every rank
         random.seed(seed)
         self.generator = Generator(opt.model, opt.rendering).to(device)
@@ -247,7 +254,7 @@ class FullPipelineTrainer:
                                             betas=(0 ** d_ratio, 0.99 ** d_ratio))
         accumulate(self.generator_test, self.generator, 0)
         self.g_module, self.d_module = self.generator, self.discriminator
-        if self.world > 1:
+        if self.dist:
             from torch.nn.parallel import DistributedDataParallel as DDP
             kw = dict(broadcast_buffers=False)
             if device.type == "cuda":
@@ -371,7 +378,7 @@ class FullPipelineTrainer:
                     w.backward()
             self.optimizer.step()
             self.g_module.zero_grad(set_to_none=True)
-            if self.world > 1:
+            if self.dist:
                 mpl = torch.as_tensor(self.mean_path_length, device=dev, dtype=torch.float32)
                 dist.all_reduce(mpl)
                 self.mean_path_length = mpl / self.world
@@ -587,6 +594,7 @@ class RendererTrainer:
     def __init__(self, opt, device, seed=0):
         self.opt, self.t, self.device = opt, opt.training, device
         self.world = _world()
+        self.dist = _dist_on()
         torch.manual_seed(seed)
         random.seed(seed)
         self.generator = Generator(opt.model, opt.rendering, full_pipeline=False).to(device)
@@ -598,7 +606,7 @@ class RendererTrainer:
         self.optimizer_d = torch.optim.Adam(self.discriminator.parameters(), lr=2e-4,
                                             betas=(0.0, 0.9))
         self.g_module, self.d_module = self.generator, self.discriminator
-        if self.world > 1:
+        if self.dist:
             from torch.nn.parallel import DistributedDataParallel as DDP
             kw = dict(broadcast_buffers=False)
             if device.type == "cuda":
