@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 8
+#define SDFR_ABI_VERSION 9
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -220,12 +220,42 @@ typedef struct sdfr_siren_weights {
 
 size_t sdfr_render_siren_workspace_bytes(uint32_t B);
 
+/* ---------------------------------------------------------------------------
+ * Fused FCGenerator renderer forward (rendering.fc == 1, sdf_model.py:1599-1670:
+ * the "plain Fourier MLP" of BASELINE configs[4]): positional encodings of the
+ * normalised sample point (10 frequencies) -> x_in + style_in(styles) -> ReLU ->
+ * 7 x (Linear 256, ReLU) -> sigma | [h, encodings of the view direction (4
+ * frequencies)] -> views_linears (the colour features) -> rgb_linear, then the
+ * same SDF -> density and compositing as the other networks
+ * (sdf_model.py:231-301).  Replaces VolumeFeatureRenderer.forward for fc == 1
+ * (sdf_model.py:411-423).  Same render args (field_precision must be
+ * SDFR_FIELD_F16X3); workspace from sdfr_render_fc_workspace_bytes.
+ * stage_events[1] == [2] (no encode stage).
+ * ------------------------------------------------------------------------- */
+typedef struct sdfr_fc_weights {
+    uint32_t depth;                     /* D (8)                                    */
+    uint32_t width;                     /* W (256)                                  */
+    const float *x_in_w, *x_in_b;       /* [256,60], [256]                          */
+    const float *style_w, *style_b;     /* style_in [256,256], [256]                */
+    const float *pts_w[7], *pts_b[7];   /* [256,256], [256]                         */
+    const float *views_w, *views_b;     /* [256,280], [256]                         */
+    const float *sigma_w, *sigma_b;     /* [1,256], [1]                             */
+    const float *rgb_w, *rgb_b;         /* [3,256], [3]                             */
+    const float *sigmoid_beta;          /* [1] (renderer.sigmoid_beta)              */
+} sdfr_fc_weights;
+
+size_t sdfr_render_fc_workspace_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t N);
+
+int sdfr_render_fc_forward(const sdfr_fc_weights *w,
+                           const sdfr_ngp_render_args *a, void *stream);
+
 /* Split-fp16 weight packing of the field kernel (row scales, scaled biases, MFMA
  * A-fragments), done once per weight version by the caller instead of per call:
- * `packed` holds sdfr_render_pack_bytes(net) bytes (net 0 ngp, 1 siren). */
+ * `packed` holds sdfr_render_pack_bytes(net) bytes (net 0 ngp, 1 siren, 2 fc). */
 size_t sdfr_render_pack_bytes(int net);
 int sdfr_render_ngp_pack(const sdfr_ngp_weights *w, void *packed, void *stream);
 int sdfr_render_siren_pack(const sdfr_siren_weights *w, void *packed, void *stream);
+int sdfr_render_fc_pack(const sdfr_fc_weights *w, void *packed, void *stream);
 
 int sdfr_render_siren_forward(const sdfr_siren_weights *w,
                               const sdfr_ngp_render_args *a, void *stream);

@@ -382,6 +382,60 @@ def render_siren(sd, cam, focal, near, far, styles, *, N=24, res=64, t_rand=None
                       output_features)
 
 
+def _posenc(p, L):
+    """FCGenerator.transform_points (sdf_model.py:1628-1640): p / 2, then per frequency i
+    sin and cos of (2^i pi) p, concatenated (torch CPU fp32, the reference's op order)."""
+    import torch
+    p = p / 2
+    return torch.cat([torch.cat([torch.sin((2 ** i) * np.pi * p), torch.cos((2 ** i) * np.pi * p)],
+                                dim=-1) for i in range(L)], dim=-1)
+
+
+def render_fc(sd, cam, focal, near, far, styles, *, N=24, res=64, t_rand=None,
+              offset_sampling=True, static_viewdirs=False, z_normalize=True,
+              force_background=False, output_features=True, with_sdf=True, depth=8,
+              prefix="renderer."):
+    """fp32 CPU restatement of VolumeFeatureRenderer(fc=1).forward: render_rays'
+    ray / sample chain (sdf_model.py:310-351) feeding FCGenerator (sdf_model.py:1599-1670:
+    positional encodings, x_in + style_in, ReLU MLP, sigma, views_linears, rgb_linear),
+    then volume_integration.  Same arguments and outputs as render_ngp."""
+    import torch
+    import torch.nn.functional as F
+
+    def P(k):
+        v = sd[prefix + k]
+        return v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
+
+    cam = torch.as_tensor(cam, dtype=torch.float32).reshape(-1, 3, 4)
+    B = cam.shape[0]
+    near = np.asarray(near, np.float32).reshape(B)
+    far = np.asarray(far, np.float32).reshape(B)
+    ray = sample_rays(cam.numpy(), np.asarray(focal).reshape(B), near, far, res, res, N,
+                      t_rand=t_rand, offset_sampling=offset_sampling,
+                      static_viewdirs=static_viewdirs, z_normalize=z_normalize)
+    pts = torch.from_numpy(ray["pts"])
+    if z_normalize:
+        span = torch.from_numpy(far - near).view(B, 1, 1, 1, 1)
+        x = pts * 2 / span
+    else:
+        x = pts
+    vd = torch.from_numpy(np.ascontiguousarray(
+        np.broadcast_to(ray["viewdirs"][:, :, :, None, :], (B, res, res, N, 3))))
+    sty = torch.as_tensor(styles, dtype=torch.float32)
+    net = "network."
+    h = _linear(_posenc(x, 10), P(net + "x_in.weight"), P(net + "x_in.bias"))
+    s = _linear(sty, P(net + "style_in.weight"), P(net + "style_in.bias")).view(B, 1, 1, 1, -1)
+    h = F.relu(h + s)
+    for i in range(depth - 1):
+        h = F.relu(_linear(h, P(f"{net}pts_linears.{i}.weight"), P(f"{net}pts_linears.{i}.bias")))
+    sdf = _linear(h, P(net + "sigma_linear.weight"), P(net + "sigma_linear.bias"))
+    feat = _linear(torch.cat([h, _posenc(vd, 4)], -1), P(net + "views_linears.weight"),
+                   P(net + "views_linears.bias"))
+    rgb_raw = _linear(feat, P(net + "rgb_linear.weight"), P(net + "rgb_linear.bias"))
+    return _integrate(ray, sdf, rgb_raw, feat, P("sigmoid_beta"), with_sdf, force_background,
+                      output_features)
+
+
 # --------------------------------------------------------------------------
 # StyleGAN2 decoder ops (im2scene/sdf/models/sdf_op.py), numpy
 # --------------------------------------------------------------------------

@@ -23,7 +23,7 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 8
+ABI_VERSION = 9
 FIELD_F16X3 = 0
 FIELD_FP32 = 1
 
@@ -40,6 +40,7 @@ EXPORTS = (
     "sdfr_debug_sin_rev_probe", "sdfr_camera_extrinsics",
     "sdfr_render_siren_workspace_bytes", "sdfr_render_siren_forward",
     "sdfr_render_pack_bytes", "sdfr_render_ngp_pack", "sdfr_render_siren_pack",
+    "sdfr_render_fc_workspace_bytes", "sdfr_render_fc_forward", "sdfr_render_fc_pack",
     "sdfr_fused_bias_act", "sdfr_mapping_linear", "sdfr_decoder_styles", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
     "sdfr_modulate_to_nhwc_split",
     "sdfr_conv_pack_bytes", "sdfr_conv_pack_weights", "sdfr_conv3x3_f16x3",
@@ -77,6 +78,18 @@ class SirenWeights(ctypes.Structure):
         ("pts_bw", _vp * 8), ("pts_bb", _vp * 8),
         ("views_w", _vp), ("views_b", _vp),
         ("views_gw", _vp), ("views_gb", _vp), ("views_bw", _vp), ("views_bb", _vp),
+        ("sigma_w", _vp), ("sigma_b", _vp), ("rgb_w", _vp), ("rgb_b", _vp),
+        ("sigmoid_beta", _vp),
+    ]
+
+
+class FcWeights(ctypes.Structure):
+    """sdfr_fc_weights (include/sdfr.h)."""
+    _fields_ = [
+        ("depth", _u32), ("width", _u32),
+        ("x_in_w", _vp), ("x_in_b", _vp), ("style_w", _vp), ("style_b", _vp),
+        ("pts_w", _vp * 7), ("pts_b", _vp * 7),
+        ("views_w", _vp), ("views_b", _vp),
         ("sigma_w", _vp), ("sigma_b", _vp), ("rgb_w", _vp), ("rgb_b", _vp),
         ("sigmoid_beta", _vp),
     ]
@@ -174,6 +187,11 @@ def lib():
     L.sdfr_render_siren_pack.argtypes = [ctypes.POINTER(SirenWeights), _vp, _vp]
     L.sdfr_render_siren_forward.argtypes = [ctypes.POINTER(SirenWeights),
                                             ctypes.POINTER(NgpRenderArgs), _vp]
+    L.sdfr_render_fc_workspace_bytes.restype = ctypes.c_size_t
+    L.sdfr_render_fc_workspace_bytes.argtypes = [_u32, _u32, _u32, _u32]
+    L.sdfr_render_fc_pack.argtypes = [ctypes.POINTER(FcWeights), _vp, _vp]
+    L.sdfr_render_fc_forward.argtypes = [ctypes.POINTER(FcWeights),
+                                         ctypes.POINTER(NgpRenderArgs), _vp]
     L.sdfr_debug_sin_probe.argtypes = [_vp, _vp, _vp, _u32, _vp]
     L.sdfr_debug_sin_rev_probe.argtypes = [_vp, _vp, _u32, _vp]
     L.sdfr_camera_extrinsics.argtypes = [_vp, _vp, _u32, _f32, _f32, _f32, _vp, _vp, _vp, _vp,

@@ -54,6 +54,11 @@ constexpr uint32_t kXSliceF4 = 1024;             // 16 KB: [8 tiles][hi,lo][64 l
 // ----------------------------------------------------------------------------
 struct NgpNet {
     static constexpr bool kSiren = false;
+    static constexpr bool kGrid = true;        // layer-0 inputs from the hash-grid encode kernel
+    static constexpr bool kPosEnc = false;     // layer-0 / views inputs: positional encodings
+    static constexpr bool kSinAct = true;      // FiLM sin activations (else ReLU)
+    static constexpr int kL0 = 2;              // layer-0 k-steps of 16 K
+    static constexpr int kViewSteps = 17;      // views-layer k-steps (256 hidden + 16 SH)
     static constexpr bool kFieldR = true;      // field_r_kernel (else field_p_kernel)
     // input_linear (LinearLayer, affine: sdf_model.py:37-39) feeds pts_linears.0's
     // linear with no nonlinearity between them (:1574-1577), so the two are ONE affine
@@ -72,6 +77,11 @@ struct NgpNet {
 };
 struct SirenNet {
     static constexpr bool kSiren = true;
+    static constexpr bool kGrid = false;
+    static constexpr bool kPosEnc = false;
+    static constexpr bool kSinAct = true;
+    static constexpr int kL0 = 1;
+    static constexpr int kViewSteps = 17;
     static constexpr bool kFieldR = false;
     static constexpr bool kCompose = false;
     static constexpr bool kSlice2 = false;
@@ -81,6 +91,31 @@ struct SirenNet {
     static constexpr uint32_t kSlices = 2 + 16 * 7 + 18;     // field_p_kernel's half-slices
     __host__ __device__ static constexpr uint32_t K(int l) {
         return l == 0 ? 3u : (l == 8 ? kW + 3 : kW);
+    }
+    __host__ __device__ static constexpr int film_layer(int f) { return f; }
+};
+// FCGenerator (rendering.fc == 1, sdf_model.py:1599-1670): positional encodings of the
+// normalised point (3 x 10 frequencies x sin, cos = 60) -> x_in (+ style_in(styles), a
+// per-face bias) -> ReLU -> 7 x (256 -> 256, ReLU) -> sigma | [h7, posenc(view) (24)] ->
+// views (no activation: the colour features) -> rgb.  Every layer is affine then ReLU,
+// run as ReLU(fma(1/su, z, b)) on the row-scaled GEMM output z (1/su exact), i.e. the
+// FiLM slot with gamma'' = 1/su and beta'' = the bias.
+struct FcNet {
+    static constexpr bool kSiren = false;
+    static constexpr bool kGrid = false;
+    static constexpr bool kPosEnc = true;
+    static constexpr bool kSinAct = false;
+    static constexpr int kL0 = 4;              // 60 encodings (+ 4 zero pad)
+    static constexpr int kViewSteps = 18;      // 256 hidden + 24 view encodings (+ 8 pad)
+    static constexpr bool kFieldR = true;
+    static constexpr bool kCompose = false;
+    static constexpr int kLayers = 9;          // x_in, pts_linears.0-6, views
+    static constexpr int kFilmN = 9;           // (1/su, bias) per layer; layer 0 per face
+    static constexpr int kHidden = 7;
+    static constexpr uint32_t kSlices = 4 + 16 * 7 + 18;
+    static constexpr uint32_t kPosIn = 60, kPosViews = 24;
+    __host__ __device__ static constexpr uint32_t K(int l) {
+        return l == 0 ? kPosIn : (l == 8 ? kW + kPosViews : kW);
     }
     __host__ __device__ static constexpr int film_layer(int f) { return f; }
 };
@@ -122,8 +157,8 @@ __device__ __forceinline__ f16v mfma32(f4 a, f4 b, f16v c) {
 
 template <class Net>
 struct RNet {
-    static constexpr int kL0 = Net::kSiren ? 1 : 2;                // layer-0 k-steps (K 3 / 32)
-    static constexpr int kSteps = kL0 + 16 * Net::kHidden + 17;    // k-steps (slices) per pass
+    static constexpr int kL0 = Net::kL0;                           // layer-0 k-steps (K 3 / 32 / 60)
+    static constexpr int kSteps = kL0 + 16 * Net::kHidden + Net::kViewSteps;   // (slices) per pass
     static constexpr int kViews = kL0 + 16 * Net::kHidden;         // first views k-step
     static_assert(!Net::kFieldR || kSteps == (int)Net::kSlices, "one packed slice per k-step");
 };
@@ -141,10 +176,13 @@ __device__ __forceinline__ int rperm_k(int l, uint32_t s, uint32_t h, uint32_t j
     const uint32_t e = 8 * h + j;
     if (l == 0) {
         if constexpr (Net::kSiren) return e < 3 ? (int)e : -1;   // xyz
+        if constexpr (Net::kPosEnc) return 16 * s + e < Net::kPosIn ? (int)(16 * s + e) : -1;
         return (int)(16 * s + e);                               // 32 grid features
     }
-    if (l == Net::kLayers - 1 && s == 16) {
+    if (l == Net::kLayers - 1 && s >= 16) {
         if constexpr (Net::kSiren) return e < 3 ? (int)(kW + e) : -1;   // viewdir
+        if constexpr (Net::kPosEnc)                                     // view encodings
+            return 16 * (s - 16) + e < Net::kPosViews ? (int)(kW + 16 * (s - 16) + e) : -1;
         return (int)(kW + e);                                           // SH 0-15
     }
     return (int)(32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3));
@@ -265,6 +303,20 @@ __global__ void __launch_bounds__(256) xprep_kernel(const XPrepArgs a) {
             for (int o = 32; o > 0; o >>= 1) p = __fadd_rn(p, __shfl_xor(p, o));
             return p;
         };
+        if constexpr (Net::kPosEnc) {
+            // FCGenerator: gamma'' = 1/su (exact), beta'' = the layer bias, + style_in(s)
+            // for x_in (sdf_model.py:1654-1658: x_in(p) + style_in(styles), then ReLU)
+            const int l = Net::film_layer(f);
+            float v;
+            if (which == 0) {
+                v = __fdiv_rn(1.0f, a.su[l * kW + jr]);
+            } else {
+                v = a.lb[l][jr];
+                if (f == 0) v = __fadd_rn(v, __fadd_rn(dot(a.gw[0]), a.gb[0][jr]));
+            }
+            if (lane == 0) a.film[(((size_t)b * NF + f) * 2 + which) * kW + jr] = v;
+            return;
+        }
         const float lin = __fadd_rn(dot(which ? a.bw[f] : a.gw[f]), (which ? a.bb[f] : a.gb[f])[jr]);
         // LinearLayer: std_init * linear + bias_init (sdf_model.py:39, 58-59).  The
         // activation sin(gamma (W x + b) + beta) of the modulated layer runs as
@@ -1170,8 +1222,9 @@ __device__ __forceinline__ void r_na(RRing &R, uint32_t slot) {
 }
 
 // FiLM activation of registers 8 s' .. 8 s' + 7 of output tile T into v[8] (element j =
-// register 8 s' + j): film rows 32 T + 16 s' + 4 h + (0..3) (gm0, bt0, w0) and + 8 (gm1, ...)
-template <int MODE>
+// register 8 s' + j): film rows 32 T + 16 s' + 4 h + (0..3) (gm0, bt0, w0) and + 8 (gm1, ...);
+// SIN false: ReLU(fma(1/su, z, b)) (FcNet)
+template <int MODE, bool SIN = true>
 __device__ __forceinline__ void r_act(const f16v &z, int sp, const f4 &gm0, const f4 &bt0,
                                       const f4 &w0, const f4 &gm1, const f4 &bt1, const f4 &w1,
                                       float &sdfp, int es, float (&v)[8]) {
@@ -1180,6 +1233,7 @@ __device__ __forceinline__ void r_act(const f16v &z, int sp, const f4 &gm0, cons
         const float zz = z[8 * sp + j];
         const float g = j < 4 ? gm0[j & 3] : gm1[j & 3], b = j < 4 ? bt0[j & 3] : bt1[j & 3];
         if constexpr (kFAbl & 4) v[j] = zz;
+        else if constexpr (!SIN) v[j] = fmaxf(__fmaf_rn(g, zz, b), 0.0f);
         else if constexpr (MODE == 0) v[j] = sin_rev(__fmaf_rn(g, __builtin_ldexpf(zz, -es), b));
         else v[j] = sin_rev(__fmaf_rn(g, zz, b));
         if constexpr (MODE == 2) sdfp = __fmaf_rn(v[j], j < 4 ? w0[j & 3] : w1[j & 3], sdfp);
@@ -1196,6 +1250,22 @@ __device__ __forceinline__ float row_pair_sum(float pa, float pb) {
     uint32_t r0 = sw[0], r1 = sw[1];
     asm volatile("" : "+v"(r0), "+v"(r1));
     return __fadd_rn(__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1));
+}
+
+// Element e of FCGenerator.transform_points (sdf_model.py:1628-1640) of ph = p / 2:
+// e = 6 i + r, sin (r < 3) or cos (r >= 3) of (2^i pi) ph[r mod 3], with the reference's
+// fp32 argument RN(RN32(2^i pi) ph) (a Python float times an fp32 tensor).  The sine of
+// that fp32 argument: reduced to revolutions in fp64 (exact product, fraction to 2^-40),
+// then v_sin_f32 (< 1e-6 absolute, tests/test_gpu_encoders.py).
+__device__ __forceinline__ float posenc_val(const float (&ph)[3], uint32_t e) {
+    const uint32_t i = e / 6u, r = e - 6u * i;
+    const uint32_t c = r < 3u ? r : r - 3u;
+    const float pc = c == 0u ? ph[0] : (c == 1u ? ph[1] : ph[2]);
+    const float arg = __fmul_rn(__builtin_ldexpf(3.14159265358979323846f, (int)i), pc);
+    double u = (double)arg * 0.15915494309189533577;     // 1 / (2 pi)
+    if (r >= 3u) u += 0.25;                               // cos x = sin(x + pi / 2)
+    u -= floor(u);
+    return sin_rev((float)u);
 }
 
 template <class Net>
@@ -1267,7 +1337,8 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
     const float nr = G.near_[b], fr = G.far_[b];
     const float span = __fsub_rn(fr, nr);
     const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
-    f4 vx[2];                                               // the views layer's k-step 16
+    constexpr int NVX = Net::kViewSteps - 16;
+    f4 vx[NVX][2];                                          // the views layer's k-steps 16 (, 17)
     {
         const float v0 = G.static_viewdirs ? ray.dir[0] : ray.d[0];
         const float v1 = G.static_viewdirs ? ray.dir[1] : ray.d[1];
@@ -1275,7 +1346,22 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
         const float vn = norm3_torch(v0, v1, v2);
         const float ux = __fdiv_rn(v0, vn), uy = __fdiv_rn(v1, vn), uz = __fdiv_rn(v2, vn);
         float v[8];
-        if constexpr (Net::kSiren) {
+        if constexpr (Net::kPosEnc) {
+            // transform_points(views, True) (sdf_model.py:1628-1640): p / 2, 4 frequencies
+            const float ph[3] = {__fmul_rn(ux, 0.5f), __fmul_rn(uy, 0.5f), __fmul_rn(uz, 0.5f)};
+#pragma unroll
+            for (int st = 1; st < NVX; ++st) {
+                float w[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t e = 16 * st + 8 * h + j;
+                    w[j] = e < Net::kPosViews ? posenc_val(ph, e) : 0.0f;
+                }
+                split8(w, vx[st][0], vx[st][1]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = posenc_val(ph, 8 * h + j);
+        } else if constexpr (Net::kSiren) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] = 0.0f;
             if (h == 0) {
@@ -1291,18 +1377,26 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
                 v[4 + r] = qb[r];
             }
         }
-        split8(v, vx[0], vx[1]);
+        split8(v, vx[0][0], vx[0][1]);
     }
     float T = 1.0f, wsum = 0.0f, racc0 = 0.0f, racc1 = 0.0f, racc2 = 0.0f;
     float xacc0 = 0.0f, xacc1 = 0.0f, xacc2 = 0.0f, w_last = 0.0f;
     const size_t tile_sid = (size_t)(tile * G.N) * kTileRays + r16;
     const __amdgpu_buffer_rsrc_t enc_r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(a.enc), (short)0, Net::kSiren ? 0 : (int)(16u * G.S_total * 8u), 0x00020000);
+        const_cast<float *>(a.enc), (short)0, Net::kGrid ? (int)(16u * G.S_total * 8u) : 0, 0x00020000);
     float2 en[2][4];                                        // [layer-0 k-step][level pair]
+    float pin[3];                                           // FcNet: normalised point / 2
     auto load_inputs = [&](uint32_t p) {
         uint32_t s = kRSamples * p + (odd ? 1u : 0u);
         if (s >= G.N) s = G.N - 1;
-        if constexpr (Net::kSiren) {
+        if constexpr (Net::kPosEnc) {
+            const float z = sample_z(G.sc, nr, fr, ray_index, s);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float pp = __fadd_rn(ray.o[k], __fmul_rn(ray.d[k], z));
+                pin[k] = __fmul_rn(G.z_normalize ? __fdiv_rn(__fmul_rn(pp, 2.0f), span) : pp, 0.5f);
+            }
+        } else if constexpr (Net::kSiren) {
             const float z = sample_z(G.sc, nr, fr, ray_index, s);
             float np_[3];
 #pragma unroll
@@ -1337,9 +1431,22 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
         R.ubase = __builtin_amdgcn_readfirstlane(((p - p_begin) * (uint32_t)((NS + 1) / 2)) & 1u);
         r_na(R, r_slot<Net>(R, 0));
         f16v X[8], Y[8];
-        f4 bf[2], e1[2];                                   // B fragments: current, layer-0 step 1
+        f4 bf[2], E[KL0][2];                               // B fragments: current, layer 0's
         int es = 0;
-        {
+        if constexpr (Net::kPosEnc) {
+            // transform_points(p) (sdf_model.py:1628-1640): 10 frequencies x (sin, cos) of
+            // the 3 coordinates; this lane half's 8 of each k-step's 16 (zero past 60)
+#pragma unroll
+            for (int st = 0; st < KL0; ++st) {
+                float w[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t e = 16 * st + 8 * h + j;
+                    w[j] = e < Net::kPosIn ? posenc_val(pin, e) : 0.0f;
+                }
+                split8(w, E[st][0], E[st][1]);
+            }
+        } else {
             float v[16];
 #pragma unroll
             for (int st = 0; st < 2; ++st)
@@ -1348,7 +1455,7 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
                     v[8 * st + 2 * k] = en[st][k].x;
                     v[8 * st + 2 * k + 1] = en[st][k].y;
                 }
-            if constexpr (!Net::kSiren) {
+            if constexpr (Net::kGrid) {
                 // the sample's 32 features over both lane halves -> 2^es into [0.5, 1)
                 float m = 0.0f;
 #pragma unroll
@@ -1367,8 +1474,8 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
                 u0[j] = v[j];
                 u1[j] = v[8 + j];
             }
-            split8(u0, bf[0], bf[1]);
-            split8(u1, e1[0], e1[1]);
+            split8(u0, E[0][0], E[0][1]);
+            if constexpr (KL0 > 1) split8(u1, E[KL0 - 1][0], E[KL0 - 1][1]);
         }
         float sdfp = 0.0f;
         f4 bn[2];
@@ -1383,7 +1490,7 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
         auto act_side = [&](auto L, f16v (&o)[8], int q, auto GI, auto G0) {
             constexpr int l = decltype(L)::value;
             constexpr int gi = decltype(GI)::value, g0 = decltype(G0)::value;
-            constexpr int MODE = (l == 0 && !Net::kSiren) ? 0 : (l == NL - 2 ? 2 : 1);
+            constexpr int MODE = (l == 0 && Net::kGrid) ? 0 : (l == NL - 2 ? 2 : 1);
             const int f = Net::film_layer(l);
             const int r0 = 32 * (q >> 1) + 16 * (q & 1) + 4 * (int)h;
             if constexpr (gi == g0) {
@@ -1396,20 +1503,19 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
                     as.w1 = *reinterpret_cast<const f4 *>(sig_w + r0 + 8);
                 }
             } else if constexpr (gi == g0 + 1) {
-                r_act<MODE>(o[q >> 1], q & 1, as.gm0, as.bt0, as.w0, as.gm1, as.bt1, as.w1, sdfp, es,
+                r_act<MODE, Net::kSinAct>(o[q >> 1], q & 1, as.gm0, as.bt0, as.w0, as.gm1, as.bt1, as.w1, sdfp, es,
                             as.v);
             } else if constexpr (gi == g0 + 2) {
                 split8(as.v, bn[0], bn[1]);
             }
         };
-        // layer 0: K = 32 (ngp, 2 k-steps) or 3 (siren, 1); chunk 0 of its output (tile 0
-        // registers 0-7, final after group 0 of the last layer-0 k-step) from group 1 on
+        // layer 0: K = 32 (ngp, 2 k-steps), 3 (siren, 1) or 60 (fc, 4); chunk 0 of its
+        // output (tile 0 registers 0-7, final after group 0 of the last layer-0 k-step)
+        // from group 1 on
         sfor<0, KL0>([&](auto J) {
             constexpr int j = decltype(J)::value;
-            if constexpr (j == 1) {
-                bf[0] = e1[0];
-                bf[1] = e1[1];
-            }
+            bf[0] = E[j][0];
+            bf[1] = E[j][1];
             rstep<Net, j, j == 0>(R, X, bf, [&](auto GI) {
                 if constexpr (j == KL0 - 1)
                     act_side(std::integral_constant<int, 0>{}, X, 0, GI, std::integral_constant<int, 2>{});
@@ -1446,12 +1552,12 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
         const uint32_t sc_ = s_ok ? s_own : G.N - 1;
         float z = 0.0f, dist = 0.0f, al = 0.0f, sdf_c = 0.0f, w_own = 0.0f;
         float wj[2] = {0.0f, 0.0f};
-        sfor<0, 17>([&](auto J) {
+        sfor<0, Net::kViewSteps>([&](auto J) {
             constexpr int j = decltype(J)::value;
             constexpr int KS = KV + j;
             bf[0] = bn[0];
             bf[1] = bn[1];
-            if constexpr (j == 14 && !Net::kSiren) {
+            if constexpr (j == 14 && Net::kGrid) {
                 const float2 v = a.zd[tile_sid + (size_t)sc_ * kTileRays];
                 z = v.x;
                 dist = v.y;
@@ -1465,11 +1571,14 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
                     act_side(std::integral_constant<int, NL - 2>{}, vin, j + 1, GI,
                              std::integral_constant<int, 0>{});
                 } else if constexpr (j == 15 && gi == 0) {
-                    bn[0] = vx[0];                          // k-step 16's B: the direction
-                    bn[1] = vx[1];
+                    bn[0] = vx[0][0];                       // k-step 16's B: the direction
+                    bn[1] = vx[0][1];
                     sdf_c = __fadd_rn(__fadd_rn(sdfp, __shfl_xor(sdfp, 32)), sig_b);
+                } else if constexpr (j == 16 && gi == 0 && NVX > 1) {
+                    bn[0] = vx[NVX - 1][0];                 // fc: k-step 17's B
+                    bn[1] = vx[NVX - 1][1];
                 } else if constexpr (j == 15 && gi == 1) {
-                    if constexpr (Net::kSiren) {
+                    if constexpr (!Net::kGrid) {
                         z = sample_z(G.sc, nr, fr, ray_index, sc_);
                         dist = (sc_ + 1 < G.N)
                                    ? __fmul_rn(__fsub_rn(sample_z(G.sc, nr, fr, ray_index, sc_ + 1), z), dnorm)
@@ -1551,7 +1660,8 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
             for (int u = 0; u < 2; ++u)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float f = sin_rev(__fmaf_rn(T.gm[u][r], vout[t + 4 * u][4 * bq + r], T.bt[u][r]));
+                    const float y = __fmaf_rn(T.gm[u][r], vout[t + 4 * u][4 * bq + r], T.bt[u][r]);
+                    const float f = Net::kSinAct ? sin_rev(y) : y;   // fc: views_linears output
                     Pc[0][r] = __fmaf_rn(f, T.w0[u][r], Pc[0][r]);
                     Pc[1][r] = __fmaf_rn(f, T.w1[u][r], Pc[1][r]);
                     Pc[2][r] = __fmaf_rn(f, T.w2[u][r], Pc[2][r]);
@@ -1728,7 +1838,9 @@ static float *xws_composed(char *xws) {
 
 // workspace region of this path: packed [slices][1024] f4 | su [L][256] | bias_s [L][256]
 // (| composed layer 0, ngp)
-size_t f16x3_ws_bytes(int net) { return net ? xws_bytes<SirenNet>() : xws_bytes<NgpNet>(); }
+size_t f16x3_ws_bytes(int net) {
+    return net == 2 ? xws_bytes<FcNet>() : (net ? xws_bytes<SirenNet>() : xws_bytes<NgpNet>());
+}
 
 // The network's tensors in policy order (layer 0, dense layers, views; FiLM sets); for
 // ngp also the two reference layers that make the composed layer 0 (xws_composed).
@@ -1962,17 +2074,107 @@ static int siren_validate(const sdfr_siren_weights *w, const sdfr_ngp_render_arg
     return SDFR_OK;
 }
 
+// ----------------------------------------------------------------------------
+// FCGenerator entry points
+// ----------------------------------------------------------------------------
+// film [B][9][2][256] | split-fp16 region | sample-segment partials (small batches)
+static size_t fc_ws_layout(uint32_t B, uint32_t H, uint32_t W, uint32_t N, size_t *o_x,
+                           size_t *o_part) {
+    size_t off = align256x((size_t)B * FcNet::kFilmN * 2 * kW * sizeof(float));
+    if (o_x) *o_x = off;
+    off += align256x(xws_bytes<FcNet>());
+    if (o_part) *o_part = off;
+    off += align256x(field_part_bytes(B, (H * W + kTileRays - 1) / kTileRays, N));
+    return off;
+}
+
+static NetPtrs fc_ptrs(const sdfr_fc_weights *w) {
+    NetPtrs P{};
+    P.w[0] = w->x_in_w;
+    P.b[0] = w->x_in_b;
+    P.gw[0] = w->style_w;                      // style_in: layer 0's per-face bias
+    P.gb[0] = w->style_b;
+    for (int l = 0; l < 7; ++l) {
+        P.w[1 + l] = w->pts_w[l];
+        P.b[1 + l] = w->pts_b[l];
+    }
+    P.w[8] = w->views_w;
+    P.b[8] = w->views_b;
+    P.sigma_w = w->sigma_w;
+    P.sigma_b = w->sigma_b;
+    P.rgb_w = w->rgb_w;
+    P.rgb_b = w->rgb_b;
+    P.sigmoid_beta = w->sigmoid_beta;
+    return P;
+}
+
+static int fc_validate(const sdfr_fc_weights *w, const sdfr_ngp_render_args *a) {
+    if (!w || !a) return fail(SDFR_EINVAL, "render_fc: null args");
+    if (w->depth != 8 || w->width != 256)
+        return fail(SDFR_EUNSUPPORTED, "render_fc: fused path needs depth 8, width 256");
+    if (a->field_precision != SDFR_FIELD_F16X3)
+        return fail(SDFR_EUNSUPPORTED, "render_fc: only field_precision 0 (f16x3)");
+    if (a->B == 0 || a->H == 0 || a->W == 0 || a->N == 0)
+        return fail(SDFR_EINVAL, "render_fc: empty batch / image / sample count");
+    if (a->max_field_segments > kFieldSplitMax || a->max_field_segments == 3)
+        return fail(SDFR_EINVAL, "render_fc: max_field_segments must be 0, 1, 2 or 4");
+    if (!a->cam || !a->focal || !a->near_ || !a->far_ || !a->styles || !a->pix_x ||
+        !a->pix_y || !a->t_vals || !a->rgb || !a->workspace)
+        return fail(SDFR_EINVAL, "render_fc: required pointer is null");
+    for (int l = 0; l < 7; ++l)
+        if (!w->pts_w[l] || !w->pts_b[l]) return fail(SDFR_EINVAL, "render_fc: weight pointer is null");
+    const void *need[] = {w->x_in_w, w->x_in_b, w->style_w, w->style_b, w->views_w, w->views_b,
+                          w->sigma_w, w->sigma_b, w->rgb_w, w->rgb_b};
+    for (const void *p : need)
+        if (!p) return fail(SDFR_EINVAL, "render_fc: weight pointer is null");
+    if (a->with_sdf && !w->sigmoid_beta)
+        return fail(SDFR_EINVAL, "render_fc: sigmoid_beta is required when with_sdf");
+    if (a->workspace_bytes < fc_ws_layout(a->B, a->H, a->W, a->N, nullptr, nullptr))
+        return fail(SDFR_EINVAL, "render_fc: workspace too small");
+    return SDFR_OK;
+}
+
 }  // namespace sdfr
 
 using namespace sdfr;
 
 extern "C" {
 
+size_t sdfr_render_fc_workspace_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t N) {
+    return fc_ws_layout(B, H, W, N, nullptr, nullptr);
+}
+
+int sdfr_render_fc_pack(const sdfr_fc_weights *w, void *packed, void *stream) {
+    if (!w || !packed) return fail(SDFR_EINVAL, "render_fc_pack: null pointer");
+    return launch_xpack<FcNet>(fc_ptrs(w), 0, nullptr, reinterpret_cast<char *>(packed), nullptr,
+                               true, (hipStream_t)stream);
+}
+
+int sdfr_render_fc_forward(const sdfr_fc_weights *w, const sdfr_ngp_render_args *a, void *stream) {
+    int rc = fc_validate(w, a);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    size_t o_x, o_part;
+    fc_ws_layout(a->B, a->H, a->W, a->N, &o_x, &o_part);
+    char *ws = reinterpret_cast<char *>(a->workspace);
+    float *film = reinterpret_cast<float *>(ws);
+    const NetPtrs P = fc_ptrs(w);
+    GeomArgs g;
+    fill_geom_args(a, 1.0f, g);
+    record_event(a->stage_events[0], st);
+    if ((rc = launch_xprep<FcNet>(P, a, ws + o_x, film, st))) return rc;
+    record_event(a->stage_events[1], st);
+    record_event(a->stage_events[2], st);
+    if ((rc = launch_xfield<FcNet>(P, a, g, nullptr, ws + o_x, film, st,
+                                   reinterpret_cast<float *>(ws + o_part))))
+        return rc;
+    record_event(a->stage_events[3], st);
+    return SDFR_OK;
+}
+
 size_t sdfr_render_siren_workspace_bytes(uint32_t B) { return siren_ws_layout(B, nullptr); }
 
-size_t sdfr_render_pack_bytes(int net) {
-    return net ? xws_bytes<SirenNet>() : xws_bytes<NgpNet>();
-}
+size_t sdfr_render_pack_bytes(int net) { return f16x3_ws_bytes(net); }
 
 int sdfr_render_ngp_pack(const sdfr_ngp_weights *w, void *packed, void *stream) {
     if (!w || !packed) return fail(SDFR_EINVAL, "render_ngp_pack: null pointer");

@@ -483,14 +483,25 @@ class VolumeFeatureRenderer(nn.Module):
         return sdf, target_values
 
     # ---------------------------------------------------------------- fused HIP path
+    def _net_kind(self):
+        """0 ngp, 1 siren, 2 fc (the library's net index), None: no fused kernel."""
+        net = self.network
+        if isinstance(net, NGPSIRENGenerator):
+            return 0
+        if isinstance(net, SirenGenerator):
+            return 1
+        if isinstance(net, FCGenerator):
+            return 2
+        return None
+
     def _fused_ok(self, cam_poses, styles, return_eikonal):
         if not self.use_fused:
             return False
-        siren = isinstance(self.network, SirenGenerator)
-        if not (isinstance(self.network, NGPSIRENGenerator) or siren):
+        kind = self._net_kind()
+        if kind is None:
             return False
-        if siren and (self.field_precision != "f16x3" or self.network.D != 8 or
-                      len(self.network.pts_linears) != 8):
+        if kind and (self.field_precision != "f16x3" or self.network.D != 8 or
+                     len(self.network.pts_linears) != (8 if kind == 1 else 7)):
             return False
         if return_eikonal or not cam_poses.is_cuda or styles is None:
             return False
@@ -543,9 +554,32 @@ class VolumeFeatureRenderer(nn.Module):
         w.sigmoid_beta = P(self.sigmoid_beta) if self.with_sdf else None
         return w
 
+    def _fc_weight_struct(self):
+        net = self.network
+        P = lambda t: _lib.ptr(t)  # noqa: E731
+        w = _lib.FcWeights()
+        w.depth, w.width = net.D, net.W
+        w.x_in_w, w.x_in_b = P(net.x_in.weight), P(net.x_in.bias)
+        w.style_w, w.style_b = P(net.style_in.weight), P(net.style_in.bias)
+        for l, layer in enumerate(net.pts_linears):
+            w.pts_w[l], w.pts_b[l] = P(layer.weight), P(layer.bias)
+        w.views_w, w.views_b = P(net.views_linears.weight), P(net.views_linears.bias)
+        w.sigma_w, w.sigma_b = P(net.sigma_linear.weight), P(net.sigma_linear.bias)
+        w.rgb_w, w.rgb_b = P(net.rgb_linear.weight), P(net.rgb_linear.bias)
+        w.sigmoid_beta = P(self.sigmoid_beta) if self.with_sdf else None
+        return w
+
+    def _weight_struct(self, kind):
+        return (self._ngp_weight_struct, self._siren_weight_struct,
+                self._fc_weight_struct)[kind]()
+
     def _fused_check_params(self):
         net = self.network
-        if isinstance(net, SirenGenerator):
+        if isinstance(net, FCGenerator):
+            if net.D != 8 or net.W != 256 or len(net.pts_linears) != 7:
+                raise RuntimeError("fused fc renderer supports the SDFace FCGenerator "
+                                   "(D=8, W=256) only")
+        elif isinstance(net, SirenGenerator):
             if net.D != 8 or net.W != 256 or net.input_ch_views != 3:
                 raise RuntimeError("fused siren renderer supports the SDFace SirenGenerator "
                                    "(D=8, W=256) only")
@@ -586,8 +620,11 @@ class VolumeFeatureRenderer(nn.Module):
         sdf = torch.empty(B, H, W, N, 1, device=dev) if self.return_sdf else None
         xyz = torch.empty(B, 3, H, W, device=dev) if self.return_xyz else None
         mask = torch.empty(B, 1, H, W, device=dev) if self.return_xyz else None
-        siren = isinstance(self.network, SirenGenerator)
-        if siren:
+        kind = self._net_kind()
+        siren = kind == 1
+        if kind == 2:
+            ws_bytes = _lib.lib().sdfr_render_fc_workspace_bytes(B, H, W, N)
+        elif siren:
             ws_bytes = _lib.lib().sdfr_render_siren_workspace_bytes(B)
         else:
             L = self.network.encoder.num_levels
@@ -622,14 +659,14 @@ class VolumeFeatureRenderer(nn.Module):
             for k, ev in enumerate(self.stage_events):
                 a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)
         if self.field_precision == "f16x3":
-            a.prepacked = _lib.ptr(self._prepacked(siren, cam))
-        if siren:
+            a.prepacked = _lib.ptr(self._prepacked(kind, cam))
+        if kind:
             if encode_only:
-                raise RuntimeError("the siren renderer has no hash-grid encode stage")
-            w = self._siren_weight_struct()
-            _lib.check(_lib.lib().sdfr_render_siren_forward(ctypes.byref(w), ctypes.byref(a),
-                                                            _lib.stream_of(cam)),
-                       "sdfr_render_siren_forward")
+                raise RuntimeError("only the ngp renderer has a hash-grid encode stage")
+            w = self._weight_struct(kind)
+            name = "sdfr_render_siren_forward" if siren else "sdfr_render_fc_forward"
+            _lib.check(getattr(_lib.lib(), name)(ctypes.byref(w), ctypes.byref(a),
+                                                 _lib.stream_of(cam)), name)
             return rgb, features, sdf, mask, xyz, None
         w = self._ngp_weight_struct()
         fn = (_lib.lib().sdfr_render_ngp_encode_only if encode_only
@@ -640,25 +677,20 @@ class VolumeFeatureRenderer(nn.Module):
             return ws
         return rgb, features, sdf, mask, xyz, None
 
-    def _prepacked(self, siren, like):
+    def _prepacked(self, kind, like):
         """The field kernel's split-fp16 weight packing (row scales, scaled biases,
         MFMA fragments: sdfr_render_*_pack), redone only when a network parameter
         changed (data pointer or in-place version), not per call."""
-        key = (siren,) + tuple((p.data_ptr(), p._version) for p in self.network.parameters())
+        key = (kind,) + tuple((p.data_ptr(), p._version) for p in self.network.parameters())
         cache = getattr(self, "_pack_cache", None)
         if cache is not None and cache[0] == key:
             return cache[1]
         L = _lib.lib()
-        buf = torch.empty(L.sdfr_render_pack_bytes(int(siren)), dtype=torch.uint8,
+        buf = torch.empty(L.sdfr_render_pack_bytes(int(kind)), dtype=torch.uint8,
                           device=like.device)
-        if siren:
-            w = self._siren_weight_struct()
-            _lib.check(L.sdfr_render_siren_pack(ctypes.byref(w), _lib.ptr(buf),
-                                                _lib.stream_of(like)), "sdfr_render_siren_pack")
-        else:
-            w = self._ngp_weight_struct()
-            _lib.check(L.sdfr_render_ngp_pack(ctypes.byref(w), _lib.ptr(buf), _lib.stream_of(like)),
-                       "sdfr_render_ngp_pack")
+        name = ("sdfr_render_ngp_pack", "sdfr_render_siren_pack", "sdfr_render_fc_pack")[kind]
+        w = self._weight_struct(kind)
+        _lib.check(getattr(L, name)(ctypes.byref(w), _lib.ptr(buf), _lib.stream_of(like)), name)
         self._pack_cache = (key, buf)
         return buf
 

@@ -228,6 +228,19 @@ def test_siren_restatement_matches_reference(oracle_mod, golden_dir, name, kw):
             np.testing.assert_allclose(a, g[k], rtol=0, atol=2e-7, err_msg=k)
 
 
+def test_fc_restatement_matches_reference(oracle_mod, golden_dir):
+    """oracle.render_fc (the CPU checker of the fused FCGenerator kernel) against the
+    reference's own FCGenerator renderer (rendering.fc = 1) on the same inputs."""
+    g = np.load(golden_dir / "render_fc_small.npz")
+    sd = W.det_state_dict(W.golden_entries(golden_dir, kind="fc"), "renderer.")
+    out = oracle_mod.render_fc(sd, g["ext"], g["focal"], g["near"], g["far"], g["latent"],
+                               N=int(g["n_samples"]), res=int(g["res"]), t_rand=g["t_rand"])
+    for k in ["rgb", "features", "sdf", "xyz", "mask"]:
+        a = out[k].numpy().reshape(g[k].shape)
+        np.testing.assert_allclose(a, g[k], rtol=0, atol=5e-7,
+                                   err_msg=k)
+
+
 def _grid_ref(oracle_mod, grid_in):
     offsets, pls = oracle_mod.grid_offsets()
     emb = W.det_table(int(offsets[-1]), 2, seed=7)
