@@ -42,6 +42,8 @@ FLOP_PER_SAMPLE = 550912          # renderer MLP as the reference runs it, SURVE
 # hardware runs), roofline.algorithmic_equivalent the reference's
 FLOP_PER_SAMPLE_FUSED = 417792
 FLOP_PER_SAMPLE_SIREN = 1053696   # SirenGenerator MLP, SURVEY.md §8(d)
+# FCGenerator MLP (sdf_model.py:1599-1670): 2 (60 + 7 x 256 + 280) 256 + heads 2 (1 + 3) 256
+FLOP_PER_SAMPLE_FC = 1093632
 GATHER_BYTES_PER_SAMPLE = 1024    # 16 levels x 8 corners x 2 x fp32
 MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
 MFMA_F16_PEAK_TFLOPS = 2500.0     # MI355X dense fp16/bf16 MFMA peak (no sparsity)
@@ -59,8 +61,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--field-precision", default="f16x3", choices=["f16x3", "fp32"],
                    help="field-stage GEMM arithmetic (DESIGN.md section 5)")
-    p.add_argument("--net", default="ngp", choices=["ngp", "siren"],
-                   help="renderer network: ngp (headline, configs[1]) or siren "
+    p.add_argument("--net", default="ngp", choices=["ngp", "siren", "fc"],
+                   help="renderer network: ngp (headline, configs[1]), fc (FCGenerator, "
+                        "rendering.fc = 1: configs[4]'s plain Fourier MLP) or siren "
                         "(rendering.type 'sdf', configs[4]'s generator)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-extras", action="store_true",
@@ -159,8 +162,8 @@ def host_info():
             len(groups), "cgroup_cpu_quota": quota, "cpu_model": model, "cores": cores}
 
 
-def build_generator(sdfr, device, seed, ngp=True):
-    opt = sdfr.vol_render_opt(ngp=ngp)
+def build_generator(sdfr, device, seed, ngp=True, fc=False):
+    opt = sdfr.vol_render_opt(ngp=ngp, fc=fc)
     torch.manual_seed(seed)
     g = sdfr.Generator(opt.model, opt.rendering).to(device)
     g.eval()
@@ -169,7 +172,7 @@ def build_generator(sdfr, device, seed, ngp=True):
     return g, opt
 
 
-def cpu_baseline(seconds, siren=False):
+def cpu_baseline(seconds, siren=False, fc=False):
     """Oracle renderer (torch-CPU fp32 + C encoders) + PyTorch-CPU decoder, one face
     per call as eval.py does, on the host cores; bounded to ~`seconds`."""
     from oracle import oracle
@@ -179,10 +182,10 @@ def cpu_baseline(seconds, siren=False):
     host = host_info()
     prev_threads = torch.get_num_threads()
     torch.set_num_threads(host["cores"])
-    opt = sdfr.vol_render_opt(ngp=not siren)
+    opt = sdfr.vol_render_opt(ngp=not (siren or fc), fc=fc)
     torch.manual_seed(1)
     g = sdfr.Generator(opt.model, opt.rendering).eval()
-    render = oracle.render_siren if siren else oracle.render_ngp
+    render = oracle.render_fc if fc else (oracle.render_siren if siren else oracle.render_ngp)
     sd = {k: v for k, v in g.state_dict().items() if k.startswith("renderer.")}
     faces, t0 = 0, time.perf_counter()
     with torch.no_grad():
@@ -233,8 +236,10 @@ def main():
     world, rank, device = setup_dist(args)
     from sdfr_loader import load
     sdfr = load()
+    fc = args.net == "fc"
     siren = args.net == "siren"
-    g, opt = build_generator(sdfr, device, args.seed, ngp=not siren)
+    g, opt = build_generator(sdfr, device, args.seed, ngp=args.net == "ngp", fc=fc)
+    siren = siren or fc                         # no hash-grid stage
     g.renderer.field_precision = args.field_precision
     B = args.batch
     res = opt.model.renderer_spatial_output_dim
@@ -291,12 +296,14 @@ def main():
     render_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args.steps
     samples = B * res * res * N
     f16x3 = args.field_precision == "f16x3"
-    flop = FLOP_PER_SAMPLE_SIREN if siren else (FLOP_PER_SAMPLE_FUSED if f16x3 else FLOP_PER_SAMPLE)
+    flop = (FLOP_PER_SAMPLE_FC if fc else FLOP_PER_SAMPLE_SIREN) if siren else (
+        FLOP_PER_SAMPLE_FUSED if f16x3 else FLOP_PER_SAMPLE)
     field_tflops = flop * samples / (field_ms * 1e-3) / 1e12
     gather_gbps = GATHER_BYTES_PER_SAMPLE * samples / (enc_ms * 1e-3) / 1e9 if not siren else 0.0
-    field_kernel = ("field_p_kernel<sdfr::SirenNet>" if siren else
+    field_kernel = ("field_r_kernel<sdfr::FcNet>" if fc else
+                    "field_p_kernel<sdfr::SirenNet>" if siren else
                     "field_r_kernel<sdfr::NgpNet>") if f16x3 else "ngp_field_kernel"
-    field_mfma = "v_mfma_f32_16x16x32_f16" if siren else "v_mfma_f32_32x32x16_f16"
+    field_mfma = "v_mfma_f32_16x16x32_f16" if siren and not fc else "v_mfma_f32_32x32x16_f16"
     def traffic_of(kernel):
         """HBM bytes per launch of `kernel` at this batch, from the committed
         rocprofv3 PMC passes (profiles/, scripts/summarize_profiles.py), or None."""
@@ -345,7 +352,7 @@ def main():
         # pts_linears.0 composed into one layer, 417,792 FLOP/sample) -- the hardware
         # utilisation; `algorithmic_equivalent` prices the same time at SURVEY.md
         # §8(d)'s per-sample FLOPs of the reference's network (550,912)
-        ref_flop = FLOP_PER_SAMPLE_SIREN if siren else FLOP_PER_SAMPLE
+        ref_flop = flop if siren else FLOP_PER_SAMPLE
         alg_tflops = field_tflops * ref_flop / flop
         peak = MFMA_F16_PEAK_TFLOPS / 3
         roof = {"kernel": f"{field_kernel} (MLP as 3 split-fp16 {field_mfma} "
@@ -384,7 +391,9 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (random z, random cameras, random-init weights)",
         "config": {"workload": ("eval.py generation, SirenGenerator renderer (type 'sdf', "
-                                "configs[4]'s generator)") if siren else
+                                "configs[4]'s generator)") if siren and not fc else
+                               ("eval.py generation, FCGenerator renderer (rendering.fc = 1, "
+                                "configs[4]'s plain Fourier MLP)") if fc else
                                "eval.py 5000-image generation (ffhq_256_sdf_ngp, configs[1])",
                    "faces_per_step_per_gpu": B, "renderer": f"{res}x{res} rays x {N} samples",
                    "output": "256x256 RGB", "parallelism": f"dp{world} (independent faces)",
@@ -435,7 +444,7 @@ def main():
                 "field_tflops": FLOP_PER_SAMPLE * samples / (f32_ms * 1e-3) / 1e12,
                 "peak_tflops": MFMA_F32_PEAK_TFLOPS}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, siren)
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, siren and not fc, fc)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist.is_available() and dist.is_initialized():

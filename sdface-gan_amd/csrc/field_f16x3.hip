@@ -492,7 +492,7 @@ struct PNet {
 
 struct PRing {
     f4 *lds;          // weight ring: 4 half-slice slots of kXSliceF4
-    f4 *xch;          // this pair's exchange: [2 slots][2 blocks][hi, lo][64 lanes]
+    uint2 *xch;       // this pair's exchange: [2 slots][2 blocks][hi, lo][wave h][64 lanes]
     v4i drsrc;
     uint32_t tid, wave, h;
     f4 na[4];         // the next k-step's group-0 A fragments (t0 hi, t0 lo, t1 hi, t1 lo)
@@ -520,13 +520,19 @@ __device__ __forceinline__ void p_dma_i(const PRing &R) {
     }
 }
 
-// B fragments of exchange chunk q (both blocks): (hi0, lo0, hi1, lo1)
+// B fragments of exchange chunk q (both blocks): (hi0, lo0, hi1, lo1).  Each 16-B
+// fragment element is wave 0's 8 bytes then wave 1's, kept in two planes (one
+// ds_write_b64 per wave writes 64 x 8 contiguous bytes: conflict-free; interleaved at a
+// 16-B lane stride, as through round 4, the writes were 2-way bank conflicts), read back
+// as two ds_read_b64 (conflict-free).
 __device__ __forceinline__ void p_read_chunk(const PRing &R, int q, f4 (&b)[4]) {
-    const f4 *s = R.xch + (q & 1) * 256 + (R.tid & 63u);
-    b[0] = s[0];
-    b[1] = s[64];
-    b[2] = s[128];
-    b[3] = s[192];
+    const uint2 *s = R.xch + (q & 1) * 512 + (R.tid & 63u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint2 u0 = s[128 * k], u1 = s[128 * k + 64];
+        const uint32_t w[4] = {u0.x, u0.y, u1.x, u1.y};
+        b[k] = __builtin_bit_cast(f4, w);
+    }
 }
 
 // One k-step of one wave: 8 own output tiles x 2 sample blocks x 3 split terms = 48
@@ -611,7 +617,7 @@ __device__ __forceinline__ void p_act(const PRing &R, f4 (&in)[16], int q, const
     const f4 bt = *reinterpret_cast<const f4 *>(bet + f0);
     f4 w4;
     if constexpr (MODE == 2) w4 = *reinterpret_cast<const f4 *>(sw + f0);
-    char *dst = reinterpret_cast<char *>(R.xch + (q & 1) * 256 + (R.tid & 63u)) + 8 * R.h;
+    uint2 *dst = R.xch + (q & 1) * 512 + R.h * 64 + (R.tid & 63u);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const f4 z = in[2 * q + c];
@@ -638,8 +644,8 @@ __device__ __forceinline__ void p_act(const PRing &R, f4 (&in)[16], int q, const
                 : "+v"(l) : "v"(hp[j]), "v"(v[2 * j + 1]));
             lp[j] = l;
         }
-        *reinterpret_cast<uint2 *>(dst + 128 * 16 * c) = make_uint2(hp[0], hp[1]);
-        *reinterpret_cast<uint2 *>(dst + 128 * 16 * c + 64 * 16) = make_uint2(lp[0], lp[1]);
+        dst[256 * c] = make_uint2(hp[0], hp[1]);
+        dst[256 * c + 128] = make_uint2(lp[0], lp[1]);
     }
 }
 
@@ -649,7 +655,7 @@ __global__ void __launch_bounds__(kPThreads, 2) field_p_kernel(const XFieldArgs 
     constexpr int KV = PNet<Net>::kViews;
     constexpr int NL = Net::kLayers;
     __shared__ f4 ring_lds[kRingSlots * kXSliceF4];           // 64 KB weight ring
-    __shared__ f4 xch_lds[4][2 * 2 * 2 * 64];               // 32 KB: [pair][slot][block][hi,lo][lane]
+    __shared__ uint2 xch_lds[4][2 * 2 * 2 * 2 * 64];        // 32 KB: [pair][slot][block][hi,lo][h][lane]
     __shared__ f4 facc_lds[kPWaves][8 * 4 * 8];             // 32 KB: [wave][tile][g][ray] feature sums
     __shared__ float film_lds[NF * 2 * kW];                 // the workgroup's face
     __shared__ float cst[4 * kW];                           // sigma_w, rgb_w[3]

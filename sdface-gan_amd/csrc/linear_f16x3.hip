@@ -882,14 +882,18 @@ int sdfr_linear_f16x3(float *out, const float *x, const void *packed, const floa
     a.K = K;
     hipStream_t st = (hipStream_t)stream;
     const uint32_t NT = ceil_div(N, 16), KS = ceil_div(K, 32);
-    // the renderer networks' shapes: K in {32, 256, 272} -> N 256; N in {32, 256, 272} <- K 256
+    // the renderer networks' shapes: K in {32, 64, 256, 288} -> N 256; N in {32, 64, 256,
+    // 272, 288} <- K 256 (ngp / siren; the FCGenerator's x_in (60) and views (280) layers)
     if (NT == 16 && KS == 1) return launch_fwd<16, 1>(a, st);
+    if (NT == 16 && KS == 2) return launch_fwd<16, 2>(a, st);
     if (NT == 16 && KS == 8) return launch_fwd<16, 8>(a, st);
     if (NT == 16 && KS == 9) return launch_fwd<16, 9>(a, st);
     if (NT == 2 && KS == 8) return launch_fwd<2, 8>(a, st);
+    if (NT == 4 && KS == 8) return launch_fwd<4, 8>(a, st);
     if (NT == 17 && KS == 8) return launch_fwd<17, 8>(a, st);
-    return fail(SDFR_EUNSUPPORTED, "linear_f16x3: (N, K) must be (256, <=32 | <=256 | <=288) or "
-                                   "(<=32 | <=272, <=256)");
+    if (NT == 18 && KS == 8) return launch_fwd<18, 8>(a, st);
+    return fail(SDFR_EUNSUPPORTED, "linear_f16x3: (N, K) must be (256, <=32 | <=64 | <=256 | <=288) "
+                                   "or (<=32 | <=64 | <=288, <=256)");
 }
 
 size_t sdfr_linear_wgrad_ws_bytes(uint32_t M, uint32_t N, uint32_t K) {

@@ -190,8 +190,11 @@ def _kp(K: int) -> int:
 
 def _np_t(K: int) -> int:
     """Output width of the input-gradient GEMM (B = W^T [K, N]): the kernels take 32,
-    256 or 272 (a multiple of 16), so W^T gets zero rows up to that."""
-    return 32 if K <= 32 else (256 if K <= 256 else 272)
+    64, 256, 272 or 288 (a multiple of 16), so W^T gets zero rows up to that."""
+    for n in (32, 64, 256, 272, 288):
+        if K <= n:
+            return n
+    raise ValueError(f"no input-gradient GEMM for {K} in features")
 
 
 def _xk(x: torch.Tensor, K: int) -> torch.Tensor:
@@ -473,8 +476,9 @@ def _routable(x: torch.Tensor, weight: torch.Tensor) -> bool:
         return False
     N, K = weight.shape
     # in features padded to a multiple of 4 (forward) and the input gradient's output
-    # to 32 / 256 / 272 (_np_t): the shapes both directions take
-    if N != 256 or not (K <= 32 or K == 256 or 256 < K <= 272):
+    # to 32 / 64 / 256 / 272 / 288 (_np_t): the shapes both directions take (ngp, siren,
+    # and the FCGenerator's 60-wide x_in and 280-wide views layers)
+    if N != 256 or not (K <= 64 or K == 256 or 256 < K <= 288):
         return False
     return x.numel() // K >= 1024            # the per-face gamma / beta layers stay on F.linear
 

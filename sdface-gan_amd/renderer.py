@@ -210,11 +210,12 @@ class NGPSIRENGenerator(nn.Module):
 
 class FCGenerator(nn.Module):
     """Positional-encoding ReLU MLP, ``rendering.fc == 1`` (sdf_model.py:1599-1670).
-    On the GPU its seven 256 -> 256 layers and the sigma / rgb heads run on the
-    split-fp16 training GEMMs (``linear.linear``; twice-differentiable: the eikonal
-    term differentiates through them with create_graph); the 60-wide input layer and
-    the 280-wide views layer stay on F.linear (shapes the kernels' backward does not
-    take).  CPU tensors take F.linear throughout."""
+    Inference on the GPU (no gradients) runs the fused HIP renderer
+    (``sdfr_render_fc_forward``); with gradients its 60-wide x_in, seven 256 -> 256,
+    280-wide views layers and the sigma / rgb heads run on the split-fp16 training
+    GEMMs (``linear.linear``; twice-differentiable: the eikonal term differentiates
+    through them with create_graph); the per-face style_in (2 rows) stays on F.linear.
+    CPU tensors take F.linear throughout."""
 
     def __init__(self, D=8, W=256, style_dim=256, input_ch=3, input_ch_views=3, output_ch=4,
                  output_features=True):
@@ -247,14 +248,15 @@ class FCGenerator(nn.Module):
         pts, views = torch.split(x, [self.input_ch, self.input_ch_views], dim=-1)
         pts = self.transform_points(pts)
         views = self.transform_points(views, True)
-        h = self.x_in(pts)
+        h = linear(pts, self.x_in.weight, self.x_in.bias, twice=True)
         s = self.style_in(styles)
         s = s.view((s.shape[0],) + (1,) * (h.dim() - 2) + (s.shape[-1],))
         h = F.relu(h + s)
         for layer in self.pts_linears:
             h = F.relu(linear(h, layer.weight, layer.bias, twice=True))
         sdf = linear(h, self.sigma_linear.weight, self.sigma_linear.bias, twice=True)
-        feat = self.views_linears(torch.cat([h, views], -1))
+        feat = linear(torch.cat([h, views], -1), self.views_linears.weight,
+                      self.views_linears.bias, twice=True)
         rgb = linear(feat, self.rgb_linear.weight, self.rgb_linear.bias, twice=True)
         out = torch.cat([rgb, sdf], -1)
         return torch.cat([out, feat], -1) if self.output_features else out

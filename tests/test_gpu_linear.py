@@ -33,7 +33,7 @@ def _bound_check(name, got, exact, scale, c=32.0):
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 256, 32), (3000, 256, 256), (2048, 256, 272),
-                                   (1001, 256, 256)])
+                                   (1001, 256, 256), (2048, 256, 60), (2048, 256, 280)])
 @pytest.mark.parametrize("mag", ["unit", "rows", "tiny"])
 def test_linear_forward_and_backward_vs_float64(sdfr, M, N, K, mag):
     from sdface_gan_amd.linear import _LinearF16x3
@@ -75,9 +75,10 @@ def test_linear_routing_and_deterministic(sdfr):
         assert lin.linear(x, w).grad_fn is None             # inference: F.linear
     s = torch.randn(8, 256, device=DEV)
     assert "LinearF16x3" not in type(lin.linear(s.requires_grad_(), w).grad_fn).__name__
-    # in features up to 272 take both directions (padded); 276 would need a 288-wide input
-    # gradient, which the kernels do not take: F.linear
-    for K, routed in ((259, True), (272, True), (276, False)):
+    # in features up to 288 take both directions (padded: the FCGenerator's 280-wide views
+    # layer); 292 would need a 304-wide input gradient, which the kernels do not take:
+    # F.linear
+    for K, routed in ((60, True), (259, True), (272, True), (280, True), (292, False)):
         xk = torch.randn(4096, K, device=DEV, requires_grad=True)
         wk = torch.randn(256, K, device=DEV, requires_grad=True)
         yk = lin.linear(xk, wk)

@@ -149,10 +149,11 @@ def test_eikonal_pass_skips_weight_gradients(cpu_kernels):
 
 
 def test_padded_shapes_route_and_match(cpu_kernels):
-    """In features 3 (SIREN layer 0), 259 (views) and 1 (a head's transposed weight)
-    take the kernels with zero padding; gradients equal F.linear's."""
+    """In features 3 (SIREN layer 0), 259 (views), 60 / 280 (FCGenerator x_in / views)
+    and 1 (a head's transposed weight) take the kernels with zero padding; gradients
+    equal F.linear's."""
     torch.manual_seed(3)
-    for K in (3, 259, 268, 272):
+    for K in (3, 60, 259, 268, 272, 280):
         x = torch.randn(1024, K, requires_grad=True)
         w = torch.randn(256, K, requires_grad=True)
         bias = torch.randn(256, requires_grad=True)
@@ -165,5 +166,7 @@ def test_padded_shapes_route_and_match(cpu_kernels):
         assert gx.shape == x.shape and gw.shape == w.shape
         torch.testing.assert_close(gx, g @ w.detach(), rtol=1e-4, atol=1e-4)
         torch.testing.assert_close(gw, g.t() @ x.detach(), rtol=1e-4, atol=1e-3)
-    w = torch.randn(256, 276)
-    assert not lin._routable(torch.randn(1024, 276), w)      # input gradient would exceed 272
+    w = torch.randn(256, 292)
+    assert not lin._routable(torch.randn(1024, 292), w)      # input gradient would exceed 288
+    w = torch.randn(256, 100)
+    assert not lin._routable(torch.randn(1024, 100), w)      # 64 < K < 256: no such kernel
