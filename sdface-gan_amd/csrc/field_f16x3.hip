@@ -1161,6 +1161,41 @@ __device__ __forceinline__ void r_dma_unit(const RRing &R, uint32_t half) {
     if constexpr (2 * V + PIECE < NS) r_dma<2 * V + PIECE>(R, 2u * half + PIECE);
 }
 
+// One LDS-DMA piece: this wave's 1 KB at offset K KB of its 4 KB share of slice SLICE
+template <uint32_t SLICE, uint32_t K>
+__device__ __forceinline__ void r_dma1(const RRing &R, uint32_t slot) {
+    const uint32_t sbase = R.wave * 4096u;
+    const uint32_t lbase = lds_addr(R.lds) + sbase + slot * (kRSliceF4 * 16u);
+    const uint32_t voff = (R.tid & 63u) * 16u;
+    uint32_t so;
+    // (M0 is not restored: no compiler-generated code in field_r_kernel reads M0 --
+    // checked in the ISA, as for the conv kernels' set_m0)
+    asm volatile(
+        "s_mov_b32 m0, %3\n\ts_add_u32 %0, %4, %5\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %0 offen offset:%6 lds"
+        : "=&s"(so)
+        : "v"(voff), "s"(R.drsrc), "s"(lbase), "s"(sbase), "i"(SLICE * kRSliceF4 * 16u),
+          "i"(K * 1024u)
+        : "memory", "scc");
+}
+
+// Piece P (0..7: slice P >> 2, 1 KB part P & 3) of in-pass unit V (V >= units per pass:
+// the next pass's unit V - UPP) into ring half `half`
+template <class Net, int V, int P>
+__device__ __forceinline__ void r_dma_piece(const RRing &R, uint32_t half) {
+    constexpr int NS = RNet<Net>::kSteps, UPP = (NS + 1) / 2;
+    constexpr int S = 2 * (V % UPP) + (P >> 2);
+    if constexpr (S < NS) r_dma1<(uint32_t)S, (uint32_t)(P & 3)>(R, 2u * half + (uint32_t)(P >> 2));
+}
+
+// field_r_kernel's weight DMA placement: 1 = one piece per MFMA group, three behind the
+// unit's barrier (groups 5-7) and five in the next k-step (groups 0-4); 0 = a whole
+// slice at each of groups 5 and 6 (round 4)
+#ifndef SDFR_RSPREAD
+#define SDFR_RSPREAD 1
+#endif
+constexpr bool kRSpread = SDFR_RSPREAD != 0;
+
 // One k-step of one wave: 8 output tiles x 3 split terms = 24 MFMAs in 8 groups of one
 // tile.  Group gi's A fragments (hi, lo) were read during group gi - 3 (groups 0-2: by the
 // previous k-step, R.na).  In a unit's last k-step the barrier (this wave's DMA of the next
@@ -1191,8 +1226,32 @@ __device__ __forceinline__ void rstep(RRing &R, f16v (&acc)[8], const f4 (&bf)[2
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if constexpr (!(kFAbl & 1)) __builtin_amdgcn_s_barrier();
         }
-        if constexpr (kBar && gi == 5 && !(kFAbl & 2)) r_dma_unit<Net, VN, 0>(R, half);
-        if constexpr (kBar && gi == 6 && !(kFAbl & 2)) r_dma_unit<Net, VN, 1>(R, half);
+        if constexpr (kRSpread && !(kFAbl & 2)) {
+            // the unit's barrier releases unit U + 2's pieces 0-2 here (groups 5-7) and
+            // 3-7 in the first k-step of unit U + 1 (groups 0-4): at KS (a unit's first
+            // k-step) those are unit U + 1's (behind the previous k-step's barrier; in a
+            // workgroup's first pass they repeat the prologue's bytes)
+            // (a pass with an odd k-step count ends in a one-k-step unit whose barrier
+            // would wait on pieces issued just before it: the unit before it issues all
+            // eight of unit U + 2's pieces behind its own barrier, 3 + 3 + 2)
+            constexpr bool kOdd = (NS & 1) != 0;
+            constexpr bool kLastSingle = kOdd && KS == NS - 1;
+            constexpr bool kBeforeSingle = kOdd && KS == NS - 2;
+            if constexpr (kBar && gi >= 5) {
+                if constexpr (kBeforeSingle) {
+                    sfor<3 * (gi - 5), (3 * (gi - 4) < 8 ? 3 * (gi - 4) : 8)>([&](auto PP) {
+                        r_dma_piece<Net, U + 2, decltype(PP)::value>(R, half);
+                    });
+                } else {
+                    r_dma_piece<Net, U + 2, gi - 5>(R, half);
+                }
+            }
+            if constexpr ((KS & 1) == 0 && !kLastSingle && gi < 5)
+                r_dma_piece<Net, U + 1, gi + 3>(R, (R.ubase + (uint32_t)U + 1u) & 1u);
+        } else {
+            if constexpr (kBar && gi == 5 && !(kFAbl & 2)) r_dma_unit<Net, VN, 0>(R, half);
+            if constexpr (kBar && gi == 6 && !(kFAbl & 2)) r_dma_unit<Net, VN, 1>(R, half);
+        }
         if constexpr (gi + 3 < 8) {
             a[gi + 3][0] = A[(gi + 3) * 128];
             a[gi + 3][1] = A[(gi + 3) * 128 + 64];

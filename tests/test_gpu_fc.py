@@ -21,18 +21,25 @@ from tests.golden import weights as W
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
-# max |HIP - reference| / max |reference|, per output
-RTOL = {"rgb": 2e-5, "features": 2e-5, "sdf": 2e-5, "xyz": 2e-6, "mask": 2e-5}
+# max |HIP - reference| / max |reference| per output; rgb absolute (-1 + 2 sum w sigmoid:
+# random-init FC colours sit near 0, so a relative bound would measure fp32 rounding of
+# the 0.5-ish sigmoid sums; ngp's bound, tests/test_gpu_render.py).  Measured (MI355X,
+# round 5): features <= 4.3e-7, sdf 2.4e-7, xyz 7.5e-7, mask 1.4e-6 relative; rgb 3.6e-7.
+RTOL = {"features": 2e-6, "sdf": 2e-6, "xyz": 4e-6, "mask": 6e-6}
+ATOL = {"rgb": 2e-6}
 _record = {}
 
 
 def _cmp(name, key, got, ref):
     got = np.asarray(got, np.float64).reshape(np.shape(ref))
     ref = np.asarray(ref, np.float64)
-    scale = max(float(np.abs(ref).max()), 1e-30)
-    err = float(np.abs(got - ref).max()) / scale
+    if key in ATOL:
+        err, bound, kind = float(np.abs(got - ref).max()), ATOL[key], "abs"
+    else:
+        scale = max(float(np.abs(ref).max()), 1e-30)
+        err, bound, kind = float(np.abs(got - ref).max()) / scale, RTOL[key], "rel"
     _record[f"{name}:{key}"] = err
-    assert err <= RTOL[key], f"{name}:{key} rel max err {err:.3e} > {RTOL[key]:.1e}"
+    assert err <= bound, f"{name}:{key} {kind} max err {err:.3e} > {bound:.1e}"
 
 
 def teardown_module(module):
@@ -59,7 +66,9 @@ def make_fc(sdfr, sd, res, N, **flags):
     for k, v in flags.items():
         r[k] = v
     ren = sdfr.VolumeFeatureRenderer(r, style_dim=256, out_im_res=res)
-    ren.load_state_dict({k[len("renderer."):]: v for k, v in sd.items()}, strict=True)
+    own = ren.state_dict()
+    ren.load_state_dict({k[len("renderer."):]: v for k, v in sd.items()
+                         if k[len("renderer."):] in own}, strict=True)
     return ren.to(DEV).eval()
 
 
