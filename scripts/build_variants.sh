@@ -6,6 +6,7 @@
 set -eu
 cd "$(dirname "$0")/../sdface-gan_amd"
 SRC=${VAR_SRC:-field_f16x3}
+VD=${VAR_DIR:-lib_var}
 ALL="encoders render_ngp field_f16x3 decoder conv_f16x3 mesh linear_f16x3 linear_head"
 FIXED=""
 for s in $ALL; do [ "$s" = "$SRC" ] || FIXED="$FIXED build/$s.o"; done
@@ -15,10 +16,10 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall"
 pids=()
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
-  mkdir -p lib_var/$name
-  ( /opt/rocm/bin/hipcc $FLAGS $defs -c csrc/$SRC.hip -o lib_var/$name/$SRC.o &&
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib_var/$name/libsdfr.so \
-        $FIXED lib_var/$name/$SRC.o &&
+  mkdir -p $VD/$name
+  ( /opt/rocm/bin/hipcc $FLAGS $defs -c csrc/$SRC.hip -o $VD/$name/$SRC.o &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $VD/$name/libsdfr.so \
+        $FIXED $VD/$name/$SRC.o &&
     echo "built $name ($defs)" ) &
   pids+=($!)
 done

@@ -8,3 +8,5 @@ SDFR_PARITY_JSON=gpurun_out/parity_b.json timeout -k 10 900 python -u -m pytest 
 grep -E "passed|failed|FAILED|varying" gpurun_out/b.log | tail -12
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 REPS=3 bash scripts/gpu_var.sh
+timeout -k 10 400 python scripts/conv_time.py sdface-gan_amd/lib/libsdfr.so sdface-gan_amd/lib_cvar/*/libsdfr.so \
+    > gpurun_out/conv_var.txt 2>&1; echo "conv_time rc=$?"; grep -E "lib|total|T " gpurun_out/conv_var.txt | head -60

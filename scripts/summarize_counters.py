@@ -58,7 +58,7 @@ def main():
         c = e.get("counters", {})
         d = {"counters": c, "duration_s_by_pass": e["duration_s_by_pass"]}
         grbm = c.get("GRBM_GUI_ACTIVE")
-        t2 = next((v for n, v in e["duration_s_by_pass"].items() if n.endswith("sq2")), None)
+        t2 = next((v for n, v in e["duration_s_by_pass"].items() if n.endswith("2")), None)
         if grbm and t2:
             clk = grbm / 8 / t2
             d["effective_clock_GHz"] = clk / 1e9

@@ -43,6 +43,14 @@ constexpr int kPT = 256;        // output pixels per workgroup
 constexpr int kStepF4 = 1024;   // f4 of weight fragments per K-step (16 KB)
 constexpr int kStages = 3;   // LDS-DMA ring depth (kStages - 1 K-steps in flight)
 constexpr uint32_t kCusPerXcd = 32;   // MI355X: 256 CUs in 8 XCDs (persistent grids)
+// profiling-only ablations of conv_x_kernel (wrong results by construction): 1 = the
+// raw-output epilogue stores only when a (never occurring) sentinel matches; 16 + c =
+// only parity class c runs (the other classes' workgroups exit at once)
+#ifndef SDFR_CABL
+#define SDFR_CABL 0
+#endif
+constexpr int kCAbl = SDFR_CABL;
+
 
 __device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a),
@@ -305,7 +313,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4]
         const uint32_t oy = a.sy * (rem / Wc) + py, ox = a.sy * (rem % Wc) + px;
         float *dst = a.out + (((size_t)b * a.Hf + oy) * a.Wf + ox) * a.Cout + cb * kCT + 4 * g;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) *reinterpret_cast<f4 *>(dst + (4 * wm + i) * 16) = acc[i][j];
+        for (int i = 0; i < 4; ++i) {
+            if constexpr (kCAbl & 1) {
+                if (acc[i][j][0] == 1.2345e-33f) *reinterpret_cast<f4 *>(dst + (4 * wm + i) * 16) = acc[i][j];
+            } else {
+                *reinterpret_cast<f4 *>(dst + (4 * wm + i) * 16) = acc[i][j];
+            }
+        }
     }
 }
 
@@ -337,6 +351,9 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
     const uint32_t wm = wave & 1u, wn = wave >> 1;
     uint32_t ci, tile;
     if (!slot_tile(a, blockIdx.x, ci, tile)) return;  // padding slot (whole workgroup)
+    if constexpr (kCAbl >= 16) {
+        if (ci != (uint32_t)(kCAbl - 16)) return;
+    }
     const ConvClass &cl = a.cls[ci];
     const uint32_t Hc = cl.Hc, Wc = cl.Wc, py = cl.py, px = cl.px;
     const uint32_t ntaps = cl.ntaps;
