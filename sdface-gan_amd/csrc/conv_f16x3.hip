@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 
 #include "sdfr_common.h"
@@ -125,7 +126,8 @@ __global__ void __launch_bounds__(256) conv_pack_kernel(const float *__restrict_
 // one launch, heaviest first, so their tails overlap.
 struct ConvClass {
     uint32_t Hc, Wc;               // the class's output grid
-    uint32_t py, px;               // output pixel (a, c) -> (sy a + py, sy c + px)
+    uint32_t py, px;               // output pixel (a, c) -> (sy (a + a0) + py, sy (c + c0) + px)
+    uint32_t a0, c0;               // grid origin (0; conv_t_kernel's edge rows / columns)
     uint32_t ntaps, t0;            // its taps: dy/dx/tap[t0 .. t0 + ntaps)
     uint32_t tile0, ntiles;        // workgroups [tile0, tile0 + pad8(ntiles)) of the grid
     uint32_t td[3];                // tap descriptors, 8 bits per tap (tap | dy+1 << 4 | dx+1 << 6)
@@ -155,6 +157,7 @@ struct ConvArgs {
     uint32_t ksplit;               // split-K factor (1: the epilogue runs in the conv kernel)
     uint32_t grid;                 // workgroup slots per split (padded class tiles)
     f4 *partial;                   // [ksplit][grid][16 (i, j)][512 threads] f4 when ksplit > 1
+    uint32_t tiles_t;              // conv_t_kernel: 64-channel x 16 x 16-position tiles
 };
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -235,7 +238,8 @@ template <bool ACT>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4], uint32_t lane,
                                               uint32_t wm, uint32_t wn, uint32_t cb, uint32_t pix0,
                                               uint32_t npix, uint32_t Hc, uint32_t Wc, uint32_t py,
-                                              uint32_t px, uint32_t rs = 16) {
+                                              uint32_t px, uint32_t rs = 16, uint32_t a0 = 0,
+                                              uint32_t c0 = 0) {
     // epilogue: lane (n, g) of tile (i, j) holds channels 16 mt + 4 g .. +3 of pixel 16 nt + n
     const uint32_t n = lane & 15u, g = lane >> 4;
     if constexpr (ACT) {
@@ -310,7 +314,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4]
         if (P >= npix) continue;
         const uint32_t hw = Hc * Wc;
         const uint32_t b = P / hw, rem = P % hw;
-        const uint32_t oy = a.sy * (rem / Wc) + py, ox = a.sy * (rem % Wc) + px;
+        const uint32_t oy = a.sy * (rem / Wc + a0) + py, ox = a.sy * (rem % Wc + c0) + px;
         float *dst = a.out + (((size_t)b * a.Hf + oy) * a.Wf + ox) * a.Cout + cb * kCT + 4 * g;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -394,7 +398,7 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
         const bool pv = P < npix;
         const uint32_t Pc = pv ? P : 0;
         const uint32_t hw = Hc * Wc;
-        const uint32_t pb = Pc / hw, rem = Pc % hw, pa = rem / Wc, pc = rem % Wc;
+        const uint32_t pb = Pc / hw, rem = Pc % hw, pa = rem / Wc + cl.a0, pc = rem % Wc + cl.c0;
         xoff[k] = ((pb * a.Hin + pa) * a.Win + pc) * a.Cin * 4u + loff;
         uint32_t m = 0;
         for (uint32_t t = 0; t < ntaps; ++t) {
@@ -532,7 +536,7 @@ __global__ void __launch_bounds__(512, 1) conv_x_kernel(const ConvArgs a) {
             for (int j = 0; j < 4; ++j) pp[(i * 4 + j) * 512] = acc[i][j];
         return;
     }
-    conv_epilogue<ACT>(a, acc, lane, wm, wn, cb, pix0, npix, Hc, Wc, py, px);
+    conv_epilogue<ACT>(a, acc, lane, wm, wn, cb, pix0, npix, Hc, Wc, py, px, 16, cl.a0, cl.c0);
 }
 
 // Split-K finish: the ksplit partial tiles summed in split order (deterministic),
@@ -569,7 +573,7 @@ __global__ void __launch_bounds__(512, 1) conv_splitk_kernel(const ConvArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[i][j] += t[s - 1][i * 4 + j];
     conv_epilogue<ACT>(a, acc, lane, wm, wn, cb, pix0, a.B * cl.Hc * cl.Wc, cl.Hc, cl.Wc, cl.py,
-                       cl.px);
+                       cl.px, 16, cl.a0, cl.c0);
 }
 
 // ----------------------------------------------------------------------------
@@ -979,6 +983,272 @@ uint32_t conv_h_grid(uint32_t ntiles) {
     return 8u * (per < kCusPerXcd ? per : kCusPerXcd);
 }
 
+// ----------------------------------------------------------------------------
+// conv_t_kernel: the stride-2 transposed convolution of an upsampling StyledConv
+// (sdf_model.py:660-701, conv_transpose2d before the blur) for all four output parity
+// classes of a 16 x 16 block of INPUT positions (a, c) in one workgroup, over one
+// input halo per channel group (conv_h_kernel's 18 x 18 staging, anchored at
+// (a - 1, c - 1)).  Class (py, px) of position (a, c) is output pixel
+// (2 a + py, 2 c + px) and takes taps ky in {0, 2} (py = 0: inputs a, a - 1) or
+// ky = 1 (py = 1: input a), likewise x: the four classes' 4 + 2 + 2 + 1 taps are nine
+// K-steps per channel group over four input positions (dy, dx) in {0, -1}^2, ordered
+// by position so a B fragment read from the halo serves every class-tap at it:
+//     s    0     1     2     3  |  4     5  |  6     7  |  8
+//   (ky,kx) (0,0) (0,1) (1,0) (1,1) | (2,0) (2,1) | (0,2) (1,2) | (2,2)
+//   (dy,dx)        (0, 0)         |  (-1, 0)  |  (0, -1)  | (-1,-1)
+// Every K-step is the same work for every wave (2 m-tiles x 4 n-tiles x 3 split terms
+// into the step's class accumulators), so the nine taps of a channel group run like
+// conv_h_kernel's nine: weight ring of 3 x 8 KB (64 channels x 32), halo of the next
+// group fired over the first six steps, one barrier per step, persistent tiles.
+// conv_x_kernel staged 256 shifted pixels per tap and ran each class as its own
+// workgroups (a 1-tap class: 8-16 K-steps per 128 KB of fp32 stores).
+// Output: the raw fp32 (2H + 1)^2 grid for rows / columns < 2H, 2W; the last row and
+// column (even classes at a = H, c = W) are four thin classes of conv_x_kernel.
+// ----------------------------------------------------------------------------
+constexpr uint32_t kTCT = 64;          // output channels per conv_t workgroup
+constexpr uint32_t kTStepF4 = 512;     // f4 of weight fragments per K-step (8 KB)
+
+__host__ __device__ constexpr int t_ky(int s) {
+    return (s == 2 || s == 3 || s == 7) ? 1 : ((s == 4 || s == 5 || s == 8) ? 2 : 0);
+}
+__host__ __device__ constexpr int t_kx(int s) { return s < 6 ? (s & 1) : 2; }
+__host__ __device__ constexpr int t_pos(int s) { return s < 4 ? 0 : (s < 6 ? 1 : (s < 8 ? 2 : 3)); }
+
+__global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
+    __shared__ f4 As[3][kTStepF4];       // weight ring [mt 4][hi,lo][64]
+    __shared__ f4 Hs[2][kHaloF4];        // halo images, by channel-group parity
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t wm = wave & 1u, wn = wave >> 1;
+    const uint32_t H = a.Hin, W = a.Win;
+    const uint32_t nC = a.Cin / 32, nB = a.Cout / kCT, nT = a.Cout / kTCT;
+    const uint32_t nbx = W / 16, nby = H / 16;
+    const v4i rw = make_rsrc(a.wpk, 9u * nC * nB * kStepF4 * 16u);
+    const v4i rx = make_rsrc(a.xs, a.B * H * W * a.Cin * 4);
+    // tile -> 64-channel block cb, image b, block origin (y0, x0); this wave's halo
+    // pieces k = wave + 8 i (per-lane source offsets at channel group 0)
+    uint32_t cb = 0, bimg = 0, y0 = 0, x0 = 0, hoff[6];
+    auto setup = [&](uint32_t tile) {
+        uint32_t ln = lane, wv = wave;        // opaque: computed here, not hoisted
+        asm volatile("" : "+v"(ln), "+s"(wv));
+        cb = tile % nT;
+        uint32_t blk = tile / nT;
+        const uint32_t bx = blk % nbx;
+        blk /= nbx;
+        const uint32_t by = blk % nby, b = blk / nby;
+        bimg = b;
+        y0 = by * 16;
+        x0 = bx * 16;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const uint32_t h = 8u * (wv + 8u * i) + (ln >> 3);
+            const uint32_t hy = h / kHaloW, hx = h - hy * kHaloW;
+            const uint32_t q = (ln & 7u) ^ halo_swz(hx);
+            const int y = (int)(y0 + hy) - 1, x = (int)(x0 + hx) - 1;
+            const bool ok = h < kHaloPx && y >= 0 && y < (int)H && x >= 0 && x < (int)W;
+            hoff[i] = ok ? (((b * H + (uint32_t)y) * W + (uint32_t)x) * a.Cin * 4u + q * 16u)
+                         : 0x7FFFFFF0u;
+        }
+    };
+    const uint32_t n = lane & 15u, g = lane >> 4;
+    // B fragment lane bases (bytes within a halo buffer): [column offset dx + 1][lo]
+    uint32_t fb0[2][2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int lo = 0; lo < 2; ++lo)
+            fb0[d][lo] = (4u * wn * kHaloW + n) * 128u + (((2u * g + lo) ^ halo_swz(n + d)) << 4);
+    const uint32_t hs0 = lds_addr(&Hs[0][0]), hs1 = lds_addr(&Hs[1][0]);
+
+    auto uni = [](v4i r) {
+        return v4i{__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),
+                   __builtin_amdgcn_readfirstlane(r.z), __builtin_amdgcn_readfirstlane(r.w)};
+    };
+    // weights of K-step S of group c (tap 3 ky + kx): this block's 4 m-tiles are 8 KB,
+    // one 1 KB piece per wave
+    auto fire_w = [&](uint32_t c, auto sc, uint32_t stage) {
+        constexpr int S = decltype(sc)::value;
+        constexpr uint32_t tap = 3 * t_ky(S) + t_kx(S);
+        const uint32_t wsoff = __builtin_amdgcn_readfirstlane(
+            ((tap * nC + c) * nB + (cb >> 1)) * kStepF4 * 16u + (cb & 1u) * kTStepF4 * 16u +
+            wave * 1024u);
+        set_m0(lds_addr(&As[stage][wave * 64]));
+        dma16<0>(uni(rw), lane * 16u, wsoff);
+    };
+    uint32_t hsoff = 0;                   // soffset of the group being fetched (c * 128 B)
+    auto fire_h = [&](int buf, int i) {
+        set_m0(lds_addr(&Hs[buf][(wave + 8u * i) * 64]));
+        dma16<0>(uni(rx), hoff[i], __builtin_amdgcn_readfirstlane(hsoff));
+    };
+
+    f4 acc[4][2][4];                      // [class 2 py + px][m-tile i][n-tile j]
+    f4 Aset[2][4];                        // [hi i0, hi i1, lo i0, lo i1] by step parity
+    f4 Bset[2][8];                        // [hi j0..3, lo j0..3] by position parity
+    auto read_a = [&](f4 (&A)[4], uint32_t st) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            A[i] = As[st][((2 * wm + i) * 2) * 64 + lane];
+            A[2 + i] = As[st][((2 * wm + i) * 2 + 1) * 64 + lane];
+        }
+    };
+    auto read_b = [&](f4 (&Bf)[8], auto posc, uint32_t hs) {
+        constexpr int pos = decltype(posc)::value;
+        constexpr uint32_t dyp = (pos == 1 || pos == 3) ? 0 : 1, dxp = pos >= 2 ? 0 : 1;
+        const uint32_t bh = hs + fb0[dxp][0], bl = hs + fb0[dxp][1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t imm = ((j + dyp) * kHaloW + dxp) * 128u;
+            Bf[j] = lds_f4(bh + imm);
+            Bf[4 + j] = lds_f4(bl + imm);
+        }
+    };
+    // split term t (0: lo.hi, 1: hi.lo, 2: hi.hi) of m-tile i into class cl
+    auto mfma_quad = [&](auto clc, const f4 (&A)[4], const f4 (&Bf)[8], int i, int t) {
+        constexpr int cl = decltype(clc)::value;
+        const f4 &ra = t == 0 ? A[2 + i] : A[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc[cl][i][j] = mfma16(ra, t == 1 ? Bf[4 + j] : Bf[j], acc[cl][i][j]);
+    };
+
+    auto prologue = [&] {
+        hsoff = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) fire_h(0, i);
+        hsoff = 128u;
+        fire_w(0, std::integral_constant<int, 0>{}, 0);
+        fire_w(0, std::integral_constant<int, 1>{}, 1);
+        fire_w(0, std::integral_constant<int, 2>{}, 2);
+    };
+
+    const uint32_t ntiles = a.tiles_t, per = (ntiles + 7) >> 3;
+    const uint32_t xcd = blockIdx.x & 7u, nwg = gridDim.x >> 3;
+    const uint32_t tend = min(xcd * per + per, ntiles);
+    uint32_t tile = __builtin_amdgcn_readfirstlane(xcd * per + (blockIdx.x >> 3));
+    if (tile >= tend) return;
+    uint32_t next = tile + nwg;
+    bool has_next = next < tend;
+
+    // K-step (c, S): MFMAs of m-tile 0; wait (in flight may stay only what step -1
+    // fired: its weight piece and halo piece); barrier; read step +1's A fragments and,
+    // at a position change, its B fragments; MFMAs of m-tile 1 with step +3's weight
+    // piece and (S <= 5) a halo piece of group c + 1 between the split terms.  PAR:
+    // parity of group c (its halo buffer and the fragment sets), compile-time.
+    auto step = [&](uint32_t c, auto sc, auto parc) {
+        constexpr int S = decltype(sc)::value, PAR = decltype(parc)::value;
+        constexpr int cl = 2 * (t_ky(S) & 1) + (t_kx(S) & 1);
+        constexpr int ka = (9 * PAR + S) & 1, kb = (4 * PAR + t_pos(S)) & 1;
+        f4 (&A)[4] = Aset[ka];
+        f4 (&An)[4] = Aset[ka ^ 1];
+        f4 (&Bf)[8] = Bset[kb];
+        f4 (&Bn)[8] = Bset[kb ^ 1];
+        const auto CL = std::integral_constant<int, cl>{};
+        const uint32_t k = c * 9 + S, nk = nC * 9;
+        const bool prev_w = k + 2 < nk;
+        const bool prev_h = S != 0 && S - 1 <= 5 && c + 1 < nC;
+        mfma_quad(CL, A, Bf, 0, 0);
+        mfma_quad(CL, A, Bf, 0, 1);
+        mfma_quad(CL, A, Bf, 0, 2);
+        if (prev_w && prev_h) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+        else if (prev_w || prev_h) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(An, (S + 1) % 3);
+        if constexpr (S == 3 || S == 5 || S == 7)
+            read_b(Bn, std::integral_constant<int, t_pos(S + 1)>{}, PAR ? hs1 : hs0);
+        else if constexpr (S == 8)
+            read_b(Bn, std::integral_constant<int, 0>{}, PAR ? hs0 : hs1);
+        mfma_quad(CL, A, Bf, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (k + 3 < nk)
+            fire_w(c + (S + 3) / 9, std::integral_constant<int, (S + 3) % 9>{}, S % 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_quad(CL, A, Bf, 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (S <= 5) {
+            if (c + 1 < nC) fire_h(1 - PAR, S);
+        }
+        if constexpr (S == 8) {
+            if (k + 1 == nk && has_next) {
+                setup(next);
+                prologue();
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_quad(CL, A, Bf, 1, 2);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto group = [&](uint32_t c, auto parc) {
+        step(c, std::integral_constant<int, 0>{}, parc);
+        step(c, std::integral_constant<int, 1>{}, parc);
+        step(c, std::integral_constant<int, 2>{}, parc);
+        step(c, std::integral_constant<int, 3>{}, parc);
+        step(c, std::integral_constant<int, 4>{}, parc);
+        step(c, std::integral_constant<int, 5>{}, parc);
+        hsoff += 128u;
+        step(c, std::integral_constant<int, 6>{}, parc);
+        step(c, std::integral_constant<int, 7>{}, parc);
+        step(c, std::integral_constant<int, 8>{}, parc);
+    };
+
+    setup(tile);
+    prologue();
+    bool first = true;
+    for (;;) {
+        const uint32_t ecb = cb, eb = bimg, ey0 = y0, ex0 = x0;   // this tile (setup moves on)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[q][i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        // everything but step 2's weight piece (and, after the first tile, the previous
+        // epilogue's 32 stores, younger than this tile's prologue) has landed; the
+        // epilogue reads no LDS
+        if (first) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(33) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        read_a(Aset[0], 0);
+        read_b(Bset[0], std::integral_constant<int, 0>{}, hs0);
+        uint32_t c = 0;
+        for (; c + 1 < nC; c += 2) {
+            group(c, std::integral_constant<int, 0>{});
+            group(c + 1, std::integral_constant<int, 1>{});
+        }
+        if (c < nC) group(c, std::integral_constant<int, 0>{});
+        {   // raw fp32 outputs of the four classes
+            uint32_t ln = lane, wmm = wm, wnn = wn;   // opaque: nothing hoisted into the K loop
+            asm volatile("" : "+v"(ln), "+s"(wmm), "+s"(wnn));
+            const uint32_t nn = ln & 15u, gg = ln >> 4;
+            const uint32_t Wf = a.Wf, C = a.Cout;
+            float *base = a.out + ecb * kTCT + 4u * gg;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t oy = 2u * (ey0 + 4u * wnn + j) + (uint32_t)(q >> 1);
+                    const uint32_t ox = 2u * (ex0 + nn) + (uint32_t)(q & 1);
+                    float *dst = base + ((size_t)(eb * a.Hf + oy) * Wf + ox) * C;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        *reinterpret_cast<f4 *>(dst + (2u * wmm + i) * 16u) = acc[q][i][j];
+                }
+        }
+        if (!has_next) break;
+        tile = next;
+        next = tile + nwg;
+        has_next = next < tend;
+        first = false;
+    }
+}
+
 
 }  // namespace
 }  // namespace sdfr
@@ -1020,6 +1290,17 @@ uint32_t conv_ksplit(uint32_t grid) {
     return 1;
 }
 
+// The transposed conv on conv_t_kernel (+ its edge classes): raw output, 16-aligned
+// input, and at least one tile per CU (smaller batches keep conv_x_kernel's split-K).
+// SDFR_CONV_T in the environment: 0 selects conv_x_kernel (A/B measurements), 2 takes
+// conv_t_kernel at any tile count (tests).
+bool use_conv_t(bool act, uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
+    const char *e = getenv("SDFR_CONV_T");
+    const int env = e ? atoi(e) : 1;
+    return env != 0 && !act && H % 16 == 0 && W % 16 == 0 && Cout % kTCT == 0 &&
+           (env == 2 || B * (H / 16) * (W / 16) * (Cout / kTCT) >= 256);
+}
+
 uint32_t conv_grid(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {   // regular conv
     return ((B * H * W + kPT - 1) / kPT * (Cout / kCT) + 7) & ~7u;
 }
@@ -1050,12 +1331,15 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
     a.Cout = Cout;
     // classes (heaviest first) -> contiguous workgroup ranges padded to multiples of 8
     uint32_t grid = 0, ntap = 0;
-    auto add_class = [&](uint32_t Hc, uint32_t Wc, uint32_t py, uint32_t px, uint32_t nt) {
+    auto add_class = [&](uint32_t Hc, uint32_t Wc, uint32_t py, uint32_t px, uint32_t nt,
+                         uint32_t a0 = 0, uint32_t c0 = 0) {
         ConvClass &c = a.cls[a.ncls++];
         c.Hc = Hc;
         c.Wc = Wc;
         c.py = py;
         c.px = px;
+        c.a0 = a0;
+        c.c0 = c0;
         c.t0 = ntap - nt;
         c.ntaps = nt;
         c.tile0 = grid;
@@ -1085,6 +1369,34 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
         a.Hf = 2 * H + 1;
         a.Wf = 2 * W + 1;
         a.sy = 2;
+        if (use_conv_t(act, B, H, W, Cout)) {
+            // conv_t_kernel: every output row / column < 2H, 2W; here the last row
+            // (even classes at a = H: only the ky = 2 taps reach it) and column as four
+            // thin classes of conv_x_kernel
+            auto tap = [&](int ky, int kx) {
+                a.dy[ntap] = -(ky >> 1);
+                a.dx[ntap] = -(kx >> 1);
+                a.tap[ntap] = (uint32_t)(ky * 3 + kx);
+                ++ntap;
+            };
+            tap(2, 0), tap(2, 2);
+            add_class(1, W + 1, 0, 0, 2, H, 0);       // row 2H, even columns
+            tap(2, 1);
+            add_class(1, W, 0, 1, 1, H, 0);           // row 2H, odd columns
+            tap(0, 2), tap(2, 2);
+            add_class(H, 1, 0, 0, 2, 0, W);           // column 2W, even rows < 2H
+            tap(1, 2);
+            add_class(H, 1, 1, 0, 1, 0, W);           // column 2W, odd rows
+            a.grid = grid;
+            a.ksplit = 1;
+            a.partial = nullptr;
+            a.tiles_t = B * (H / 16) * (W / 16) * (Cout / kTCT);
+            hipLaunchKernelGGL(conv_t_kernel, dim3(conv_h_grid(a.tiles_t)), dim3(512), 0, st, a);
+            int rc = check_launch(what);
+            if (rc) return rc;
+            hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, 1), dim3(512), 0, st, a);
+            return check_launch(what);
+        }
         for (uint32_t py = 0; py < 2; ++py)
             for (uint32_t px = 0; px < 2; ++px) {
                 uint32_t nt = 0;

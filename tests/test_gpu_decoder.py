@@ -249,6 +249,47 @@ def test_conv3x3_f16x3_vs_fp64(ops, B, Cin, Cout, H, W, transposed):
     _close(f"{name}_splitk", o2.cpu(), o1.cpu(), 2e-6 * scale, 2e-7 * scale)
 
 
+@pytest.mark.parametrize("B,Cin,Cout,H,W", [
+    (1, 64, 128, 16, 16),        # one tile per 64-channel block, the four edge classes
+    (2, 96, 256, 32, 48),        # odd channel-group count, non-square, 4 channel blocks
+    (1, 512, 256, 64, 64),       # the decoder's 64 -> 128 layer at one face
+    (1, 256, 128, 128, 128),     # ... and its 128 -> 256 layer
+])
+def test_conv_t_kernel_vs_fp64_and_strip_kernel(ops, monkeypatch, B, Cin, Cout, H, W):
+    """The transposed conv on conv_t_kernel (all four parity classes of a 16 x 16 input
+    block per workgroup, one halo per channel group; the last output row / column as
+    thin conv_x_kernel classes), forced at any tile count (SDFR_CONV_T=2): against
+    float64 (the same bound as the strip kernel's, PyTorch-ROCm fp32 for scale) and
+    against conv_x_kernel (SDFR_CONV_T=0) to fp32 summation-order rounding;
+    deterministic."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(B * 11 + Cin + H)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g)
+    scale = 1 / math.sqrt(Cin * 9)
+    w32 = (scale * w).float()
+    packed, su = ops.conv_pack_weights(w.to(DEV), scale)
+    xs = ops.split_nhwc(x.to(DEV))
+    monkeypatch.setenv("SDFR_CONV_T", "2")
+    out = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
+    out2 = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
+    monkeypatch.setenv("SDFR_CONV_T", "0")
+    strip = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    got = (out / su.view(1, -1, 1, 1)).cpu().double()
+    ref = F.conv_transpose2d(x.double(), w32.double().transpose(0, 1), stride=2)
+    r32 = F.conv_transpose2d(x.to(DEV), w32.to(DEV).transpose(0, 1).contiguous(), stride=2)
+    assert got.shape == ref.shape == (B, Cout, 2 * H + 1, 2 * W + 1)
+    e16 = float((got - ref).abs().max())
+    e32 = float((r32.cpu().double() - ref).abs().max())
+    name = f"conv_t_B{B}_{Cin}x{Cout}_{H}x{W}"
+    _record[name] = [e16, e32]
+    assert e16 <= 4 * e32 + 1e-6, (e16, e32)
+    s = float(strip.abs().max())
+    _close(f"{name}_vs_strip", out.cpu(), strip.cpu(), 2e-6 * s, 2e-7 * s)
+
+
 @pytest.mark.parametrize("B,Cin,Cout,H,W,rgb,skip,store_y", [
     (2, 64, 128, 16, 16, True, True, True),     # one Cout block, ToRGB with skip
     (1, 256, 512, 16, 32, True, False, True),   # four Cout blocks (partials), no skip
