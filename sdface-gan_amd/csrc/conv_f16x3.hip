@@ -51,6 +51,12 @@ constexpr uint32_t kCusPerXcd = 32;   // MI355X: 256 CUs in 8 XCDs (persistent g
 #define SDFR_CABL 0
 #endif
 constexpr int kCAbl = SDFR_CABL;
+// conv_t_kernel ablations (profiling only): 1 no output stores (sentinel), 2 no barrier,
+// 4 no weight DMA after the prologue, 8 no halo DMA after the prologue
+#ifndef SDFR_TABL
+#define SDFR_TABL 0
+#endif
+constexpr int kTAbl = SDFR_TABL;
 
 
 __device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
@@ -158,6 +164,8 @@ struct ConvArgs {
     uint32_t grid;                 // workgroup slots per split (padded class tiles)
     f4 *partial;                   // [ksplit][grid][16 (i, j)][512 threads] f4 when ksplit > 1
     uint32_t tiles_t;              // conv_t_kernel: 64-channel x 16 x 16-position tiles
+    uint32_t ksplit_t;             // conv_t_kernel: channel-group split of a tile (1, 2, 4)
+    float *ptl;                    // ksplit_t > 1: [ksplit_t][B, Hf, Wf, Cout] partial outputs
 };
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -1027,10 +1035,16 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
     const v4i rx = make_rsrc(a.xs, a.B * H * W * a.Cin * 4);
     // tile -> 64-channel block cb, image b, block origin (y0, x0); this wave's halo
     // pieces k = wave + 8 i (per-lane source offsets at channel group 0)
-    uint32_t cb = 0, bimg = 0, y0 = 0, x0 = 0, hoff[6];
-    auto setup = [&](uint32_t tile) {
+    // work item = (tile, K split): the split's channel groups [cg0, cg1)
+    const uint32_t ks = a.ksplit_t;
+    uint32_t cb = 0, bimg = 0, y0 = 0, x0 = 0, split = 0, cg0 = 0, cg1 = 0, hoff[6];
+    auto setup = [&](uint32_t item) {
         uint32_t ln = lane, wv = wave;        // opaque: computed here, not hoisted
         asm volatile("" : "+v"(ln), "+s"(wv));
+        const uint32_t tile = item / ks;
+        split = item - tile * ks;
+        cg0 = split * nC / ks;
+        cg1 = (split + 1) * nC / ks;
         cb = tile % nT;
         uint32_t blk = tile / nT;
         const uint32_t bx = blk % nbx;
@@ -1050,6 +1064,7 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
                          : 0x7FFFFFF0u;
         }
     };
+    uint32_t c0 = 0, c1 = 0;              // the running item's channel groups
     const uint32_t n = lane & 15u, g = lane >> 4;
     // B fragment lane bases (bytes within a halo buffer): [column offset dx + 1][lo]
     uint32_t fb0[2][2];
@@ -1112,16 +1127,16 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
     };
 
     auto prologue = [&] {
-        hsoff = 0;
+        hsoff = cg0 * 128u;
 #pragma unroll
         for (int i = 0; i < 6; ++i) fire_h(0, i);
-        hsoff = 128u;
-        fire_w(0, std::integral_constant<int, 0>{}, 0);
-        fire_w(0, std::integral_constant<int, 1>{}, 1);
-        fire_w(0, std::integral_constant<int, 2>{}, 2);
+        hsoff += 128u;
+        fire_w(cg0, std::integral_constant<int, 0>{}, 0);
+        fire_w(cg0, std::integral_constant<int, 1>{}, 1);
+        fire_w(cg0, std::integral_constant<int, 2>{}, 2);
     };
 
-    const uint32_t ntiles = a.tiles_t, per = (ntiles + 7) >> 3;
+    const uint32_t ntiles = a.tiles_t * ks, per = (ntiles + 7) >> 3;
     const uint32_t xcd = blockIdx.x & 7u, nwg = gridDim.x >> 3;
     const uint32_t tend = min(xcd * per + per, ntiles);
     uint32_t tile = __builtin_amdgcn_readfirstlane(xcd * per + (blockIdx.x >> 3));
@@ -1143,16 +1158,16 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
         f4 (&Bf)[8] = Bset[kb];
         f4 (&Bn)[8] = Bset[kb ^ 1];
         const auto CL = std::integral_constant<int, cl>{};
-        const uint32_t k = c * 9 + S, nk = nC * 9;
+        const uint32_t k = (c - c0) * 9 + S, nk = (c1 - c0) * 9;
         const bool prev_w = k + 2 < nk;
-        const bool prev_h = S != 0 && S - 1 <= 5 && c + 1 < nC;
+        const bool prev_h = S != 0 && S - 1 <= 5 && c + 1 < c1;
         mfma_quad(CL, A, Bf, 0, 0);
         mfma_quad(CL, A, Bf, 0, 1);
         mfma_quad(CL, A, Bf, 0, 2);
         if (prev_w && prev_h) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
         else if (prev_w || prev_h) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if constexpr (!(kTAbl & 2)) __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         read_a(An, (S + 1) % 3);
         if constexpr (S == 3 || S == 5 || S == 7)
@@ -1167,13 +1182,13 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (k + 3 < nk)
+        if (!(kTAbl & 4) && k + 3 < nk)
             fire_w(c + (S + 3) / 9, std::integral_constant<int, (S + 3) % 9>{}, S % 3);
         __builtin_amdgcn_sched_barrier(0);
         mfma_quad(CL, A, Bf, 1, 1);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (S <= 5) {
-            if (c + 1 < nC) fire_h(1 - PAR, S);
+        if constexpr (S <= 5 && !(kTAbl & 8)) {
+            if (c + 1 < c1) fire_h(1 - PAR, S);
         }
         if constexpr (S == 8) {
             if (k + 1 == nk && has_next) {
@@ -1202,7 +1217,9 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
     prologue();
     bool first = true;
     for (;;) {
-        const uint32_t ecb = cb, eb = bimg, ey0 = y0, ex0 = x0;   // this tile (setup moves on)
+        const uint32_t ecb = cb, eb = bimg, ey0 = y0, ex0 = x0, esp = split;  // (setup moves on)
+        c0 = cg0;
+        c1 = cg1;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1217,18 +1234,20 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
         __builtin_amdgcn_s_barrier();
         read_a(Aset[0], 0);
         read_b(Bset[0], std::integral_constant<int, 0>{}, hs0);
-        uint32_t c = 0;
-        for (; c + 1 < nC; c += 2) {
+        uint32_t c = c0;
+        for (; c + 1 < c1; c += 2) {
             group(c, std::integral_constant<int, 0>{});
             group(c + 1, std::integral_constant<int, 1>{});
         }
-        if (c < nC) group(c, std::integral_constant<int, 0>{});
+        if (c < c1) group(c, std::integral_constant<int, 0>{});
         {   // raw fp32 outputs of the four classes
             uint32_t ln = lane, wmm = wm, wnn = wn;   // opaque: nothing hoisted into the K loop
             asm volatile("" : "+v"(ln), "+s"(wmm), "+s"(wnn));
             const uint32_t nn = ln & 15u, gg = ln >> 4;
             const uint32_t Wf = a.Wf, C = a.Cout;
-            float *base = a.out + ecb * kTCT + 4u * gg;
+            // (a K split writes its partial output; conv_t_finish_kernel sums them)
+            float *base = (ks > 1 ? a.ptl + (size_t)esp * a.B * a.Hf * Wf * C : a.out) + ecb * kTCT +
+                          4u * gg;
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1237,8 +1256,14 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
                     const uint32_t ox = 2u * (ex0 + nn) + (uint32_t)(q & 1);
                     float *dst = base + ((size_t)(eb * a.Hf + oy) * Wf + ox) * C;
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
-                        *reinterpret_cast<f4 *>(dst + (2u * wmm + i) * 16u) = acc[q][i][j];
+                    for (int i = 0; i < 2; ++i) {
+                        if constexpr (kTAbl & 1) {
+                            if (acc[q][i][j][0] == 1.2345e-33f)
+                                *reinterpret_cast<f4 *>(dst + (2u * wmm + i) * 16u) = acc[q][i][j];
+                        } else {
+                            *reinterpret_cast<f4 *>(dst + (2u * wmm + i) * 16u) = acc[q][i][j];
+                        }
+                    }
                 }
         }
         if (!has_next) break;
@@ -1290,15 +1315,60 @@ uint32_t conv_ksplit(uint32_t grid) {
     return 1;
 }
 
+// conv_t_kernel's K-split finish: out = sum of the ksplit_t partials, in split order
+// (deterministic), for every output row / column < 2H, 2W (the edge classes write theirs)
+__global__ void __launch_bounds__(256) conv_t_finish_kernel(const ConvArgs a) {
+    const uint32_t C4 = a.Cout / 4, W2 = 2 * a.Win, H2 = 2 * a.Hin;
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (uint64_t)a.B * H2 * W2 * C4) return;
+    const uint32_t q = (uint32_t)(t % C4);
+    uint64_t r = t / C4;
+    const uint32_t ox = (uint32_t)(r % W2);
+    r /= W2;
+    const uint32_t oy = (uint32_t)(r % H2), b = (uint32_t)(r / H2);
+    const size_t idx = (((size_t)b * a.Hf + oy) * a.Wf + ox) * a.Cout + 4 * q;
+    const size_t stride = (size_t)a.B * a.Hf * a.Wf * a.Cout;
+    f4 v = *reinterpret_cast<const f4 *>(a.ptl + idx);
+    for (uint32_t k = 1; k < a.ksplit_t; ++k) v += *reinterpret_cast<const f4 *>(a.ptl + k * stride + idx);
+    *reinterpret_cast<f4 *>(a.out + idx) = v;
+}
+
 // The transposed conv on conv_t_kernel (+ its edge classes): raw output, 16-aligned
 // input, and at least one tile per CU (smaller batches keep conv_x_kernel's split-K).
 // SDFR_CONV_T in the environment: 0 selects conv_x_kernel (A/B measurements), 2 takes
-// conv_t_kernel at any tile count (tests).
-bool use_conv_t(bool act, uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
+// conv_t_kernel at any tile count (tests), 3 also splits each tile's channel groups 2 or 4
+// ways below 256 tiles (*ks) when the caller's workspace holds the partial outputs
+// (has_ws; sdfr_conv_ws_bytes sizes it).
+bool use_conv_t(bool act, uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
+                bool has_ws, uint32_t *ks) {
     const char *e = getenv("SDFR_CONV_T");
     const int env = e ? atoi(e) : 1;
-    return env != 0 && !act && H % 16 == 0 && W % 16 == 0 && Cout % kTCT == 0 &&
-           (env == 2 || B * (H / 16) * (W / 16) * (Cout / kTCT) >= 256);
+    *ks = 1;
+    if (env == 0 || act || H % 16 || W % 16 || Cout % kTCT) return false;
+    const uint32_t tiles = B * (H / 16) * (W / 16) * (Cout / kTCT), nC = Cin / 32;
+    if (tiles >= 256) return true;
+    // (the K split -- env 3 -- measured slower than conv_x_kernel's split-K at one face:
+    // its thin edge-class launch alone is a 29 us serial chain there)
+    if (has_ws && env == 3)
+        for (uint32_t k = 4; k > 1; k /= 2)
+            if (tiles * k <= 256 && nC >= 2 * k) {
+                *ks = k;
+                return true;
+            }
+    return env >= 2;
+}
+
+// the partial outputs of conv_t_kernel's K split (for any Cin: an upper bound)
+size_t conv_t_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
+    const char *e = getenv("SDFR_CONV_T");
+    if (!e || atoi(e) != 3) return 0;
+    uint32_t ks = 1;
+    const uint32_t tiles = B * (H / 16) * (W / 16) * (Cout / kTCT);
+    if (H % 16 || W % 16 || Cout % kTCT || tiles >= 256) return 0;
+    for (uint32_t k = 4; k > 1 && ks == 1; k /= 2)
+        if (tiles * k <= 256) ks = k;
+    if (ks == 1) return 0;
+    return (size_t)ks * B * (2 * H + 1) * (2 * W + 1) * Cout * sizeof(float);
 }
 
 uint32_t conv_grid(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {   // regular conv
@@ -1369,7 +1439,9 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
         a.Hf = 2 * H + 1;
         a.Wf = 2 * W + 1;
         a.sy = 2;
-        if (use_conv_t(act, B, H, W, Cout)) {
+        uint32_t kst = 1;
+        if (use_conv_t(act, B, H, W, Cin, Cout,
+                       ws != nullptr && ws_bytes >= conv_t_ws_bytes(B, H, W, Cout), &kst)) {
             // conv_t_kernel: every output row / column < 2H, 2W; here the last row
             // (even classes at a = H: only the ky = 2 taps reach it) and column as four
             // thin classes of conv_x_kernel
@@ -1391,9 +1463,17 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
             a.ksplit = 1;
             a.partial = nullptr;
             a.tiles_t = B * (H / 16) * (W / 16) * (Cout / kTCT);
-            hipLaunchKernelGGL(conv_t_kernel, dim3(conv_h_grid(a.tiles_t)), dim3(512), 0, st, a);
+            a.ksplit_t = kst;
+            a.ptl = kst > 1 ? reinterpret_cast<float *>(ws) : nullptr;
+            hipLaunchKernelGGL(conv_t_kernel, dim3(conv_h_grid(a.tiles_t * kst)), dim3(512), 0, st, a);
             int rc = check_launch(what);
             if (rc) return rc;
+            if (kst > 1) {
+                const uint64_t n4 = (uint64_t)B * 4 * H * W * (Cout / 4);
+                hipLaunchKernelGGL(conv_t_finish_kernel, dim3((uint32_t)((n4 + 255) / 256)), dim3(256),
+                                   0, st, a);
+                if ((rc = check_launch(what))) return rc;
+            }
             hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, 1), dim3(512), 0, st, a);
             return check_launch(what);
         }
@@ -1455,7 +1535,9 @@ size_t sdfr_conv_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout, int
     if (Cout % kCT || B == 0 || H == 0 || W == 0) return 0;
     const uint32_t grid = transposed ? conv_grid_t(B, H, W, Cout) : conv_grid(B, H, W, Cout);
     const uint32_t ks = conv_ksplit(grid);
-    return ks > 1 ? (size_t)ks * grid * 16 * 512 * sizeof(f4) : 0;
+    const size_t strip = ks > 1 ? (size_t)ks * grid * 16 * 512 * sizeof(f4) : 0;
+    const size_t tk = transposed ? conv_t_ws_bytes(B, H, W, Cout) : 0;
+    return strip > tk ? strip : tk;
 }
 
 int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *p, void *stream) {

@@ -322,7 +322,9 @@ constexpr int kBlurGroup = BLUR_GROUP;   // input rows loaded together (kBlurRow
 #endif
 constexpr int kBlurCols = BLUR_COLS;     // adjacent output columns per thread
 
-__global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg) {
+// rps: output rows per segment (a multiple of kBlurGroup, at most kBlurRows): small
+// batches use shorter segments so the grid still covers the chip
+__global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg, uint32_t rps) {
     constexpr int NC = kBlurCols;                     // output columns per thread
     const uint32_t Q = a.C >> 2;
     const uint32_t WG = (a.W + NC - 1) / NC;           // column groups
@@ -366,8 +368,8 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg)
     const float4 bs = ld4(a.bias + c);
     const float4 sn = a.s_next ? ld4(a.s_next + (size_t)b * C + c) : make_float4(1.f, 1.f, 1.f, 1.f);
     const float nw = a.noise ? *a.noise_weight : 0.0f;
-    const uint32_t y0 = seg * kBlurRows;
-    const uint32_t y1 = min(a.H, y0 + kBlurRows);
+    const uint32_t y0 = seg * rps;
+    const uint32_t y1 = min(a.H, y0 + rps);
     float4 h0[NC], h1[NC], h2[NC];
     {
         float4 v0[NC + 3], v1[NC + 3], v2[NC + 3];
@@ -518,6 +520,14 @@ __global__ __launch_bounds__(256) void mapping_linear_kernel(const MapArgs a) {
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t o = blockIdx.x * kMapOut + wv;
     const uint32_t kl = a.K / 64, k0 = lane * kl;
+    // this lane's weight slice (K <= 512: at most 2 float4) is loaded before the
+    // activations, so the two global-memory round trips of a layer overlap (a small
+    // batch's launch is that latency)
+    float4 wpre[kMapMaxK / 256];
+#pragma unroll
+    for (uint32_t k = 0; k < kMapMaxK / 256; ++k)
+        wpre[k] = (o < a.O && 4 * k < kl) ? *reinterpret_cast<const float4 *>(a.w + (size_t)o * a.K + k0 + 4 * k)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
     for (uint32_t b0 = blockIdx.y * kMapB; b0 < a.B; b0 += gridDim.y * kMapB) {
         const uint32_t nb = min(kMapB, a.B - b0);
         for (uint32_t i = t; i < nb * a.K; i += 256) xs[i] = a.x[(size_t)b0 * a.K + i];
@@ -538,9 +548,11 @@ __global__ __launch_bounds__(256) void mapping_linear_kernel(const MapArgs a) {
 #pragma unroll
         for (uint32_t b = 0; b < kMapB; ++b) acc[b] = 0.0f;
         if (o < a.O) {
-            const float *wr = a.w + (size_t)o * a.K + k0;
-            for (uint32_t k = 0; k < kl; k += 4) {
-                const float4 w4 = *reinterpret_cast<const float4 *>(wr + k);
+#pragma unroll
+            for (uint32_t kq = 0; kq < kMapMaxK / 256; ++kq) {
+                const uint32_t k = 4 * kq;
+                if (k >= kl) break;
+                const float4 w4 = wpre[kq];
                 const float wq[4] = {__fmul_rn(w4.x, a.wscale), __fmul_rn(w4.y, a.wscale),
                                      __fmul_rn(w4.z, a.wscale), __fmul_rn(w4.w, a.wscale)};
 #pragma unroll
@@ -792,9 +804,17 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
               reinterpret_cast<_Float16 *>(s.y_split)};
     hipStream_t st = (hipStream_t)stream;
     if (s.blur_up) {
-        const uint32_t nseg = (s.H + kBlurRows - 1) / kBlurRows;
-        const uint64_t total = (uint64_t)s.B * nseg * ((s.W + kBlurCols - 1) / kBlurCols) * (s.C / 4);
-        epi_blur_kernel<<<(uint32_t)((total + 255) / 256), 256, 0, st>>>(a, nseg);
+        // row segments of kBlurRows (3 extra input rows each), halved while the grid
+        // would leave CUs idle (eval.py's batch of 1: 64-128 blocks at 16 rows)
+        uint32_t rps = kBlurRows, nseg = 0;
+        uint64_t total = 0;
+        for (;;) {
+            nseg = (s.H + rps - 1) / rps;
+            total = (uint64_t)s.B * nseg * ((s.W + kBlurCols - 1) / kBlurCols) * (s.C / 4);
+            if (total >= 1024ull * 256 || rps <= (uint32_t)kBlurGroup) break;
+            rps /= 2;
+        }
+        epi_blur_kernel<<<(uint32_t)((total + 255) / 256), 256, 0, st>>>(a, nseg, rps);
         return check_launch("styled_epilogue(blur)");
     }
     const uint32_t Q = s.C / 4;

@@ -291,11 +291,16 @@ __global__ void __launch_bounds__(256) ngp_encode_kernel(const EncodeArgs a) {
 //   zd [S]  depth z and segment length dist = (z_{s+1} - z_s) |d| (1e10 |d| for the last
 //           sample), sdf_model.py:240-243 -- the compositing inputs field_r_kernel reads
 //           (null: not wanted).
+//   One thread per (ray, chunk of spt samples), ray fastest within a tile (coalesced
+//   stores); spt = N at large batches, smaller when the rays alone would leave the chip
+//   idle (eval.py's batch of 1: 4096 rays = 16 workgroups at one thread per ray).
 __global__ void __launch_bounds__(256) sample_geom_kernel(const GeomArgs g, float2 *__restrict__ zd,
-                                                          f4 *__restrict__ gu) {
-    const uint32_t rid = blockIdx.x * 256 + threadIdx.x;          // tile-order ray id
-    if (rid >= g.total_tiles * kTileRays) return;
-    const uint32_t tile = rid / kTileRays, n = rid % kTileRays;
+                                                          f4 *__restrict__ gu, uint32_t spt) {
+    const uint32_t nchunk = (g.N + spt - 1) / spt;
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= g.total_tiles * nchunk * kTileRays) return;
+    const uint32_t n = t % kTileRays, tc = t / kTileRays;
+    const uint32_t tile = tc / nchunk, chunk = tc % nchunk;
     const uint32_t b = tile / g.tiles_per_face;
     uint32_t rl = (tile % g.tiles_per_face) * kTileRays + n;
     const bool ray_ok = rl < g.H * g.W;
@@ -308,8 +313,9 @@ __global__ void __launch_bounds__(256) sample_geom_kernel(const GeomArgs g, floa
     const float span = __fsub_rn(fr, nr);
     const float dnorm = norm3_torch(ray.d[0], ray.d[1], ray.d[2]);
     const size_t base = (size_t)tile * g.N * kTileRays + n;
-    float z = sample_z(g.sc, nr, fr, ray_index, 0);
-    for (uint32_t s = 0; s < g.N; ++s) {
+    const uint32_t s_end = min(g.N, (chunk + 1) * spt);
+    float z = sample_z(g.sc, nr, fr, ray_index, chunk * spt);
+    for (uint32_t s = chunk * spt; s < s_end; ++s) {
         const float zn = s + 1 < g.N ? sample_z(g.sc, nr, fr, ray_index, s + 1) : 0.0f;
         if (zd) {
             const float dist = s + 1 < g.N ? __fmul_rn(__fsub_rn(zn, z), dnorm) : __fmul_rn(1e10f, dnorm);
@@ -958,8 +964,13 @@ static void launch_encode_mode(hipStream_t st, const EncodeArgs &e) {
 
 // the per-sample geometry (sample_geom_kernel: gu always, zd when wanted)
 static int launch_geom(const GeomArgs &g, float2 *zd, f4 *gu, hipStream_t st) {
-    hipLaunchKernelGGL(sample_geom_kernel, dim3((g.total_tiles * kTileRays + 255) / 256), dim3(256),
-                       0, st, g, zd, gu);
+    // samples per thread: all N, split while fewer than 64 k threads would run
+    uint32_t spt = g.N;
+    while (spt > 1 && (uint64_t)g.total_tiles * kTileRays * ((g.N + spt - 1) / spt) < 65536)
+        spt = (spt + 1) / 2;
+    const uint64_t threads = (uint64_t)g.total_tiles * kTileRays * ((g.N + spt - 1) / spt);
+    hipLaunchKernelGGL(sample_geom_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256),
+                       0, st, g, zd, gu, spt);
     return check_launch("render_ngp: sample geometry");
 }
 

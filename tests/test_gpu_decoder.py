@@ -273,10 +273,15 @@ def test_conv_t_kernel_vs_fp64_and_strip_kernel(ops, monkeypatch, B, Cin, Cout, 
     monkeypatch.setenv("SDFR_CONV_T", "2")
     out = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
     out2 = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
+    monkeypatch.setenv("SDFR_CONV_T", "3")
+    # with a workspace and SDFR_CONV_T=3: at one face (64 / 128 tiles) each tile's
+    # channel groups split 4 / 2 ways, partials summed in split order
+    sk = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True)
+    sk2 = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True)
     monkeypatch.setenv("SDFR_CONV_T", "0")
     strip = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
     torch.cuda.synchronize()
-    assert torch.equal(out, out2)
+    assert torch.equal(out, out2) and torch.equal(sk, sk2)
     got = (out / su.view(1, -1, 1, 1)).cpu().double()
     ref = F.conv_transpose2d(x.double(), w32.double().transpose(0, 1), stride=2)
     r32 = F.conv_transpose2d(x.to(DEV), w32.to(DEV).transpose(0, 1).contiguous(), stride=2)
@@ -288,6 +293,7 @@ def test_conv_t_kernel_vs_fp64_and_strip_kernel(ops, monkeypatch, B, Cin, Cout, 
     assert e16 <= 4 * e32 + 1e-6, (e16, e32)
     s = float(strip.abs().max())
     _close(f"{name}_vs_strip", out.cpu(), strip.cpu(), 2e-6 * s, 2e-7 * s)
+    _close(f"{name}_ksplit", sk.cpu(), out.cpu(), 2e-6 * s, 2e-7 * s)
 
 
 @pytest.mark.parametrize("B,Cin,Cout,H,W,rgb,skip,store_y", [
