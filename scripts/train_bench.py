@@ -1,6 +1,6 @@
 """BASELINE configs[2] / configs[4]: training throughput, DDP over RCCL.
 
-    python scripts/train_bench.py [--stage 1|2] [--net ngp|siren] [--steps K] [--warmup W]
+    python scripts/train_bench.py [--stage 1|2] [--net ngp|siren|fc] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 scripts/train_bench.py ...
 
 Random-init G/D (no checkpoints offline), synthetic real images; per GPU batch 8 in
@@ -38,7 +38,7 @@ class _NoCache(dict):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--stage", type=int, default=2, choices=[1, 2])
-    p.add_argument("--net", default="ngp", choices=["ngp", "siren"])
+    p.add_argument("--net", default="ngp", choices=["ngp", "siren", "fc"])
     p.add_argument("--steps", type=int, default=8)
     p.add_argument("--warmup", type=int, default=4)
     p.add_argument("--batch", type=int, default=8)
@@ -76,7 +76,7 @@ def main():
     if a.no_coord_cache:
         import sdface_gan_amd.training as training_mod
         training_mod._COORD_PLANES = _NoCache()
-    opt = sdfr.vol_render_opt(ngp=a.net == "ngp", batch=a.batch, chunk=a.chunk,
+    opt = sdfr.vol_render_opt(ngp=a.net == "ngp", fc=a.net == "fc", batch=a.batch, chunk=a.chunk,
                               train_renderer=a.stage == 1)
     if a.stage == 1:
         tr = RendererTrainer(opt, dev, seed=0)

@@ -16,10 +16,11 @@ fp32 accumulation, power-of-two row / column scaling: fp32-level accuracy):
   narrow heads     J <= 4 outputs (sigma 1, rgb 3): sdfr_linear_head_forward / _backward
                    (HBM-streaming fp32 FMA kernels in place of rocBLAS's N = 1..3 GEMMs)
 
-Shapes the kernels take: out features 256 with in features <= 32, 256 or 257..272
-(the networks' input / first layers, dense and views layers; in features padded with
-zero columns to a multiple of 4 and the input gradient's width to 32 / 256 / 272), and
-J <= 4 outputs with K <= 256 (the 3- and 1-wide heads).  Everything else (the per-face
+Shapes the kernels take: out features 256 with in features <= 64, 256 or 257..288
+(the networks' input / first layers, dense and views layers, the FCGenerator's 60-wide
+x_in and 280-wide views; in features padded with zero columns to a multiple of 4 and the
+input gradient's width to 32 / 64 / 256 / 272 / 288), and J <= 4 outputs with K <= 256
+(the 3- and 1-wide heads).  Everything else (the per-face
 gamma / beta layers on the styles, CPU tensors, inference) stays on F.linear.
 ``set_train_gemm("torch")`` turns the routing off.
 
@@ -248,6 +249,34 @@ def _wanted(need: bool, edge) -> bool:
         return True
 
 
+def _once(grads, inputs):
+    """The gradients a kernel backward computed outside autograd, returned from a
+    backward that runs with grad enabled (create_graph) for a layer not marked
+    ``twice``: marked like torch.autograd.function.once_differentiable's outputs, so a
+    double backward through them raises instead of silently dropping its second-order
+    term.  The ngp network's eikonal pass never differentiates them again:
+    the grid encoder's backward ends that graph."""
+    if not torch.is_grad_enabled() or not any(
+            isinstance(t, torch.Tensor) and t.requires_grad for t in inputs):
+        return grads
+    from torch._C import _functions
+    live = [g for g in grads if g is not None]
+    if not live:
+        return grads
+    err = _functions.DelayedError(
+        b"trying to differentiate twice a split-fp16 linear layer built without "
+        b"double_backward (linear(..., twice=True))", len(live))
+
+    def fake(v):
+        v = v.detach()
+        v.requires_grad = True
+        return v
+    out = err(*[fake(g) for g in live])
+    out = list(out) if isinstance(out, tuple) else [out]
+    it = iter(out)
+    return tuple(next(it) if g is not None else None for g in grads)
+
+
 def _linear_backward(gy, x, w, has_bias, needs, edges, twice=True):
     """Gradients of y = x W^T + b.  Inside a backward that builds a graph
     (autograd.grad(..., create_graph=True): the SIREN eikonal term) as differentiable
@@ -275,7 +304,7 @@ def _linear_backward(gy, x, w, has_bias, needs, edges, twice=True):
         gw = _gw(gy2, x, K)
     if nb:
         gb = gy2.sum(0)
-    return gx, gw, gb
+    return _once((gx, gw, gb), (gy, x, w))
 
 
 class _LinearF16x3(torch.autograd.Function):
@@ -387,7 +416,7 @@ class _FiLMLinearF16x3(torch.autograd.Function):
             gb = dbf.sum(0)
         gg = dg.view(gamma.shape) if ng else None
         gbt = db_.view(beta.shape) if nbe else None
-        return gx, gw, gb, gg, gbt, None
+        return (*_once((gx, gw, gb, gg, gbt), (ds, x, w, gamma, beta)), None)
 
 
 def _head_fwd(x2, w, bias):
@@ -449,7 +478,8 @@ class _LinearHead(torch.autograd.Function):
             return gx, gw, gb, None
         gx, gw, gb = _head_bwd(gy.reshape(-1, J).contiguous(), _a16(x.reshape(-1, K)),
                                _a16(weight), need_x, need_w, need_b)
-        return (gx.view(*lead, K) if gx is not None else None), gw, gb, None
+        return (*_once(((gx.view(*lead, K) if gx is not None else None), gw, gb),
+                       (gy, x, weight)), None)
 
 
 def film_linear(x, weight, bias, gamma, beta, kernels=True, twice=False):

@@ -170,3 +170,24 @@ def test_padded_shapes_route_and_match(cpu_kernels):
     assert not lin._routable(torch.randn(1024, 292), w)      # input gradient would exceed 288
     w = torch.randn(256, 100)
     assert not lin._routable(torch.randn(1024, 100), w)      # 64 < K < 256: no such kernel
+
+
+def test_single_backward_layer_refuses_double_backward(cpu_kernels):
+    """A layer routed with twice=False (the ngp network's) computes its backward on the
+    kernels; run with create_graph its gradients are marked like once_differentiable's,
+    so differentiating them again raises instead of silently dropping the second-order
+    term -- while first-order use under create_graph still works."""
+    torch.manual_seed(5)
+    x = torch.randn(1024, 256, requires_grad=True)
+    w = torch.randn(256, 256, requires_grad=True)
+    y = lin.linear(x, w, None, True, False)
+    assert "LinearF16x3" in type(y.grad_fn).__name__
+    gx = torch.autograd.grad(y.square().sum(), x, create_graph=True)[0]
+    torch.testing.assert_close(gx.detach(), (2 * y.detach()) @ w.detach(), rtol=1e-4, atol=1e-3)
+    with pytest.raises(RuntimeError, match="differentiate twice"):
+        gx.sum().backward()
+    # the twice=True route stays differentiable
+    y2 = lin.linear(x, w, None, True, True)
+    gx2 = torch.autograd.grad(y2.square().sum(), x, create_graph=True)[0]
+    gx2.sum().backward()
+    assert w.grad is not None
