@@ -1358,15 +1358,6 @@ bool use_conv_t(bool act, uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint
     return env >= 2;
 }
 
-// the split-K partials of conv_t_kernel's four thin edge classes (conv_launch)
-size_t conv_t_edge_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
-    const uint32_t nB = Cout / kCT;
-    auto cls = [&](uint32_t px) { return ((px + kPT - 1) / kPT * nB + 7) & ~7u; };
-    const uint32_t grid = cls(B * (W + 1)) + cls(B * W) + 2 * cls(B * H);
-    const uint32_t ks = conv_ksplit(grid);
-    return ks > 1 ? (size_t)ks * grid * 16 * 512 * sizeof(f4) : 0;
-}
-
 // the partial outputs of conv_t_kernel's K split (for any Cin: an upper bound)
 size_t conv_t_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
     const char *e = getenv("SDFR_CONV_T");
@@ -1483,21 +1474,10 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
                                    0, st, a);
                 if ((rc = check_launch(what))) return rc;
             }
-            // the edge classes: ~100 thin tiles with the full K loop each at B = 32 -- split
-            // K over 2-4 workgroups when the workspace holds the partials (ws is sized
-            // for the strip kernel's whole class grid, far more than this)
-            const uint32_t eks = conv_ksplit(grid);
-            if (ws && eks > 1 && ws_bytes >= (size_t)eks * grid * 16 * 512 * sizeof(f4)) {
-                a.ksplit = eks;
-                a.partial = reinterpret_cast<f4 *>(ws);
-            }
-            hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
-            if ((rc = check_launch(what))) return rc;
-            if (a.ksplit > 1) {
-                hipLaunchKernelGGL(conv_splitk_kernel<false>, dim3(grid), dim3(512), 0, st, a);
-                rc = check_launch(what);
-            }
-            return rc;
+            // the edge classes: ~100 thin tiles at B = 32, each the full K loop (20 us; a
+            // 2-way K split measured 20 + 14 us with its finish, not kept)
+            hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, 1), dim3(512), 0, st, a);
+            return check_launch(what);
         }
         for (uint32_t py = 0; py < 2; ++py)
             for (uint32_t px = 0; px < 2; ++px) {
@@ -1558,14 +1538,7 @@ size_t sdfr_conv_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout, int
     const uint32_t grid = transposed ? conv_grid_t(B, H, W, Cout) : conv_grid(B, H, W, Cout);
     const uint32_t ks = conv_ksplit(grid);
     const size_t strip = ks > 1 ? (size_t)ks * grid * 16 * 512 * sizeof(f4) : 0;
-    size_t tk = 0;
-    if (transposed) {
-        uint32_t kst;
-        const size_t e = use_conv_t(false, B, H, W, 1024, Cout, true, &kst)
-                             ? conv_t_edge_ws_bytes(B, H, W, Cout) : 0;
-        tk = conv_t_ws_bytes(B, H, W, Cout);
-        tk = tk > e ? tk : e;
-    }
+    const size_t tk = transposed ? conv_t_ws_bytes(B, H, W, Cout) : 0;
     return strip > tk ? strip : tk;
 }
 
