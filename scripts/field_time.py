@@ -1,6 +1,6 @@
 """Median field-stage time of the fused renderer for each libsdfr.so variant given on
 the command line (each in its own subprocess; profiling aid, not a test).  NET=siren
-times the SIREN renderer (configs[4]'s generator) instead of ngp.
+(or fc) times the SIREN (FC) renderer instead of ngp.
     python scripts/field_time.py sdface-gan_amd/lib_var/a/libsdfr.so ..."""
 import os
 import statistics
@@ -17,8 +17,8 @@ from sdfr_loader import load
 sdfr = load()
 dev = "cuda:0"; B = 32
 import os
-siren = os.environ.get("NET", "ngp") == "siren"
-opt = sdfr.vol_render_opt(ngp=not siren)
+net = os.environ.get("NET", "ngp")
+opt = sdfr.vol_render_opt(ngp=net == "ngp", fc=net == "fc")
 torch.manual_seed(0)
 g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
 ren = g.renderer; ren.rng_device = "device"; ren.field_precision = sys.argv[2]
@@ -37,7 +37,7 @@ with torch.no_grad():
 med = statistics.median(ts)
 import hashlib
 h = hashlib.sha1(b"".join(t.detach().float().cpu().numpy().tobytes() for t in out[:2])).hexdigest()[:12]
-flop = 1053696 if siren else 417792
+flop = {"siren": 1053696, "fc": 1093632}.get(net, 417792)
 print(f"out {h}  {med:.3f} ms  {flop * B * 4096 * 24 / med / 1e9:.1f} TFLOP/s")
 '''
 

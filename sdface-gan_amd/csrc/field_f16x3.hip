@@ -190,6 +190,16 @@ __device__ __forceinline__ int rperm_k(int l, uint32_t s, uint32_t h, uint32_t j
 
 __device__ __forceinline__ void xpin(f4 &x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void xpin(float &x) { asm volatile("" : "+v"(x)); }
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void xpin(f2v &x) { asm volatile("" : "+v"(x)); }
+
+// field_r_kernel's colour tail (no MFMA beside it: the issue-bound stretch of a pass)
+// on packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of the same
+// element-wise IEEE ops per instruction, results bit-identical); 0 = scalar
+#ifndef SDFR_RTAILPK
+#define SDFR_RTAILPK 1
+#endif
+constexpr bool kRTailPk = SDFR_RTAILPK != 0;
 
 // ----------------------------------------------------------------------------
 // prep 1: per-row power-of-two scales and scaled biases (one wave per row)
@@ -1687,6 +1697,7 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
         // rgb dot products in 4 independent chains per channel (one per row r of a 4-row
         // group), added at the end: no 128-long serial fma chain for the scheduler to wait on
         float Pc[3][4] = {};
+        f2v Pk[3][2] = {};                                 // (kRTailPk) the same sums, packed
         // 16 steps (tile t and its permlane partner t + 4, 4-row group bq), software
         // pipelined: the next step's film / rgb vectors and feature partials are read
         // (LDS) while this step's values are computed
@@ -1713,6 +1724,46 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
             TailIn &T = tin[it & 1];
             if constexpr (it + 1 < 16) tail_load(it + 1, tin[(it + 1) & 1]);
             float fp[2][4];
+            if constexpr (kRTailPk && !(kFAbl & 8)) {
+                // packed: rows (2 rp, 2 rp + 1) of each tile as one f2v
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int rp = 0; rp < 2; ++rp) {
+                        float fs[2];
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int r = 2 * rp + h;
+                            const float y = __fmaf_rn(T.gm[u][r], vout[t + 4 * u][4 * bq + r], T.bt[u][r]);
+                            fs[h] = Net::kSinAct ? sin_rev(y) : y;
+                        }
+                        const f2v fv = {fs[0], fs[1]};
+                        const f2v w0 = {T.w0[u][2 * rp], T.w0[u][2 * rp + 1]};
+                        const f2v w1 = {T.w1[u][2 * rp], T.w1[u][2 * rp + 1]};
+                        const f2v w2 = {T.w2[u][2 * rp], T.w2[u][2 * rp + 1]};
+                        Pk[0][rp] = __builtin_elementwise_fma(fv, w0, Pk[0][rp]);
+                        Pk[1][rp] = __builtin_elementwise_fma(fv, w1, Pk[1][rp]);
+                        Pk[2][rp] = __builtin_elementwise_fma(fv, w2, Pk[2][rp]);
+                        fp[u][2 * rp] = fv.x;
+                        fp[u][2 * rp + 1] = fv.y;
+                    }
+                f4 acc4 = T.fa;
+                const f2v wo = {w_own, w_own};
+#pragma unroll
+                for (int rp = 0; rp < 2; ++rp) {
+                    const f2v pa = wo * f2v{fp[0][2 * rp], fp[0][2 * rp + 1]};
+                    const f2v pb = wo * f2v{fp[1][2 * rp], fp[1][2 * rp + 1]};
+                    acc4[2 * rp] = __fadd_rn(acc4[2 * rp], row_pair_sum(pa.x, pb.x));
+                    acc4[2 * rp + 1] = __fadd_rn(acc4[2 * rp + 1], row_pair_sum(pa.y, pb.y));
+                }
+                facc[(4 * t + bq) * 64] = acc4;
+#pragma unroll
+                for (int o = 0; o < 3; ++o)
+#pragma unroll
+                    for (int rp = 0; rp < 2; ++rp) xpin(Pk[o][rp]);
+                __builtin_amdgcn_sched_barrier(0);
+                return;
+            }
             if constexpr (kFAbl & 8) {
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
@@ -1749,6 +1800,12 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
                 for (int r = 0; r < 4; ++r) xpin(Pc[o][r]);
             __builtin_amdgcn_sched_barrier(0);     // one step of look-ahead (VGPRs)
         });
+        if constexpr (kRTailPk && !(kFAbl & 8)) {
+#pragma unroll
+            for (int o = 0; o < 3; ++o)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Pc[o][r] = Pk[o][r >> 1][r & 1];
+        }
         float P0 = __fadd_rn(__fadd_rn(Pc[0][0], Pc[0][1]), __fadd_rn(Pc[0][2], Pc[0][3]));
         float P1 = __fadd_rn(__fadd_rn(Pc[1][0], Pc[1][1]), __fadd_rn(Pc[1][2], Pc[1][3]));
         float P2 = __fadd_rn(__fadd_rn(Pc[2][0], Pc[2][1]), __fadd_rn(Pc[2][2], Pc[2][3]));
