@@ -1,6 +1,6 @@
 """Run only the fused renderer (B faces, 64^2 x 24) K times: a short, clean target
 for rocprofv3 counter passes on the field kernel (profiling aid, not a test).
-    python scripts/render_only.py [f16x3|fp32] [ngp|siren]"""
+    python scripts/render_only.py [f16x3|fp32] [ngp|siren|fc]"""
 import sys
 from pathlib import Path
 
@@ -13,7 +13,7 @@ from sdfr_loader import load  # noqa: E402
 def main(B=32, K=3, precision="f16x3", net="ngp"):
     sdfr = load()
     dev = "cuda:0"
-    opt = sdfr.vol_render_opt(ngp=net == "ngp")
+    opt = sdfr.vol_render_opt(ngp=net == "ngp", fc=net == "fc")
     torch.manual_seed(0)
     g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
     ren = g.renderer

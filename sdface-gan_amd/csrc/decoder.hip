@@ -321,6 +321,13 @@ constexpr int kBlurGroup = BLUR_GROUP;   // input rows loaded together (kBlurRow
 #define BLUR_COLS 4
 #endif
 constexpr int kBlurCols = BLUR_COLS;     // adjacent output columns per thread
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs, so
+// logically adjacent blocks (which share 3 input columns) would each fill the shared
+// lines into a different L2; remapped, blocks p and p + 8 (same XCD, dispatched
+// together) take adjacent column groups.  The grid is padded to a multiple of 8.
+#ifndef BLUR_XCD
+#define BLUR_XCD 1
+#endif
 
 // rps: output rows per segment (a multiple of kBlurGroup, at most kBlurRows): small
 // batches use shorter segments so the grid still covers the chip
@@ -328,7 +335,9 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg,
     constexpr int NC = kBlurCols;                     // output columns per thread
     const uint32_t Q = a.C >> 2;
     const uint32_t WG = (a.W + NC - 1) / NC;           // column groups
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t bid = blockIdx.x;
+    if (BLUR_XCD) bid = (bid & 7u) * (gridDim.x >> 3) + (bid >> 3);
+    const uint64_t t = (uint64_t)bid * blockDim.x + threadIdx.x;
     const uint64_t total = (uint64_t)a.B * nseg * WG * Q;
     if (t >= total) return;
     const uint32_t q = (uint32_t)(t % Q);
@@ -814,7 +823,8 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
             if (total >= 1024ull * 256 || rps <= (uint32_t)kBlurGroup) break;
             rps /= 2;
         }
-        epi_blur_kernel<<<(uint32_t)((total + 255) / 256), 256, 0, st>>>(a, nseg, rps);
+        const uint32_t nb = (uint32_t)((total + 255) / 256);
+        epi_blur_kernel<<<BLUR_XCD ? (nb + 7) & ~7u : nb, 256, 0, st>>>(a, nseg, rps);
         return check_launch("styled_epilogue(blur)");
     }
     const uint32_t Q = s.C / 4;
