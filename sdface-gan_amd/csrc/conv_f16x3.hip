@@ -57,6 +57,12 @@ constexpr int kCAbl = SDFR_CABL;
 #define SDFR_TABL 0
 #endif
 constexpr int kTAbl = SDFR_TABL;
+// conv_h_kernel ablations (profiling only): 1 y stores only on a sentinel, 2 no epilogue
+// (the accumulators stored on a sentinel), 4 no ToRGB partials
+#ifndef SDFR_HABL
+#define SDFR_HABL 0
+#endif
+constexpr int kHAbl = SDFR_HABL;
 
 
 __device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
@@ -664,14 +670,18 @@ __device__ __forceinline__ void conv_h_epilogue(const ConvArgs &a, f4 (&acc)[4][
             f4 v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = act1(acc[i][j][q], dm[q], nz, bs[q], e.slope, e.scale);
-            if (e.ys) store_split8_pair(e.ys, (size_t)P * a.Cout + (ch & ~7u), v * sn, g);
+            if constexpr (kHAbl & 1) {
+                if (e.ys && v[0] == 1.2345e-33f) store_split8_pair(e.ys, (size_t)P * a.Cout + (ch & ~7u), v * sn, g);
+            } else {
+                if (e.ys) store_split8_pair(e.ys, (size_t)P * a.Cout + (ch & ~7u), v * sn, g);
+            }
 #pragma unroll
             for (int o = 0; o < 3; ++o)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) part[j][o] = fmaf(v[q], rw[o][q], part[j][o]);
         }
     }
-    if (e.rgb_w) {
+    if (!(kHAbl & 4) && e.rgb_w) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -976,7 +986,16 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
             step(c, std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, R1, R0);
             step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
         }
-        conv_h_epilogue(a, acc, Ep, lane, wm, wn, ecb, epix0, eb);
+        if constexpr (kHAbl & 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (acc[i][j][0] == 1.2345e-33f)
+                        *reinterpret_cast<f4 *>(a.e.ys + (size_t)(epix0 + lane) * 8u + 4u * (4u * i + j)) = acc[i][j];
+        } else {
+            conv_h_epilogue(a, acc, Ep, lane, wm, wn, ecb, epix0, eb);
+        }
         if (!has_next) break;
         tile = next;
         next = tile + nwg;
