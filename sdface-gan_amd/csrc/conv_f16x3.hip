@@ -63,6 +63,11 @@ constexpr int kTAbl = SDFR_TABL;
 #define SDFR_HABL 0
 #endif
 constexpr int kHAbl = SDFR_HABL;
+// small batches: K-split conv_h_kernel + conv_h_finish_kernel (0: conv_x_kernel split-K)
+#ifndef SDFR_HSPLIT
+#define SDFR_HSPLIT 1
+#endif
+constexpr bool kHSplit = SDFR_HSPLIT != 0;
 
 
 __device__ __forceinline__ f4 mfma16(f4 a, f4 b, f4 c) {
@@ -711,6 +716,7 @@ __device__ __forceinline__ void conv_h_epilogue(const ConvArgs &a, f4 (&acc)[4][
     }
 }
 
+template <bool SPLIT>
 __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     __shared__ f4 As[3][kStepF4];        // weight ring [mt 8][hi,lo][64]
     __shared__ f4 Hs[2][kHaloF4];        // halo images, by channel-group parity
@@ -726,10 +732,21 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     // tile -> Cout block cb, first pixel pix0 (image b, block origin y0, x0) and this
     // wave's halo pieces k = wave + 8 i (per-lane source offsets at channel group 0;
     // the group moves the buffer's soffset by 128 B)
-    uint32_t cb = 0, pix0 = 0, bimg = 0, y0 = 0, x0 = 0, hoff[6];
-    auto setup = [&](uint32_t tile) {
+    // K split (a.ksplit > 1, small batches): item = split * ntiles + tile takes channel
+    // groups [cg0, cg1) of its tile and stores the raw partial accumulators;
+    // conv_h_finish_kernel sums them and runs the epilogue
+    const uint32_t ks = SPLIT ? a.ksplit : 1u, ntiles = a.cls[0].ntiles;
+    uint32_t cb = 0, pix0 = 0, bimg = 0, y0 = 0, x0 = 0, hoff[6], cg0 = 0, cg1 = nC;
+    auto setup = [&](uint32_t item) {
         uint32_t ln = lane, wv = wave;        // opaque: computed here, not hoisted
         asm volatile("" : "+v"(ln), "+s"(wv));
+        uint32_t tile = item;
+        if constexpr (SPLIT) {
+            const uint32_t split = item / ntiles;
+            tile = item - split * ntiles;
+            cg0 = split * nC / ks;
+            cg1 = (split + 1) * nC / ks;
+        }
         cb = tile % nB;
         uint32_t blk = tile / nB;
         const uint32_t bx = blk % nbx;
@@ -851,21 +868,21 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     // prologue of a tile: halo of group 0, weights of steps 0-2 (every LDS buffer is
     // free once all waves passed the previous tile's last barrier)
     auto prologue = [&] {
-        hsoff = 0;
+        hsoff = cg0 * 128u;
 #pragma unroll
         for (int i = 0; i < 6; ++i) fire_h(0, i);
-        hsoff = 128u;                     // next: group 1
-        fire_w(0, 0, 0);
-        fire_w(0, 1, 1);
-        fire_w(0, 2, 2);
+        hsoff += 128u;                    // next: group cg0 + 1
+        fire_w(cg0, 0, 0);
+        fire_w(cg0, 1, 1);
+        fire_w(cg0, 2, 2);
     };
 
     // persistent schedule: XCD x owns tiles [x per, (x + 1) per) (Cout block fastest,
     // as slot_tile); its workgroups take them with stride nwg, so the ones running
     // together share halos and weights in the XCD's L2
-    const uint32_t ntiles = a.cls[0].ntiles, per = (ntiles + 7) >> 3;
+    const uint32_t nitems = ntiles * ks, per = (nitems + 7) >> 3;
     const uint32_t xcd = blockIdx.x & 7u, nwg = gridDim.x >> 3;
-    const uint32_t tend = min(xcd * per + per, ntiles);
+    const uint32_t tend = min(xcd * per + per, nitems);
     uint32_t tile = __builtin_amdgcn_readfirstlane(xcd * per + (blockIdx.x >> 3));
     if (tile >= tend) return;    // idle workgroup (whole)
     uint32_t next = tile + nwg;
@@ -882,16 +899,16 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     auto step = [&](uint32_t c, auto tapc, auto parc, const f4 (&R)[16], f4 (&Rn)[16]) {
         constexpr int T = decltype(tapc)::value;
         constexpr int P = decltype(parc)::value;
-        const uint32_t s = c * 9 + T, nk = nC * 9;
+        const uint32_t s = (c - cg0) * 9 + T, nk = (cg1 - cg0) * 9;
         const bool prev_w = s + 2 < nk;                     // step s-1 fired weights
-        const bool prev_h = T != 0 && T - 1 <= 5 && c + 1 < nC;   // ... and a halo piece
+        const bool prev_h = T != 0 && T - 1 <= 5 && c + 1 < cg1;  // ... and a halo piece
         mfma_rows(R, 0, 2);
         if (prev_w && prev_h) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
         else if (prev_w) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if constexpr (T == 1) {
-            if (c == 0) fire_ep();
+            if (c == cg0 && !SPLIT) fire_ep();
         }
         // Issue order after the barrier, pinned by scheduling fences (left to itself
         // the compiler clumps all DMAs and reads in front of the MFMAs, and an LDS-DMA
@@ -921,7 +938,7 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         mfma_quad(R, 3, 1);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (T <= 5) {
-            if (c + 1 < nC) fire_h(1 - P, T);
+            if (c + 1 < cg1) fire_h(1 - P, T);
         }
         if constexpr (T == 8) {
             if (s + 1 == nk && has_next) {
@@ -939,6 +956,7 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
     bool first = true;
     for (;;) {
         const uint32_t ecb = cb, epix0 = pix0, eb = bimg;    // this tile (setup moves on)
+        const uint32_t eitem = tile, c1 = cg1;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -952,8 +970,8 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
         f4 R0[16], R1[16];
         read_frags(R0, std::integral_constant<int, 0>{}, hs0);
         // two channel groups per iteration: 18 steps alternate R0 / R1
-        uint32_t c = 0;
-        for (; c + 1 < nC; c += 2) {
+        uint32_t c = cg0;
+        for (; c + 1 < c1; c += 2) {
             step(c, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, R0, R1);
             step(c, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}, R1, R0);
             step(c, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{}, R0, R1);
@@ -975,7 +993,7 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
             step(c + 1, std::integral_constant<int, 7>{}, std::integral_constant<int, 1>{}, R0, R1);
             step(c + 1, std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{}, R1, R0);
         }
-        if (c < nC) {
+        if (c < c1) {
             step(c, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, R0, R1);
             step(c, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}, R1, R0);
             step(c, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{}, R0, R1);
@@ -986,7 +1004,13 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
             step(c, std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, R1, R0);
             step(c, std::integral_constant<int, 8>{}, std::integral_constant<int, 0>{}, R0, R1);
         }
-        if constexpr (kHAbl & 2) {
+        if (SPLIT) {    // raw partials of this split: [item][16 (i, j)][512 threads] f4
+            f4 *pp = a.partial + (size_t)eitem * 16 * 512 + tid;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) pp[(i * 4 + j) * 512] = acc[i][j];
+        } else if constexpr (kHAbl & 2) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1008,6 +1032,44 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
 uint32_t conv_h_grid(uint32_t ntiles) {
     const uint32_t per = (ntiles + 7) >> 3;
     return 8u * (per < kCusPerXcd ? per : kCusPerXcd);
+}
+
+// conv_h_kernel's K-split finish: the ksplit partial tiles summed in split order
+// (deterministic; the same K ranges and order as conv_x_kernel's split), then the
+// fused epilogue.  A workgroup is a QUARTER tile: the two waves (wm = 0, 1) of one
+// n-tile row group wn = blockIdx.y, so the finish of a batch-1 layer spreads over 4x the
+// CUs of the conv (64 -> 256 workgroups at 64^2).
+__global__ void __launch_bounds__(128) conv_h_finish_kernel(const ConvArgs a) {
+    const uint32_t tile = blockIdx.x, wn = blockIdx.y;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wm = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t ntiles = a.cls[0].ntiles;
+    const uint32_t tid = (wm + 2u * wn) * 64u + lane;       // conv_h_kernel's thread of it
+    const uint32_t nB = a.Cout / kCT, nbx = a.Win / 16, nby = a.Hin / 16;
+    const uint32_t cb = tile % nB, blk = tile / nB;
+    const uint32_t bx = blk % nbx, by = (blk / nbx) % nby, b = blk / (nbx * nby);
+    const uint32_t pix0 = (b * a.Hin + by * 16u) * a.Win + bx * 16u;
+    f4 acc[4][4], t[3][16];
+    const f4 *pp = a.partial + (size_t)tile * 16 * 512 + tid;
+    const size_t sstride = (size_t)ntiles * 16 * 512;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = pp[(i * 4 + j) * 512];
+#pragma unroll
+    for (uint32_t s = 1; s < 4; ++s)
+        if (s < a.ksplit)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t[s - 1][q] = pp[s * sstride + q * 512];
+#pragma unroll
+    for (uint32_t s = 1; s < 4; ++s)
+        if (s < a.ksplit)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] += t[s - 1][i * 4 + j];
+    conv_epilogue<true>(a, acc, lane, wm, wn, cb, pix0, a.B * a.Hin * a.Win, a.Hin, a.Win, 0, 0,
+                        a.Win, 0, 0);
 }
 
 // ----------------------------------------------------------------------------
@@ -1520,9 +1582,22 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
         a.ksplit = ks;
         a.partial = reinterpret_cast<f4 *>(ws);
     }
-    if (act && !transposed && a.ksplit == 1 && H % 16 == 0 && W % 16 == 0)
-        hipLaunchKernelGGL(conv_h_kernel, dim3(conv_h_grid(a.cls[0].ntiles)), dim3(512), 0, st, a);
-    else if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
+    // the fused regular conv on conv_h_kernel; its K split (whole channel groups: the
+    // same K ranges as conv_x_kernel's split-K when nC % ks == 0) at small batches
+    if (act && !transposed && H % 16 == 0 && W % 16 == 0 &&
+        (a.ksplit == 1 || (kHSplit && (Cin / 32) % a.ksplit == 0))) {
+        const uint32_t nt = a.cls[0].ntiles;
+        if (a.ksplit > 1) {
+            hipLaunchKernelGGL(conv_h_kernel<true>, dim3(conv_h_grid(nt * a.ksplit)), dim3(512), 0, st, a);
+            int rc = check_launch(what);
+            if (rc) return rc;
+            hipLaunchKernelGGL(conv_h_finish_kernel, dim3(nt, 4), dim3(128), 0, st, a);
+        } else {
+            hipLaunchKernelGGL(conv_h_kernel<false>, dim3(conv_h_grid(nt)), dim3(512), 0, st, a);
+        }
+        return check_launch(what);
+    }
+    if (act) hipLaunchKernelGGL(conv_x_kernel<true>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
     if (a.ksplit > 1) {
         if (act) hipLaunchKernelGGL(conv_splitk_kernel<true>, dim3(grid), dim3(512), 0, st, a);

@@ -303,6 +303,7 @@ def test_conv_t_kernel_vs_fp64_and_strip_kernel(ops, monkeypatch, B, Cin, Cout, 
     (1, 32, 256, 16, 16, False, False, True),   # y only
     (2, 96, 128, 32, 48, True, True, True),     # halo kernel: odd channel-group count, 2x3 blocks
     (1, 256, 256, 64, 64, True, False, True),   # halo kernel: decoder-sized layer
+    (1, 256, 512, 64, 64, True, False, True),   # batch-1 conv1: halo kernel, 4-way K split
     (3, 32, 256, 128, 128, True, False, True),  # persistent halo kernel: 384 tiles (2 per
                                                 # workgroup on half the CUs), one group
     (2, 64, 128, 256, 256, True, True, False),  # ... 512 tiles (2 per workgroup), rgb only
@@ -344,7 +345,8 @@ def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, 
                1e-6 * scale)
     else:
         assert part is None
-    # split-K (small grids: K over 2 or 4 workgroups, partial tiles summed in a fixed
+    # split-K (small grids: K over 2 or 4 workgroups -- conv_h_kernel's channel-group
+    # split + conv_h_finish_kernel, or conv_x_kernel's -- partial tiles summed in a fixed
     # order, then the same epilogue): fp32 summation-order rounding of the conv
     ys2, part2 = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_w=rgb_w, **kw)
     ys3, _ = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_w=rgb_w, **kw)
