@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 9
+#define SDFR_ABI_VERSION 10
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -524,7 +524,10 @@ size_t sdfr_conv_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout, int
  *             negative_slope) * act_scale         (demod already divided by su)
  *   y_split = v * s_next[b,c] in split-NHWC (s_next NULL -> v), when y_split
  *   rgb_partial[k,b,o,h,w] = sum_{c in [128k, 128k+128)} v * rgb_w[b,o,c], when
- *   rgb_w (k < Cout/128; sdfr_rgb_finish adds the parts, bias and skip).
+ *   rgb_w (k < Cout/128; sdfr_rgb_finish adds the parts, bias and skip); or, with
+ *   rgb_base instead of rgb_w, rgb_w[b,o,c] = rgb_base[o,c] * rgb_s[b,c] (fp32 product
+ *   formed in the kernel: ToRGB's scaled 1x1 weight times the face's style, the
+ *   caller's [B,3,Cout] multiply saved).
  * Same operation order as sdfr_styled_epilogue for v and y.  H*W % 256 == 0. */
 typedef struct sdfr_conv_act_args {
     const void *x_split;          /* [B,H,W,Cin/8,2,8] fp16                         */
@@ -541,6 +544,8 @@ typedef struct sdfr_conv_act_args {
     float *rgb_partial;           /* [Cout/128,B,3,H,W] fp32 (with rgb_w)           */
     void *ws;                     /* split-K partials or NULL                       */
     size_t ws_bytes;              /* >= sdfr_conv_act_ws_bytes(...) to split        */
+    const float *rgb_base;        /* [3,Cout] (rgb_w NULL) or NULL         (ABI 10) */
+    const float *rgb_s;           /* [B,Cout] with rgb_base                (ABI 10) */
 } sdfr_conv_act_args;
 
 int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *a, void *stream);

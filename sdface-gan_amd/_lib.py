@@ -23,7 +23,7 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 9
+ABI_VERSION = 10
 FIELD_F16X3 = 0
 FIELD_FP32 = 1
 
@@ -142,6 +142,7 @@ class ConvActArgs(ctypes.Structure):
         ("negative_slope", _f32), ("act_scale", _f32),
         ("s_next", _vp), ("y_split", _vp), ("rgb_w", _vp), ("rgb_partial", _vp),
         ("ws", _vp), ("ws_bytes", ctypes.c_size_t),
+        ("rgb_base", _vp), ("rgb_s", _vp),
     ]
 
 

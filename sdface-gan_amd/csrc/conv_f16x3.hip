@@ -158,6 +158,9 @@ struct ActEpi {
     _Float16 *ys;                  // split-NHWC [B,H,W,Cout] or null
     const float *rgb_w;            // [B,3,Cout] or null
     float *rgbp;                   // [Cout/128, B, 3, H*W] ToRGB partial sums
+    // or (rgb_w null) the ToRGB weight as base [3,Cout] x style [B,Cout], multiplied
+    // here (the same fp32 product the caller would form: one launch less per layer)
+    const float *rgb_base, *rgb_s;
 };
 
 struct ConvArgs {
@@ -282,10 +285,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4]
             const f4 sn = e.s_next ? *reinterpret_cast<const f4 *>(e.s_next + (size_t)b * a.Cout + ch)
                                    : f4{1.0f, 1.0f, 1.0f, 1.0f};
             f4 rw[3];
+            const f4 rsty = e.rgb_base ? *reinterpret_cast<const f4 *>(e.rgb_s + (size_t)b * a.Cout + ch)
+                                       : f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int o = 0; o < 3; ++o)
                 rw[o] = e.rgb_w ? *reinterpret_cast<const f4 *>(e.rgb_w + ((size_t)b * 3 + o) * a.Cout + ch)
-                                : f4{0.0f, 0.0f, 0.0f, 0.0f};
+                      : e.rgb_base ? *reinterpret_cast<const f4 *>(e.rgb_base + (size_t)o * a.Cout + ch) * rsty
+                                   : f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint32_t P = pix0 + (4 * wn + j) * rs + n;
@@ -300,7 +306,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs &a, f4 (&acc)[4][4]
                     for (int r = 0; r < 4; ++r) part[j][o] = fmaf(v[r], rw[o][r], part[j][o]);
             }
         }
-        if (e.rgb_w) {
+        if (e.rgb_w || e.rgb_base) {
             // sum over the 4 channel groups g (lanes n + 16 g), then over wm (LDS)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -630,9 +636,10 @@ constexpr uint32_t kHaloW = 18;
 constexpr uint32_t kHaloPx = kHaloW * kHaloW;          // 324
 constexpr uint32_t kHaloPieces = 48;                  // 6 per wave; 41 carry pixels
 constexpr uint32_t kHaloF4 = kHaloPieces * 64;        // 48 KB per buffer
-// epilogue operand pieces (1 KB, one per wave 0..5): demod, bias, s_next (128
-// channels in lanes 0-31 each), ToRGB weights o = 0 | 1, o = 2, noise (16 rows x 16)
-constexpr uint32_t kEpPieces = 6;
+// epilogue operand pieces (1 KB, one per wave 0..6): demod, bias, s_next (128
+// channels in lanes 0-31 each), ToRGB weights o = 0 | 1, o = 2 (the face's rows of
+// rgb_w, or rgb_base's), noise (16 rows x 16), the face's rgb_s row (rgb_base only)
+constexpr uint32_t kEpPieces = 7;
 
 __device__ __forceinline__ uint32_t halo_swz(uint32_t hx) { return (hx & 4u) | ((hx >> 1) & 1u); }
 
@@ -666,7 +673,12 @@ __device__ __forceinline__ void conv_h_epilogue(const ConvArgs &a, f4 (&acc)[4][
         const uint32_t ch = cb * kCT + 4 * lq;
         const f4 dm = Ep[lq], bs = Ep[64 + lq];
         const f4 sn = e.s_next ? Ep[128 + lq] : f4{1.0f, 1.0f, 1.0f, 1.0f};
-        const f4 rw[3] = {Ep[192 + lq], Ep[224 + lq], Ep[256 + lq]};
+        f4 rw[3] = {Ep[192 + lq], Ep[224 + lq], Ep[256 + lq]};
+        if (e.rgb_base) {                               // base rows x the face's style
+            const f4 rs = Ep[384 + lq];
+#pragma unroll
+            for (int o = 0; o < 3; ++o) rw[o] = rw[o] * rs;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t r = 4 * wn + j;
@@ -686,7 +698,7 @@ __device__ __forceinline__ void conv_h_epilogue(const ConvArgs &a, f4 (&acc)[4][
                 for (int q = 0; q < 4; ++q) part[j][o] = fmaf(v[q], rw[o][q], part[j][o]);
         }
     }
-    if (!(kHAbl & 4) && e.rgb_w) {
+    if (!(kHAbl & 4) && (e.rgb_w || e.rgb_base)) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -811,15 +823,20 @@ __global__ void __launch_bounds__(512, 1) conv_h_kernel(const ConvArgs a) {
             base = e.bias; bytes = a.Cout * 4u; off = lo ? ch * 4u : OOB;
         } else if (wave == 2) {
             base = e.s_next; bytes = e.s_next ? bc : 0u; off = lo ? (bimg * a.Cout + ch) * 4u : OOB;
-        } else if (wave == 3) {
-            base = e.rgb_w; bytes = e.rgb_w ? 3u * bc : 0u;
-            off = ((bimg * 3u + (lane >> 5)) * a.Cout + ch) * 4u;
-        } else if (wave == 4) {
-            base = e.rgb_w; bytes = e.rgb_w ? 3u * bc : 0u;
-            off = lo ? ((bimg * 3u + 2u) * a.Cout + ch) * 4u : OOB;
-        } else {
+        } else if (wave == 3 || wave == 4) {
+            const uint32_t o = wave == 3 ? (lane >> 5) : 2u;
+            const bool ok = wave == 3 || lo;
+            if (e.rgb_base) {
+                base = e.rgb_base; bytes = 3u * a.Cout * 4u; off = ok ? (o * a.Cout + ch) * 4u : OOB;
+            } else {
+                base = e.rgb_w; bytes = e.rgb_w ? 3u * bc : 0u;
+                off = ok ? ((bimg * 3u + o) * a.Cout + ch) * 4u : OOB;
+            }
+        } else if (wave == 5) {
             base = e.noise; bytes = e.noise ? a.B * H * W * 4u : 0u;
             off = ((bimg * H + y0 + (lane >> 2)) * W + x0 + 4u * (lane & 3u)) * 4u;
+        } else {
+            base = e.rgb_s; bytes = e.rgb_base ? bc : 0u; off = lo ? (bimg * a.Cout + ch) * 4u : OOB;
         }
         set_m0(lds_addr(&Ep[wave * 64]));
         dma16<0>(uni(make_rsrc(base, bytes)), off, 0u);
@@ -1388,11 +1405,17 @@ namespace {
 
 // Shared setup of both entry points: shape checks, tap tables, classes; launches
 // conv_x_kernel<ACT>.
-// split-K factor: the largest of 4, 2 that keeps every split's grid within one
-// round of workgroups on the 256 CUs (one 512-thread workgroup per CU)
+// split-K factor: the largest of 4, 3, 2 that keeps the split grid within ~1.25 rounds
+// of workgroups on the 256 CUs (one 512-thread workgroup per CU).  The 1.25: the
+// batch-1 64 -> 128 transposed conv (136 workgroups, four unequal parity classes)
+// measured 82 -> 66 us with a 2-way split over 272 (a one-round bound leaves it unsplit);
+// 384 made the regular convs' 3-way splits slower.
+#ifndef SDFR_KSPLIT_MAX
+#define SDFR_KSPLIT_MAX 320
+#endif
 uint32_t conv_ksplit(uint32_t grid) {
     for (uint32_t k = 4; k > 1; --k)
-        if (grid * k <= 256) return k;
+        if (grid * k <= SDFR_KSPLIT_MAX) return k;
     return 1;
 }
 
@@ -1585,7 +1608,10 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
     // the fused regular conv on conv_h_kernel; its K split (whole channel groups: the
     // same K ranges as conv_x_kernel's split-K when nC % ks == 0) at small batches
     if (act && !transposed && H % 16 == 0 && W % 16 == 0 &&
-        (a.ksplit == 1 || (kHSplit && (Cin / 32) % a.ksplit == 0))) {
+        (a.ksplit == 1 || kHSplit)) {
+        // its split takes whole channel groups: the largest factor <= conv_ksplit's that
+        // divides the group count
+        while (a.ksplit > 1 && (Cin / 32) % a.ksplit) --a.ksplit;
         const uint32_t nt = a.cls[0].ntiles;
         if (a.ksplit > 1) {
             hipLaunchKernelGGL(conv_h_kernel<true>, dim3(conv_h_grid(nt * a.ksplit)), dim3(512), 0, st, a);
@@ -1641,12 +1667,16 @@ int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *p, void *stream) {
     const sdfr_conv_act_args &s = *p;
     if (!s.demod || !s.bias || (s.noise && !s.noise_weight))
         return fail(SDFR_EINVAL, "conv3x3_f16x3_act: null tensor pointer");
-    if (!s.y_split && !s.rgb_w) return fail(SDFR_EINVAL, "conv3x3_f16x3_act: nothing to write");
-    if (s.rgb_w && !s.rgb_partial) return fail(SDFR_EINVAL, "conv3x3_f16x3_act: rgb_partial missing");
+    const bool rgb = s.rgb_w || s.rgb_base;
+    if (s.rgb_w && s.rgb_base) return fail(SDFR_EINVAL, "conv3x3_f16x3_act: rgb_w and rgb_base are exclusive");
+    if (s.rgb_base && !s.rgb_s) return fail(SDFR_EINVAL, "conv3x3_f16x3_act: rgb_base needs rgb_s");
+    if (!s.y_split && !rgb) return fail(SDFR_EINVAL, "conv3x3_f16x3_act: nothing to write");
+    if (rgb && !s.rgb_partial) return fail(SDFR_EINVAL, "conv3x3_f16x3_act: rgb_partial missing");
     if (((uint64_t)s.H * s.W) % kPT)
         return fail(SDFR_EUNSUPPORTED, "conv3x3_f16x3_act: H*W must be a multiple of 256");
     for (const void *q : {(const void *)s.demod, (const void *)s.bias, (const void *)s.s_next,
-                          (const void *)s.rgb_w, (const void *)s.y_split})
+                          (const void *)s.rgb_w, (const void *)s.y_split, (const void *)s.rgb_base,
+                          (const void *)s.rgb_s})
         if (q && reinterpret_cast<uintptr_t>(q) % 16)
             return fail(SDFR_EINVAL, "conv3x3_f16x3_act: pointers must be 16-B aligned");
     ConvArgs a{};
@@ -1660,6 +1690,8 @@ int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *p, void *stream) {
     a.e.ys = reinterpret_cast<_Float16 *>(s.y_split);
     a.e.rgb_w = s.rgb_w;
     a.e.rgbp = s.rgb_partial;
+    a.e.rgb_base = s.rgb_base;
+    a.e.rgb_s = s.rgb_s;
     return conv_launch(a, s.x_split, s.packed, s.B, s.H, s.W, s.Cin, s.Cout, 0, true,
                        (hipStream_t)stream, "conv3x3_f16x3_act", s.ws, s.ws_bytes);
 }

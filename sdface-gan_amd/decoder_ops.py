@@ -362,11 +362,15 @@ def conv3x3_f16x3(x_split, packed, Cout, transposed=False, split_k=True):
 
 def conv3x3_f16x3_act(x_split, packed, Cout, *, demod, bias, noise_weight, noise=None,
                       s_next=None, store_y=True, rgb_w=None, negative_slope=0.2,
-                      act_scale=math.sqrt(2), split_k=True):
+                      act_scale=math.sqrt(2), split_k=True, rgb_base=None, rgb_s=None):
     """Regular conv with the plain styled epilogue fused (sdfr_conv3x3_f16x3_act):
     returns (y split-NHWC [B,H,W,Cout/8,2,8] or None, ToRGB partial sums
     [Cout/128,B,3,H,W] or None).  demod must already carry 1/su.  ``split_k``: give
-    the kernel a workspace so that small batches split K over 2 or 4 workgroups."""
+    the kernel a workspace so that small batches split K over 2 or 4 workgroups.
+    The ToRGB weight is ``rgb_w`` [B,3,Cout], or ``rgb_base`` [3,Cout] x ``rgb_s``
+    [B,Cout] multiplied in the kernel (the same fp32 products, one launch less)."""
+    if rgb_w is not None and rgb_base is not None:
+        raise RuntimeError("conv3x3_f16x3_act: rgb_w and rgb_base are exclusive")
     _require_cuda(x_split)
     if x_split.dtype != torch.float16 or x_split.dim() != 6 or x_split.shape[4:] != (2, 8) \
             or not x_split.is_contiguous():
@@ -376,7 +380,8 @@ def conv3x3_f16x3_act(x_split, packed, Cout, *, demod, bias, noise_weight, noise
     dev = x_split.device
     ys = (torch.empty(B, H, W, Cout // 8, 2, 8, device=dev, dtype=torch.float16)
           if store_y else None)
-    part = (torch.empty(Cout // 128, B, 3, H, W, device=dev) if rgb_w is not None else None)
+    rgb = rgb_w is not None or rgb_base is not None
+    part = torch.empty(Cout // 128, B, 3, H, W, device=dev) if rgb else None
     if noise is not None:
         noise = noise.expand(B, 1, H, W).contiguous()
     keep = []
@@ -399,6 +404,8 @@ def conv3x3_f16x3_act(x_split, packed, Cout, *, demod, bias, noise_weight, noise
     a.s_next = cptr(s_next)
     a.y_split = _lib.ptr(ys)
     a.rgb_w = cptr(rgb_w)
+    a.rgb_base = cptr(rgb_base)
+    a.rgb_s = cptr(rgb_s)
     a.rgb_partial = _lib.ptr(part)
     wsb = _lib.lib().sdfr_conv_act_ws_bytes(B, H, W, Cout) if split_k else 0
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev) if wsb else None

@@ -631,12 +631,14 @@ class Decoder(nn.Module):
                 # regular conv with the epilogue fused: the conv output stays on chip
                 H, W = x.shape[1], x.shape[2]
                 n = noise[i]
-                rgb_w = None
+                rgb_base = rgb_s = None
                 if i % 2 == 0:
+                    # ToRGB's modulated weight base[o, c] * s[b, c] is formed inside the
+                    # conv's epilogue (the same fp32 products as the module path's
+                    # weight * style, without a [B, 3, C] multiply launch)
                     to_rgb = self.to_rgb1 if i == 0 else self.to_rgbs[i // 2 - 1]
                     tc = to_rgb.conv
-                    s_rgb = rgb_mods[i // 2]
-                    rgb_w = self._rgb_base(tc)[None] * s_rgb[:, None, :]
+                    rgb_base, rgb_s = self._rgb_base(tc), rgb_mods[i // 2]
                 # (events run out: later convolutions go unrecorded, not an IndexError)
                 ev = self.conv_events if (self.conv_events is not None
                                           and self._conv_ev < len(self.conv_events)) else None
@@ -645,7 +647,8 @@ class Decoder(nn.Module):
                 x, part = conv3x3_f16x3_act(
                     x, packed, cout, demod=demod_su, bias=sc.activate.bias,
                     noise_weight=sc.noise.weight, noise=n,
-                    s_next=None if last else mods[i + 1], store_y=not last, rgb_w=rgb_w)
+                    s_next=None if last else mods[i + 1], store_y=not last, rgb_base=rgb_base,
+                    rgb_s=rgb_s)
                 if ev is not None:
                     ev[self._conv_ev][1].record()
                     self._conv_ev += 1

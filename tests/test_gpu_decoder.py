@@ -324,7 +324,10 @@ def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, 
               noise=torch.randn(B, 1, H, W, generator=g).to(DEV),
               s_next=(torch.rand(B, Cout, generator=g) + 0.5).to(DEV) if store_y else None,
               store_y=store_y)
-    rgb_w = torch.randn(B, 3, Cout, generator=g).to(DEV) if rgb else None
+    # ToRGB's weight as the generator forms it: scaled base [3, Cout] x style [B, Cout]
+    rgb_base = torch.randn(3, Cout, generator=g).to(DEV)
+    rgb_s = (torch.rand(B, Cout, generator=g) + 0.5).to(DEV)
+    rgb_w = rgb_base[None] * rgb_s[:, None, :] if rgb else None
     rgb_b = torch.randn(3, generator=g).to(DEV)
     sk = torch.randn(B, 3, H // 2, W // 2, generator=g).to(DEV) if skip else None
     ys, part = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_w=rgb_w, split_k=False,
@@ -339,6 +342,12 @@ def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, 
         assert ys is None
     if rgb:
         assert part.shape == (Cout // 128, B, 3, H, W)
+        # the product formed inside the kernel (rgb_base x rgb_s): bit-identical
+        ysb, partb = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_base=rgb_base,
+                                           rgb_s=rgb_s, split_k=False, **kw)
+        assert torch.equal(part, partb)
+        if store_y:
+            assert torch.equal(ys, ysb)
         got = ops.rgb_finish(part, rgb_b, skip=sk, fir=fir)
         scale = float(rgb_ref.abs().max())
         _close(f"conv_act_rgb_{Cin}x{Cout}_{H}x{W}", got.cpu(), rgb_ref.cpu(), 1e-5 * scale,
@@ -359,6 +368,9 @@ def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, 
                2e-7 * scale)
         assert torch.equal(ys2, ys3)                      # deterministic
     if rgb:
+        _, part2b = ops.conv3x3_f16x3_act(xs, packed, Cout, demod=demod, rgb_base=rgb_base,
+                                          rgb_s=rgb_s, **kw)
+        assert torch.equal(part2, part2b)
         got2 = ops.rgb_finish(part2, rgb_b, skip=sk, fir=fir)
         scale = float(rgb_ref.abs().max())
         _close(f"conv_act_splitk_rgb_{Cin}x{Cout}_{H}x{W}", got2.cpu(), rgb_ref.cpu(),
