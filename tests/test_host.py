@@ -105,17 +105,20 @@ def test_workspace_size(sdfr):
 def test_conv_split_k_workspace(sdfr):
     """Split-K decisions of the decoder convolutions (host arithmetic, no launch):
     a workspace only when the unsplit grid leaves CUs idle, sized ksplit x slots x one
-    128 x 256 fp32 partial tile."""
+    128 x 256 fp32 partial tile; the factor is the largest of 4, 3, 2 whose split grid
+    stays within 320 workgroups (1.25 rounds of the 256 CUs)."""
     lib = sdfr._lib.lib()
     tile = 16 * 512 * 16
     assert lib.sdfr_conv_ws_bytes(32, 64, 64, 512, 0) == 0            # 2048 workgroups
     assert lib.sdfr_conv_ws_bytes(1, 64, 64, 512, 0) == 4 * 64 * tile  # 64 -> 4 x 64
     assert lib.sdfr_conv_ws_bytes(1, 128, 128, 256, 0) == 2 * 128 * tile
-    assert lib.sdfr_conv_ws_bytes(5, 64, 64, 128, 0) == 3 * 80 * tile  # 80 slots: 3-way split
+    assert lib.sdfr_conv_ws_bytes(5, 64, 64, 128, 0) == 4 * 80 * tile  # 80 slots: 4-way split
+    assert lib.sdfr_conv_ws_bytes(6, 64, 64, 128, 0) == 3 * 96 * tile  # 96 slots: 3-way split
     assert lib.sdfr_conv_act_ws_bytes(1, 64, 64, 512) == lib.sdfr_conv_ws_bytes(1, 64, 64, 512, 0)
     # transposed: four parity classes (17x17, 17x16, 16x17, 16x16 at 16^2), 8-padded
     assert lib.sdfr_conv_ws_bytes(1, 16, 16, 128, 1) == 4 * 32 * tile
-    assert lib.sdfr_conv_ws_bytes(1, 64, 64, 256, 1) == 0             # 152 slots: no split
+    assert lib.sdfr_conv_ws_bytes(1, 64, 64, 256, 1) == 2 * 152 * tile  # 152 slots: 2-way
+    assert lib.sdfr_conv_ws_bytes(1, 128, 128, 128, 1) == 0           # 280 slots: no split
     assert lib.sdfr_conv_ws_bytes(1, 64, 64, 100, 1) == 0             # Cout % 128
 
 
