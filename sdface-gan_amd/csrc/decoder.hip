@@ -337,13 +337,16 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg,
     const uint32_t WG = (a.W + NC - 1) / NC;           // column groups
     uint32_t bid = blockIdx.x;
     if (BLUR_XCD) bid = (bid & 7u) * (gridDim.x >> 3) + (bid >> 3);
-    const uint64_t t = (uint64_t)bid * blockDim.x + threadIdx.x;
-    const uint64_t total = (uint64_t)a.B * nseg * WG * Q;
+    // (32-bit index arithmetic: the host keeps the thread count below 2^31)
+    const uint32_t t = bid * blockDim.x + threadIdx.x;
+    const uint32_t total = a.B * nseg * WG * Q;
     if (t >= total) return;
-    const uint32_t q = (uint32_t)(t % Q);
-    const uint32_t ox0 = (uint32_t)((t / Q) % WG) * NC;
-    const uint32_t seg = (uint32_t)((t / ((uint64_t)Q * WG)) % nseg);
-    const uint32_t b = (uint32_t)(t / ((uint64_t)Q * WG * nseg));
+    const uint32_t q = t % Q;
+    const uint32_t r1 = t / Q;
+    const uint32_t ox0 = (r1 % WG) * NC;
+    const uint32_t r2 = r1 / WG;
+    const uint32_t seg = r2 % nseg;
+    const uint32_t b = r2 / nseg;
     const uint32_t c = 4 * q;
     const uint32_t Hi = a.H + 1, Wi = a.W + 1, C = a.C;
     const float *src = a.conv + (size_t)b * Hi * Wi * C + c;
@@ -435,11 +438,12 @@ __global__ __launch_bounds__(256) void rgb_finish_kernel(float *__restrict__ rgb
                                                          const float *__restrict__ skip,
                                                          float f0, float f1, float f2, float f3,
                                                          uint32_t B, uint32_t H, uint32_t W) {
+    // grid (pixels / 256, B * 3): plane bo = blockIdx.y, 32-bit pixel index (a 64-bit
+    // t / HW, t % HW per thread was most of this streaming kernel's time)
     const uint32_t HW = H * W;
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t n = (uint64_t)B * 3 * HW;
-    if (t >= n) return;
-    const uint32_t p = (uint32_t)(t % HW), bo = (uint32_t)(t / HW), o = bo % 3;
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x, bo = blockIdx.y, o = bo % 3;
+    if (p >= HW) return;
+    const size_t n = (size_t)B * 3 * HW, t = (size_t)bo * HW + p;
     float v = part[t];
     for (uint32_t k = 1; k < nparts; ++k) v += part[k * n + t];
     v = v + rgb_b[o];
@@ -823,6 +827,7 @@ int sdfr_styled_epilogue(const sdfr_styled_epilogue_args *p, void *stream) {
             if (total >= 1024ull * 256 || rps <= (uint32_t)kBlurGroup) break;
             rps /= 2;
         }
+        if (total >= (1ull << 31)) return fail(SDFR_EINVAL, "styled_epilogue(blur): too large");
         const uint32_t nb = (uint32_t)((total + 255) / 256);
         epi_blur_kernel<<<BLUR_XCD ? (nb + 7) & ~7u : nb, 256, 0, st>>>(a, nseg, rps);
         return check_launch("styled_epilogue(blur)");
@@ -886,7 +891,9 @@ int sdfr_rgb_finish(float *rgb, const float *partial, uint32_t nparts, const flo
     const uint64_t n = (uint64_t)B * 3 * H * W;
     const float f[4] = {skip ? fir[0] : 0.f, skip ? fir[1] : 0.f, skip ? fir[2] : 0.f,
                         skip ? fir[3] : 0.f};
-    rgb_finish_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+    if (B * 3 > 65535 || (uint64_t)H * W >= (1ull << 31)) return fail(SDFR_EINVAL, "rgb_finish: too large");
+    (void)n;
+    rgb_finish_kernel<<<dim3((H * W + 255) / 256, B * 3), 256, 0, (hipStream_t)stream>>>(
         rgb, partial, nparts, rgb_b, skip, f[0], f[1], f[2], f[3], B, H, W);
     return check_launch("rgb_finish");
 }
