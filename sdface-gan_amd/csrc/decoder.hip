@@ -431,27 +431,60 @@ __global__ __launch_bounds__(256) void epi_blur_kernel(EpiArgs a, uint32_t nseg,
     }
 }
 
-// ToRGB finish after the conv-fused epilogue: one thread per (b, o, pixel).
+// ToRGB finish after the conv-fused epilogue: one thread per 4 adjacent pixels of a
+// row (float4), grid (W/4 / 64, H / 4, B * 3 planes).  The upsampled skip
+// (upfirdn2d up 2, pad (2, 1), outer(fir, fir)) in closed form: a pixel of row / column
+// parity p takes source rows / columns (y - 2 + p) / 2 + {0, 1} with taps fir[3 - p],
+// fir[1 - p] -- the same products summed in the same order as skip_up's loop (which
+// skips the odd taps), out-of-image sources as zeros (fma of 0 leaves the sum as is):
+// bit-identical, without skip_up's 16-iteration branchy loop per pixel (the kernel was
+// VALU-bound at 1.2 TB/s on the 256^2 layer).
 __global__ __launch_bounds__(256) void rgb_finish_kernel(float *__restrict__ rgb,
                                                          const float *__restrict__ part,
                                                          uint32_t nparts, const float *rgb_b,
                                                          const float *__restrict__ skip,
                                                          float f0, float f1, float f2, float f3,
                                                          uint32_t B, uint32_t H, uint32_t W) {
-    // grid (pixels / 256, B * 3): plane bo = blockIdx.y, 32-bit pixel index (a 64-bit
-    // t / HW, t % HW per thread was most of this streaming kernel's time)
-    const uint32_t HW = H * W;
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x, bo = blockIdx.y, o = bo % 3;
-    if (p >= HW) return;
-    const size_t n = (size_t)B * 3 * HW, t = (size_t)bo * HW + p;
-    float v = part[t];
-    for (uint32_t k = 1; k < nparts; ++k) v += part[k * n + t];
-    v = v + rgb_b[o];
+    const uint32_t q = blockIdx.x * 64 + (threadIdx.x & 63u), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const uint32_t bo = blockIdx.z, o = bo % 3;
+    if (4 * q >= W || y >= H) return;
+    const size_t HW = (size_t)H * W, n = (size_t)B * 3 * HW;
+    const size_t t = (size_t)bo * HW + (size_t)y * W + 4 * q;
+    float4 v = ld4(part + t);
+    for (uint32_t k = 1; k < nparts; ++k) {
+        const float4 u = ld4(part + k * n + t);
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    const float bias = rgb_b[o];
+    v.x = v.x + bias; v.y = v.y + bias; v.z = v.z + bias; v.w = v.w + bias;
     if (skip) {
         const float fir[4] = {f0, f1, f2, f3};
-        v = v + skip_up(skip + (size_t)bo * (HW / 4), H / 2, W / 2, (int)(p / W), (int)(p % W), fir);
+        const int h2 = (int)(H / 2), w2 = (int)(W / 2);
+        const float *img = skip + (size_t)bo * (HW / 4);
+        const int py = (int)(y & 1u), r0 = ((int)y - 2 + py) / 2;    // rows r0, r0 + 1
+        const float wy0 = fir[3 - py], wy1 = fir[1 - py];
+        // source columns 2q - 1 .. 2q + 2 of rows r0, r0 + 1
+        float s[2][4];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int r = r0 + a, cc = 2 * (int)q - 1 + c;
+                s[a][c] = (r >= 0 && r < h2 && cc >= 0 && cc < w2) ? img[r * w2 + cc] : 0.0f;
+            }
+        float out[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int px = d & 1, c0 = (d >> 1) + px;      // column index into s: 2q-1+c0
+            const float wx0 = fir[3 - px], wx1 = fir[1 - px];
+            float row[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) row[a] = fmaf(s[a][c0 + 1], wx1, fmaf(s[a][c0], wx0, 0.0f));
+            out[d] = fmaf(row[1], wy1, fmaf(row[0], wy0, 0.0f));
+        }
+        v.x = v.x + out[0]; v.y = v.y + out[1]; v.z = v.z + out[2]; v.w = v.w + out[3];
     }
-    rgb[t] = v;
+    *reinterpret_cast<float4 *>(rgb + t) = v;
 }
 
 // ----------------------------------------------------------------------------
@@ -528,7 +561,7 @@ struct MapArgs {
 };
 
 __global__ __launch_bounds__(256) void mapping_linear_kernel(const MapArgs a) {
-    __shared__ float xs[kMapB * kMapMaxK];
+    __shared__ __attribute__((aligned(16))) float xs[kMapB * kMapMaxK];
     __shared__ float nrm[kMapB];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t o = blockIdx.x * kMapOut + wv;
@@ -543,7 +576,17 @@ __global__ __launch_bounds__(256) void mapping_linear_kernel(const MapArgs a) {
                                           : make_float4(0.f, 0.f, 0.f, 0.f);
     for (uint32_t b0 = blockIdx.y * kMapB; b0 < a.B; b0 += gridDim.y * kMapB) {
         const uint32_t nb = min(kMapB, a.B - b0);
-        for (uint32_t i = t; i < nb * a.K; i += 256) xs[i] = a.x[(size_t)b0 * a.K + i];
+        if ((reinterpret_cast<uintptr_t>(a.x) & 15u) == 0) {
+            // 16-B loads, up to 8 in flight per thread (a one-float-per-iteration loop
+            // was a chain of up to 32 dependent L2 round trips at 16 samples)
+            const float4 *x4 = reinterpret_cast<const float4 *>(a.x + (size_t)b0 * a.K);
+            float4 *xs4 = reinterpret_cast<float4 *>(xs);
+            const uint32_t n4 = nb * a.K / 4;
+#pragma unroll 8
+            for (uint32_t i = t; i < n4; i += 256) xs4[i] = x4[i];
+        } else {
+            for (uint32_t i = t; i < nb * a.K; i += 256) xs[i] = a.x[(size_t)b0 * a.K + i];
+        }
         __syncthreads();
         if (a.pixelnorm) {                       // x * rsqrt(mean(x^2) + 1e-8)
             for (uint32_t b = wv; b < nb; b += 4) {
@@ -609,15 +652,26 @@ __global__ __launch_bounds__(256) void mapping_linear_kernel(const MapArgs a) {
 // a wave per output channel, lanes over the reduction, butterfly sum.
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void style_mod_kernel(const sdfr_style_args a) {
-    __shared__ float xs[kMapB * kMapMaxK];
+    __shared__ __attribute__((aligned(16))) float xs[kMapB * kMapMaxK];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t k = blockIdx.y, c = blockIdx.x * kMapOut + wv;
     const uint32_t ck = a.mod_c[k], K = a.K, kl = K / 64, k0 = lane * kl;
     for (uint32_t b0 = blockIdx.z * kMapB; b0 < a.B; b0 += gridDim.z * kMapB) {
         const uint32_t nb = min(kMapB, a.B - b0);
-        for (uint32_t i = t; i < nb * K; i += 256) {
-            const uint32_t b = i / K, j = i - b * K;
-            xs[i] = a.latent[((size_t)(b0 + b) * a.n_latent + a.mod_index[k]) * K + j];
+        if ((reinterpret_cast<uintptr_t>(a.latent) & 15u) == 0) {
+            // 16-B loads, several in flight per thread (see mapping_linear_kernel)
+            const uint32_t K4 = K / 4;
+#pragma unroll 8
+            for (uint32_t i = t; i < nb * K4; i += 256) {
+                const uint32_t b = i / K4, j = i - b * K4;
+                reinterpret_cast<float4 *>(xs)[i] = *reinterpret_cast<const float4 *>(
+                    a.latent + ((size_t)(b0 + b) * a.n_latent + a.mod_index[k]) * K + 4 * j);
+            }
+        } else {
+            for (uint32_t i = t; i < nb * K; i += 256) {
+                const uint32_t b = i / K, j = i - b * K;
+                xs[i] = a.latent[((size_t)(b0 + b) * a.n_latent + a.mod_index[k]) * K + j];
+            }
         }
         __syncthreads();
         float acc[kMapB];
@@ -657,7 +711,7 @@ __global__ __launch_bounds__(256) void style_mod_kernel(const sdfr_style_args a)
 }
 
 __global__ __launch_bounds__(256) void style_demod_kernel(const sdfr_style_args a) {
-    __shared__ float xs[kMapB * kMapMaxK];
+    __shared__ __attribute__((aligned(16))) float xs[kMapB * kMapMaxK];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t j = blockIdx.y, o = blockIdx.x * kMapOut + wv;
     const uint32_t layer = a.dem_layer[j], cin = a.mod_c[layer], oj = a.dem_c[j];
@@ -665,10 +719,22 @@ __global__ __launch_bounds__(256) void style_demod_kernel(const sdfr_style_args 
     const float *mk = a.mods + a.mod_off[layer];
     for (uint32_t b0 = blockIdx.z * kMapB; b0 < a.B; b0 += gridDim.z * kMapB) {
         const uint32_t nb = min(kMapB, a.B - b0);
-        for (uint32_t i = t; i < nb * C; i += 256) {
-            const uint32_t b = i / C, cc = i - b * C;
-            const float m = cc < cin ? mk[(size_t)(b0 + b) * cin + cc] : 0.0f;
-            xs[i] = __fmul_rn(m, m);
+        if ((reinterpret_cast<uintptr_t>(mk) & 15u) == 0 && cin % 4 == 0) {
+            const uint32_t C4 = C / 4;
+#pragma unroll 8
+            for (uint32_t i = t; i < nb * C4; i += 256) {
+                const uint32_t b = i / C4, c4 = i - b * C4;
+                float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (4 * c4 < cin) m = *reinterpret_cast<const float4 *>(mk + (size_t)(b0 + b) * cin + 4 * c4);
+                reinterpret_cast<float4 *>(xs)[i] =
+                    make_float4(__fmul_rn(m.x, m.x), __fmul_rn(m.y, m.y), __fmul_rn(m.z, m.z), __fmul_rn(m.w, m.w));
+            }
+        } else {
+            for (uint32_t i = t; i < nb * C; i += 256) {
+                const uint32_t b = i / C, cc = i - b * C;
+                const float m = cc < cin ? mk[(size_t)(b0 + b) * cin + cc] : 0.0f;
+                xs[i] = __fmul_rn(m, m);
+            }
         }
         __syncthreads();
         float acc[kMapB];
@@ -892,8 +958,9 @@ int sdfr_rgb_finish(float *rgb, const float *partial, uint32_t nparts, const flo
     const float f[4] = {skip ? fir[0] : 0.f, skip ? fir[1] : 0.f, skip ? fir[2] : 0.f,
                         skip ? fir[3] : 0.f};
     if (B * 3 > 65535 || (uint64_t)H * W >= (1ull << 31)) return fail(SDFR_EINVAL, "rgb_finish: too large");
+    if (W % 4) return fail(SDFR_EINVAL, "rgb_finish: W must be a multiple of 4");
     (void)n;
-    rgb_finish_kernel<<<dim3((H * W + 255) / 256, B * 3), 256, 0, (hipStream_t)stream>>>(
+    rgb_finish_kernel<<<dim3((W / 4 + 63) / 64, (H + 3) / 4, B * 3), 256, 0, (hipStream_t)stream>>>(
         rgb, partial, nparts, rgb_b, skip, f[0], f[1], f[2], f[3], B, H, W);
     return check_launch("rgb_finish");
 }

@@ -377,6 +377,33 @@ def test_conv_act_equals_conv_then_epilogue(ops, B, Cin, Cout, H, W, rgb, skip, 
                1e-5 * scale, 1e-6 * scale)
 
 
+@pytest.mark.parametrize("B,H,W,nparts", [(2, 16, 16, 1), (3, 32, 24, 2), (1, 64, 64, 4)])
+def test_rgb_finish_skip_bit_exact(ops, B, H, W, nparts):
+    """sdfr_rgb_finish's closed-form 2x upsampled skip equals skip_up's tap loop (the
+    one sdfr_styled_epilogue runs) bit for bit: with ToRGB weights of zero the epilogue's
+    rgb is bias + skip_up exactly, and rgb_finish of zero partials the same sum."""
+    g = torch.Generator().manual_seed(B * H + W)
+    C = 128
+    conv = torch.randn(B, C, H, W, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    fir = [0.125, 0.375, 0.375, 0.125]
+    rgb_b = torch.randn(3, generator=g).to(DEV)
+    skip = torch.randn(B, 3, H // 2, W // 2, generator=g).to(DEV)
+    _, rgb_ref = ops.styled_epilogue(conv, fir=fir, bias=torch.zeros(C, device=DEV),
+                                     noise_weight=torch.zeros(1, device=DEV), store_y=False,
+                                     rgb_w=torch.zeros(B, 3, C, device=DEV), rgb_b=rgb_b, skip=skip)
+    part = torch.zeros(nparts, B, 3, H, W, device=DEV)
+    got = ops.rgb_finish(part, rgb_b, skip=skip, fir=fir)
+    assert torch.equal(got, rgb_ref)
+    # and the partial sums add in order before the bias
+    part = torch.randn(nparts, B, 3, H, W, generator=g).to(DEV)
+    got = ops.rgb_finish(part, rgb_b, skip=skip, fir=fir)
+    want = part[0]
+    for k in range(1, nparts):
+        want = want + part[k]
+    want = (want + rgb_b[None, :, None, None]) + (rgb_ref - rgb_b[None, :, None, None])
+    torch.testing.assert_close(got, want, rtol=0, atol=2e-6)
+
+
 def test_prepared_fallback_draws_nothing_twice(sdfr):
     """Decoder.forward(prepared=...) falling back to the module path (features that
     require grad) runs on the prep's latent and noise maps: no second draw of the
