@@ -726,11 +726,13 @@ class Generator(nn.Module):
                                               out_im_res=model_opt.renderer_spatial_output_dim)
         if self.full_pipeline:
             self.decoder = Decoder(model_opt, blur_kernel=blur_kernel)
-        # fused inference: decoder style prep on a side stream beside the renderer.
-        # Off by default: measured in one process (scripts/overlap_ab.py,
-        # profiles/round3_overlap_ab.json) it saves 0.04 ms of 11.4 per 32 faces, within
-        # noise, and slows the hash-grid gather beside it (0.774 -> 0.801 ms)
-        self.overlap_decoder_prep = False
+        # fused inference: decoder prep (its mapping network, noise, modulations and
+        # demodulations) on a side stream beside the renderer.  Round 3 measured it
+        # within noise (profiles/round3_overlap_ab.json: the gather beside it slowed
+        # 0.774 -> 0.801 ms); since the prep's small kernels were shortened in round 5
+        # it is +0.8 % at 32 faces (3251 -> 3278 faces/s, six interleaved samples each,
+        # scripts/overlap_b32.py) and neutral at one face, so it is on by default
+        self.overlap_decoder_prep = True
         self._dec_key = None
 
     def _decoder_weights_unchanged(self):
