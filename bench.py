@@ -262,8 +262,10 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # per-step stage events on the renderer's stream
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    # per-step stage events on the renderer's stream: [0] entry, [1] before / [2] after
+    # the hash-grid gather, [3] after the field kernel, [4] right before it (after the
+    # FiLM prep, which the renderer enqueues behind the gather: ABI 11)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
     for e4 in evs:
         for e in e4:
             e.record()              # materialise the event handles before the timed loop
@@ -284,17 +286,19 @@ def main():
     def set_events(k):
         if k > 0:
             conv_flops.append(g.decoder.conv_flops)
-        g.renderer.stage_events = evs[k]
+        g.renderer.stage_events = evs[k][:4]
+        g.renderer.field_event = evs[k][4]
         g.decoder.profile_convs(dev_evs[k])
     elapsed = timed_steps(step, args.steps, world, device, before_step=set_events)
     conv_flops.append(g.decoder.conv_flops)
     n_conv = g.decoder._conv_ev
     g.renderer.stage_events = None
+    g.renderer.field_event = None
     g.decoder.profile_convs(None)
 
     conv_ms = sum(a_.elapsed_time(b_) for pairs in dev_evs for a_, b_ in pairs[:n_conv]) / args.steps
     enc_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    field_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
+    field_ms = sum(e[4].elapsed_time(e[3]) for e in evs) / args.steps
     render_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args.steps
     samples = B * res * res * N
     f16x3 = args.field_precision == "f16x3"
@@ -426,18 +430,20 @@ def main():
             g.renderer.field_precision = "fp32"
             for _ in range(2):
                 step()
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
             for e in ev:
                 e.record()          # materialise the handles (as for the timed steps)
             torch.cuda.synchronize()
-            g.renderer.stage_events = ev
+            g.renderer.stage_events = ev[:4]
+            g.renderer.field_event = ev[4]
             t0 = time.perf_counter()
             step()
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             g.renderer.stage_events = None
+            g.renderer.field_event = None
             g.renderer.field_precision = args.field_precision
-            f32_ms = ev[2].elapsed_time(ev[3])
+            f32_ms = ev[4].elapsed_time(ev[3])
             # ngp_field_kernel runs the uncomposed network (input_linear, then
             # pts_linears.0): the reference's 550,912 FLOP/sample
             line["extras"]["fp32_field"] = {

@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 10
+#define SDFR_ABI_VERSION 11
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -163,8 +163,8 @@ typedef struct sdfr_ngp_render_args {
     void *workspace;              /* >= sdfr_render_ngp_workspace_bytes()          */
     size_t workspace_bytes;
     /* Optional hipEvent_t handles (NULL = skip), recorded on `stream`:
-     * [0] before the prep kernel, [1] before the hash-grid kernel,
-     * [2] before the field (MLP + compositing) kernel, [3] after it. */
+     * [0] at entry, [1] before the hash-grid kernel, [2] after it (ngp f16x3;
+     * before the FiLM prep), [3] after the field (MLP + compositing) kernel. */
     void *stage_events[4];
     /* Field-stage GEMM arithmetic (both accumulate in fp32):
      * SDFR_FIELD_F16X3 (0, default) three v_mfma_f32_16x16x32_f16 per tile on a
@@ -184,6 +184,13 @@ typedef struct sdfr_ngp_render_args {
      * differences).  1 disables the split; 2 or 4 otherwise.  The workspace size
      * (sdfr_render_ngp_workspace_bytes) covers the default bound. */
     uint32_t max_field_segments;
+    /* ABI 11.  styles_event: NULL, or a hipEvent_t that `stream` waits on before the
+     * first use of `styles` (the FiLM prep; the ngp f16x3 path enqueues the sample
+     * geometry and the hash-grid gather ahead of that wait, so a caller may still be
+     * computing the styles on another stream).  field_event: NULL, or a hipEvent_t
+     * recorded right before the field kernel (after the FiLM prep). */
+    void *styles_event;
+    void *field_event;
 } sdfr_ngp_render_args;
 
 #define SDFR_FIELD_F16X3 0

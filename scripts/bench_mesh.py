@@ -33,10 +33,11 @@ def main(reps=5):
         g.renderer.rng_device = "device"
         ext, focal, near, far, _ = sdfr.generate_camera_params(res, dev, batch=1)
         z = torch.randn(1, 256, device=dev)
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
         for e in evs:
             e.record()
-        g.renderer.stage_events = evs
+        g.renderer.stage_events = evs[:4]
+        g.renderer.field_event = evs[4]          # right before the field kernel
         times, field = [], []
         with torch.no_grad():
             for r in range(reps + 1):
@@ -47,10 +48,11 @@ def main(reps=5):
                 torch.cuda.synchronize()
                 if r:
                     times.append(time.perf_counter() - t0)
-                    field.append(evs[2].elapsed_time(evs[3]))
+                    field.append(evs[4].elapsed_time(evs[3]))
         ms = sorted(times)[len(times) // 2] * 1e3
         fms = sorted(field)[len(field) // 2]
         g.renderer.stage_events = None
+        g.renderer.field_event = None
         mtimes = []
         with torch.no_grad():
             for r in range(reps + 1):

@@ -23,17 +23,18 @@ torch.manual_seed(0)
 g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
 ren = g.renderer; ren.rng_device = "device"; ren.field_precision = sys.argv[2]
 ext, focal, near, far, _ = sdfr.generate_camera_params(64, dev, batch=B)
-evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+evs = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
 for e in evs: e.record()
 ts = []
 with torch.no_grad():
     lat = g.style(torch.randn(B, 256, device=dev))
     for r in range(8):
-        ren.stage_events = evs
+        ren.stage_events = evs[:4]
+        ren.field_event = evs[4]                  # right before the field kernel
         torch.manual_seed(5)
         out = ren(ext, focal, near, far, styles=lat)
         torch.cuda.synchronize()
-        if r >= 2: ts.append(evs[2].elapsed_time(evs[3]))
+        if r >= 2: ts.append(evs[4].elapsed_time(evs[3]))
 med = statistics.median(ts)
 import hashlib
 h = hashlib.sha1(b"".join(t.detach().float().cpu().numpy().tobytes() for t in out[:2])).hexdigest()[:12]

@@ -2284,9 +2284,11 @@ int sdfr_render_fc_forward(const sdfr_fc_weights *w, const sdfr_ngp_render_args 
     GeomArgs g;
     fill_geom_args(a, 1.0f, g);
     record_event(a->stage_events[0], st);
+    wait_event(a->styles_event, st);
     if ((rc = launch_xprep<FcNet>(P, a, ws + o_x, film, st))) return rc;
     record_event(a->stage_events[1], st);
     record_event(a->stage_events[2], st);
+    record_event(a->field_event, st);
     if ((rc = launch_xfield<FcNet>(P, a, g, nullptr, ws + o_x, film, st,
                                    reinterpret_cast<float *>(ws + o_part))))
         return rc;
@@ -2323,9 +2325,11 @@ int sdfr_render_siren_forward(const sdfr_siren_weights *w, const sdfr_ngp_render
     GeomArgs g;
     fill_geom_args(a, 1.0f, g);
     record_event(a->stage_events[0], st);
+    wait_event(a->styles_event, st);
     if ((rc = launch_xprep<SirenNet>(P, a, ws + o_x, film, st))) return rc;
     record_event(a->stage_events[1], st);
     record_event(a->stage_events[2], st);
+    record_event(a->field_event, st);
     if ((rc = launch_xfield<SirenNet>(P, a, g, nullptr, ws + o_x, film, st))) return rc;
     record_event(a->stage_events[3], st);
     return SDFR_OK;

@@ -143,6 +143,8 @@ uint32_t field_nseg(uint32_t B, uint32_t tiles_per_face, uint32_t N, int force_b
 size_t field_part_bytes(uint32_t B, uint32_t tiles_per_face, uint32_t N);
 void fill_geom_args(const sdfr_ngp_render_args *a, float bound, GeomArgs &g);
 void record_event(void *ev, hipStream_t st);
+// stream waits on a caller's hipEvent_t (NULL: nothing)
+void wait_event(void *ev, hipStream_t st);
 
 // LDS-DMA: buffer resource over [base, base + bytes) (range-checked: offsets past
 // it read zeros) and one 64-lane x 16-B piece from (voff + soff) to the LDS byte

@@ -891,6 +891,10 @@ void record_event(void *ev, hipStream_t st) {
     if (ev) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev), st);
 }
 
+void wait_event(void *ev, hipStream_t st) {
+    if (ev) (void)hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(ev), 0);
+}
+
 #ifdef SDFR_ABLATION
 static int g_field_variant = 0;   // profiling ablations only (see ABL_*)
 int field_variant() { return g_field_variant; }
@@ -1099,22 +1103,28 @@ int sdfr_render_ngp_forward(const sdfr_ngp_weights *w, const sdfr_ngp_render_arg
     fill_geom(w, a, g);
     record_event(a->stage_events[0], st);
     if (a->field_precision == SDFR_FIELD_F16X3) {
-        if ((rc = launch_xprep_ngp(w, a, ws + o_x, film, st))) return rc;
+        // geometry and gather first (they do not read the styles), then the wait on
+        // the caller's styles (ABI 11), the FiLM prep and the field kernel
         float2 *zd = reinterpret_cast<float2 *>(ws + o_zd);
         if ((rc = launch_geom(g, zd, gu, st))) return rc;
         record_event(a->stage_events[1], st);                  // the encode stage is the gather alone
         if ((rc = launch_encode(w, a, g, enc, gu, st))) return rc;
         record_event(a->stage_events[2], st);
+        wait_event(a->styles_event, st);
+        if ((rc = launch_xprep_ngp(w, a, ws + o_x, film, st))) return rc;
+        record_event(a->field_event, st);
         float *part = reinterpret_cast<float *>(ws + o_part);
         if ((rc = launch_xfield_ngp(w, a, g, enc, ws + o_x, film, st, part, zd))) return rc;
         record_event(a->stage_events[3], st);
         return SDFR_OK;
     }
+    wait_event(a->styles_event, st);
     if ((rc = launch_prep(w, a, packed, film, st))) return rc;
     if ((rc = launch_geom(g, nullptr, gu, st))) return rc;
     record_event(a->stage_events[1], st);
     if ((rc = launch_encode(w, a, g, enc, gu, st))) return rc;
     record_event(a->stage_events[2], st);
+    record_event(a->field_event, st);
 
     FieldArgs f;
     f.g = g;

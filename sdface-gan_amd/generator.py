@@ -779,47 +779,62 @@ class Generator(nn.Module):
                 inject_index=None, truncation=1, truncation_latent=None, input_is_latent=False,
                 noise=None, randomize_noise=True, return_sdf=False, return_xyz=False,
                 return_eikonal=False, project_noise=False, mesh_path=None, t_rand=None):
-        with torch.set_grad_enabled(self.is_train and self.train_renderer):
-            latent = self.styles_and_noise_forward(styles, inject_index, truncation,
-                                                   truncation_latent, input_is_latent)
+        grad_on = self.is_train and self.train_renderer
         # Fused inference: the decoder's feature-independent prep (its mapping network,
         # noise maps, per-layer modulations / demodulations: ~12 small launches) runs
         # before the renderer -- on a side stream beside it while the decoder's weight
         # caches are warm (weights unchanged since the previous call), else in order
         # on this stream, so the caches a weight update rebuilds, and the ones it
-        # frees, never cross streams.  Either way the device RNG is drawn in the same
-        # order (decoder noise, then the renderer's sampling offsets).
-        prepared, side = None, None
+        # frees, never cross streams.  On the side stream the renderer's own mapping
+        # network goes there too: the renderer enqueues its sample geometry and hash-grid
+        # gather (which do not read the styles) ahead of its wait on `styles_ev` (ABI 11).
+        # Either way the device RNG is drawn in the same order (decoder noise, then the
+        # renderer's sampling offsets).
+        prepared, side, styles_ev = None, None, None
+        B, dev = cam_poses.shape[0], cam_poses.device
+        kw = dict(noise=noise, inject_index=inject_index, truncation=truncation,
+                  truncation_latent=truncation_latent, input_is_latent=input_is_latent,
+                  randomize_noise=randomize_noise)
         # features needing grad (renderer trained, or latents requiring grad) take the
         # decoder's autograd path: no prep then (Decoder.forward re-checks as well)
-        render_grad = (self.is_train and self.train_renderer) and (
+        pre_grad = grad_on and (
             any(p.requires_grad for p in self.renderer.parameters())
-            or any(s.requires_grad for s in latent))
-        if (self.full_pipeline and cam_poses.is_cuda and not project_noise and not render_grad
-                and self.decoder.fused_ready(cam_poses.device)):
-            kw = dict(noise=noise, inject_index=inject_index, truncation=truncation,
-                      truncation_latent=truncation_latent, input_is_latent=input_is_latent,
-                      randomize_noise=randomize_noise)
-            B, dev = cam_poses.shape[0], cam_poses.device
-            # (a small eager batch is host-bound: the stream switch would cost more than
-            # the overlap saves; inside a graph capture it costs nothing at replay)
-            if (self.overlap_decoder_prep and (B >= 8 or torch.cuda.is_current_stream_capturing())
-                    and self._decoder_weights_unchanged()):
-                main = torch.cuda.current_stream(dev)
-                side = self._side_stream(dev)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    prepared = self.decoder.prepare_fused(latent, B, dev, **kw)
-                if not torch.cuda.is_current_stream_capturing():
-                    for t in _tensors_of(prepared):
-                        t.record_stream(main)        # made on `side`, used on `main`
-            else:
+            or any(p.requires_grad for p in self.style.parameters())
+            or any(s.requires_grad for s in styles))
+        capturing = cam_poses.is_cuda and torch.cuda.is_current_stream_capturing()
+        # (a small eager batch is host-bound: the stream switch would cost more than
+        # the overlap saves; inside a graph capture it costs nothing at replay)
+        if (self.full_pipeline and cam_poses.is_cuda and not project_noise and not pre_grad
+                and self.overlap_decoder_prep and (B >= 8 or capturing)
+                and self.decoder.fused_ready(dev) and self._decoder_weights_unchanged()):
+            main = torch.cuda.current_stream(dev)
+            side = self._side_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                with torch.set_grad_enabled(grad_on):
+                    latent = self.styles_and_noise_forward(styles, inject_index, truncation,
+                                                           truncation_latent, input_is_latent)
+                styles_ev = torch.cuda.Event()
+                styles_ev.record(side)
                 prepared = self.decoder.prepare_fused(latent, B, dev, **kw)
-        with torch.set_grad_enabled(self.is_train and self.train_renderer):
+            if not capturing:
+                for t in list(_tensors_of(prepared)) + list(_tensors_of(latent)):
+                    t.record_stream(main)            # made on `side`, used on `main`
+        else:
+            with torch.set_grad_enabled(grad_on):
+                latent = self.styles_and_noise_forward(styles, inject_index, truncation,
+                                                       truncation_latent, input_is_latent)
+            render_grad = grad_on and (
+                any(p.requires_grad for p in self.renderer.parameters())
+                or any(s.requires_grad for s in latent))
+            if (self.full_pipeline and cam_poses.is_cuda and not project_noise and not render_grad
+                    and self.decoder.fused_ready(dev)):
+                prepared = self.decoder.prepare_fused(latent, B, dev, **kw)
+        with torch.set_grad_enabled(grad_on):
             lat0 = latent[0][:, 0] if input_is_latent else latent[0]
             thumb_rgb, features, sdf, mask, xyz, eikonal_term = self.renderer(
                 cam_poses, focals, near, far, styles=lat0, return_eikonal=return_eikonal,
-                t_rand=t_rand)
+                t_rand=t_rand, styles_event=styles_ev)
         if self.full_pipeline:
             if side is not None:
                 torch.cuda.current_stream(cam_poses.device).wait_stream(side)

@@ -345,6 +345,7 @@ class VolumeFeatureRenderer(nn.Module):
         # optional 4 torch.cuda.Event(enable_timing=True) recorded around the
         # fused stages (prep | hash grid | field | end), see include/sdfr.h
         self.stage_events = None
+        self.field_event = None        # hipEvent recorded right before the field kernel
         # upper bound on the per-ray sample segments of the fused field stage at small
         # batches (0 = the library default 4; 1 = whole rays), include/sdfr.h
         self.max_field_segments = 0
@@ -592,11 +593,20 @@ class VolumeFeatureRenderer(nn.Module):
             if not p.is_contiguous() or p.dtype != torch.float32:
                 raise RuntimeError("fused ngp renderer needs contiguous fp32 parameters")
 
-    def fused_forward(self, cam_poses, focal, near, far, styles, t_rand=None, encode_only=False):
+    def fused_forward(self, cam_poses, focal, near, far, styles, t_rand=None, encode_only=False,
+                      styles_event=None):
         """The whole ngp render on libsdfr (no autograd).  Returns the same tuple
-        as ``forward`` (rgb, features, sdf, mask, xyz, None)."""
+        as ``forward`` (rgb, features, sdf, mask, xyz, None).  ``styles_event``: a
+        torch.cuda.Event after which ``styles`` is ready (computed on another
+        stream): the library enqueues the sample geometry and the hash-grid gather
+        before its wait on it (ABI 11)."""
         self._fused_check_params()
         dev = cam_poses.device
+        if styles_event is not None and not (styles.dtype == torch.float32
+                                             and styles.is_contiguous()):
+            # a conversion would read the styles on this stream: wait here instead
+            torch.cuda.current_stream(dev).wait_event(styles_event)
+            styles_event = None
         B = cam_poses.shape[0]
         H = W = self.out_im_res
         N = self.N_samples
@@ -660,6 +670,10 @@ class VolumeFeatureRenderer(nn.Module):
         if self.stage_events is not None:
             for k, ev in enumerate(self.stage_events):
                 a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)
+        if self.field_event is not None:
+            a.field_event = ctypes.c_void_p(self.field_event.cuda_event)
+        if styles_event is not None:
+            a.styles_event = ctypes.c_void_p(styles_event.cuda_event)
         if self.field_precision == "f16x3":
             a.prepacked = _lib.ptr(self._prepacked(kind, cam))
         if kind:
@@ -698,9 +712,12 @@ class VolumeFeatureRenderer(nn.Module):
 
     # ---------------------------------------------------------------- API
     def forward(self, cam_poses, focal, near, far, styles=None, return_eikonal=False,
-                t_rand=None):
+                t_rand=None, styles_event=None):
         if self._fused_ok(cam_poses, styles, return_eikonal):
-            return self.fused_forward(cam_poses, focal, near, far, styles, t_rand=t_rand)
+            return self.fused_forward(cam_poses, focal, near, far, styles, t_rand=t_rand,
+                                      styles_event=styles_event)
+        if styles_event is not None:
+            torch.cuda.current_stream(cam_poses.device).wait_event(styles_event)
         rgb, features, sdf, mask, xyz, eikonal_term = self.render(
             focal, c2w=cam_poses, near=near, far=far, styles=styles,
             return_eikonal=return_eikonal, t_rand=t_rand)
