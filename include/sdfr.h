@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 11
+#define SDFR_ABI_VERSION 12
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -191,6 +191,12 @@ typedef struct sdfr_ngp_render_args {
      * recorded right before the field kernel (after the FiLM prep). */
     void *styles_event;
     void *field_event;
+    /* ABI 12 (f16x3 ngp / FC only): NULL, or [B,H,W,32,2,8] fp16 -- the features
+     * times features_mod[b,c] in the decoder's split-NHWC layout (hi / lo halves of
+     * each 8-channel group, sdfr_modulate_to_nhwc_split's output, bit for bit), written
+     * instead of the NCHW `features` (which must then be NULL). */
+    void *features_split;
+    const float *features_mod;    /* [B,256] with features_split                    */
 } sdfr_ngp_render_args;
 
 #define SDFR_FIELD_F16X3 0

@@ -23,7 +23,7 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 11
+ABI_VERSION = 12
 FIELD_F16X3 = 0
 FIELD_FP32 = 1
 
@@ -108,6 +108,7 @@ class NgpRenderArgs(ctypes.Structure):
         ("stage_events", _vp * 4), ("field_precision", _int), ("prepacked", _vp),
         ("max_field_segments", _u32),
         ("styles_event", _vp), ("field_event", _vp),
+        ("features_split", _vp), ("features_mod", _vp),
     ]
 
 

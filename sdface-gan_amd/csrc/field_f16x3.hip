@@ -395,6 +395,8 @@ struct XFieldArgs {
     const float *sigma_noise;      // [B,H,W,N] or null (no_sdf only)
     int force_background, with_sdf;
     float *rgb, *features, *sdf, *xyz, *mask;
+    _Float16 *feat_split;          // or the features x feat_mod in split-NHWC (ABI 12)
+    const float *feat_mod;         // [B][256]
     uint32_t nseg;                 // sample segments per ray (1: whole rays, no merge)
     float *part;                   // nseg > 1: [nseg][kPartQ][rays] segment partials
 };
@@ -1327,6 +1329,38 @@ __device__ __forceinline__ float row_pair_sum(float pa, float pb) {
     return __fadd_rn(__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1));
 }
 
+// Round-to-nearest hi / lo fp16 split of channels c .. c + 3 of an 8-channel group held
+// by lane half h (lanes l, l ^ 32 hold channels 0-3 and 4-7) into split-NHWC
+// ([pixel][C / 8][hi 8, lo 8]; idx8 = NHWC element index of the group's channel 0): one
+// v_permlane32_swap per dword gives lane h = 0 both hi halves and lane h = 1 both lo
+// halves, so each lane issues one 16-B store.  Both lanes of a pair must execute it.
+// (integer operands, results pinned as for row_pair_sum)
+typedef _Float16 h4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_split8_pair32(_Float16 *ys, size_t idx8, f4 v, uint32_t h) {
+    // v pinned: hipcc otherwise folds the caller's fp32 product into the fp16 conversion
+    // (v_fma_mixlo_f16: one rounding instead of modulate_nhwc_kernel's two -- a tie of
+    // the fp32 product then rounds the other way)
+    asm volatile("" : "+v"(v));
+    h4f hi, lo;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        hi[r] = (_Float16)v[r];
+        lo[r] = (_Float16)(v[r] - (float)hi[r]);
+    }
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    const u2 hd = __builtin_bit_cast(u2, hi), ld = __builtin_bit_cast(u2, lo);
+    uint32_t q[4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(hd[k], ld[k], false, false);
+        uint32_t r0 = sw[0], r1 = sw[1];
+        asm volatile("" : "+v"(r0), "+v"(r1));
+        q[k] = r0;          // h = 0: own hi / h = 1: partner's lo
+        q[2 + k] = r1;      // h = 0: partner's hi / h = 1: own lo
+    }
+    *reinterpret_cast<f4 *>(ys + 2 * idx8 + (h ? 8 : 0)) = __builtin_bit_cast(f4, q);
+}
+
 // Element e of FCGenerator.transform_points (sdf_model.py:1628-1640) of ph = p / 2:
 // e = 6 i + r, sin (r < 3) or cos (r >= 3) of (2^i pi) ph[r mod 3], with the reference's
 // fp32 argument RN(RN32(2^i pi) ph) (a Python float times an fp32 tensor).  The sine of
@@ -1843,7 +1877,7 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
     if (a.nseg > 1) {
         const size_t Rr = (size_t)G.total_tiles * kTileRays;
         float *pp = a.part + (size_t)seg * kPartQ * Rr + (size_t)tile * kTileRays + r16;
-        if (a.features) {
+        if (a.features || a.feat_split) {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -1885,6 +1919,21 @@ __global__ void __launch_bounds__(kRThreads, 1) field_r_kernel(const XFieldArgs 
 #pragma unroll
                 for (int r = 0; r < 4; ++r) fbp[(size_t)(jf + r) * HW] = v[r];
             }
+    } else if (a.feat_split) {
+        // the decoder's first input directly: v * mod[b, c] split hi / lo (fp32 product and
+        // RN splits as modulate_nhwc_kernel); lanes h = 0, 1 (lane ^ 32) hold channels
+        // 0-3 and 4-7 of an 8-channel group: one permlane32 swap per dword gives lane
+        // h = 0 the group's 8 hi halves and lane h = 1 its 8 lo halves, one 16-B store each
+        const float *fm = a.feat_mod + (size_t)b * kW;
+        const size_t P = (size_t)b * HW + pix;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int bq = 0; bq < 4; ++bq) {
+                const uint32_t jf = 32 * (tb + t) + 8 * bq + 4 * h;
+                const f4 v = facc[(4 * t + bq) * 64] * *reinterpret_cast<const f4 *>(fm + jf);
+                store_split8_pair32(a.feat_split, P * kW + (jf & ~7u), v, h);
+            }
     }
 }
 
@@ -1900,7 +1949,9 @@ __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
     const size_t HW = (size_t)G.H * G.W;
     if (ray_local >= HW) return;
     float *dst;
-    if (q < kW) dst = a.features ? a.features + ((size_t)b * kW + q) * HW + ray_local : nullptr;
+    float fsplit = 0.0f;                                 // (any non-null marker)
+    if (q < kW) dst = a.features ? a.features + ((size_t)b * kW + q) * HW + ray_local
+                                 : (a.feat_split ? &fsplit : nullptr);
     else if (q < kW + 3) dst = a.rgb + ((size_t)b * 3 + (q - kW)) * HW + ray_local;
     else if (q < kW + 6) dst = a.xyz ? a.xyz + ((size_t)b * 3 + (q - kW - 3)) * HW + ray_local
                                      : nullptr;
@@ -1916,6 +1967,15 @@ __global__ void __launch_bounds__(256) field_merge_kernel(const XFieldArgs a) {
         Tp = __fmul_rn(Tp, pp[k * segq + (size_t)(kW + 6) * R]);
     }
     if (q >= kW && q < kW + 3) acc = __fadd_rn(-1.0f, __fmul_rn(2.0f, acc));
+    if (dst == &fsplit) {                                // split-NHWC, times the modulation
+        float v = __fmul_rn(acc, a.feat_mod[(size_t)b * kW + q]);
+        asm volatile("" : "+v"(v));      // (no v_fma_mix fold of the product: see above)
+        const _Float16 hv = (_Float16)v, lv = (_Float16)(v - (float)hv);
+        const size_t o = 2 * (((size_t)b * HW + ray_local) * kW + (q & ~7u)) + (q & 7u);
+        a.feat_split[o] = hv;
+        a.feat_split[o + 8] = lv;
+        return;
+    }
     *dst = acc;
 }
 
@@ -2066,10 +2126,15 @@ static int launch_xfield(const NetPtrs &P, const sdfr_ngp_render_args *a, const 
     f.with_sdf = a->with_sdf;
     f.rgb = a->rgb;
     f.features = a->features;
+    f.feat_split = reinterpret_cast<_Float16 *>(a->features_split);
+    f.feat_mod = a->features_mod;
     f.sdf = a->sdf;
     f.xyz = a->xyz;
     f.mask = a->mask;
     f.part = part;
+    if (f.feat_split && (!f.feat_mod || f.features || !Net::kFieldR))
+        return fail(SDFR_EUNSUPPORTED, "render: features_split needs features_mod, no NCHW "
+                                       "features, and the ngp / FC field kernel");
     // field_r_kernel for ngp; the SIREN net (nine FiLM layers, no encode stage, no
     // sample-segment split) keeps field_p_kernel, 6 % faster on it (7.76 vs 8.25 ms per
     // 32 faces, interleaved A/B on one box; field_r_kernel is 3.5 % faster on ngp)

@@ -845,6 +845,12 @@ static int validate(const sdfr_ngp_weights *w, const sdfr_ngp_render_args *a) {
         if (!p) return fail(SDFR_EINVAL, "render_ngp: weight pointer is null");
     if (a->with_sdf && !w->sigmoid_beta)
         return fail(SDFR_EINVAL, "render_ngp: sigmoid_beta is required when with_sdf");
+    if (a->features_split) {
+        if (a->field_precision != SDFR_FIELD_F16X3)
+            return fail(SDFR_EUNSUPPORTED, "render_ngp: features_split needs the f16x3 field");
+        if (a->features || !a->features_mod)
+            return fail(SDFR_EINVAL, "render_ngp: features_split takes features_mod and no features");
+    }
     for (int l = 0; l < 3; ++l)
         if (!w->pts_w[l] || !w->pts_b[l] || !w->pts_gw[l] || !w->pts_gb[l] || !w->pts_bw[l] ||
             !w->pts_bb[l])

@@ -617,7 +617,13 @@ class Decoder(nn.Module):
             noise = self._fused_noise(noise, B, features.device, features.dtype)
             sty = self._fused_styles(latent, seq, split)
         mods, rgb_mods, demods = sty
-        x = (modulate_to_nhwc_split if split[0] else modulate_to_nhwc)(features, mods[0])
+        if features.dtype == torch.float16 and features.dim() == 6:
+            # the renderer wrote features * mods[0] in the split layout already (ABI 12)
+            if not split[0]:
+                raise RuntimeError("decoder: split-NHWC features for a non-split first layer")
+            x = features
+        else:
+            x = (modulate_to_nhwc_split if split[0] else modulate_to_nhwc)(features, mods[0])
         rgb = None
         for i, sc in enumerate(seq):
             mc = sc.conv
@@ -733,6 +739,9 @@ class Generator(nn.Module):
         # it is +0.8 % at 32 faces (3251 -> 3278 faces/s, six interleaved samples each,
         # scripts/overlap_b32.py) and neutral at one face, so it is on by default
         self.overlap_decoder_prep = True
+        # the field kernel stores the decoder's first input (features x modulation,
+        # split-NHWC) instead of NCHW features for modulate_nhwc_kernel to convert
+        self.fuse_feature_split = True
         self._dec_key = None
 
     def _decoder_weights_unchanged(self):
@@ -814,9 +823,10 @@ class Generator(nn.Module):
                 with torch.set_grad_enabled(grad_on):
                     latent = self.styles_and_noise_forward(styles, inject_index, truncation,
                                                            truncation_latent, input_is_latent)
+                prepared = self.decoder.prepare_fused(latent, B, dev, **kw)
+                # (after the prep: the field kernel also reads its first modulation)
                 styles_ev = torch.cuda.Event()
                 styles_ev.record(side)
-                prepared = self.decoder.prepare_fused(latent, B, dev, **kw)
             if not capturing:
                 for t in list(_tensors_of(prepared)) + list(_tensors_of(latent)):
                     t.record_stream(main)            # made on `side`, used on `main`
@@ -830,11 +840,19 @@ class Generator(nn.Module):
             if (self.full_pipeline and cam_poses.is_cuda and not project_noise and not render_grad
                     and self.decoder.fused_ready(dev)):
                 prepared = self.decoder.prepare_fused(latent, B, dev, **kw)
+        # the fused decoder's first layer input (features x its modulation, split-NHWC)
+        # straight from the field kernel's feature store (ABI 12): one streaming pass less
+        # (from 4 faces: below that the field kernel splits rays into segments and the
+        # merge kernel would scatter 2-B split stores instead of coalesced NCHW rows)
+        feat_mod = None
+        if (prepared is not None and self.fuse_feature_split and B >= 4
+                and self.decoder._conv_x(self.decoder.conv1.conv)):
+            feat_mod = prepared[2][0][0]
         with torch.set_grad_enabled(grad_on):
             lat0 = latent[0][:, 0] if input_is_latent else latent[0]
             thumb_rgb, features, sdf, mask, xyz, eikonal_term = self.renderer(
                 cam_poses, focals, near, far, styles=lat0, return_eikonal=return_eikonal,
-                t_rand=t_rand, styles_event=styles_ev)
+                t_rand=t_rand, styles_event=styles_ev, feat_mod=feat_mod)
         if self.full_pipeline:
             if side is not None:
                 torch.cuda.current_stream(cam_poses.device).wait_stream(side)

@@ -594,12 +594,15 @@ class VolumeFeatureRenderer(nn.Module):
                 raise RuntimeError("fused ngp renderer needs contiguous fp32 parameters")
 
     def fused_forward(self, cam_poses, focal, near, far, styles, t_rand=None, encode_only=False,
-                      styles_event=None):
+                      styles_event=None, feat_mod=None):
         """The whole ngp render on libsdfr (no autograd).  Returns the same tuple
         as ``forward`` (rgb, features, sdf, mask, xyz, None).  ``styles_event``: a
         torch.cuda.Event after which ``styles`` is ready (computed on another
         stream): the library enqueues the sample geometry and the hash-grid gather
-        before its wait on it (ABI 11)."""
+        before its wait on it (ABI 11).  ``feat_mod`` [B,256] (ngp / FC f16x3): the
+        features come back as features * feat_mod in the decoder's split-NHWC fp16
+        layout [B,H,W,32,2,8] (ABI 12; sdfr_modulate_to_nhwc_split's output, bit for bit)
+        instead of NCHW fp32."""
         self._fused_check_params()
         dev = cam_poses.device
         if styles_event is not None and not (styles.dtype == torch.float32
@@ -628,11 +631,17 @@ class VolumeFeatureRenderer(nn.Module):
         if not self.with_sdf and self.raw_noise_std > 0:
             noise = torch.randn(B, H, W, N, device=dev) * self.raw_noise_std
         rgb = torch.empty(B, 3, H, W, device=dev)
-        features = torch.empty(B, 256, H, W, device=dev) if self.output_features else None
+        kind = self._net_kind()
+        if feat_mod is not None and (kind == 1 or self.field_precision != "f16x3"
+                                     or not self.output_features):
+            feat_mod = None                      # SIREN / fp32 field: NCHW features
+        features = (torch.empty(B, 256, H, W, device=dev)
+                    if self.output_features and feat_mod is None else None)
+        feat_split = (torch.empty(B, H, W, 32, 2, 8, device=dev, dtype=torch.float16)
+                      if feat_mod is not None else None)
         sdf = torch.empty(B, H, W, N, 1, device=dev) if self.return_sdf else None
         xyz = torch.empty(B, 3, H, W, device=dev) if self.return_xyz else None
         mask = torch.empty(B, 1, H, W, device=dev) if self.return_xyz else None
-        kind = self._net_kind()
         siren = kind == 1
         if kind == 2:
             ws_bytes = _lib.lib().sdfr_render_fc_workspace_bytes(B, H, W, N)
@@ -674,6 +683,10 @@ class VolumeFeatureRenderer(nn.Module):
             a.field_event = ctypes.c_void_p(self.field_event.cuda_event)
         if styles_event is not None:
             a.styles_event = ctypes.c_void_p(styles_event.cuda_event)
+        if feat_split is not None:
+            feat_mod = feat_mod.detach().float().contiguous()
+            a.features_split, a.features_mod = _lib.ptr(feat_split), _lib.ptr(feat_mod)
+            features = feat_split
         if self.field_precision == "f16x3":
             a.prepacked = _lib.ptr(self._prepacked(kind, cam))
         if kind:
@@ -712,10 +725,11 @@ class VolumeFeatureRenderer(nn.Module):
 
     # ---------------------------------------------------------------- API
     def forward(self, cam_poses, focal, near, far, styles=None, return_eikonal=False,
-                t_rand=None, styles_event=None):
+                t_rand=None, styles_event=None, feat_mod=None):
+        """``feat_mod``: see fused_forward (the module path returns NCHW features)."""
         if self._fused_ok(cam_poses, styles, return_eikonal):
             return self.fused_forward(cam_poses, focal, near, far, styles, t_rand=t_rand,
-                                      styles_event=styles_event)
+                                      styles_event=styles_event, feat_mod=feat_mod)
         if styles_event is not None:
             torch.cuda.current_stream(cam_poses.device).wait_event(styles_event)
         rgb, features, sdf, mask, xyz, eikonal_term = self.render(

@@ -561,6 +561,52 @@ def test_graft_entry_smoke():
     __graft_entry__.smoke()
 
 
+@pytest.mark.parametrize("B,fc", [(8, False), (4, True)])
+def test_feature_split_store_matches_modulate_pass(sdfr, B, fc):
+    """Generator.forward with the field kernel writing the decoder's first input
+    (features x modulation in split-NHWC, ABI 12) gives the images of the NCHW features
+    + modulate_nhwc path bit for bit (same fp32 product, same round-to-nearest hi / lo
+    split; the product pinned so hipcc cannot fold it into a one-rounding v_fma_mix)."""
+    dev = torch.device("cuda", 0)
+    opt = sdfr.vol_render_opt(ngp=not fc, fc=fc)
+    torch.manual_seed(7)
+    g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
+    g.renderer.rng_device = "device"
+    z = torch.randn(B, 256, device=dev)
+    cam, focal, near, far, _ = sdfr.generate_camera_params(64, dev, batch=B)
+    outs = []
+    for split in (False, True, True):
+        g.fuse_feature_split = split
+        torch.cuda.manual_seed(31)
+        with torch.no_grad():
+            outs.append(g([z], cam, focal, near, far))
+    torch.cuda.synchronize()
+    for rgb, thumb in outs[1:]:
+        assert torch.equal(rgb, outs[0][0]) and torch.equal(thumb, outs[0][1])
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_feature_split_store_through_segment_merge(sdfr, B):
+    """The split-NHWC feature store of the segment-merge kernel (small batches, where
+    the Generator keeps the NCHW path) equals sdfr_modulate_to_nhwc_split of the NCHW
+    features of the same render, bit for bit."""
+    from sdface_gan_amd import decoder_ops as ops
+    dev = torch.device("cuda", 0)
+    opt = sdfr.vol_render_opt()
+    torch.manual_seed(9)
+    g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()
+    ren = g.renderer
+    cam, focal, near, far, _ = sdfr.generate_camera_params(64, dev, batch=B)
+    lat = torch.randn(B, 256, device=dev)
+    mod = torch.rand(B, 256, device=dev) + 0.5
+    tr = torch.rand(B, 64, 64, device=dev)
+    with torch.no_grad():
+        o1 = ren.fused_forward(cam, focal, near, far, lat, t_rand=tr)
+        o2 = ren.fused_forward(cam, focal, near, far, lat, t_rand=tr, feat_mod=mod)
+    assert torch.equal(o1[0], o2[0])
+    assert torch.equal(o2[1], ops.modulate_to_nhwc_split(o1[1], mod))
+
+
 def test_decoder_prep_overlap_matches_in_order(sdfr):
     """Generator.forward's decoder prep on the side stream (batch >= 8, warm weight
     caches) gives the images of the in-order prep from the same RNG state, and the
