@@ -1475,6 +1475,24 @@ size_t conv_t_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
     return (size_t)ks * B * (2 * H + 1) * (2 * W + 1) * Cout * sizeof(float);
 }
 
+// conv_t_kernel's four edge classes (row 2H: W + 1 and W pixels, column 2W: H and H
+// pixels per face) as conv_x_kernel workgroup slots, and their split-K factor: ~70 thin
+// tiles of a full-K loop each at 32 faces would leave most CUs idle (SDFR_EDGE_SPLIT)
+#ifndef SDFR_EDGE_SPLIT
+#define SDFR_EDGE_SPLIT 1
+#endif
+uint32_t conv_edge_grid(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
+    uint32_t g = 0;
+    for (uint32_t n : {W + 1, W, H, H}) g += ((B * n + kPT - 1) / kPT * (Cout / kCT) + 7) & ~7u;
+    return g;
+}
+size_t conv_edge_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
+    if (!SDFR_EDGE_SPLIT || H % 16 || W % 16 || Cout % kCT) return 0;
+    if (B * (H / 16) * (W / 16) * (Cout / kTCT) < 256) return 0;    // no conv_t_kernel (use_conv_t)
+    const uint32_t g = conv_edge_grid(B, H, W, Cout), ks = conv_ksplit(g);
+    return ks > 1 ? (size_t)ks * g * 16 * 512 * sizeof(f4) : 0;
+}
+
 uint32_t conv_grid(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {   // regular conv
     return ((B * H * W + kPT - 1) / kPT * (Cout / kCT) + 7) & ~7u;
 }
@@ -1578,9 +1596,21 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
                                    0, st, a);
                 if ((rc = check_launch(what))) return rc;
             }
-            // the edge classes: ~100 thin tiles at B = 32, each the full K loop (20 us; a
-            // 2-way K split measured 20 + 14 us with its finish, not kept)
-            hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, 1), dim3(512), 0, st, a);
+            // the edge classes: ~70 thin tiles at B = 32, each a full-K loop, split-K
+            // over up to 1.25 rounds of the chip when the workspace allows (the conv_t
+            // K-split partials, if any, are consumed by the finish kernel above)
+            a.grid = grid;
+            const uint32_t eks = conv_ksplit(grid);
+            if (SDFR_EDGE_SPLIT && ws && eks > 1 && kst == 1 &&
+                ws_bytes >= (size_t)eks * grid * 16 * 512 * sizeof(f4)) {
+                a.ksplit = eks;
+                a.partial = reinterpret_cast<f4 *>(ws);
+            }
+            hipLaunchKernelGGL(conv_x_kernel<false>, dim3(grid, a.ksplit), dim3(512), 0, st, a);
+            if (a.ksplit > 1) {
+                if ((rc = check_launch(what))) return rc;
+                hipLaunchKernelGGL(conv_splitk_kernel<false>, dim3(grid), dim3(512), 0, st, a);
+            }
             return check_launch(what);
         }
         for (uint32_t py = 0; py < 2; ++py)
@@ -1658,7 +1688,11 @@ size_t sdfr_conv_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout, int
     const uint32_t grid = transposed ? conv_grid_t(B, H, W, Cout) : conv_grid(B, H, W, Cout);
     const uint32_t ks = conv_ksplit(grid);
     const size_t strip = ks > 1 ? (size_t)ks * grid * 16 * 512 * sizeof(f4) : 0;
-    const size_t tk = transposed ? conv_t_ws_bytes(B, H, W, Cout) : 0;
+    size_t tk = transposed ? conv_t_ws_bytes(B, H, W, Cout) : 0;
+    if (transposed) {
+        const size_t te = conv_edge_ws_bytes(B, H, W, Cout);
+        tk = tk > te ? tk : te;
+    }
     return strip > tk ? strip : tk;
 }
 
