@@ -1476,10 +1476,12 @@ size_t conv_t_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
 }
 
 // conv_t_kernel's four edge classes (row 2H: W + 1 and W pixels, column 2W: H and H
-// pixels per face) as conv_x_kernel workgroup slots, and their split-K factor: ~70 thin
-// tiles of a full-K loop each at 32 faces would leave most CUs idle (SDFR_EDGE_SPLIT)
+// pixels per face) as conv_x_kernel workgroup slots, and their split-K factor
+// (SDFR_EDGE_SPLIT=1): ~70 thin tiles of a full-K loop at 32 faces leave most CUs
+// idle, but the 4-way split measured 27 + 16 us per launch in the bench trace against
+// 36 unsplit (the finish pass costs what the split saves), so it is off
 #ifndef SDFR_EDGE_SPLIT
-#define SDFR_EDGE_SPLIT 1
+#define SDFR_EDGE_SPLIT 0
 #endif
 uint32_t conv_edge_grid(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
     uint32_t g = 0;

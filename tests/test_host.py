@@ -119,8 +119,8 @@ def test_conv_split_k_workspace(sdfr):
     assert lib.sdfr_conv_ws_bytes(1, 16, 16, 128, 1) == 4 * 32 * tile
     assert lib.sdfr_conv_ws_bytes(1, 64, 64, 256, 1) == 2 * 152 * tile  # 152 slots: 2-way
     assert lib.sdfr_conv_ws_bytes(1, 128, 128, 128, 1) == 0           # 280 slots: no split
-    # 32 faces: conv_t_kernel, whose four thin edge classes (72 slots) split 4 ways
-    assert lib.sdfr_conv_ws_bytes(32, 64, 64, 256, 1) == 4 * 72 * tile
+    # 32 faces: conv_t_kernel (its edge classes unsplit: SDFR_EDGE_SPLIT off)
+    assert lib.sdfr_conv_ws_bytes(32, 64, 64, 256, 1) == 0
     assert lib.sdfr_conv_ws_bytes(1, 64, 64, 100, 1) == 0             # Cout % 128
 
 
