@@ -63,6 +63,12 @@ constexpr int kTAbl = SDFR_TABL;
 #define SDFR_HABL 0
 #endif
 constexpr int kHAbl = SDFR_HABL;
+// conv_h_kernel's epilogue activation and ToRGB partials on packed fp32 (0: scalar)
+#ifndef SDFR_HEPK
+#define SDFR_HEPK 1
+#endif
+constexpr bool kHEpk = SDFR_HEPK != 0;
+typedef float f2c __attribute__((ext_vector_type(2)));
 // small batches: K-split conv_h_kernel + conv_h_finish_kernel (0: conv_x_kernel split-K)
 #ifndef SDFR_HSPLIT
 #define SDFR_HSPLIT 1
@@ -685,17 +691,48 @@ __device__ __forceinline__ void conv_h_epilogue(const ConvArgs &a, f4 (&acc)[4][
             const uint32_t P = pix0 + r * W + n;
             const float nz = e.noise ? nw * epn[r * 16 + n] : 0.0f;
             f4 v;
+            if constexpr (kHEpk) {
+                // packed fp32 (two channels per v_pk_* op, each the same IEEE operation
+                // in the same order as act1: bit-identical; no MFMA runs beside the
+                // epilogue, where packed fp32 would cost issue slots)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = act1(acc[i][j][q], dm[q], nz, bs[q], e.slope, e.scale);
+                for (int hp = 0; hp < 2; ++hp) {
+                    const f2c c2 = {acc[i][j][2 * hp], acc[i][j][2 * hp + 1]};
+                    f2c u = c2 * f2c{dm[2 * hp], dm[2 * hp + 1]};
+                    u = u + f2c{nz, nz};
+                    u = u + f2c{bs[2 * hp], bs[2 * hp + 1]};
+                    const f2c neg = u * f2c{e.slope, e.slope};
+                    u = f2c{u.x > 0.0f ? u.x : neg.x, u.y > 0.0f ? u.y : neg.y};
+                    u = u * f2c{e.scale, e.scale};
+                    v[2 * hp] = u.x;
+                    v[2 * hp + 1] = u.y;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = act1(acc[i][j][q], dm[q], nz, bs[q], e.slope, e.scale);
+            }
             if constexpr (kHAbl & 1) {
                 if (e.ys && v[0] == 1.2345e-33f) store_split8_pair(e.ys, (size_t)P * a.Cout + (ch & ~7u), v * sn, g);
             } else {
                 if (e.ys) store_split8_pair(e.ys, (size_t)P * a.Cout + (ch & ~7u), v * sn, g);
             }
+            if constexpr (kHEpk) {
+                // channels o = 0, 1 of the ToRGB partials as one packed chain (the same
+                // fma per element, the same q order), o = 2 alone
+                f2c p01 = {part[j][0], part[j][1]};
 #pragma unroll
-            for (int o = 0; o < 3; ++o)
+                for (int q = 0; q < 4; ++q) {
+                    p01 = __builtin_elementwise_fma(f2c{v[q], v[q]}, f2c{rw[0][q], rw[1][q]}, p01);
+                    part[j][2] = fmaf(v[q], rw[2][q], part[j][2]);
+                }
+                part[j][0] = p01.x;
+                part[j][1] = p01.y;
+            } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) part[j][o] = fmaf(v[q], rw[o][q], part[j][o]);
+                for (int o = 0; o < 3; ++o)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) part[j][o] = fmaf(v[q], rw[o][q], part[j][o]);
+            }
         }
     }
     if (!(kHAbl & 4) && (e.rgb_w || e.rgb_base)) {
