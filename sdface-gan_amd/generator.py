@@ -602,6 +602,22 @@ class Decoder(nn.Module):
         the next forward (None: stop); `conv_flops` counts their fp32-equivalent FLOPs."""
         self.conv_events, self._conv_ev, self.conv_flops = events, 0, 0
 
+    @staticmethod
+    def _fused_chunk(features, seq):
+        """Faces per fused call: the largest activation of one face (a layer's input,
+        or its raw output -- (2H+1) x (2W+1) for an upsampling layer -- in 4-byte
+        elements) times the batch stays below 2^31 bytes (the 256^2 decoder: 63 faces)."""
+        h, w = (features.shape[1:3] if features.dim() == 6 else features.shape[2:4])
+        per_face = 0
+        for sc in seq:
+            cout, cin = sc.conv.weight.shape[1], sc.conv.weight.shape[2]
+            per_face = max(per_face, h * w * cin * 4)
+            if sc.conv.upsample:
+                per_face = max(per_face, (2 * h + 1) * (2 * w + 1) * cout * 4)
+                h, w = 2 * h, 2 * w
+            per_face = max(per_face, h * w * cout * 4)
+        return max(1, ((1 << 31) - 1) // per_face)
+
     def _fused_forward(self, features, latent, noise, sty=None):
         """Same computation as the module path: per layer one split-fp16 convolution
         (or MIOpen's) plus one sdfr_styled_epilogue on NHWC activations -- for the
@@ -616,6 +632,24 @@ class Decoder(nn.Module):
         if sty is None:
             noise = self._fused_noise(noise, B, features.device, features.dtype)
             sty = self._fused_styles(latent, seq, split)
+        chunk = self._fused_chunk(features, seq)
+        if B > chunk:
+            # the kernels index activations with 32-bit offsets (conv_launch: < 2^31 bytes
+            # per tensor): larger batches run as chunks on the same noise maps and styles
+            def cut(t, sl):
+                if isinstance(t, dict):                   # the demodulations, by layer
+                    return {k: cut(v, sl) for k, v in t.items()}
+                if isinstance(t, (list, tuple)):
+                    return [cut(v, sl) for v in t]
+                return t[sl] if isinstance(t, torch.Tensor) and t.dim() and t.shape[0] == B else t
+            n_chunks = -(-B // chunk)
+            chunk = -(-B // n_chunks)                     # balanced: 64 faces -> 2 x 32
+            outs = []
+            for b0 in range(0, B, chunk):
+                sl = slice(b0, min(B, b0 + chunk))
+                outs.append(self._fused_forward(features[sl], latent[sl], cut(noise, sl),
+                                                tuple(cut(part, sl) for part in sty)))
+            return torch.cat(outs, 0)
         mods, rgb_mods, demods = sty
         if features.dtype == torch.float16 and features.dim() == 6:
             # the renderer wrote features * mods[0] in the split layout already (ABI 12)

@@ -429,6 +429,29 @@ def test_prepared_fallback_draws_nothing_twice(sdfr):
     torch.testing.assert_close(img, ref, rtol=0, atol=1e-6)
 
 
+def test_decoder_fused_batch_chunks(sdfr):
+    """64 faces exceed the fused kernels' 32-bit activation offsets (the 256^2 layers'
+    (257^2 x 128) fp32 per face: 63 faces per call): the fused decoder runs them as two
+    chunks of 32 on the same styles and noise maps -- bit-identical to two 32-face calls
+    (conv_launch rejected the whole batch before)."""
+    opt = sdfr.vol_render_opt()
+    opt.model.feature_encoder_in_channels = opt.rendering.width
+    torch.manual_seed(0)
+    dec = sdfr.Decoder(opt.model).to(DEV).eval()
+    B = 64
+    feats = torch.randn(B, 256, 64, 64, device=DEV) * 0.3
+    z = torch.randn(B, 256, device=DEV)
+    noise = [torch.randn(B, 1, 2 ** r, 2 ** r, device=DEV) for r in (6, 7, 7, 8, 8)]
+    with torch.no_grad():
+        assert dec._fused_ok(feats, None, None)
+        assert dec._fused_chunk(feats, [dec.conv1] + list(dec.convs)) == 63
+        whole, _ = dec(feats, [z], noise=noise)
+        halves = [dec(feats[s], [z[s]], noise=[n[s] for n in noise])[0]
+                  for s in (slice(0, 32), slice(32, 64))]
+    assert whole.shape == (B, 3, 256, 256)
+    assert torch.equal(whole, torch.cat(halves, 0))
+
+
 @pytest.mark.parametrize("conv_impl,fuse", [("f16x3", True), ("f16x3", False), ("miopen", False)])
 def test_decoder_fused_equals_module_path(sdfr, conv_impl, fuse):
     """Same weights, latents and noise: HIP-epilogue decoder == op-by-op decoder."""

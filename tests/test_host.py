@@ -124,6 +124,20 @@ def test_conv_split_k_workspace(sdfr):
     assert lib.sdfr_conv_ws_bytes(1, 64, 64, 100, 1) == 0             # Cout % 128
 
 
+def test_fused_decoder_batch_chunk(sdfr):
+    """Faces per fused decoder call (host arithmetic): the largest per-face activation
+    of the 64^2 -> 256^2 decoder is the 257^2 x 128 raw output of the last transposed
+    convolution, so 63 faces stay under the kernels' 2^31-byte offsets; the split-NHWC
+    features the renderer hands over give the same bound."""
+    opt = sdfr.vol_render_opt()
+    opt.model.feature_encoder_in_channels = opt.rendering.width
+    dec = sdfr.Decoder(opt.model)
+    seq = [dec.conv1] + list(dec.convs)
+    assert dec._fused_chunk(torch.empty(1, 256, 64, 64, device="meta"), seq) == 63
+    assert dec._fused_chunk(torch.empty(1, 64, 64, 32, 2, 8, device="meta"), seq) == 63
+    assert (2 ** 31 - 1) // (257 * 257 * 128 * 4) == 63
+
+
 def test_state_dict_matches_reference(sdfr, golden_dir):
     opt = sdfr.vol_render_opt()
     g = sdfr.Generator(opt.model, opt.rendering)
