@@ -152,8 +152,8 @@ def test_encode_stage_bit_exact(sdfr, oracle_mod, golden_dir, renderer_sd, name,
     B = cam.shape[0]
     L = sdfr._lib
     ablation = hasattr(L.lib(), "sdfr_debug_set_encode_mode")
-    if mode != 289 and not ablation:
-        pytest.skip("gather variants other than the product's (289) exist only in "
+    if mode != 257 and not ablation:      # 257: kEncDefault (render_ngp.hip)
+        pytest.skip("gather variants other than the product's (257) exist only in "
                     "`make ABLATION=1` builds (SDFR_LIB=sdface-gan_amd/lib_abl/libsdfr.so)")
     if ablation:
         L.check(L.lib().sdfr_debug_set_encode_mode(mode), "sdfr_debug_set_encode_mode")
