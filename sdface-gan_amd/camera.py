@@ -73,6 +73,13 @@ def generate_camera_params(resolution, device, batch=1, locations=None, sweep=Fa
     return extrinsics, focal, near, far, viewpoint
 
 
+def _scaled_randn(n, scale, device):
+    """scale * torch.randn(n, 1) as [n] in one launch: normal_(0, scale) makes the same
+    draw (randn is normal_(0, 1)) and scales it in the sampling kernel by the same fp32
+    product (x * scale + 0); tests/test_gpu_render.py pins the equality."""
+    return torch.empty(n, device=device).normal_(0.0, scale)
+
+
 def _camera_cuda(resolution, device, batch, locations, sweep, uniform, azim_range, elev_range,
                  fov_ang, dist_radius):
     """The GPU branch: the reference's random draws (same torch calls, same order, on
@@ -93,8 +100,8 @@ def _camera_cuda(resolution, device, batch, locations, sweep, uniform, azim_rang
         azim = (-azim_range + 2 * azim_range * torch.rand(batch, 1, device=device)).view(-1)
         elev = (-elev_range + 2 * elev_range * torch.rand(batch, 1, device=device)).view(-1)
     else:
-        azim = (azim_range * torch.randn(batch, 1, device=device)).view(-1)
-        elev = (elev_range * torch.randn(batch, 1, device=device)).view(-1)
+        azim = _scaled_randn(batch, azim_range, device)
+        elev = _scaled_randn(batch, elev_range, device)
     azim, elev = azim.float().contiguous(), elev.float().contiguous()
     n = azim.shape[0]
     ext = torch.empty(n, 3, 4, device=device)

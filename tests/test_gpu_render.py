@@ -518,11 +518,32 @@ def test_camera_on_device_matches_reference(sdfr, golden_dir, monkeypatch):
         return draw
     monkeypatch.setattr(cam_mod.torch, "rand", cpu_draw(real_rand))
     monkeypatch.setattr(cam_mod.torch, "randn", cpu_draw(real_randn))
+    # the gauss branch draws through _scaled_randn (normal_(0, s)): the reference's
+    # scale * randn on the CPU stands in for it (test_scaled_randn_is_scale_times_randn)
+    monkeypatch.setattr(cam_mod, "_scaled_randn",
+                        lambda n, s, device: (s * real_randn(n, 1)).view(-1).to(device))
     for name, kw in [("gauss", {}), ("uniform", {"uniform": True}), ("sweep", {"sweep": True})]:
         torch.manual_seed(123)
         out = sdfr.generate_camera_params(64, DEV, batch=5, **kw)
         assert out[0].is_cuda
         check(out, name)
+
+
+def test_scaled_randn_is_scale_times_randn(sdfr):
+    """The GPU camera branch's one-launch draw normal_(0, s) equals the reference's
+    s * torch.randn(n, 1) (sdf_utils.py:118-119) bit for bit from the same generator
+    state, and leaves the generator where the reference's draw leaves it."""
+    from importlib import import_module
+    cam_mod = import_module(sdfr.generate_camera_params.__module__)
+    for n, s in [(1, 0.3), (5, 0.15), (32, 0.3), (1000, 0.7)]:
+        torch.manual_seed(11)
+        ref = (s * torch.randn(n, 1, device=DEV)).view(-1)
+        after_ref = torch.randn(3, device=DEV)
+        torch.manual_seed(11)
+        got = cam_mod._scaled_randn(n, s, DEV)
+        after_got = torch.randn(3, device=DEV)
+        assert torch.equal(got, ref), (n, s)
+        assert torch.equal(after_got, after_ref), (n, s)
 
 
 def test_get_rays_on_device_bit_exact(sdfr, golden_dir):
