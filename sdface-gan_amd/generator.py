@@ -776,6 +776,7 @@ class Generator(nn.Module):
         # the field kernel stores the decoder's first input (features x modulation,
         # split-NHWC) instead of NCHW features for modulate_nhwc_kernel to convert
         self.fuse_feature_split = True
+        self.feature_split_min_batch = 4
         self._dec_key = None
 
     def _decoder_weights_unchanged(self):
@@ -879,7 +880,8 @@ class Generator(nn.Module):
         # (from 4 faces: below that the field kernel splits rays into segments and the
         # merge kernel would scatter 2-B split stores instead of coalesced NCHW rows)
         feat_mod = None
-        if (prepared is not None and self.fuse_feature_split and B >= 4
+        if (prepared is not None and self.fuse_feature_split
+                and B >= self.feature_split_min_batch
                 and self.decoder._conv_x(self.decoder.conv1.conv)):
             feat_mod = prepared[2][0][0]
         with torch.set_grad_enabled(grad_on):
