@@ -209,12 +209,15 @@ def cpu_baseline(seconds, siren=False, fc=False):
                       "(physical cores of the affinity mask, capped by the cgroup quota)"}
 
 
-def extras(step, B, graphed_step, steps=10, warm=3):
-    """Outside the timed region (this rank only): faces/s at B = 1 and 8 (eager,
-    and at B = 1 also replayed from a HIP graph, GraphedGenerator), and at B with
-    each step's images copied to pinned host memory as eval.py's PNG writer needs
-    them (the copy of step k overlaps step k+1's kernels).  At least 200 faces per
-    rate: ten batch-1 replays (~6 ms) read 4-5 % low against the steady state."""
+def extras(step, B, graphed_step, g, steps=10, warm=3):
+    """Outside the timed region (this rank only): faces/s at B = 1 and 8 through the
+    plain API call (``faces_per_s_b1``: eval.py's unchanged loop, which
+    Generator.forward serves from its own graph cache after the first call;
+    ``_nocache``: the same with that cache off, every call eager), at B = 1 from
+    GraphedGenerator with the draws inside the graph too, and at B with each step's
+    images copied to pinned host memory as eval.py's PNG writer needs them (the copy
+    of step k overlaps step k+1's kernels).  At least 200 faces per rate: ten batch-1
+    replays (~6 ms) read 4-5 % low against the steady state."""
     def rate(nb, host=False, fn=step):
         buf = torch.empty(nb, 3, 256, 256, pin_memory=True) if host else None
         n = max(steps, -(-200 // nb))
@@ -228,7 +231,11 @@ def extras(step, B, graphed_step, steps=10, warm=3):
                 buf.copy_(img, non_blocking=True)
         torch.cuda.synchronize()
         return nb * n / (time.perf_counter() - t0)
-    return {"faces_per_s_b1": rate(1), "faces_per_s_b1_graph": rate(1, fn=graphed_step),
+    out = {"faces_per_s_b1": rate(1)}
+    g.graph_inference = False
+    out["faces_per_s_b1_nocache"] = rate(1)
+    g.graph_inference = True
+    return {**out, "faces_per_s_b1_graph": rate(1, fn=graphed_step),
             "faces_per_s_b8": rate(8),
             f"faces_per_s_b{B}_with_host_copy": rate(B, host=True), "unit": "faces/s (one GPU)"}
 
@@ -423,7 +430,7 @@ def main():
             return gg.random_faces(nb, res, azim_range=opt.camera.azim,
                                    elev_range=opt.camera.elev, fov_ang=opt.camera.fov,
                                    dist_radius=opt.camera.dist_radius)[0]
-        line["extras"] = extras(step, B, graphed_step)
+        line["extras"] = extras(step, B, graphed_step, g)
         if f16x3 and not siren:
             # the exact-fp32 field (v_mfma_f32_16x16x4_f32) on the same workload: the
             # cost of exact arithmetic, outside the timed region

@@ -42,7 +42,7 @@ extern "C" {
 #define SDFR_ELAUNCH (-2)      /* HIP launch or runtime error                 */
 #define SDFR_EUNSUPPORTED (-3) /* valid for the reference, not implemented    */
 
-#define SDFR_ABI_VERSION 12
+#define SDFR_ABI_VERSION 13
 
 int sdfr_abi_version(void);
 /* Thread-local message for the last non-zero status of this thread. */
@@ -530,6 +530,14 @@ int sdfr_conv3x3_f16x3_ws(float *out, const void *x_split, const void *packed,
                           uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
                           int transposed, void *ws, size_t ws_bytes, void *stream);
 size_t sdfr_conv_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout, int transposed);
+/* Which kernel runs the transposed convolution (a process-wide setting, read by both
+ * the launch and sdfr_conv_ws_bytes, so they always agree): 1 (default) conv_t_kernel
+ * from 256 tiles of 64 channels x 16 x 16 positions, conv_x_kernel's split-K below;
+ * 0 always conv_x_kernel; 2 conv_t_kernel at any tile count; 3 as 2 with each tile's
+ * channel groups split 2 or 4 ways below 256 tiles (needs the workspace).  The
+ * initial value is SDFR_CONV_T from the environment when the library loads (else 1);
+ * mode -1 restores it.  Returns the previous mode, or SDFR_EINVAL for another value. */
+int sdfr_set_conv_t_mode(int mode);
 
 /* The regular (transposed = 0) convolution with the plain styled epilogue fused
  * into it (the conv output never goes to memory): per pixel and channel

@@ -1,4 +1,4 @@
-"""Summarise the rocprofv3 --pmc passes of scripts/prof_counters.sh into one JSON
+"""Summarise the rocprofv3 --pmc passes of scripts/gpu.sh (task `counters`) into one JSON
 (profiles/<tag>_counters.json): per kernel the mean counter value per dispatch and
 derived ratios.
 

@@ -89,8 +89,11 @@ def main():
     torch.manual_seed(1000 + rank)
     real = [torch.rand(a.batch, 3, size, size, device=dev) * 2 - 1 for _ in range(4)]
     for k in range(a.warmup):
+        t0 = time.perf_counter()
         tr.step(real[k % 4])
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        if rank == 0:          # progress (MIOpen find spends minutes in the first steps)
+            print(f"warmup step {k}: {time.perf_counter() - t0:.2f} s", flush=True)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()

@@ -1,7 +1,10 @@
-"""Stage-1 training step under torch.profiler (profiling aid, not a test): which aten ops
-and which Python call sites issue the small elementwise kernels around the HIP ones.
+"""A training step under torch.profiler (profiling aid, not a test): which aten ops
+and which Python call sites issue the kernels around the HIP ones.  Stage 2 also
+gets a per-phase table (the trainer's record_function ranges: D step incl. R1, G
+step, path regularisation) with the device time of the kernels inside each.
 
-    python scripts/train_prof.py [--steps 2] [--out gpurun_out/train_prof.txt]"""
+    python scripts/train_prof.py [--stage 1|2] [--steps 2] [--miopen-find]
+                                 [--out gpurun_out/train_prof.txt]"""
 import argparse
 import sys
 from pathlib import Path
@@ -18,28 +21,47 @@ def main():
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--out", default="gpurun_out/train_prof.txt")
     p.add_argument("--net", default="ngp", choices=["ngp", "siren"])
+    p.add_argument("--stage", type=int, default=1, choices=[1, 2])
+    p.add_argument("--miopen-find", action="store_true")
     a = p.parse_args()
+    torch.backends.cudnn.benchmark = a.miopen_find
     dev = torch.device("cuda", 0)
     sdfr = load()
-    from sdface_gan_amd.training import CoordConv2d, RendererTrainer
+    from sdface_gan_amd.training import CoordConv2d, FullPipelineTrainer, RendererTrainer
     CoordConv2d.pad_to = 8
-    opt = sdfr.vol_render_opt(ngp=a.net == "ngp", batch=8, chunk=2, train_renderer=True)
-    tr = RendererTrainer(opt, dev, seed=0)
+    opt = sdfr.vol_render_opt(ngp=a.net == "ngp", batch=8, chunk=2,
+                              train_renderer=a.stage == 1)
+    tr = (RendererTrainer if a.stage == 1 else FullPipelineTrainer)(opt, dev, seed=0)
     tr.g_module.renderer.rng_device = "device"
     tr.generator_test.renderer.rng_device = "device"
-    size = opt.training.renderer_output_size
+    size = opt.training.renderer_output_size if a.stage == 1 else opt.model.size
     torch.manual_seed(1000)
     real = [torch.rand(8, 3, size, size, device=dev) * 2 - 1 for _ in range(4)]
     for k in range(4):
         tr.step(real[k % 4])
     torch.cuda.synchronize()
+    import time
+    t0 = time.perf_counter()
+    for k in range(4):
+        tr.step(real[k % 4])
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - t0) / 4 * 1e3
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True) as prof:
         for k in range(a.steps):
             tr.step(real[k % 4])
         torch.cuda.synchronize()
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     with open(a.out, "w") as f:
-        f.write(f"# {a.steps} stage-1 steps\n")
+        f.write(f"# {a.steps} stage-{a.stage} steps (steps 4-7 of the trainer; 4 unprofiled "
+                f"steps before: {wall_ms:.1f} ms per step wall), miopen_find={a.miopen_find}\n")
+        ranges = [ev for ev in prof.key_averages() if ev.key.startswith("stage")]
+        if ranges:
+            f.write("# per phase (record_function ranges): CPU wall ms/step, device ms/step\n")
+            for ev in sorted(ranges, key=lambda e: e.key):
+                f.write(f"{ev.key:24s} {ev.cpu_time_total / 1e3 / a.steps:9.2f} "
+                        f"{ev.device_time_total / 1e3 / a.steps:9.2f}  x{ev.count / a.steps:.2f}\n")
+        tot = sum(ev.self_device_time_total for ev in prof.key_averages()) / 1e3 / a.steps
+        f.write(f"# device time, all kernels: {tot:.2f} ms per step\n\n")
         f.write(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=70,
                                           max_name_column_width=70))
         f.write("\n\n# by call site (5 frames)\n")

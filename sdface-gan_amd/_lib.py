@@ -23,7 +23,7 @@ SDFR_OK = 0
 SDFR_EINVAL = -1
 SDFR_ELAUNCH = -2
 SDFR_EUNSUPPORTED = -3
-ABI_VERSION = 12
+ABI_VERSION = 13
 FIELD_F16X3 = 0
 FIELD_FP32 = 1
 
@@ -44,7 +44,7 @@ EXPORTS = (
     "sdfr_fused_bias_act", "sdfr_mapping_linear", "sdfr_decoder_styles", "sdfr_upfirdn2d", "sdfr_styled_epilogue", "sdfr_modulate_to_nhwc",
     "sdfr_modulate_to_nhwc_split",
     "sdfr_conv_pack_bytes", "sdfr_conv_pack_weights", "sdfr_conv3x3_f16x3",
-    "sdfr_conv3x3_f16x3_ws", "sdfr_conv_ws_bytes",
+    "sdfr_conv3x3_f16x3_ws", "sdfr_conv_ws_bytes", "sdfr_set_conv_t_mode",
     "sdfr_conv3x3_f16x3_act", "sdfr_conv_act_ws_bytes", "sdfr_rgb_finish",
     "sdfr_mc_workspace_bytes", "sdfr_mc_count", "sdfr_mc_emit",
     "sdfr_linear_pack_bytes", "sdfr_linear_pack", "sdfr_linear_f16x3",
@@ -216,6 +216,8 @@ def lib():
                                         ctypes.c_size_t, _vp]
     L.sdfr_conv_ws_bytes.argtypes = [_u32, _u32, _u32, _u32, _int]
     L.sdfr_conv_ws_bytes.restype = ctypes.c_size_t
+    L.sdfr_set_conv_t_mode.argtypes = [_int]
+    L.sdfr_set_conv_t_mode.restype = _int
     L.sdfr_conv3x3_f16x3_act.argtypes = [ctypes.POINTER(ConvActArgs), _vp]
     L.sdfr_conv_act_ws_bytes.argtypes = [_u32, _u32, _u32, _u32]
     L.sdfr_conv_act_ws_bytes.restype = ctypes.c_size_t

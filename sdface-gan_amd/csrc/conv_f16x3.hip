@@ -1476,14 +1476,20 @@ __global__ void __launch_bounds__(256) conv_t_finish_kernel(const ConvArgs a) {
 
 // The transposed conv on conv_t_kernel (+ its edge classes): raw output, 16-aligned
 // input, and at least one tile per CU (smaller batches keep conv_x_kernel's split-K).
-// SDFR_CONV_T in the environment: 0 selects conv_x_kernel (A/B measurements), 2 takes
+// The mode (sdfr_set_conv_t_mode, SDFR_CONV_T): 0 selects conv_x_kernel (A/B measurements), 2 takes
 // conv_t_kernel at any tile count (tests), 3 also splits each tile's channel groups 2 or 4
 // ways below 256 tiles (*ks) when the caller's workspace holds the partial outputs
 // (has_ws; sdfr_conv_ws_bytes sizes it).
+// The mode (sdfr_set_conv_t_mode): SDFR_CONV_T read once when the library loads.
+int conv_t_env_mode() {
+    const char *e = getenv("SDFR_CONV_T");
+    return e ? atoi(e) : 1;
+}
+int g_conv_t_mode = conv_t_env_mode();
+
 bool use_conv_t(bool act, uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout,
                 bool has_ws, uint32_t *ks) {
-    const char *e = getenv("SDFR_CONV_T");
-    const int env = e ? atoi(e) : 1;
+    const int env = g_conv_t_mode;
     *ks = 1;
     if (env == 0 || act || H % 16 || W % 16 || Cout % kTCT) return false;
     const uint32_t tiles = B * (H / 16) * (W / 16) * (Cout / kTCT), nC = Cin / 32;
@@ -1501,8 +1507,7 @@ bool use_conv_t(bool act, uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint
 
 // the partial outputs of conv_t_kernel's K split (for any Cin: an upper bound)
 size_t conv_t_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {
-    const char *e = getenv("SDFR_CONV_T");
-    if (!e || atoi(e) != 3) return 0;
+    if (g_conv_t_mode != 3) return 0;
     uint32_t ks = 1;
     const uint32_t tiles = B * (H / 16) * (W / 16) * (Cout / kTCT);
     if (H % 16 || W % 16 || Cout % kTCT || tiles >= 256) return 0;
@@ -1720,6 +1725,13 @@ int sdfr_conv3x3_f16x3(float *out, const void *x_split, const void *packed,
                        int transposed, void *stream) {
     return sdfr_conv3x3_f16x3_ws(out, x_split, packed, B, H, W, Cin, Cout, transposed, nullptr, 0,
                                  stream);
+}
+
+int sdfr_set_conv_t_mode(int mode) {
+    if (mode < -1 || mode > 3) return fail(SDFR_EINVAL, "set_conv_t_mode: mode must be -1..3");
+    const int prev = g_conv_t_mode;
+    g_conv_t_mode = mode == -1 ? conv_t_env_mode() : mode;
+    return prev;
 }
 
 size_t sdfr_conv_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout, int transposed) {

@@ -618,6 +618,20 @@ class Decoder(nn.Module):
             per_face = max(per_face, h * w * cout * 4)
         return max(1, ((1 << 31) - 1) // per_face)
 
+    @staticmethod
+    def _noise_rows(noise, sl, B):
+        """Faces ``sl`` of the per-layer noise maps: a [B, 1, h, w] map is sliced, a
+        shared [1, 1, h, w] map (the decoder's fixed noise buffers) is kept."""
+        return [n[sl] if n is not None and n.shape[0] == B else n for n in noise]
+
+    @staticmethod
+    def _style_rows(sty, sl):
+        """Faces ``sl`` of _fused_styles' (mods, rgb_mods, demods): every modulation and
+        demodulation is [B, C]."""
+        mods, rgb_mods, demods = sty
+        return ([m[sl] for m in mods], [m[sl] for m in rgb_mods],
+                {i: d[sl] for i, d in demods.items()})
+
     def _fused_forward(self, features, latent, noise, sty=None):
         """Same computation as the module path: per layer one split-fp16 convolution
         (or MIOpen's) plus one sdfr_styled_epilogue on NHWC activations -- for the
@@ -636,19 +650,14 @@ class Decoder(nn.Module):
         if B > chunk:
             # the kernels index activations with 32-bit offsets (conv_launch: < 2^31 bytes
             # per tensor): larger batches run as chunks on the same noise maps and styles
-            def cut(t, sl):
-                if isinstance(t, dict):                   # the demodulations, by layer
-                    return {k: cut(v, sl) for k, v in t.items()}
-                if isinstance(t, (list, tuple)):
-                    return [cut(v, sl) for v in t]
-                return t[sl] if isinstance(t, torch.Tensor) and t.dim() and t.shape[0] == B else t
             n_chunks = -(-B // chunk)
             chunk = -(-B // n_chunks)                     # balanced: 64 faces -> 2 x 32
             outs = []
             for b0 in range(0, B, chunk):
                 sl = slice(b0, min(B, b0 + chunk))
-                outs.append(self._fused_forward(features[sl], latent[sl], cut(noise, sl),
-                                                tuple(cut(part, sl) for part in sty)))
+                outs.append(self._fused_forward(features[sl], latent[sl],
+                                                self._noise_rows(noise, sl, B),
+                                                self._style_rows(sty, sl)))
             return torch.cat(outs, 0)
         mods, rgb_mods, demods = sty
         if features.dtype == torch.float16 and features.dim() == 6:
@@ -735,9 +744,13 @@ _SIDE_STREAMS = {}
 
 
 def _tensors_of(x):
-    """Every tensor inside nested tuples / lists (Decoder.prepare_fused's result)."""
+    """Every tensor inside nested tuples / lists / dicts (Decoder.prepare_fused's result:
+    the demodulations are a dict of views of one flat buffer)."""
     if isinstance(x, torch.Tensor):
         yield x
+    elif isinstance(x, dict):
+        for y in x.values():
+            yield from _tensors_of(y)
     elif isinstance(x, (tuple, list)):
         for y in x:
             yield from _tensors_of(y)
@@ -777,6 +790,10 @@ class Generator(nn.Module):
         # split-NHWC) instead of NCHW features for modulate_nhwc_kernel to convert
         self.fuse_feature_split = True
         self.feature_split_min_batch = 4
+        # repeated plain inference calls (eval.py's loop) replay a HIP graph of the
+        # whole forward, captured on the second sighting of the call (graphs.py,
+        # ForwardGraphCache): same results and random streams as the eager path
+        self.graph_inference = True
         self._dec_key = None
 
     def _decoder_weights_unchanged(self):
@@ -823,6 +840,25 @@ class Generator(nn.Module):
                 inject_index=None, truncation=1, truncation_latent=None, input_is_latent=False,
                 noise=None, randomize_noise=True, return_sdf=False, return_xyz=False,
                 return_eikonal=False, project_noise=False, mesh_path=None, t_rand=None):
+        kw = dict(return_latents=return_latents, inject_index=inject_index,
+                  truncation=truncation, truncation_latent=truncation_latent,
+                  input_is_latent=input_is_latent, noise=noise, randomize_noise=randomize_noise,
+                  return_sdf=return_sdf, return_xyz=return_xyz, return_eikonal=return_eikonal,
+                  project_noise=project_noise, mesh_path=mesh_path, t_rand=t_rand)
+        if self.graph_inference and not self.training and not torch.is_grad_enabled():
+            from .graphs import forward_cache
+            cache = forward_cache(self)
+            if cache.eligible(self, styles, cam_poses, focals, near, far, kw):
+                out = cache(self, styles, cam_poses, focals, near, far, kw)
+                if out is not None:
+                    return out
+        return self._forward_eager(styles, cam_poses, focals, near, far, **kw)
+
+    def _forward_eager(self, styles, cam_poses, focals, near=0.88, far=1.12,
+                       return_latents=False, inject_index=None, truncation=1,
+                       truncation_latent=None, input_is_latent=False, noise=None,
+                       randomize_noise=True, return_sdf=False, return_xyz=False,
+                       return_eikonal=False, project_noise=False, mesh_path=None, t_rand=None):
         grad_on = self.is_train and self.train_renderer
         # Fused inference: the decoder's feature-independent prep (its mapping network,
         # noise maps, per-layer modulations / demodulations: ~12 small launches) runs

@@ -9,10 +9,11 @@ stages and their checkpoints (train.py:69-147, training_utils.py:197-881).
 stage 2 (the reference's lmdb MultiResolutionDataset yields both; dataset IO is out
 of scope).  Each function returns its trainer.
 
-Deliberate difference: on a stage-2 RESUME the reference re-initialises g_ema to
-the generator's weights (training_utils.py:614 runs after the checkpoint load),
-discarding the saved EMA; here a resumed run keeps the checkpoint's g_ema, so a
-resumed run equals an uninterrupted one.
+Stage-2 resume: the reference re-initialises g_ema to the generator's weights after
+loading a checkpoint (training_utils.py:615-616 runs on every start, resumed or not),
+discarding the saved EMA.  ``train_full_pipeline(..., reference_resume_ema=True)`` (the
+default) does the same, so a resumed run follows the reference's; with ``False`` a
+resumed run keeps the checkpoint's g_ema and equals an uninterrupted run.
 """
 from __future__ import annotations
 
@@ -39,6 +40,7 @@ def train_vol_render(opt, expname, loader, device, checkpoints_dir, iters=10000,
         else:
             for _ in range(sphere_init_iters):
                 tr.sphere_init_step()
+            tr.sphere_init_finish()
             accumulate(tr.generator_test, tr.g_module, 0)
             ck.save(init_path, tr, with_optim=False)
     for idx in range(iters):
@@ -56,17 +58,20 @@ def train_vol_render(opt, expname, loader, device, checkpoints_dir, iters=10000,
 
 
 def train_full_pipeline(opt, expname, loader, device, checkpoints_dir, iters=None, wod=False,
-                        seed=0, on_step=None):
+                        seed=0, on_step=None, reference_resume_ema=True):
     """Stage 2 (training_utils.py:552-881): resume from the newest
     full_pipeline/models_*.pt, else copy the size-matching g_ema entries of
-    vol_renderer.pt (sdf_init_models.pt with ``wod``) into the generator and set
-    g_ema := g; then train with periodic checkpoints and the final full_pipeline.pt."""
+    vol_renderer.pt (sdf_init_models.pt with ``wod``) into the generator; then set
+    g_ema := g (on a resume only with ``reference_resume_ema``, as the reference
+    does, training_utils.py:615-616) and train with periodic checkpoints and the
+    final full_pipeline.pt."""
     tr = FullPipelineTrainer(opt, device, seed=seed)
     t = opt.training
     start = ck.resume(tr, checkpoints_dir, expname, 2)
     if start == 0:
         src = ck.exp_dir(checkpoints_dir, expname) / (ck.SPHERE_INIT if wod else ck.STAGE_FINAL[1])
         ck.load_size_matched(tr.g_module, ck.load_file(src)["g_ema"])
+    if start == 0 or reference_resume_ema:
         accumulate(tr.generator_test, tr.g_module, 0)
     n = t.iter if iters is None else iters
     for idx in range(n):

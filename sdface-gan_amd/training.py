@@ -23,6 +23,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 from torch import autograd, nn
+from torch.profiler import record_function
 
 from .camera import generate_camera_params
 from .decoder_ops import FusedLeakyReLU
@@ -225,7 +226,14 @@ class FullPipelineTrainer:
     """Generator + EMA copy + Discriminator + optimizers of stage 2, each rank
     holding full replicas; ``step(real_imgs)`` is one iteration of the reference
     loop (D step with R1 every d_reg_every, G step, path regularisation every
-    g_reg_every, EMA)."""
+    g_reg_every, EMA).
+
+    The renderer is frozen here, as in the reference (training_utils.py:176).  A
+    variant that trains it in stage 2 AND keeps path regularisation would
+    differentiate the renderer's HIP training GEMMs twice (autograd.grad with
+    create_graph through the ngp FiLM layers): their once-differentiable backward
+    raises then (linear.py ``_once``) rather than dropping that term -- such a run
+    needs the layers built with ``twice=True``, as the SIREN eikonal path uses."""
 
     def __init__(self, opt, device, seed=0):
         self.opt, self.t, self.device = opt, opt.training, device
@@ -327,6 +335,36 @@ class FullPipelineTrainer:
                 (g_gan_loss + 0.001 * g_content_loss(fake_img, fake_up)).backward()
         return g_gan_loss
 
+    def _path_step(self, style_dim, batch, chunk):
+        """Path length regularisation (training_utils.py:744-776).  As the reference,
+        every pass of the chunk loop runs the WHOLE path batch (its loop index is
+        unused, :760-763): path_batch / chunk passes on the same latents and cameras
+        (fresh decoder noise each), gradients and the path-length EMA accumulated
+        over them."""
+        t, dev = self.t, self.device
+        pbs = max(1, batch // t.path_batch_shrink)
+        noise = mixing_noise(pbs, style_dim, t.mixing, dev)
+        cam, focal, near, far, _ = self._cams(pbs)
+        for j in range(0, pbs, chunk):
+            last = j + chunk >= pbs
+            with self._sync(self.generator, last):
+                img, latents = self.generator(noise, cam, focal, near, far,
+                                              return_latents=True,
+                                              randomize_noise=self.randomize_noise)
+                path_loss, self.mean_path_length, path_lengths = g_path_regularize(
+                    img, latents, self.mean_path_length)
+                w = t.path_regularize * t.g_reg_every * path_loss
+                if t.path_batch_shrink:
+                    w = w + 0 * img[0, 0, 0, 0]
+                w.backward()
+        self.optimizer.step()
+        self.g_module.zero_grad(set_to_none=True)
+        if self.dist:
+            mpl = torch.as_tensor(self.mean_path_length, device=dev, dtype=torch.float32)
+            dist.all_reduce(mpl)
+            self.mean_path_length = mpl / self.world
+        return path_loss, path_lengths
+
     def step(self, real_imgs):
         t, dev = self.t, self.device
         i = self.iteration
@@ -336,11 +374,12 @@ class FullPipelineTrainer:
 
         # --- discriminator (training_utils.py:652-716)
         d_regularize = i % t.d_reg_every == 0
-        noise = mixing_noise(batch, style_dim, t.mixing, dev)
-        cams = self._cams(batch)
-        d_gan_loss, r1_loss, real_pred, fake_pred = self.d_backward(noise, cams, real_imgs,
-                                                                    d_regularize)
-        self.optimizer_d.step()
+        with record_function("stage2.d_step"):
+            noise = mixing_noise(batch, style_dim, t.mixing, dev)
+            cams = self._cams(batch)
+            d_gan_loss, r1_loss, real_pred, fake_pred = self.d_backward(noise, cams, real_imgs,
+                                                                        d_regularize)
+            self.optimizer_d.step()
         loss.update(d=d_gan_loss, real_score=real_pred.mean(), fake_score=fake_pred.mean(),
                     r1=r1_loss.mean())
 
@@ -348,40 +387,18 @@ class FullPipelineTrainer:
         n_chunks = len(range(0, batch, chunk))
         inputs = ((mixing_noise(chunk, style_dim, t.mixing, dev), self._cams(chunk))
                   for _ in range(n_chunks))
-        g_gan_loss = self.g_backward(inputs, n_chunks)
-        self.optimizer.step()
-        self.g_module.zero_grad(set_to_none=True)
+        with record_function("stage2.g_step"):
+            g_gan_loss = self.g_backward(inputs, n_chunks)
+            self.optimizer.step()
+            self.g_module.zero_grad(set_to_none=True)
         loss["g"] = g_gan_loss
 
-        # --- path length regularisation (training_utils.py:744-776).  As the reference,
-        # every pass of the chunk loop runs the WHOLE path batch (its loop index is
-        # unused, :760-763): path_batch / chunk passes on the same latents and
-        # cameras (fresh decoder noise each), gradients and the path-length EMA
-        # accumulated over them.
+        # --- path length regularisation (training_utils.py:744-776)
         path_loss = torch.zeros((), device=dev)
         path_lengths = torch.zeros((), device=dev)
         if t.g_reg_every > 0 and i % t.g_reg_every == 0:
-            pbs = max(1, batch // t.path_batch_shrink)
-            noise = mixing_noise(pbs, style_dim, t.mixing, dev)
-            cam, focal, near, far, _ = self._cams(pbs)
-            for j in range(0, pbs, chunk):
-                last = j + chunk >= pbs
-                with self._sync(self.generator, last):
-                    img, latents = self.generator(noise, cam, focal, near, far,
-                                                  return_latents=True,
-                                                  randomize_noise=self.randomize_noise)
-                    path_loss, self.mean_path_length, path_lengths = g_path_regularize(
-                        img, latents, self.mean_path_length)
-                    w = t.path_regularize * t.g_reg_every * path_loss
-                    if t.path_batch_shrink:
-                        w = w + 0 * img[0, 0, 0, 0]
-                    w.backward()
-            self.optimizer.step()
-            self.g_module.zero_grad(set_to_none=True)
-            if self.dist:
-                mpl = torch.as_tensor(self.mean_path_length, device=dev, dtype=torch.float32)
-                dist.all_reduce(mpl)
-                self.mean_path_length = mpl / self.world
+            with record_function("stage2.path_reg"):
+                path_loss, path_lengths = self._path_step(style_dim, batch, chunk)
         loss.update(path=path_loss, path_length=path_lengths.mean())
 
         accumulate(self.generator_test, self.g_module, self.accum)
@@ -624,6 +641,14 @@ class RendererTrainer:
 
     _sync = staticmethod(FullPipelineTrainer._sync)
 
+    # how the ranks agree on the sphere initialisation: "broadcast" -- every rank runs
+    # the reference's single-GPU loop (batch 3 per step, no collective per step) and
+    # sphere_init_finish() broadcasts rank 0's generator and optimizer state once;
+    # "allreduce" -- the gradients of every step are averaged over the ranks (one flat
+    # all-reduce of all 54.6 MB per 6.4 ms step: the hash table's gradient is the last
+    # one the backward produces, so it cannot overlap it)
+    sphere_init_sync = "broadcast"
+
     def sphere_init_step(self, batch=3):
         """MLP init to a sphere SDF (training_utils.py:287-317): L1(sdf, |x| - r)."""
         noise = mixing_noise(batch, self.t.style_dim, self.t.mixing, self.device)
@@ -631,10 +656,26 @@ class RendererTrainer:
         sdf, target = self.g_module.init_forward(noise, cam, focal, near, far)
         loss = F.l1_loss(sdf, target)
         loss.backward()
-        allreduce_grads(list(self.g_module.parameters()))
+        if self.sphere_init_sync == "allreduce":
+            allreduce_grads(list(self.g_module.parameters()))
         self.optimizer.step()
         self.g_module.zero_grad(set_to_none=True)
         return loss.detach()
+
+    def sphere_init_finish(self):
+        """End of the sphere initialisation: with ``sphere_init_sync == "broadcast"`` every
+        rank takes rank 0's generator parameters and Adam moments (one broadcast per
+        tensor, once), so the replicas enter stage-1 training identical."""
+        if not _dist_on() or self.sphere_init_sync != "broadcast":
+            return
+        with torch.no_grad():
+            for p in self.g_module.parameters():
+                dist.broadcast(p.data, 0)
+                st = self.optimizer.state.get(p, {})
+                for k in sorted(st):
+                    v = st[k]
+                    if isinstance(v, torch.Tensor) and v.device == p.device:
+                        dist.broadcast(v, 0)
 
     def d_backward(self, noise, cams, real_imgs):
         """The discriminator half-step's gradients (training_utils.py:346-389): fake

@@ -82,6 +82,32 @@ def test_stage2_save_resume_bit_identical(sdfr, tmp_path):
     assert a.iteration == b.iteration == 4
 
 
+@pytest.mark.parametrize("reference_resume_ema", [True, False])
+def test_stage2_resume_ema(sdfr, tmp_path, reference_resume_ema):
+    """Stage-2 resume: by default g_ema := g after the checkpoint load, as the reference
+    (training_utils.py:615-616 runs on every start); reference_resume_ema=False keeps
+    the checkpoint's g_ema."""
+    from sdface_gan_amd import checkpoint as ck
+    from sdface_gan_amd import pipeline
+    from sdface_gan_amd.training import FullPipelineTrainer
+    opt = _stage2_opt(sdfr)
+    cpu = torch.device("cpu")
+    a = FullPipelineTrainer(opt, cpu, seed=3)
+    data = _loader(32, 0)
+    for _ in range(2):
+        a.step(next(data))
+    ck.save(ck.ckpt_path(tmp_path, "exp", 2, 1), a)
+    saved = ck.load_file(ck.ckpt_path(tmp_path, "exp", 2, 1))
+    dec = [k for k in saved["g"] if k.startswith("decoder.") and "weight" in k]
+    assert any(not torch.equal(saved["g"][k], saved["g_ema"][k]) for k in dec)
+    tr = pipeline.train_full_pipeline(opt, "exp", data, cpu, tmp_path, iters=0,
+                                      reference_resume_ema=reference_resume_ema)
+    want = saved["g"] if reference_resume_ema else saved["g_ema"]
+    got = tr.generator_test.state_dict()
+    for k in dec:
+        assert torch.equal(got[k], want[k]), k
+
+
 def test_load_size_matched(sdfr):
     from sdface_gan_amd import checkpoint as ck
     opt = _stage2_opt(sdfr)

@@ -99,6 +99,36 @@ def test_upfirdn2d_vs_oracle(ops, oracle_mod, up, down, pad, kshape, ch):
     _close(f"upfirdn2d_bwd_{up}{down}{pad}", xg.grad.cpu(), xc.grad, 1e-5)
 
 
+# the tiled 4x4 kernel (upfirdn2d_tile_kernel) at the discriminator / decoder-training
+# shapes, across tile edges (64-wide, 16- or 32-tall output tiles), negative pads
+UFD_TILE = [(1, 1, (2, 2), (2, 128, 64, 64)), (1, 1, (1, 1), (2, 64, 129, 131)),
+            (2, 1, (2, 1), (2, 3, 128, 128)), (1, 2, (2, 2), (2, 3, 259, 257)),
+            (1, 1, (-1, 3), (1, 4, 33, 95)), (2, 1, (0, 3), (1, 5, 40, 70)),
+            (1, 2, (1, -1), (1, 6, 70, 150))]
+
+
+@pytest.mark.parametrize("up,down,pad,shape", UFD_TILE)
+def test_upfirdn2d_tiled_vs_reference_formula(ops, up, down, pad, shape):
+    """Forward and backward against the reference's own formulation (upfirdn2d_native,
+    sdf_op.py:273-316: zero-insert, pad, F.conv2d with the flipped kernel, stride) and
+    its autograd, on the CPU in fp32, with the StyleGAN blur taps."""
+    g = torch.Generator(device=DEV).manual_seed(sum(shape) + up + 3 * down)
+    x = torch.randn(*shape, device=DEV, generator=g)
+    f = torch.tensor([1.0, 3.0, 3.0, 1.0], device=DEV)
+    k = torch.outer(f, f)
+    k = k / k.sum() * (up * up)
+    xg = x.clone().requires_grad_(True)
+    out = ops.upfirdn2d(xg, k, up=up, down=down, pad=pad)
+    xr = x.cpu().requires_grad_(True)
+    ref = ops.upfirdn2d_native(xr, k.cpu(), up, up, down, down, pad[0], pad[1], pad[0], pad[1])
+    assert out.shape == ref.shape
+    _close(f"upfirdn2d_tile_{up}{down}{pad}{shape}", out.detach().cpu(), ref.detach().cpu(), 1e-5)
+    go = torch.randn(out.shape, device=DEV, generator=g)
+    out.backward(go)
+    ref.backward(go.cpu())
+    _close(f"upfirdn2d_tile_bwd_{up}{down}{pad}{shape}", xg.grad.cpu(), xr.grad.cpu(), 1e-5)
+
+
 def test_upfirdn2d_empty_and_errors(ops, sdfr):
     k = torch.ones(4, 4, device=DEV) / 16
     assert ops.upfirdn2d(torch.zeros(0, 3, 8, 8, device=DEV), k, pad=(1, 2)).shape == (0, 3, 8, 8)
@@ -255,12 +285,12 @@ def test_conv3x3_f16x3_vs_fp64(ops, B, Cin, Cout, H, W, transposed):
     (1, 512, 256, 64, 64),       # the decoder's 64 -> 128 layer at one face
     (1, 256, 128, 128, 128),     # ... and its 128 -> 256 layer
 ])
-def test_conv_t_kernel_vs_fp64_and_strip_kernel(ops, monkeypatch, B, Cin, Cout, H, W):
+def test_conv_t_kernel_vs_fp64_and_strip_kernel(ops, sdfr, B, Cin, Cout, H, W):
     """The transposed conv on conv_t_kernel (all four parity classes of a 16 x 16 input
     block per workgroup, one halo per channel group; the last output row / column as
-    thin conv_x_kernel classes), forced at any tile count (SDFR_CONV_T=2): against
-    float64 (the same bound as the strip kernel's, PyTorch-ROCm fp32 for scale) and
-    against conv_x_kernel (SDFR_CONV_T=0) to fp32 summation-order rounding;
+    thin conv_x_kernel classes), forced at any tile count (sdfr_set_conv_t_mode(2)):
+    against float64 (the same bound as the strip kernel's, PyTorch-ROCm fp32 for scale)
+    and against conv_x_kernel (mode 0) to fp32 summation-order rounding;
     deterministic."""
     import torch.nn.functional as F
     g = torch.Generator().manual_seed(B * 11 + Cin + H)
@@ -270,16 +300,18 @@ def test_conv_t_kernel_vs_fp64_and_strip_kernel(ops, monkeypatch, B, Cin, Cout, 
     w32 = (scale * w).float()
     packed, su = ops.conv_pack_weights(w.to(DEV), scale)
     xs = ops.split_nhwc(x.to(DEV))
-    monkeypatch.setenv("SDFR_CONV_T", "2")
+    L = sdfr._lib.lib()
+    L.sdfr_set_conv_t_mode(2)
     out = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
     out2 = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
-    monkeypatch.setenv("SDFR_CONV_T", "3")
+    L.sdfr_set_conv_t_mode(3)
     # with a workspace and SDFR_CONV_T=3: at one face (64 / 128 tiles) each tile's
     # channel groups split 4 / 2 ways, partials summed in split order
     sk = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True)
     sk2 = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True)
-    monkeypatch.setenv("SDFR_CONV_T", "0")
+    L.sdfr_set_conv_t_mode(0)
     strip = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
+    assert L.sdfr_set_conv_t_mode(-1) == 0             # back to the load-time default
     torch.cuda.synchronize()
     assert torch.equal(out, out2) and torch.equal(sk, sk2)
     got = (out / su.view(1, -1, 1, 1)).cpu().double()

@@ -25,8 +25,9 @@ DEV = "cuda:0"
 # random-init FC colours sit near 0, so a relative bound would measure fp32 rounding of
 # the 0.5-ish sigmoid sums; ngp's bound, tests/test_gpu_render.py).  Measured (MI355X,
 # round 5): features <= 4.3e-7, sdf 2.4e-7, xyz 7.5e-7, mask 1.4e-6 relative; rgb 3.6e-7.
-RTOL = {"features": 2e-6, "sdf": 2e-6, "xyz": 4e-6, "mask": 6e-6}
-ATOL = {"rgb": 2e-6}
+# Bounds ~3x those (deterministic kernels on seeded inputs: regression tripwires).
+RTOL = {"features": 1.3e-6, "sdf": 7.5e-7, "xyz": 2.3e-6, "mask": 4.3e-6}
+ATOL = {"rgb": 1.1e-6}
 _record = {}
 
 

@@ -3,6 +3,9 @@ a Generator(full_pipeline=False) rendering 128^2 rays x 128 samples with
 return_sdf / return_xyz (sdf_mesh.py:244-252) through the fused HIP renderer,
 against the reference run on the same inputs (tests/golden/mesh128.npz), and
 align_volume on the resulting SDF volume.  Tolerances as tests/test_gpu_render.py."""
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -27,8 +30,19 @@ def surface_generator(sdfr, res, n_samples, precision):
     return g.to(DEV).eval()
 
 
-def _cmp(key, got, ref):
+_record = {}
+
+
+def teardown_module(module):
+    out = os.environ.get("SDFR_PARITY_JSON")
+    if out:
+        with open(out.replace(".json", "_mesh.json"), "w") as f:
+            json.dump(_record, f, indent=1, sort_keys=True)
+
+
+def _cmp(key, got, ref, name=""):
     err = np.abs(np.asarray(got, np.float64).reshape(ref.shape) - ref)
+    _record[f"{name}:{key}"] = [float(err.max()), float(err.mean())]
     tmax, tmean = TOL[key]
     assert err.max() <= tmax, f"{key} max err {err.max():.3e} > {tmax:.1e}"
     assert err.mean() <= tmean, f"{key} mean err {err.mean():.3e} > {tmean:.1e}"
@@ -47,11 +61,11 @@ def test_mesh128_vs_reference(sdfr, golden_dir, prec):
         aligned = sdfr.align_volume(sdf)
     torch.cuda.synchronize()
     assert rgb is None and sdf.shape == (1, 128, 128, 128, 1)
-    _cmp("thumb", thumb.cpu(), g["thumb"])
-    _cmp("xyz", xyz.cpu(), g["xyz"])
-    _cmp("mask", mask.cpu(), g["mask"])
-    _cmp("sdf", sdf[:, ::8, ::8].cpu(), g["sdf_sub"])
-    _cmp("aligned", aligned[:, ::8, ::8].cpu(), g["aligned_sub"])
+    _cmp("thumb", thumb.cpu(), g["thumb"], f"mesh128_{prec}")
+    _cmp("xyz", xyz.cpu(), g["xyz"], f"mesh128_{prec}")
+    _cmp("mask", mask.cpu(), g["mask"], f"mesh128_{prec}")
+    _cmp("sdf", sdf[:, ::8, ::8].cpu(), g["sdf_sub"], f"mesh128_{prec}")
+    _cmp("aligned", aligned[:, ::8, ::8].cpu(), g["aligned_sub"], f"mesh128_{prec}")
 
 
 def test_mesh256_vs_reference_subsampled(sdfr, golden_dir):
@@ -71,10 +85,10 @@ def test_mesh256_vs_reference_subsampled(sdfr, golden_dir):
                                          return_sdf=True, return_xyz=True)
     torch.cuda.synchronize()
     assert sdf.shape == (1, 256, 256, 256, 1)
-    _cmp("sdf", sdf[:, ::st, ::st].cpu(), g["sdf_sub"])
-    _cmp("thumb", thumb[:, :, ::st, ::st].cpu(), g["thumb_sub"])
-    _cmp("xyz", xyz[:, :, ::st, ::st].cpu(), g["xyz_sub"])
-    _cmp("mask", mask[:, :, ::st, ::st].cpu(), g["mask_sub"])
+    _cmp("sdf", sdf[:, ::st, ::st].cpu(), g["sdf_sub"], "mesh256")
+    _cmp("thumb", thumb[:, :, ::st, ::st].cpu(), g["thumb_sub"], "mesh256")
+    _cmp("xyz", xyz[:, :, ::st, ::st].cpu(), g["xyz_sub"], "mesh256")
+    _cmp("mask", mask[:, :, ::st, ::st].cpu(), g["mask_sub"], "mesh256")
 
 
 def test_sdf_volume_256_properties(sdfr):

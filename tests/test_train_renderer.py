@@ -87,11 +87,19 @@ def _worker(rank, world, port, out_dir):
     before = {k: v.clone() for k, v in tr.g_module.state_dict().items()}
     torch.manual_seed(200 + rank)
     init_loss = float(tr.sphere_init_step(batch=2))
+    # each rank ran its own sphere-init step (no per-step collective); the finish
+    # hands every rank rank 0's generator and Adam moments
+    sd = tr.g_module.state_dict()
+    mine = {k: v.clone() for k, v in sd.items()}
+    tr.sphere_init_finish()
+    adam = [tr.optimizer.state[p]["exp_avg"].clone() for p in tr.g_module.parameters()
+            if p in tr.optimizer.state]
     losses = []
     for _ in range(2):
         real = torch.rand(opt.training.batch, 3, 8, 8) * 2 - 1
         losses.append({k: float(v) for k, v in tr.step(real).items()})
-    torch.save({"losses": losses, "init": init_loss, "real": real,
+    torch.save({"losses": losses, "init": init_loss, "real": real, "pre_finish": mine,
+                "adam": adam,
                 "d": tr.d_module.state_dict(), "g": tr.g_module.state_dict(),
                 "g_before": before},
                os.path.join(out_dir, f"rank{rank}.pt"))
@@ -103,6 +111,11 @@ def test_stage1_ddp_two_ranks_stay_in_sync(sdfr, tmp_path):
     r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
     assert not torch.equal(r0["real"], r1["real"])
+    # before the finish the two sphere inits differed (different data per rank) ...
+    assert any(not torch.equal(v, r1["pre_finish"][k]) for k, v in r0["pre_finish"].items()
+               if k.startswith("renderer.network."))
+    # ... after it both ranks hold rank 0's generator and optimizer moments
+    assert all(torch.equal(a, b) for a, b in zip(r0["adam"], r1["adam"])) and r0["adam"]
     for k in r0["d"]:
         assert torch.equal(r0["d"][k], r1["d"][k]), f"discriminator {k} diverged"
     trained = 0
