@@ -576,6 +576,34 @@ int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *a, void *stream);
  * sums in a fixed order before the epilogue. */
 size_t sdfr_conv_act_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout);
 
+/* The upsampling StyledConv in one call (ABI 13; sdf_model.py:660-701 + 704-818):
+ * conv_transpose2d(x, w^T, stride 2) (the packed weights as sdfr_conv3x3_f16x3),
+ * Blur(outer(fir, fir), pad (1, 1)) down to 2H x 2W, then per pixel and channel
+ *   v = lrelu(blur * demod[b,o] + noise_weight * noise[b,y,x] + bias[o]) * act_scale
+ * and y_split = split-NHWC fp16 of v * s_next[b,o] (sdfr_styled_epilogue's blur_up
+ * arithmetic, in its order: the same bits as sdfr_conv3x3_f16x3 + that epilogue).
+ * The blur and epilogue run inside the conv kernel for each block's interior pixels;
+ * `raw` [B,2H+1,2W+1,Cout] fp32 is a workspace that receives only the conv values
+ * of the blocks' band rows / columns, from which a second kernel finishes the block
+ * border pixels.  Needs sdfr_conv_t_act_supported (H, W % 16 == 0 and at least 256
+ * tiles of 64 channels x 16 x 16 positions; SDFR_EUNSUPPORTED otherwise). */
+typedef struct sdfr_conv_t_act_args {
+    const void *x_split;          /* [B,H,W,Cin/8,2,8] fp16                         */
+    const void *packed;           /* sdfr_conv_pack_weights                         */
+    uint32_t B, H, W, Cin, Cout;  /* input H x W; output 2H x 2W                    */
+    float fir[4];                 /* the blur's 1-D taps                            */
+    const float *demod;           /* [B,Cout] (x 1/su)                              */
+    const float *noise;           /* [B,2H,2W] or NULL                              */
+    const float *noise_weight;    /* [1] (device)                                   */
+    const float *bias;            /* [Cout]                                         */
+    float negative_slope, act_scale;
+    const float *s_next;          /* [B,Cout] or NULL                               */
+    void *y_split;                /* [B,2H,2W,Cout/8,2,8] fp16                      */
+    float *raw;                   /* [B,2H+1,2W+1,Cout] fp32 workspace              */
+} sdfr_conv_t_act_args;
+int sdfr_conv_t_act(const sdfr_conv_t_act_args *a, void *stream);
+int sdfr_conv_t_act_supported(uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout);
+
 /* ToRGB finish: rgb [B,3,H,W] = sum_k partial[k] + rgb_b[o]
  *   + upfirdn2d(skip, outer(fir,fir), up 2, pad (2,1)) when skip != NULL
  * (partial [nparts,B,3,H,W], skip [B,3,H/2,W/2], fir: 4 host floats). */

@@ -46,6 +46,7 @@ EXPORTS = (
     "sdfr_conv_pack_bytes", "sdfr_conv_pack_weights", "sdfr_conv3x3_f16x3",
     "sdfr_conv3x3_f16x3_ws", "sdfr_conv_ws_bytes", "sdfr_set_conv_t_mode",
     "sdfr_conv3x3_f16x3_act", "sdfr_conv_act_ws_bytes", "sdfr_rgb_finish",
+    "sdfr_conv_t_act", "sdfr_conv_t_act_supported",
     "sdfr_mc_workspace_bytes", "sdfr_mc_count", "sdfr_mc_emit",
     "sdfr_linear_pack_bytes", "sdfr_linear_pack", "sdfr_linear_f16x3",
     "sdfr_linear_wgrad_ws_bytes", "sdfr_linear_wgrad_f16x3",
@@ -148,6 +149,18 @@ class ConvActArgs(ctypes.Structure):
     ]
 
 
+class ConvTActArgs(ctypes.Structure):
+    """sdfr_conv_t_act_args (include/sdfr.h, ABI 13)."""
+    _fields_ = [
+        ("x_split", _vp), ("packed", _vp),
+        ("B", _u32), ("H", _u32), ("W", _u32), ("Cin", _u32), ("Cout", _u32),
+        ("fir", _f32 * 4),
+        ("demod", _vp), ("noise", _vp), ("noise_weight", _vp), ("bias", _vp),
+        ("negative_slope", _f32), ("act_scale", _f32),
+        ("s_next", _vp), ("y_split", _vp), ("raw", _vp),
+    ]
+
+
 _lib = None
 
 
@@ -219,6 +232,9 @@ def lib():
     L.sdfr_set_conv_t_mode.argtypes = [_int]
     L.sdfr_set_conv_t_mode.restype = _int
     L.sdfr_conv3x3_f16x3_act.argtypes = [ctypes.POINTER(ConvActArgs), _vp]
+    L.sdfr_conv_t_act.argtypes = [ctypes.POINTER(ConvTActArgs), _vp]
+    L.sdfr_conv_t_act_supported.argtypes = [_u32, _u32, _u32, _u32, _u32]
+    L.sdfr_conv_t_act_supported.restype = _int
     L.sdfr_conv_act_ws_bytes.argtypes = [_u32, _u32, _u32, _u32]
     L.sdfr_conv_act_ws_bytes.restype = ctypes.c_size_t
     _i64 = ctypes.c_int64

@@ -186,6 +186,7 @@ struct ConvArgs {
     uint32_t tiles_t;              // conv_t_kernel: 64-channel x 16 x 16-position tiles
     uint32_t ksplit_t;             // conv_t_kernel: channel-group split of a tile (1, 2, 4)
     float *ptl;                    // ksplit_t > 1: [ksplit_t][B, Hf, Wf, Cout] partial outputs
+    float fir[4];                  // conv_t_kernel<true>: the blur's 1-D taps (outer(fir, fir))
 };
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -1157,9 +1158,246 @@ __host__ __device__ constexpr int t_ky(int s) {
 __host__ __device__ constexpr int t_kx(int s) { return s < 6 ? (s & 1) : 2; }
 __host__ __device__ constexpr int t_pos(int s) { return s < 4 ? 0 : (s < 6 ? 1 : (s < 8 ? 2 : 3)); }
 
+// ---- conv_t_kernel<true>: the upsampling StyledConv's blur and styled epilogue ----
+// (sdf_model.py:674-683, 704-818: Blur(pad (1, 1), 4 x 4 = outer(fir, fir)) of the
+// transposed conv's (2H + 1)^2 output, then demod, noise, bias, leaky ReLU x sqrt 2 and
+// the next layer's modulation; epi_blur_kernel's arithmetic, in its order).  A block's
+// 32 x 32 output pixels need its 35 x 35 conv outputs (one row / column before, two
+// after): the interior 29 x 29 are finished here from the accumulators -- the 4-tap
+// horizontal pass across lanes (DPP row shifts within the 16-lane rows that hold a
+// position row's 16 columns), the vertical pass across a lane's rows, the rows at the
+// 4-row wave boundaries exchanged through LDS -- and the border pixels (rows and
+// columns 0, 30, 31 of a block) by conv_t_border_kernel, from the raw conv values of
+// the band rows / columns (0-2, 29-31) that this kernel stores instead of the whole
+// fp32 output.
+__device__ __forceinline__ bool t_band(uint32_t r) { return r <= 2u || r >= 29u; }
+__device__ __forceinline__ bool t_border(uint32_t r) { return r == 0u || r >= 30u; }
+
+// value of lane n - 1 (PREV) or n + 1 of the lane's 16-lane row; 0 past the row's end
+template <bool PREV>
+__device__ __forceinline__ f4 dpp_row_shift(f4 v) {
+    f4 r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        r[k] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                   0, __builtin_bit_cast(int, v[k]), PREV ? 0x111 : 0x101, 0xF, 0xF, true));
+    return r;
+}
+
+// store_split8_pair, the store only where `live` (both lanes of a pair agree on it)
+__device__ __forceinline__ void store_split8_pair_if(_Float16 *ys, size_t idx8, f4 v, uint32_t g,
+                                                     bool live) {
+    asm volatile("" : "+v"(v));        // the fp32 product rounded first (not folded into the cvt)
+    h4 h, l;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        h[r] = (_Float16)v[r];
+        l[r] = (_Float16)(v[r] - (float)h[r]);
+    }
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    const u2 hd = __builtin_bit_cast(u2, h), ld = __builtin_bit_cast(u2, l);
+    uint32_t q[4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const auto r = __builtin_amdgcn_permlane16_swap(hd[k], ld[k], false, false);
+        uint32_t r0 = r[0], r1 = r[1];
+        asm volatile("" : "+v"(r0), "+v"(r1));
+        q[k] = r0;
+        q[2 + k] = r1;
+    }
+    if (live) *reinterpret_cast<f4 *>(ys + 2 * idx8 + (g & 1u) * 8) = __builtin_bit_cast(f4, q);
+}
+
+// 4-tap filter in epi_blur_kernel's order: fma chain from 0 (horizontal, hfilt) ...
+__device__ __forceinline__ f4 fir_h(const f4 &v0, const f4 &v1, const f4 &v2, const f4 &v3,
+                                    float f0, float f1, float f2, float f3) {
+    f4 h;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        h[k] = fmaf(v3[k], f3, fmaf(v2[k], f2, fmaf(v1[k], f1, fmaf(v0[k], f0, 0.0f))));
+    return h;
+}
+// ... and from the first product (vertical)
+__device__ __forceinline__ f4 fir_v(const f4 &h0, const f4 &h1, const f4 &h2, const f4 &h3,
+                                    float f0, float f1, float f2, float f3) {
+    f4 s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] = fmaf(h3[k], f3, fmaf(h2[k], f2, fmaf(h1[k], f1, h0[k] * f0)));
+    return s;
+}
+
+// The epilogue of one conv_t_kernel<true> tile.  acc[2 py + px][i][j]: channels
+// 16 (2 wm + i) + 4 g .. + 3 of the block's 64, input position (4 wn + j, n), output pixel
+// (2 (4 wn + j) + py, 2 n + px) of the block.  Ep: the tile's demod, bias, s_next (64
+// channels, f4 0-15 of pieces 0-2) and noise (32 x 32 floats from f4 192); Xs: 48 KB of
+// LDS free during the epilogue (the halo buffer of odd channel groups).
+__device__ __forceinline__ void conv_t_blur_epilogue(const ConvArgs &a, f4 (&acc)[4][2][4],
+                                                     const f4 *Ep, f4 *Xs, uint32_t lane,
+                                                     uint32_t wave, uint32_t cb, uint32_t b,
+                                                     uint32_t y0, uint32_t x0) {
+    asm volatile("" : "+v"(lane), "+s"(wave));
+    const uint32_t wm = wave & 1u, wn = wave >> 1;
+    const uint32_t n = lane & 15u, g = lane >> 4;
+    const uint32_t C = a.Cout, Wf = a.Wf, H2 = 2u * a.Hin, W2 = 2u * a.Win;
+    const ActEpi &e = a.e;
+    // 1. the raw conv values of the band rows / columns (conv_t_border_kernel's input)
+    {
+        float *raw = a.out + (size_t)cb * kTCT + 2u * wm * 16u + 4u * g;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t yr = 2u * (4u * wn + j) + (uint32_t)(q >> 1);
+                const uint32_t xr = 2u * n + (uint32_t)(q & 1);
+                if (t_band(yr) || t_band(xr)) {
+                    float *dst = raw + ((size_t)(b * a.Hf + 2u * y0 + yr) * Wf + 2u * x0 + xr) * C;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) *reinterpret_cast<f4 *>(dst + i * 16) = acc[q][i][j];
+                }
+            }
+    }
+    const float f0 = a.fir[3], f1 = a.fir[2], f2 = a.fir[1], f3 = a.fir[0];   // flipped taps
+    const float nw = e.noise ? *e.noise_weight : 0.0f;
+    const float *epn = reinterpret_cast<const float *>(Ep + 192);
+    const size_t pbase = (size_t)b * H2 + 2u * y0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                       // the K loop's reads of Xs are done
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {   // per 16-channel m-tile (register pressure)
+        // 2. horizontal pass in place: acc[2 py + px] <- conv row 2 a + py filtered at
+        //    column 2 c + px (columns 2c-1 .. 2c+2: lane n - 1's px 1, own px 0 / 1, lane
+        //    n + 1's px 0 / 1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int py = 0; py < 2; ++py) {
+                const f4 c0 = acc[2 * py][i][j], c1 = acc[2 * py + 1][i][j];
+                const f4 l1 = dpp_row_shift<true>(c1);
+                const f4 r0 = dpp_row_shift<false>(c0), r1 = dpp_row_shift<false>(c1);
+                acc[2 * py][i][j] = fir_h(l1, c0, c1, r0, f0, f1, f2, f3);
+                acc[2 * py + 1][i][j] = fir_h(c0, c1, r0, r1, f0, f1, f2, f3);
+            }
+        // 3. rows across the 4-row wave boundaries: wave (wm, wn) needs row 4 wn - 1's
+        //    odd conv row (wave - 2's j = 3, py = 1) and row 4 wn + 4's two (wave + 2's
+        //    j = 0).  (A barrier separates the previous m-tile's reads from these writes.)
+        if (i) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        f4 *mine = Xs + wave * 6u * 64u + lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mine[q * 64] = acc[q][i][0];
+        mine[4 * 64] = acc[2][i][3];
+        mine[5 * 64] = acc[3][i][3];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const f4 *above = Xs + (wave - 2u) * 6u * 64u + lane;   // (read only when wn > 0)
+        const f4 *below = Xs + (wave + 2u) * 6u * 64u + lane;   // (read only when wn < 3)
+        const f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+        f4 up[2], dn[4];
+        up[0] = wn > 0 ? above[4 * 64] : z;
+        up[1] = wn > 0 ? above[5 * 64] : z;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dn[q] = wn < 3 ? below[q * 64] : z;
+        // 4. vertical pass, styled epilogue, split store (interior pixels)
+        const uint32_t lq = (2u * wm + i) * 4u + g;         // f4 index of the channel quad
+        const uint32_t ch = cb * kTCT + 4u * lq;
+        const f4 dm = Ep[lq], bs = Ep[64 + lq];
+        const f4 sn = e.s_next ? Ep[128 + lq] : f4{1.0f, 1.0f, 1.0f, 1.0f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int px = 0; px < 2; ++px) {
+                const f4 hm1 = j > 0 ? acc[2 + px][i][j - 1] : up[px];        // a - 1, py 1
+                const f4 h00 = acc[px][i][j], h01 = acc[2 + px][i][j];         // a, py 0 / 1
+                const f4 hp0 = j < 3 ? acc[px][i][j + 1] : dn[px];            // a + 1, py 0
+                const f4 hp1 = j < 3 ? acc[2 + px][i][j + 1] : dn[2 + px];     // a + 1, py 1
+#pragma unroll
+                for (int py = 0; py < 2; ++py) {
+                    const f4 sv = py == 0 ? fir_v(hm1, h00, h01, hp0, f0, f1, f2, f3)
+                                          : fir_v(h00, h01, hp0, hp1, f0, f1, f2, f3);
+                    const uint32_t yr = 2u * (4u * wn + j) + py, xr = 2u * n + px;
+                    const float nz = e.noise ? nw * epn[yr * 32u + xr] : 0.0f;
+                    f4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = act1(sv[r], dm[r], nz, bs[r], e.slope, e.scale);
+                    const size_t P = (pbase + yr) * W2 + 2u * x0 + xr;
+                    store_split8_pair_if(e.ys, P * C + (ch & ~7u), v * sn, g,
+                                         !t_border(yr) && !t_border(xr));
+                }
+            }
+    }
+}
+
+// The border pixels of conv_t_kernel<true>'s blocks (rows and columns 0, 30 and 31 of
+// every 32 x 32 output block: their blur reaches a neighbouring block's conv outputs),
+// from the raw band rows / columns and the edge classes' last row / column in a.out:
+// epi_blur_kernel's arithmetic for one pixel and channel quad per thread.
+__global__ void __launch_bounds__(256) conv_t_border_kernel(const ConvArgs a) {
+    const uint32_t Q = a.Cout >> 2, H2 = 2u * a.Hin, W2 = 2u * a.Win;
+    const uint32_t nr = 3u * (H2 / 32u), nc = 3u * (W2 / 32u);
+    const uint32_t per_face = nr * W2 + nc * (H2 - nr);
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (t >= (uint64_t)a.B * per_face * Q) return;
+    const uint32_t q = (uint32_t)(t % Q);
+    const uint64_t r1 = t / Q;
+    const uint32_t k = (uint32_t)(r1 % per_face), b = (uint32_t)(r1 / per_face);
+    auto brd = [](uint32_t m) { return 32u * (m / 3u) + (m % 3u == 0u ? 0u : 29u + m % 3u); };
+    uint32_t Y, X;
+    if (k < nr * W2) {
+        Y = brd(k / W2);
+        X = k % W2;
+    } else {
+        const uint32_t kk = k - nr * W2, rr = kk / nc;
+        Y = 32u * (rr / 29u) + 1u + rr % 29u;
+        X = brd(kk % nc);
+    }
+    const uint32_t c = 4u * q, C = a.Cout, Hi = a.Hf, Wi = a.Wf;
+    const float *src = a.out + (size_t)b * Hi * Wi * C + c;
+    const float f0 = a.fir[3], f1 = a.fir[2], f2 = a.fir[1], f3 = a.fir[0];
+    f4 h[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int yy = (int)Y - 1 + r;
+        f4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int xx = (int)X - 1 + j;
+            v[j] = (yy >= 0 && yy < (int)Hi && xx >= 0 && xx < (int)Wi)
+                       ? *reinterpret_cast<const f4 *>(src + ((size_t)yy * Wi + xx) * C)
+                       : f4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+        h[r] = fir_h(v[0], v[1], v[2], v[3], f0, f1, f2, f3);
+    }
+    const f4 s = fir_v(h[0], h[1], h[2], h[3], f0, f1, f2, f3);
+    const ActEpi &e = a.e;
+    const f4 dm = *reinterpret_cast<const f4 *>(e.demod + (size_t)b * C + c);
+    const f4 bs = *reinterpret_cast<const f4 *>(e.bias + c);
+    const f4 sn = e.s_next ? *reinterpret_cast<const f4 *>(e.s_next + (size_t)b * C + c)
+                           : f4{1.0f, 1.0f, 1.0f, 1.0f};
+    const size_t P = ((size_t)b * H2 + Y) * W2 + X;
+    const float nz = e.noise ? *e.noise_weight * e.noise[P] : 0.0f;
+    f4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = act1(s[r], dm[r], nz, bs[r], e.slope, e.scale);
+    v = v * sn;
+    asm volatile("" : "+v"(v));
+    h4 hh, ll;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        hh[r] = (_Float16)v[r];
+        ll[r] = (_Float16)(v[r] - (float)hh[r]);
+    }
+    const size_t idx = P * C + c, o = 2 * idx - (idx & 7u);
+    *reinterpret_cast<h4 *>(e.ys + o) = hh;
+    *reinterpret_cast<h4 *>(e.ys + o + 8) = ll;
+}
+
+template <bool FUSE>
 __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
     __shared__ f4 As[3][kTStepF4];       // weight ring [mt 4][hi,lo][64]
     __shared__ f4 Hs[2][kHaloF4];        // halo images, by channel-group parity
+    __shared__ f4 Ep[FUSE ? 7 * 64 : 1]; // FUSE: the tile's epilogue operands (below)
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t wm = wave & 1u, wn = wave >> 1;
@@ -1229,6 +1467,36 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
     auto fire_h = [&](int buf, int i) {
         set_m0(lds_addr(&Hs[buf][(wave + 8u * i) * 64]));
         dma16<0>(uni(rx), hoff[i], __builtin_amdgcn_readfirstlane(hsoff));
+    };
+    // FUSE: the tile's epilogue operands -> Ep, one 1 KB piece per wave 0-6 during the
+    // tile's second K-step (as conv_h_kernel): demod, bias, s_next (the block's 64
+    // channels in lanes 0-15), the noise of its 32 x 32 output pixels (8 rows per piece);
+    // null tensors and idle lanes read past num_records = zeros
+    auto fire_ep = [&] {
+        if (wave >= 7) return;
+        uint32_t ln = tid & 63u;              // opaque: computed here, not hoisted
+        asm volatile("" : "+v"(ln));
+        const ActEpi &e = a.e;
+        const uint32_t OOB = 0x7FFFFFF0u;
+        const uint32_t ch = cb * kTCT + 4u * (ln & 15u);
+        const bool lo = ln < 16u;
+        const uint32_t bc = a.B * a.Cout * 4u;
+        const float *base;
+        uint32_t bytes, off;
+        if (wave == 0) {
+            base = e.demod; bytes = bc; off = lo ? (bimg * a.Cout + ch) * 4u : OOB;
+        } else if (wave == 1) {
+            base = e.bias; bytes = a.Cout * 4u; off = lo ? ch * 4u : OOB;
+        } else if (wave == 2) {
+            base = e.s_next; bytes = e.s_next ? bc : 0u; off = lo ? (bimg * a.Cout + ch) * 4u : OOB;
+        } else {
+            const uint32_t H2 = 2u * H, W2 = 2u * W;
+            base = e.noise; bytes = e.noise ? a.B * H2 * W2 * 4u : 0u;
+            off = ((bimg * H2 + 2u * y0 + 8u * (wave - 3u) + (ln >> 3)) * W2 + 2u * x0 +
+                   4u * (ln & 7u)) * 4u;
+        }
+        set_m0(lds_addr(&Ep[wave * 64]));
+        dma16<0>(uni(make_rsrc(base, bytes)), off, 0u);
     };
 
     f4 acc[4][2][4];                      // [class 2 py + px][m-tile i][n-tile j]
@@ -1303,6 +1571,9 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
         else if (prev_w || prev_h) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         if constexpr (!(kTAbl & 2)) __builtin_amdgcn_s_barrier();
+        if constexpr (FUSE && S == 1) {
+            if (c == c0) fire_ep();
+        }
         __builtin_amdgcn_sched_barrier(0);
         read_a(An, (S + 1) % 3);
         if constexpr (S == 3 || S == 5 || S == 7)
@@ -1363,8 +1634,10 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
                 for (int j = 0; j < 4; ++j) acc[q][i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
         // everything but step 2's weight piece (and, after the first tile, the previous
         // epilogue's 32 stores, younger than this tile's prologue) has landed; the
-        // epilogue reads no LDS
+        // epilogue reads no LDS.  FUSE: its stores vary per lane -- wait for them all
+        // (as conv_h_kernel); its LDS reads are done everywhere after the barrier.
         if (first) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+        else if (FUSE) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(33) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         read_a(Aset[0], 0);
@@ -1375,7 +1648,9 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
             group(c + 1, std::integral_constant<int, 1>{});
         }
         if (c < c1) group(c, std::integral_constant<int, 0>{});
-        {   // raw fp32 outputs of the four classes
+        if constexpr (FUSE) {
+            conv_t_blur_epilogue(a, acc, Ep, &Hs[1][0], lane, wave, ecb, eb, ey0, ex0);
+        } else {   // raw fp32 outputs of the four classes
             uint32_t ln = lane, wmm = wm, wnn = wn;   // opaque: nothing hoisted into the K loop
             asm volatile("" : "+v"(ln), "+s"(wmm), "+s"(wnn));
             const uint32_t nn = ln & 15u, gg = ln >> 4;
@@ -1551,7 +1826,8 @@ uint32_t conv_grid_t(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {  // tr
 
 int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B, uint32_t H,
                 uint32_t W, uint32_t Cin, uint32_t Cout, int transposed, bool act,
-                hipStream_t st, const char *what, void *ws = nullptr, size_t ws_bytes = 0) {
+                hipStream_t st, const char *what, void *ws = nullptr, size_t ws_bytes = 0,
+                bool fuse_t = false) {
     if (!x_split || !packed) return fail(SDFR_EINVAL, "conv3x3_f16x3: null pointer");
     if (B == 0 || H == 0 || W == 0 || Cout % kCT || Cin % 32 || Cin == 0 || Cout == 0)
         return fail(SDFR_EINVAL, "conv3x3_f16x3: bad shape (Cout % 128, Cin % 32)");
@@ -1607,7 +1883,8 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
         a.sy = 2;
         uint32_t kst = 1;
         if (use_conv_t(act, B, H, W, Cin, Cout,
-                       ws != nullptr && ws_bytes >= conv_t_ws_bytes(B, H, W, Cout), &kst)) {
+                       !fuse_t && ws != nullptr && ws_bytes >= conv_t_ws_bytes(B, H, W, Cout),
+                       &kst)) {
             // conv_t_kernel: every output row / column < 2H, 2W; here the last row
             // (even classes at a = H: only the ky = 2 taps reach it) and column as four
             // thin classes of conv_x_kernel
@@ -1631,7 +1908,8 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
             a.tiles_t = B * (H / 16) * (W / 16) * (Cout / kTCT);
             a.ksplit_t = kst;
             a.ptl = kst > 1 ? reinterpret_cast<float *>(ws) : nullptr;
-            hipLaunchKernelGGL(conv_t_kernel, dim3(conv_h_grid(a.tiles_t * kst)), dim3(512), 0, st, a);
+            if (fuse_t) hipLaunchKernelGGL(conv_t_kernel<true>, dim3(conv_h_grid(a.tiles_t)), dim3(512), 0, st, a);
+            else hipLaunchKernelGGL(conv_t_kernel<false>, dim3(conv_h_grid(a.tiles_t * kst)), dim3(512), 0, st, a);
             int rc = check_launch(what);
             if (rc) return rc;
             if (kst > 1) {
@@ -1655,8 +1933,16 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
                 if ((rc = check_launch(what))) return rc;
                 hipLaunchKernelGGL(conv_splitk_kernel<false>, dim3(grid), dim3(512), 0, st, a);
             }
+            if (fuse_t) {        // the blocks' border pixels, after the edge classes
+                if ((rc = check_launch(what))) return rc;
+                const uint64_t nb = (uint64_t)B * (3u * (H / 16u) * 2u * W + 3u * (W / 16u) *
+                                                   (2u * H - 3u * (H / 16u))) * (Cout / 4u);
+                hipLaunchKernelGGL(conv_t_border_kernel, dim3((uint32_t)((nb + 255) / 256)), dim3(256),
+                                   0, st, a);
+            }
             return check_launch(what);
         }
+        if (fuse_t) return fail(SDFR_EUNSUPPORTED, "conv_t_act: shape below conv_t_kernel's range");
         for (uint32_t py = 0; py < 2; ++py)
             for (uint32_t px = 0; px < 2; ++px) {
                 uint32_t nt = 0;
@@ -1779,6 +2065,41 @@ int sdfr_conv3x3_f16x3_act(const sdfr_conv_act_args *p, void *stream) {
     a.e.rgb_s = s.rgb_s;
     return conv_launch(a, s.x_split, s.packed, s.B, s.H, s.W, s.Cin, s.Cout, 0, true,
                        (hipStream_t)stream, "conv3x3_f16x3_act", s.ws, s.ws_bytes);
+}
+
+int sdfr_conv_t_act_supported(uint32_t B, uint32_t H, uint32_t W, uint32_t Cin, uint32_t Cout) {
+    uint32_t ks = 1;
+    return B && H && W && Cin && Cin % 32 == 0 && Cout % kCT == 0 &&
+           use_conv_t(false, B, H, W, Cin, Cout, false, &ks) && ks == 1;
+}
+
+int sdfr_conv_t_act(const sdfr_conv_t_act_args *p, void *stream) {
+    if (!p) return fail(SDFR_EINVAL, "conv_t_act: null args");
+    const sdfr_conv_t_act_args &s = *p;
+    if (!s.demod || !s.bias || !s.y_split || !s.raw || (s.noise && !s.noise_weight))
+        return fail(SDFR_EINVAL, "conv_t_act: null tensor pointer");
+    for (const void *q : {(const void *)s.demod, (const void *)s.bias, (const void *)s.s_next,
+                          (const void *)s.y_split, (const void *)s.raw})
+        if (q && reinterpret_cast<uintptr_t>(q) % 16)
+            return fail(SDFR_EINVAL, "conv_t_act: pointers must be 16-B aligned");
+    if (!sdfr_conv_t_act_supported(s.B, s.H, s.W, s.Cin, s.Cout))
+        return fail(SDFR_EUNSUPPORTED, "conv_t_act: shape below conv_t_kernel's range "
+                                       "(sdfr_conv_t_act_supported)");
+    if ((uint64_t)s.B * (2 * s.H + 1) * (2 * s.W + 1) * s.Cout * 4 >= (1ull << 31))
+        return fail(SDFR_EINVAL, "conv_t_act: tensor too large for 32-bit offsets (split B)");
+    ConvArgs a{};
+    a.out = s.raw;
+    a.e.demod = s.demod;
+    a.e.noise = s.noise;
+    a.e.noise_weight = s.noise_weight;
+    a.e.bias = s.bias;
+    a.e.slope = s.negative_slope;
+    a.e.scale = s.act_scale;
+    a.e.s_next = s.s_next;
+    a.e.ys = reinterpret_cast<_Float16 *>(s.y_split);
+    for (int k = 0; k < 4; ++k) a.fir[k] = s.fir[k];
+    return conv_launch(a, s.x_split, s.packed, s.B, s.H, s.W, s.Cin, s.Cout, 1, false,
+                       (hipStream_t)stream, "conv_t_act", nullptr, 0, true);
 }
 
 size_t sdfr_conv_act_ws_bytes(uint32_t B, uint32_t H, uint32_t W, uint32_t Cout) {

@@ -414,6 +414,56 @@ def conv3x3_f16x3_act(x_split, packed, Cout, *, demod, bias, noise_weight, noise
     return ys, part
 
 
+def conv_t_act_supported(x_split, Cout):
+    """Does sdfr_conv_t_act take this upsampling layer (enough 64-channel x 16 x 16
+    tiles to fill the chip: the batch sizes of the 32-face bench and above)?"""
+    B, H, W, Cin = x_split.shape[0], x_split.shape[1], x_split.shape[2], 8 * x_split.shape[3]
+    return bool(_lib.lib().sdfr_conv_t_act_supported(B, H, W, Cin, Cout))
+
+
+def conv_t_act(x_split, packed, Cout, *, fir, demod, bias, noise_weight, noise=None,
+               s_next=None, negative_slope=0.2, act_scale=math.sqrt(2)):
+    """The upsampling StyledConv with its blur and styled epilogue in the conv kernel
+    (sdfr_conv_t_act): returns y split-NHWC [B,2H,2W,Cout/8,2,8] fp16 -- the same bits
+    as conv3x3_f16x3(transposed=True) followed by styled_epilogue(blur_up=True,
+    split_y=True).  demod must already carry 1/su."""
+    _require_cuda(x_split)
+    if x_split.dtype != torch.float16 or x_split.dim() != 6 or x_split.shape[4:] != (2, 8) \
+            or not x_split.is_contiguous():
+        raise RuntimeError("conv_t_act: x_split must be a contiguous split-NHWC fp16 "
+                           "tensor [B,H,W,Cin/8,2,8]")
+    B, H, W, Cin = x_split.shape[0], x_split.shape[1], x_split.shape[2], 8 * x_split.shape[3]
+    dev = x_split.device
+    ys = torch.empty(B, 2 * H, 2 * W, Cout // 8, 2, 8, device=dev, dtype=torch.float16)
+    raw = torch.empty(B, 2 * H + 1, 2 * W + 1, Cout, device=dev)
+    if noise is not None:
+        noise = noise.expand(B, 1, 2 * H, 2 * W).contiguous()
+    keep = []
+
+    def cptr(t):
+        if t is None:
+            return None
+        t = t.contiguous()
+        keep.append(t)
+        return _lib.ptr(t)
+
+    a = _lib.ConvTActArgs()
+    a.x_split, a.packed = _lib.ptr(x_split), _lib.ptr(packed)
+    a.B, a.H, a.W, a.Cin, a.Cout = B, H, W, Cin, Cout
+    for i in range(4):
+        a.fir[i] = fir[i]
+    a.demod = cptr(demod)
+    a.noise = cptr(noise)
+    a.noise_weight = cptr(noise_weight)
+    a.bias = cptr(bias.reshape(-1))
+    a.negative_slope, a.act_scale = negative_slope, act_scale
+    a.s_next = cptr(s_next)
+    a.y_split = _lib.ptr(ys)
+    a.raw = _lib.ptr(raw)
+    _lib.check(_lib.lib().sdfr_conv_t_act(a, _lib.stream_of(x_split)), "conv_t_act")
+    return ys
+
+
 def rgb_finish(partial, rgb_b, skip=None, fir=None):
     """ToRGB output [B,3,H,W] = partial.sum(0) + rgb_b + upsampled skip (sdfr_rgb_finish)."""
     _require_cuda(partial)

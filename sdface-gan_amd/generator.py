@@ -25,7 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .decoder_ops import (conv3x3_f16x3, conv3x3_f16x3_act, conv_pack_weights,  # noqa: E402
-                          modulate_to_nhwc_split, rgb_finish)
+                          conv_t_act, conv_t_act_supported, modulate_to_nhwc_split, rgb_finish)
 from .decoder_ops import (FusedLeakyReLU, fused_leaky_relu, modulate_to_nhwc,  # noqa: F401
                           separable_taps, styled_epilogue, upfirdn2d)
 from .renderer import VolumeFeatureRenderer
@@ -303,6 +303,9 @@ class Decoder(nn.Module):
         # regular f16x3 convs with the styled epilogue fused into the conv kernel
         # (sdfr_conv3x3_f16x3_act + sdfr_rgb_finish) instead of a separate pass
         self.fuse_conv_act = True
+        # upsampling convs with the blur + styled epilogue inside conv_t_kernel
+        # (sdfr_conv_t_act) wherever that kernel runs (>= 256 tiles: batches of 4+)
+        self.fuse_conv_t_blur = True
         # profiling: (start, end) HIP event pairs recorded on the current stream around
         # the fused regular convolutions (conv_h_kernel) of the next forward, in order,
         # and their fp32-equivalent FLOPs (bench.py's decoder roofline)
@@ -704,6 +707,14 @@ class Decoder(nn.Module):
                     self.conv_flops += 2 * B * H * W * 9 * mc.weight.shape[2] * cout
                 if part is not None:
                     rgb = rgb_finish(part, to_rgb.bias, skip=rgb if i else None, fir=self._fir)
+                continue
+            if (self.fuse_conv_t_blur and split[i] and mc.upsample and not last
+                    and split[i + 1] and i % 2 == 1 and conv_t_act_supported(x, cout)):
+                # upsampling conv with its blur and styled epilogue in the conv kernel
+                # (sdfr_conv_t_act: the same bits as the two launches below)
+                x = conv_t_act(x, packed, cout, fir=self._fir, demod=demod_su,
+                               bias=sc.activate.bias, noise_weight=sc.noise.weight,
+                               noise=noise[i], s_next=mods[i + 1])
                 continue
             if split[i]:
                 out = conv3x3_f16x3(x, packed, cout, transposed=mc.upsample)

@@ -328,6 +328,59 @@ def test_conv_t_kernel_vs_fp64_and_strip_kernel(ops, sdfr, B, Cin, Cout, H, W):
     _close(f"{name}_ksplit", sk.cpu(), out.cpu(), 2e-6 * s, 2e-7 * s)
 
 
+@pytest.mark.parametrize("B,Cin,Cout,H,W,noise,s_next,mode", [
+    (1, 64, 128, 16, 16, True, True, 2),     # one block per 64 channels: every pixel
+                                             # is a block border or next to one
+    (2, 96, 256, 32, 48, True, True, 2),     # odd channel-group count, 2 x 3 blocks
+    (1, 32, 128, 32, 32, False, False, 2),   # no noise, no next modulation
+    (4, 512, 256, 64, 64, True, True, 1),    # the decoder's 64 -> 128 layer at 4 faces
+    (4, 256, 128, 128, 128, True, True, 1),  # ... and its 128 -> 256 layer (512 tiles)
+])
+def test_conv_t_act_equals_conv_then_blur_epilogue(ops, sdfr, B, Cin, Cout, H, W, noise,
+                                                     s_next, mode):
+    """sdfr_conv_t_act (blur + styled epilogue inside conv_t_kernel for each block's
+    interior, conv_t_border_kernel for the block borders from the raw band rows and
+    columns) against sdfr_conv3x3_f16x3 (transposed) + sdfr_styled_epilogue (blur_up):
+    the same fp32 operations in the same order -- y bit-exact."""
+    g = torch.Generator().manual_seed(B + Cin + Cout + H + W)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g)
+    packed, su = ops.conv_pack_weights(w.to(DEV), 1 / math.sqrt(Cin * 9))
+    xs = ops.split_nhwc(x.to(DEV))
+    demod = (torch.rand(B, Cout, generator=g) + 0.5).to(DEV) / su
+    bias = (torch.randn(Cout, generator=g) * 0.1).to(DEV)
+    nw = torch.tensor([0.3]).to(DEV)
+    nz = torch.randn(B, 1, 2 * H, 2 * W, generator=g).to(DEV) if noise else None
+    sn = (torch.rand(B, Cout, generator=g) + 0.5).to(DEV) if s_next else None
+    fir = ops.separable_taps(torch.outer(torch.tensor([1., 3., 3., 1.]),
+                                         torch.tensor([1., 3., 3., 1.])) / 64 * 4)
+    L = sdfr._lib.lib()
+    prev = L.sdfr_set_conv_t_mode(mode)
+    try:
+        assert ops.conv_t_act_supported(xs, Cout)
+        y = ops.conv_t_act(xs, packed, Cout, fir=fir, demod=demod, bias=bias, noise_weight=nw,
+                           noise=nz, s_next=sn)
+        raw = ops.conv3x3_f16x3(xs, packed, Cout, transposed=True, split_k=False)
+        ref, _ = ops.styled_epilogue(raw, fir=fir, bias=bias, noise_weight=nw, noise=nz,
+                                     demod=demod, blur_up=True, s_next=sn, store_y=True,
+                                     split_y=True)
+    finally:
+        L.sdfr_set_conv_t_mode(prev)
+    torch.cuda.synchronize()
+    assert y.shape == ref.shape == (B, 2 * H, 2 * W, Cout // 8, 2, 8)
+    bad = (y != ref).reshape(B, 2 * H, 2 * W, -1).any(-1)
+    assert not bad.any(), f"{int(bad.sum())} pixels differ, first {bad.nonzero()[:5].tolist()}"
+
+
+def test_conv_t_act_unsupported_shape(ops, sdfr):
+    """Below conv_t_kernel's range (default mode, one face at 64^2: 64 tiles) the entry
+    point refuses; the decoder then takes the two-launch path."""
+    xs = torch.zeros(1, 64, 64, 64, 2, 8, device=DEV, dtype=torch.float16)
+    assert not ops.conv_t_act_supported(xs, 256)
+    assert ops.conv_t_act_supported(torch.zeros(4, 64, 64, 64, 2, 8, device=DEV,
+                                                dtype=torch.float16), 256)
+
+
 @pytest.mark.parametrize("B,Cin,Cout,H,W,rgb,skip,store_y", [
     (2, 64, 128, 16, 16, True, True, True),     # one Cout block, ToRGB with skip
     (1, 256, 512, 16, 32, True, False, True),   # four Cout blocks (partials), no skip
@@ -515,6 +568,32 @@ def test_decoder_fused_equals_module_path(sdfr, conv_impl, fuse):
     _record[f"decoder_fused_vs_module_scale_{tag}"] = scale
     _close(f"decoder_fused_vs_module_{tag}", fused.cpu(), mod.cpu(), 1e-4 * max(1.0, scale),
            1e-5 * max(1.0, scale))
+
+
+def test_decoder_conv_t_blur_fusion_bit_exact(sdfr):
+    """The fused decoder at 4 faces (both upsampling layers on sdfr_conv_t_act) gives the
+    image of the two-launch path (conv_t_kernel raw output + epi_blur_kernel) bit for bit."""
+    opt = sdfr.vol_render_opt()
+    opt.model.feature_encoder_in_channels = opt.rendering.width
+    torch.manual_seed(0)
+    dec = sdfr.Decoder(opt.model).to(DEV).eval()
+    with torch.no_grad():
+        for m in dec.modules():
+            if isinstance(m, sdfr.NoiseInjection):
+                m.weight.fill_(0.1)
+            if isinstance(m, sdfr.FusedLeakyReLU):
+                m.bias.normal_(0, 0.1)
+    B = 4
+    feats = torch.randn(B, 256, 64, 64, device=DEV)
+    z = [torch.randn(B, 256, device=DEV)]
+    noise = [torch.randn(B, 1, 2 ** r, 2 ** r, device=DEV) for r in (6, 7, 7, 8, 8)]
+    outs = []
+    with torch.no_grad():
+        for fuse in (True, False):
+            dec.fuse_conv_t_blur = fuse
+            outs.append(dec(feats, z, noise=noise)[0])
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_ema_accumulate_invalidates_fused_caches(sdfr):
