@@ -1173,15 +1173,20 @@ __host__ __device__ constexpr int t_pos(int s) { return s < 4 ? 0 : (s < 6 ? 1 :
 __device__ __forceinline__ bool t_band(uint32_t r) { return r <= 2u || r >= 29u; }
 __device__ __forceinline__ bool t_border(uint32_t r) { return r == 0u || r >= 30u; }
 
-// value of lane n - 1 (PREV) or n + 1 of the lane's 16-lane row; 0 past the row's end
+// value of lane n - 1 (PREV) or n + 1 of the lane's 16-lane row; 0 past the row's end.
+// (The whole vector is bit-cast: hipcc (ROCm 7.2) reads element 0 for a bit_cast of one
+// element v[k] of an ext-vector, whatever k -- DESIGN.md §5.2.)
 template <bool PREV>
 __device__ __forceinline__ f4 dpp_row_shift(f4 v) {
-    f4 r;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        r[k] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                   0, __builtin_bit_cast(int, v[k]), PREV ? 0x111 : 0x101, 0xF, 0xF, true));
-    return r;
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    constexpr int ctl = PREV ? 0x111 : 0x101;           // row_shr:1 / row_shl:1
+    const i4 iv = __builtin_bit_cast(i4, v);
+    i4 r;
+    r.x = __builtin_amdgcn_update_dpp(0, iv.x, ctl, 0xF, 0xF, true);
+    r.y = __builtin_amdgcn_update_dpp(0, iv.y, ctl, 0xF, 0xF, true);
+    r.z = __builtin_amdgcn_update_dpp(0, iv.z, ctl, 0xF, 0xF, true);
+    r.w = __builtin_amdgcn_update_dpp(0, iv.w, ctl, 0xF, 0xF, true);
+    return __builtin_bit_cast(f4, r);
 }
 
 // store_split8_pair, the store only where `live` (both lanes of a pair agree on it)
@@ -1205,7 +1210,11 @@ __device__ __forceinline__ void store_split8_pair_if(_Float16 *ys, size_t idx8, 
         q[k] = r0;
         q[2 + k] = r1;
     }
+#if defined(SDFR_TVAR) && SDFR_TVAR == 2
+    if (live && q[0] == 0x12345u) *reinterpret_cast<f4 *>(ys + 2 * idx8 + (g & 1u) * 8) = __builtin_bit_cast(f4, q);
+#else
     if (live) *reinterpret_cast<f4 *>(ys + 2 * idx8 + (g & 1u) * 8) = __builtin_bit_cast(f4, q);
+#endif
 }
 
 // 4-tap filter in epi_blur_kernel's order: fma chain from 0 (horizontal, hfilt) ...
@@ -1229,17 +1238,23 @@ __device__ __forceinline__ f4 fir_v(const f4 &h0, const f4 &h1, const f4 &h2, co
 // The epilogue of one conv_t_kernel<true> tile.  acc[2 py + px][i][j]: channels
 // 16 (2 wm + i) + 4 g .. + 3 of the block's 64, input position (4 wn + j, n), output pixel
 // (2 (4 wn + j) + py, 2 n + px) of the block.  Ep: the tile's demod, bias, s_next (64
-// channels, f4 0-15 of pieces 0-2) and noise (32 x 32 floats from f4 192); Xs: 48 KB of
-// LDS free during the epilogue (the halo buffer of odd channel groups).
-__device__ __forceinline__ void conv_t_blur_epilogue(const ConvArgs &a, f4 (&acc)[4][2][4],
+// channels, f4 0-15 of pieces 0-2) and noise (32 x 32 floats from f4 192), staged at the
+// tile's start (conv_t_kernel); Xs: 48 KB of LDS free during the epilogue (the halo
+// buffer of odd channel groups).  No global load here: one issued behind the epilogue's
+// stores would wait for them to drain (vmcnt retires in order).
+__device__ __forceinline__ void conv_t_blur_epilogue(const ConvArgs &a0, f4 (&acc)[4][2][4],
                                                      const f4 *Ep, f4 *Xs, uint32_t lane,
                                                      uint32_t wave, uint32_t cb, uint32_t b,
                                                      uint32_t y0, uint32_t x0) {
     asm volatile("" : "+v"(lane), "+s"(wave));
+    const ConvArgs &a = a0;
     const uint32_t wm = wave & 1u, wn = wave >> 1;
     const uint32_t n = lane & 15u, g = lane >> 4;
     const uint32_t C = a.Cout, Wf = a.Wf, H2 = 2u * a.Hin, W2 = 2u * a.Win;
     const ActEpi &e = a.e;
+    const size_t pbase = (size_t)b * H2 + 2u * y0;
+    const float nw = e.noise ? *e.noise_weight : 0.0f;   // (a scalar load)
+    const float *epn = reinterpret_cast<const float *>(Ep + 192);
     // 1. the raw conv values of the band rows / columns (conv_t_border_kernel's input)
     {
         float *raw = a.out + (size_t)cb * kTCT + 2u * wm * 16u + 4u * g;
@@ -1257,13 +1272,13 @@ __device__ __forceinline__ void conv_t_blur_epilogue(const ConvArgs &a, f4 (&acc
             }
     }
     const float f0 = a.fir[3], f1 = a.fir[2], f2 = a.fir[1], f3 = a.fir[0];   // flipped taps
-    const float nw = e.noise ? *e.noise_weight : 0.0f;
-    const float *epn = reinterpret_cast<const float *>(Ep + 192);
-    const size_t pbase = (size_t)b * H2 + 2u * y0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                       // the K loop's reads of Xs are done
 #pragma unroll
     for (int i = 0; i < 2; ++i) {   // per 16-channel m-tile (register pressure)
+        // (scheduling fences: left free, hipcc hoists m-tile 1's DPP reads above m-tile
+        // 0's stores and spills them; a scratch reload behind the stores waits for them)
+        __builtin_amdgcn_sched_barrier(0);
         // 2. horizontal pass in place: acc[2 py + px] <- conv row 2 a + py filtered at
         //    column 2 c + px (columns 2c-1 .. 2c+2: lane n - 1's px 1, own px 0 / 1, lane
         //    n + 1's px 0 / 1)
@@ -1277,6 +1292,7 @@ __device__ __forceinline__ void conv_t_blur_epilogue(const ConvArgs &a, f4 (&acc
                 acc[2 * py][i][j] = fir_h(l1, c0, c1, r0, f0, f1, f2, f3);
                 acc[2 * py + 1][i][j] = fir_h(c0, c1, r0, r1, f0, f1, f2, f3);
             }
+        __builtin_amdgcn_sched_barrier(0);
         // 3. rows across the 4-row wave boundaries: wave (wm, wn) needs row 4 wn - 1's
         //    odd conv row (wave - 2's j = 3, py = 1) and row 4 wn + 4's two (wave + 2's
         //    j = 0).  (A barrier separates the previous m-tile's reads from these writes.)
@@ -1291,33 +1307,28 @@ __device__ __forceinline__ void conv_t_blur_epilogue(const ConvArgs &a, f4 (&acc
         mine[5 * 64] = acc[3][i][3];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        const f4 *above = Xs + (wave - 2u) * 6u * 64u + lane;   // (read only when wn > 0)
-        const f4 *below = Xs + (wave + 2u) * 6u * 64u + lane;   // (read only when wn < 3)
-        const f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-        f4 up[2], dn[4];
-        up[0] = wn > 0 ? above[4 * 64] : z;
-        up[1] = wn > 0 ? above[5 * 64] : z;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dn[q] = wn < 3 ? below[q * 64] : z;
+        // (read where used: wave - 2's rows for j = 0, wave + 2's for j = 3; the top and
+        // bottom waves read a neighbour's slot of no use -- those pixels are borders)
+        const f4 *above = Xs + ((wave - 2u) & 7u) * 6u * 64u + lane;
+        const f4 *below = Xs + ((wave + 2u) & 7u) * 6u * 64u + lane;
         // 4. vertical pass, styled epilogue, split store (interior pixels)
         const uint32_t lq = (2u * wm + i) * 4u + g;         // f4 index of the channel quad
         const uint32_t ch = cb * kTCT + 4u * lq;
-        const f4 dm = Ep[lq], bs = Ep[64 + lq];
-        const f4 sn = e.s_next ? Ep[128 + lq] : f4{1.0f, 1.0f, 1.0f, 1.0f};
+        const f4 dm = Ep[lq], bs = Ep[64 + lq], sn = Ep[128 + lq];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int px = 0; px < 2; ++px) {
-                const f4 hm1 = j > 0 ? acc[2 + px][i][j - 1] : up[px];        // a - 1, py 1
-                const f4 h00 = acc[px][i][j], h01 = acc[2 + px][i][j];         // a, py 0 / 1
-                const f4 hp0 = j < 3 ? acc[px][i][j + 1] : dn[px];            // a + 1, py 0
-                const f4 hp1 = j < 3 ? acc[2 + px][i][j + 1] : dn[2 + px];     // a + 1, py 1
+                const f4 hm1 = j > 0 ? acc[2 + px][i][j - 1] : above[(4 + px) * 64];  // a - 1, py 1
+                const f4 h00 = acc[px][i][j], h01 = acc[2 + px][i][j];                 // a, py 0 / 1
+                const f4 hp0 = j < 3 ? acc[px][i][j + 1] : below[px * 64];            // a + 1, py 0
+                const f4 hp1 = j < 3 ? acc[2 + px][i][j + 1] : below[(2 + px) * 64];  // a + 1, py 1
 #pragma unroll
                 for (int py = 0; py < 2; ++py) {
                     const f4 sv = py == 0 ? fir_v(hm1, h00, h01, hp0, f0, f1, f2, f3)
                                           : fir_v(h00, h01, hp0, hp1, f0, f1, f2, f3);
                     const uint32_t yr = 2u * (4u * wn + j) + py, xr = 2u * n + px;
-                    const float nz = e.noise ? nw * epn[yr * 32u + xr] : 0.0f;
+                    const float nz = nw * epn[yr * 32u + xr];
                     f4 v;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] = act1(sv[r], dm[r], nz, bs[r], e.slope, e.scale);
@@ -1325,58 +1336,32 @@ __device__ __forceinline__ void conv_t_blur_epilogue(const ConvArgs &a, f4 (&acc
                     store_split8_pair_if(e.ys, P * C + (ch & ~7u), v * sn, g,
                                          !t_border(yr) && !t_border(xr));
                 }
+                __builtin_amdgcn_sched_barrier(0);
             }
     }
 }
 
 // The border pixels of conv_t_kernel<true>'s blocks (rows and columns 0, 30 and 31 of
 // every 32 x 32 output block: their blur reaches a neighbouring block's conv outputs),
-// from the raw band rows / columns and the edge classes' last row / column in a.out:
-// epi_blur_kernel's arithmetic for one pixel and channel quad per thread.
-__global__ void __launch_bounds__(256) conv_t_border_kernel(const ConvArgs a) {
-    const uint32_t Q = a.Cout >> 2, H2 = 2u * a.Hin, W2 = 2u * a.Win;
-    const uint32_t nr = 3u * (H2 / 32u), nc = 3u * (W2 / 32u);
-    const uint32_t per_face = nr * W2 + nc * (H2 - nr);
-    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (t >= (uint64_t)a.B * per_face * Q) return;
-    const uint32_t q = (uint32_t)(t % Q);
-    const uint64_t r1 = t / Q;
-    const uint32_t k = (uint32_t)(r1 % per_face), b = (uint32_t)(r1 / per_face);
-    auto brd = [](uint32_t m) { return 32u * (m / 3u) + (m % 3u == 0u ? 0u : 29u + m % 3u); };
-    uint32_t Y, X;
-    if (k < nr * W2) {
-        Y = brd(k / W2);
-        X = k % W2;
-    } else {
-        const uint32_t kk = k - nr * W2, rr = kk / nc;
-        Y = 32u * (rr / 29u) + 1u + rr % 29u;
-        X = brd(kk % nc);
-    }
-    const uint32_t c = 4u * q, C = a.Cout, Hi = a.Hf, Wi = a.Wf;
-    const float *src = a.out + (size_t)b * Hi * Wi * C + c;
-    const float f0 = a.fir[3], f1 = a.fir[2], f2 = a.fir[1], f3 = a.fir[0];
-    f4 h[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int yy = (int)Y - 1 + r;
-        f4 v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int xx = (int)X - 1 + j;
-            v[j] = (yy >= 0 && yy < (int)Hi && xx >= 0 && xx < (int)Wi)
-                       ? *reinterpret_cast<const f4 *>(src + ((size_t)yy * Wi + xx) * C)
-                       : f4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-        h[r] = fir_h(v[0], v[1], v[2], v[3], f0, f1, f2, f3);
-    }
-    const f4 s = fir_v(h[0], h[1], h[2], h[3], f0, f1, f2, f3);
+// from the raw band rows / columns and the edge classes' last row / column in a.out,
+// with epi_blur_kernel's arithmetic.  The border pixels come in runs of three across
+// each block boundary (rows / columns 32 k - 2 .. 32 k); a thread takes one channel
+// quad of either a row run x 4 adjacent columns (6 x 7 raw values for 12 outputs) or a
+// column run in one non-border row (4 x 6 raw values for 3 outputs).
+__device__ __forceinline__ f4 border_ld(const float *src, int yy, int xx, uint32_t Hi, uint32_t Wi,
+                                        uint32_t C) {
+    return (yy >= 0 && yy < (int)Hi && xx >= 0 && xx < (int)Wi)
+               ? *reinterpret_cast<const f4 *>(src + ((size_t)yy * Wi + xx) * C)
+               : f4{0.0f, 0.0f, 0.0f, 0.0f};
+}
+
+__device__ __forceinline__ void border_out(const ConvArgs &a, uint32_t b, uint32_t Y, uint32_t X,
+                                           uint32_t c, f4 s, const f4 &dm, const f4 &bs,
+                                           const f4 &sn, float nw) {
     const ActEpi &e = a.e;
-    const f4 dm = *reinterpret_cast<const f4 *>(e.demod + (size_t)b * C + c);
-    const f4 bs = *reinterpret_cast<const f4 *>(e.bias + c);
-    const f4 sn = e.s_next ? *reinterpret_cast<const f4 *>(e.s_next + (size_t)b * C + c)
-                           : f4{1.0f, 1.0f, 1.0f, 1.0f};
+    const uint32_t C = a.Cout, H2 = 2u * a.Hin, W2 = 2u * a.Win;
     const size_t P = ((size_t)b * H2 + Y) * W2 + X;
-    const float nz = e.noise ? *e.noise_weight * e.noise[P] : 0.0f;
+    const float nz = e.noise ? nw * e.noise[P] : 0.0f;
     f4 v;
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = act1(s[r], dm[r], nz, bs[r], e.slope, e.scale);
@@ -1393,11 +1378,92 @@ __global__ void __launch_bounds__(256) conv_t_border_kernel(const ConvArgs a) {
     *reinterpret_cast<h4 *>(e.ys + o + 8) = ll;
 }
 
+template <bool ROWS>
+__global__ void __launch_bounds__(256) conv_t_border_kernel(const ConvArgs a) {
+    const uint32_t Q = a.Cout >> 2, H2 = 2u * a.Hin, W2 = 2u * a.Win;
+    const uint32_t kb = H2 / 32u + 1u, mb = W2 / 32u + 1u;      // row / column boundaries
+    const uint32_t items = ROWS ? kb * (W2 / 4u) : (H2 / 4u) * mb;
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (t >= (uint64_t)a.B * items * Q) return;
+    const uint32_t q = (uint32_t)(t % Q);
+    const uint64_t r1 = t / Q;
+    const uint32_t item = (uint32_t)(r1 % items);
+    const uint32_t b = (uint32_t)(r1 / items);
+    const uint32_t c = 4u * q, C = a.Cout, Hi = a.Hf, Wi = a.Wf;
+    const float *src = a.out + (size_t)b * Hi * Wi * C + c;
+    const float f0 = a.fir[3], f1 = a.fir[2], f2 = a.fir[1], f3 = a.fir[0];
+    const ActEpi &e = a.e;
+    const f4 dm = *reinterpret_cast<const f4 *>(e.demod + (size_t)b * C + c);
+    const f4 bs = *reinterpret_cast<const f4 *>(e.bias + c);
+    const f4 sn = e.s_next ? *reinterpret_cast<const f4 *>(e.s_next + (size_t)b * C + c)
+                           : f4{1.0f, 1.0f, 1.0f, 1.0f};
+    const float nw = e.noise ? *e.noise_weight : 0.0f;
+    if constexpr (ROWS) {
+        // output rows 32 k - 2 .. 32 k (those inside the image) x columns X0 .. X0 + 3
+        const uint32_t k = item / (W2 / 4u), X0 = 4u * (item % (W2 / 4u));
+        const int Yb = 32 * (int)k - 2;
+        // rows Yb - 1 .. Yb + 4 one at a time (a 4-row window of filtered rows: VGPRs)
+        f4 h[4][4];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            f4 v[7];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) v[j] = border_ld(src, Yb - 1 + r, (int)X0 - 1 + j, Hi, Wi, C);
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+                h[r & 3][x] = fir_h(v[x], v[x + 1], v[x + 2], v[x + 3], f0, f1, f2, f3);
+            if (r >= 3) {
+                const int y = r - 3, Y = Yb + y;
+                if (Y >= 0 && Y < (int)H2) {
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+                        border_out(a, b, (uint32_t)Y, X0 + x, c,
+                                   fir_v(h[y & 3][x], h[(y + 1) & 3][x], h[(y + 2) & 3][x],
+                                         h[(y + 3) & 3][x], f0, f1, f2, f3),
+                                   dm, bs, sn, nw);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        // rows 4 r .. 4 r + 3 (the non-border ones: 1 .. 29 of a block) x output columns
+        // 32 m - 2 .. 32 m, rows one at a time through a 4-row window
+        const uint32_t m = item % mb, Y0 = 4u * (item / mb);
+        const int Xb = 32 * (int)m - 2;
+        f4 h[4][3];
+#pragma unroll
+        for (int r = 0; r < 7; ++r) {
+            f4 v[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) v[j] = border_ld(src, (int)Y0 - 1 + r, Xb - 1 + j, Hi, Wi, C);
+#pragma unroll
+            for (int x = 0; x < 3; ++x)
+                h[r & 3][x] = fir_h(v[x], v[x + 1], v[x + 2], v[x + 3], f0, f1, f2, f3);
+            if (r >= 3) {
+                const int y = r - 3;
+                const uint32_t Y = Y0 + y, yb = Y & 31u;
+                if (yb != 0u && yb < 30u) {
+#pragma unroll
+                    for (int x = 0; x < 3; ++x) {
+                        const int X = Xb + x;
+                        if (X < 0 || X >= (int)W2) continue;
+                        border_out(a, b, Y, (uint32_t)X, c,
+                                   fir_v(h[y & 3][x], h[(y + 1) & 3][x], h[(y + 2) & 3][x],
+                                         h[(y + 3) & 3][x], f0, f1, f2, f3),
+                                   dm, bs, sn, nw);
+                    }
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
 template <bool FUSE>
 __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
     __shared__ f4 As[3][kTStepF4];       // weight ring [mt 4][hi,lo][64]
     __shared__ f4 Hs[2][kHaloF4];        // halo images, by channel-group parity
-    __shared__ f4 Ep[FUSE ? 7 * 64 : 1]; // FUSE: the tile's epilogue operands (below)
+    __shared__ f4 Ep[FUSE ? 7 * 64 : 1]; // FUSE: the tile's epilogue operands
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t wm = wave & 1u, wn = wave >> 1;
@@ -1468,37 +1534,6 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
         set_m0(lds_addr(&Hs[buf][(wave + 8u * i) * 64]));
         dma16<0>(uni(rx), hoff[i], __builtin_amdgcn_readfirstlane(hsoff));
     };
-    // FUSE: the tile's epilogue operands -> Ep, one 1 KB piece per wave 0-6 during the
-    // tile's second K-step (as conv_h_kernel): demod, bias, s_next (the block's 64
-    // channels in lanes 0-15), the noise of its 32 x 32 output pixels (8 rows per piece);
-    // null tensors and idle lanes read past num_records = zeros
-    auto fire_ep = [&] {
-        if (wave >= 7) return;
-        uint32_t ln = tid & 63u;              // opaque: computed here, not hoisted
-        asm volatile("" : "+v"(ln));
-        const ActEpi &e = a.e;
-        const uint32_t OOB = 0x7FFFFFF0u;
-        const uint32_t ch = cb * kTCT + 4u * (ln & 15u);
-        const bool lo = ln < 16u;
-        const uint32_t bc = a.B * a.Cout * 4u;
-        const float *base;
-        uint32_t bytes, off;
-        if (wave == 0) {
-            base = e.demod; bytes = bc; off = lo ? (bimg * a.Cout + ch) * 4u : OOB;
-        } else if (wave == 1) {
-            base = e.bias; bytes = a.Cout * 4u; off = lo ? ch * 4u : OOB;
-        } else if (wave == 2) {
-            base = e.s_next; bytes = e.s_next ? bc : 0u; off = lo ? (bimg * a.Cout + ch) * 4u : OOB;
-        } else {
-            const uint32_t H2 = 2u * H, W2 = 2u * W;
-            base = e.noise; bytes = e.noise ? a.B * H2 * W2 * 4u : 0u;
-            off = ((bimg * H2 + 2u * y0 + 8u * (wave - 3u) + (ln >> 3)) * W2 + 2u * x0 +
-                   4u * (ln & 7u)) * 4u;
-        }
-        set_m0(lds_addr(&Ep[wave * 64]));
-        dma16<0>(uni(make_rsrc(base, bytes)), off, 0u);
-    };
-
     f4 acc[4][2][4];                      // [class 2 py + px][m-tile i][n-tile j]
     f4 Aset[2][4];                        // [hi i0, hi i1, lo i0, lo i1] by step parity
     f4 Bset[2][8];                        // [hi j0..3, lo j0..3] by position parity
@@ -1571,9 +1606,6 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
         else if (prev_w || prev_h) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         if constexpr (!(kTAbl & 2)) __builtin_amdgcn_s_barrier();
-        if constexpr (FUSE && S == 1) {
-            if (c == c0) fire_ep();
-        }
         __builtin_amdgcn_sched_barrier(0);
         read_a(An, (S + 1) % 3);
         if constexpr (S == 3 || S == 5 || S == 7)
@@ -1634,12 +1666,39 @@ __global__ void __launch_bounds__(512, 1) conv_t_kernel(const ConvArgs a) {
                 for (int j = 0; j < 4; ++j) acc[q][i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
         // everything but step 2's weight piece (and, after the first tile, the previous
         // epilogue's 32 stores, younger than this tile's prologue) has landed; the
-        // epilogue reads no LDS.  FUSE: its stores vary per lane -- wait for them all
-        // (as conv_h_kernel); its LDS reads are done everywhere after the barrier.
-        if (first) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+        // epilogue reads no LDS.  FUSE: its stores and loads vary per lane -- wait for
+        // them all (as conv_h_kernel); its LDS exchange is done everywhere after the barrier.
+        // FUSE: the tile's epilogue operands, one 1 KB piece per wave 0-6 -- demod, bias,
+        // s_next (the block's 64 channels in lanes 0-15), the noise of its 32 x 32 output
+        // pixels (8 rows per wave) -- loaded here, where the wait below drains the
+        // previous epilogue's stores anyway, and written to Ep behind the barrier
+        f4 epv = {0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (FUSE) {
+            const ActEpi &e = a.e;
+            const uint32_t ln = lane;
+            const uint32_t ch = cb * kTCT + 4u * (ln & 15u);
+            const bool lo = ln < 16u;
+            const f4 *src = nullptr;
+            if (wave == 0) src = lo ? reinterpret_cast<const f4 *>(e.demod + (size_t)bimg * a.Cout + ch) : nullptr;
+            else if (wave == 1) src = lo ? reinterpret_cast<const f4 *>(e.bias + ch) : nullptr;
+            else if (wave == 2) src = lo && e.s_next ? reinterpret_cast<const f4 *>(e.s_next + (size_t)bimg * a.Cout + ch) : nullptr;
+            else if (wave < 7 && e.noise)
+                src = reinterpret_cast<const f4 *>(
+                    e.noise + ((size_t)bimg * 2u * H + 2u * y0 + 8u * (wave - 3u) + (ln >> 3)) * 2u * W +
+                    2u * x0 + 4u * (ln & 7u));
+            if (src) epv = *src;
+            else if (wave == 2) epv = f4{1.0f, 1.0f, 1.0f, 1.0f};
+        }
+        if (first && !FUSE) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+#ifdef SDFR_TVAR
+        else if (FUSE && SDFR_TVAR == 1 && !first) asm volatile("s_waitcnt vmcnt(40) lgkmcnt(0)" ::: "memory");
+#endif
         else if (FUSE) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(33) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        if constexpr (FUSE) {
+            if (wave < 7) Ep[wave * 64 + lane] = epv;
+        }
         read_a(Aset[0], 0);
         read_b(Bset[0], std::integral_constant<int, 0>{}, hs0);
         uint32_t c = c0;
@@ -1935,10 +1994,14 @@ int conv_launch(ConvArgs &a, const void *x_split, const void *packed, uint32_t B
             }
             if (fuse_t) {        // the blocks' border pixels, after the edge classes
                 if ((rc = check_launch(what))) return rc;
-                const uint64_t nb = (uint64_t)B * (3u * (H / 16u) * 2u * W + 3u * (W / 16u) *
-                                                   (2u * H - 3u * (H / 16u))) * (Cout / 4u);
-                hipLaunchKernelGGL(conv_t_border_kernel, dim3((uint32_t)((nb + 255) / 256)), dim3(256),
-                                   0, st, a);
+                const uint32_t H2 = 2u * H, W2 = 2u * W;
+                const uint64_t nr = (uint64_t)B * (H2 / 32u + 1u) * (W2 / 4u) * (Cout / 4u);
+                const uint64_t nc = (uint64_t)B * (H2 / 4u) * (W2 / 32u + 1u) * (Cout / 4u);
+                hipLaunchKernelGGL(conv_t_border_kernel<true>, dim3((uint32_t)((nr + 255) / 256)),
+                                   dim3(256), 0, st, a);
+                if ((rc = check_launch(what))) return rc;
+                hipLaunchKernelGGL(conv_t_border_kernel<false>, dim3((uint32_t)((nc + 255) / 256)),
+                                   dim3(256), 0, st, a);
             }
             return check_launch(what);
         }
