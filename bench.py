@@ -209,18 +209,19 @@ def cpu_baseline(seconds, siren=False, fc=False):
                       "(physical cores of the affinity mask, capped by the cgroup quota)"}
 
 
-def extras(step, B, graphed_step, g, steps=10, warm=3):
+def extras(step, B, graphed_step, g, steps=10, warm=5):
     """Outside the timed region (this rank only): faces/s at B = 1 and 8 through the
     plain API call (``faces_per_s_b1``: eval.py's unchanged loop, which
     Generator.forward serves from its own graph cache after the first call;
     ``_nocache``: the same with that cache off, every call eager), at B = 1 from
     GraphedGenerator with the draws inside the graph too, and at B with each step's
     images copied to pinned host memory as eval.py's PNG writer needs them (the copy
-    of step k overlaps step k+1's kernels).  At least 200 faces per rate: ten batch-1
-    replays (~6 ms) read 4-5 % low against the steady state."""
+    of step k overlaps step k+1's kernels).  At least 200 faces per rate, 600 at
+    batch 1: ten batch-1 replays (~6 ms) read 4-5 % low against the steady state, and
+    200 (~110 ms) still varied by ~5 % between boxes."""
     def rate(nb, host=False, fn=step):
         buf = torch.empty(nb, 3, 256, 256, pin_memory=True) if host else None
-        n = max(steps, -(-200 // nb))
+        n = max(steps, -(-(600 if nb == 1 else 200) // nb))
         for _ in range(warm):
             fn(nb)
         torch.cuda.synchronize()

@@ -223,7 +223,7 @@ class ForwardGraphCache:
     def _weights(self, g):
         if self.tensors is None:
             self.tensors = list(g.parameters()) + list(g.buffers())
-        return tuple((t.data_ptr(), t._version) for t in self.tensors)
+        return [(t.data_ptr(), t._version) for t in self.tensors]
 
     def call_key(self, g, z, cam_poses, focals, near, far, kw):
         tl = kw["truncation_latent"]

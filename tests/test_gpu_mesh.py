@@ -14,8 +14,10 @@ from tests.golden import weights as W
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-TOL = {"thumb": (2e-6, 5e-7), "sdf": (5e-6, 1e-6), "xyz": (5e-7, 6e-8), "mask": (2e-6, 5e-7),
-       "aligned": (5e-6, 1e-6)}
+# ~3x the largest error measured over the cases (profiles/round6_parity.json,
+# "parity_mesh"), or tighter where the earlier bound already was
+TOL = {"thumb": (2e-6, 5e-7), "sdf": (2.5e-6, 4.7e-7), "xyz": (5e-7, 6e-8), "mask": (2e-6, 5e-7),
+       "aligned": (2.2e-6, 2.5e-7)}
 
 
 def surface_generator(sdfr, res, n_samples, precision):
