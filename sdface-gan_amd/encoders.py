@@ -18,70 +18,48 @@ import torch
 import torch.nn as nn
 from torch.autograd import Function
 
-from . import _lib
+from . import ops  # noqa: F401  (registers torch.ops.sdfr.*)
 from .linear import _edge, _wanted
 
 _gridtype_to_id = {"hash": 0, "tiled": 1}
 _interp_to_id = {"linear": 0, "smoothstep": 1}
 
 
-def _check_cuda(t: torch.Tensor, name: str):
-    if not t.is_cuda:
-        raise RuntimeError(f"{name} must be a CUDA tensor")
-
-
 class _GridEncode(Function):
+    """grid.py:27-93 over torch.ops.sdfr.grid_encode_forward / _backward (ops.py)."""
     @staticmethod
     def forward(ctx, inputs, embeddings, offsets, per_level_scale, base_resolution,
                 calc_grad_inputs=False, gridtype=0, align_corners=False, interpolation=0):
         inputs = inputs.contiguous()
-        for t, n in ((inputs, "inputs"), (embeddings, "embeddings"), (offsets, "offsets")):
-            _check_cuda(t, n)
-        if inputs.dtype != torch.float32 or embeddings.dtype != torch.float32:
-            raise RuntimeError("sdface-gan_amd GridEncoder computes in fp32 (inputs and embeddings)")
-        if offsets.dtype != torch.int32:
-            raise RuntimeError("offsets must be an int tensor")
-        B, D = inputs.shape
+        B = inputs.shape[0]
         L = offsets.shape[0] - 1
         C = embeddings.shape[1]
         S = float(np.log2(per_level_scale))
         H = int(base_resolution)
-        outputs = torch.empty(L, B, C, device=inputs.device, dtype=embeddings.dtype)
-        dy_dx = (torch.empty(B, L * D * C, device=inputs.device, dtype=embeddings.dtype)
-                 if calc_grad_inputs else None)
-        _lib.check(_lib.lib().sdfr_grid_encode_forward(
-            _lib.ptr(inputs), _lib.ptr(embeddings.contiguous()), _lib.ptr(offsets.contiguous()),
-            _lib.ptr(outputs), B, D, C, L, S, H, _lib.ptr(dy_dx), gridtype, int(align_corners),
-            interpolation, _lib.stream_of(inputs)), "sdfr_grid_encode_forward")
+        outputs, dy_dx = torch.ops.sdfr.grid_encode_forward(
+            inputs, embeddings, offsets, S, H, bool(calc_grad_inputs), int(gridtype),
+            bool(align_corners), int(interpolation))
         outputs = outputs.permute(1, 0, 2).reshape(B, L * C)
         ctx.save_for_backward(inputs, embeddings, offsets, dy_dx)
-        ctx.dims = (B, D, C, L, S, H, gridtype, interpolation, bool(align_corners))
+        ctx.dims = (B, C, L, S, H, gridtype, interpolation, bool(align_corners))
         ctx.table_edge = _edge(embeddings)
         return outputs
 
     @staticmethod
     def backward(ctx, grad):
         inputs, embeddings, offsets, dy_dx = ctx.saved_tensors
-        B, D, C, L, S, H, gridtype, interpolation, align_corners = ctx.dims
+        B, C, L, S, H, gridtype, interpolation, align_corners = ctx.dims
         grad = grad.view(B, L, C).permute(1, 0, 2).contiguous()
-        grad_inputs = torch.zeros_like(inputs, dtype=embeddings.dtype) if dy_dx is not None else None
+        with_inputs = dy_dx.numel() > 0
         # a backward pass that does not use the table gradient (the eikonal term's
         # autograd.grad, which returns the points' gradient only; linear._wanted, scoped to
-        # that graph task) would discard it: skip it
-        skip = grad_inputs is not None and not _wanted(ctx.needs_input_grad[1], ctx.table_edge)
-        grad_embeddings = None if skip else torch.zeros_like(embeddings)
-        # binned table gradient (csrc/encoders.hip) in a workspace from torch's allocator
-        L_ = _lib.lib()
-        wsb = 0 if skip else L_.sdfr_grid_encode_backward_ws_bytes(B, D, C, L, S, H,
-                                                                   int(align_corners))
-        ws = torch.empty(wsb, dtype=torch.uint8, device=grad.device) if wsb else None
-        _lib.check(L_.sdfr_grid_encode_backward_ws(
-            _lib.ptr(grad), _lib.ptr(inputs), _lib.ptr(embeddings), _lib.ptr(offsets),
-            _lib.ptr(grad_embeddings), B, D, C, L, S, H, _lib.ptr(dy_dx), _lib.ptr(grad_inputs),
-            gridtype, int(align_corners), interpolation, _lib.ptr(ws), wsb, _lib.stream_of(grad)),
-            "sdfr_grid_encode_backward")
-        if grad_inputs is not None:
-            grad_inputs = grad_inputs.to(inputs.dtype)
+        # that graph task) would discard it: skip it (binned table gradient, csrc/encoders.hip)
+        want_table = not with_inputs or _wanted(ctx.needs_input_grad[1], ctx.table_edge)
+        grad_embeddings, grad_inputs = torch.ops.sdfr.grid_encode_backward(
+            grad, inputs, embeddings, offsets, dy_dx, S, H, want_table, int(gridtype),
+            bool(align_corners), int(interpolation))
+        grad_embeddings = grad_embeddings if want_table else None
+        grad_inputs = grad_inputs.to(inputs.dtype) if with_inputs else None
         return grad_inputs, grad_embeddings, None, None, None, None, None, None, None
 
 
@@ -159,33 +137,22 @@ class GridEncoder(nn.Module):
 
 
 class _SHEncode(Function):
+    """sphere_harmonics.py:14-37 over torch.ops.sdfr.sh_encode_forward / _backward."""
     @staticmethod
     def forward(ctx, inputs, degree, calc_grad_inputs=False):
         inputs = inputs.contiguous().float()
-        _check_cuda(inputs, "inputs")
-        B, input_dim = inputs.shape
-        outputs = torch.empty(B, degree ** 2, dtype=inputs.dtype, device=inputs.device)
-        dy_dx = (torch.empty(B, input_dim * degree ** 2, dtype=inputs.dtype, device=inputs.device)
-                 if calc_grad_inputs else None)
-        _lib.check(_lib.lib().sdfr_sh_encode_forward(
-            _lib.ptr(inputs), _lib.ptr(outputs), B, input_dim, degree, _lib.ptr(dy_dx),
-            _lib.stream_of(inputs)), "sdfr_sh_encode_forward")
+        outputs, dy_dx = torch.ops.sdfr.sh_encode_forward(inputs, int(degree),
+                                                          bool(calc_grad_inputs))
         ctx.save_for_backward(inputs, dy_dx)
-        ctx.dims = (B, input_dim, degree)
+        ctx.degree = degree
         return outputs
 
     @staticmethod
     def backward(ctx, grad):
         inputs, dy_dx = ctx.saved_tensors
-        if dy_dx is None:
+        if dy_dx.numel() == 0:
             return None, None, None
-        grad = grad.contiguous()
-        B, input_dim, degree = ctx.dims
-        grad_inputs = torch.zeros_like(inputs)
-        _lib.check(_lib.lib().sdfr_sh_encode_backward(
-            _lib.ptr(grad), _lib.ptr(inputs), B, input_dim, degree, _lib.ptr(dy_dx),
-            _lib.ptr(grad_inputs), _lib.stream_of(grad)), "sdfr_sh_encode_backward")
-        return grad_inputs, None, None
+        return torch.ops.sdfr.sh_encode_backward(grad, inputs, dy_dx, int(ctx.degree)), None, None
 
 
 sh_encode = _SHEncode.apply

@@ -26,7 +26,7 @@ import torch.autograd as autograd
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import _lib
+from . import _lib, ops
 from .encoders import GridEncoder, SHEncoder
 from .linear import film_linear, linear
 
@@ -515,66 +515,41 @@ class VolumeFeatureRenderer(nn.Module):
             return False
         return True
 
-    def _ngp_weight_struct(self):
+    def _weight_tensors(self, kind):
+        """The network's tensors in the order of ops.weights_struct / sdfr::render_fused
+        (ngp: table, offsets, input_linear; FC: x_in, style_in, pts, views; ngp / SIREN:
+        w, b, gamma w, b, beta w, b of every FiLM layer and views_linears; then the sigma
+        and rgb heads and sigmoid_beta -- a placeholder without an SDF)."""
         net = self.network
-        P = lambda t: _lib.ptr(t)  # noqa: E731
-        w = _lib.NgpWeights()
-        w.embeddings = P(net.encoder.embeddings)
-        w.offsets = P(net.encoder.offsets)
-        w.num_levels = net.encoder.num_levels
-        w.log2_per_level_scale = float(np.log2(net.encoder.per_level_scale))
-        w.base_resolution = net.encoder.base_resolution
-        w.bound = float(net.bound)
-        w.input_w, w.input_b = P(net.input_linear.weight), P(net.input_linear.bias)
-        for l, layer in enumerate(net.pts_linears):
-            w.pts_w[l], w.pts_b[l] = P(layer.weight), P(layer.bias)
-            w.pts_gw[l], w.pts_gb[l] = P(layer.gamma.weight), P(layer.gamma.bias)
-            w.pts_bw[l], w.pts_bb[l] = P(layer.beta.weight), P(layer.beta.bias)
-        v = net.views_linears
-        w.views_w, w.views_b = P(v.weight), P(v.bias)
-        w.views_gw, w.views_gb = P(v.gamma.weight), P(v.gamma.bias)
-        w.views_bw, w.views_bb = P(v.beta.weight), P(v.beta.bias)
-        w.sigma_w, w.sigma_b = P(net.sigma_linear.weight), P(net.sigma_linear.bias)
-        w.rgb_w, w.rgb_b = P(net.rgb_linear.weight), P(net.rgb_linear.bias)
-        w.sigmoid_beta = P(self.sigmoid_beta) if self.with_sdf else None
-        return w
+        if kind == 0:
+            ts = [net.encoder.embeddings, net.encoder.offsets, net.input_linear.weight,
+                  net.input_linear.bias]
+        elif kind == 2:
+            ts = [net.x_in.weight, net.x_in.bias, net.style_in.weight, net.style_in.bias]
+            for layer in net.pts_linears:
+                ts += [layer.weight, layer.bias]
+            ts += [net.views_linears.weight, net.views_linears.bias]
+        else:
+            ts = []
+        if kind != 2:
+            for layer in list(net.pts_linears) + [net.views_linears]:
+                ts += [layer.weight, layer.bias, layer.gamma.weight, layer.gamma.bias,
+                       layer.beta.weight, layer.beta.bias]
+        ts += [net.sigma_linear.weight, net.sigma_linear.bias, net.rgb_linear.weight,
+               net.rgb_linear.bias, self.sigmoid_beta if self.with_sdf else net.rgb_linear.bias]
+        return ts
 
-    def _siren_weight_struct(self):
+    def _weight_scalars(self, kind):
+        """(fscal, iscal) of ops.weights_struct."""
         net = self.network
-        P = lambda t: _lib.ptr(t)  # noqa: E731
-        w = _lib.SirenWeights()
-        w.depth, w.width = net.D, net.W
-        for l, layer in enumerate(net.pts_linears):
-            w.pts_w[l], w.pts_b[l] = P(layer.weight), P(layer.bias)
-            w.pts_gw[l], w.pts_gb[l] = P(layer.gamma.weight), P(layer.gamma.bias)
-            w.pts_bw[l], w.pts_bb[l] = P(layer.beta.weight), P(layer.beta.bias)
-        v = net.views_linears
-        w.views_w, w.views_b = P(v.weight), P(v.bias)
-        w.views_gw, w.views_gb = P(v.gamma.weight), P(v.gamma.bias)
-        w.views_bw, w.views_bb = P(v.beta.weight), P(v.beta.bias)
-        w.sigma_w, w.sigma_b = P(net.sigma_linear.weight), P(net.sigma_linear.bias)
-        w.rgb_w, w.rgb_b = P(net.rgb_linear.weight), P(net.rgb_linear.bias)
-        w.sigmoid_beta = P(self.sigmoid_beta) if self.with_sdf else None
-        return w
-
-    def _fc_weight_struct(self):
-        net = self.network
-        P = lambda t: _lib.ptr(t)  # noqa: E731
-        w = _lib.FcWeights()
-        w.depth, w.width = net.D, net.W
-        w.x_in_w, w.x_in_b = P(net.x_in.weight), P(net.x_in.bias)
-        w.style_w, w.style_b = P(net.style_in.weight), P(net.style_in.bias)
-        for l, layer in enumerate(net.pts_linears):
-            w.pts_w[l], w.pts_b[l] = P(layer.weight), P(layer.bias)
-        w.views_w, w.views_b = P(net.views_linears.weight), P(net.views_linears.bias)
-        w.sigma_w, w.sigma_b = P(net.sigma_linear.weight), P(net.sigma_linear.bias)
-        w.rgb_w, w.rgb_b = P(net.rgb_linear.weight), P(net.rgb_linear.bias)
-        w.sigmoid_beta = P(self.sigmoid_beta) if self.with_sdf else None
-        return w
+        if kind == 0:
+            return ([float(np.log2(net.encoder.per_level_scale)), float(net.bound)],
+                    [int(net.encoder.base_resolution)])
+        return [], [int(net.D), int(net.W)]
 
     def _weight_struct(self, kind):
-        return (self._ngp_weight_struct, self._siren_weight_struct,
-                self._fc_weight_struct)[kind]()
+        fs, is_ = self._weight_scalars(kind)
+        return ops.weights_struct(kind, self._weight_tensors(kind), fs, is_, self.with_sdf)
 
     def _fused_check_params(self):
         net = self.network
@@ -630,11 +605,41 @@ class VolumeFeatureRenderer(nn.Module):
         noise = None
         if not self.with_sdf and self.raw_noise_std > 0:
             noise = torch.randn(B, H, W, N, device=dev) * self.raw_noise_std
-        rgb = torch.empty(B, 3, H, W, device=dev)
         kind = self._net_kind()
         if feat_mod is not None and (kind == 1 or self.field_precision != "f16x3"
                                      or not self.output_features):
             feat_mod = None                      # SIREN / fp32 field: NCHW features
+        if self.field_precision not in ("f16x3", "fp32"):
+            raise ValueError(f"field_precision must be 'f16x3' or 'fp32', "
+                             f"got {self.field_precision!r}")
+        if kind and encode_only:
+            raise RuntimeError("only the ngp renderer has a hash-grid encode stage")
+        pix_x = self.i[0, 0, :].contiguous()
+        pix_y = self.j[0, :, 0].contiguous()
+        t_vals = self.t_vals.reshape(-1).contiguous()
+        flags = dict(
+            t_rand_per_sample=per_sample, offset_sampling=int(self.offset_sampling),
+            static_viewdirs=int(bool(self.static_viewdirs)), z_normalize=int(self.z_normalize),
+            force_background=int(bool(self.force_background)), with_sdf=int(self.with_sdf),
+            field_precision=(_lib.FIELD_FP32 if self.field_precision == "fp32"
+                             else _lib.FIELD_F16X3),
+            max_field_segments=int(self.max_field_segments),
+            output_features=int(bool(self.output_features)),
+            return_sdf=int(bool(self.return_sdf)), return_xyz=int(bool(self.return_xyz)))
+        prepacked = self._prepacked(kind, cam) if self.field_precision == "f16x3" else None
+        if (styles_event is None and feat_mod is None and not encode_only
+                and self.stage_events is None and self.field_event is None):
+            # the plain call: the registered op (ops.py), outputs allocated there
+            fs, is_ = self._weight_scalars(kind)
+            out = torch.ops.sdfr.render_fused(
+                kind, self._weight_tensors(kind), cam, focal, near, far, styles, t_rand, noise,
+                pix_x, pix_y, t_vals, prepacked, fs, is_, [flags[k] for k in ops.RENDER_FLAGS],
+                H, W, N)
+            rgb, features, sdf, mask, xyz = (None if t.numel() == 0 else t for t in out)
+            return rgb, features, sdf, mask, xyz, None
+        # with events (stage timing, the styles hand-off of Generator.forward), the
+        # decoder-layout feature store or the encode stage alone: the library directly
+        rgb = torch.empty(B, 3, H, W, device=dev)
         features = (torch.empty(B, 256, H, W, device=dev)
                     if self.output_features and feat_mod is None else None)
         feat_split = (torch.empty(B, H, W, 32, 2, 8, device=dev, dtype=torch.float16)
@@ -642,40 +647,11 @@ class VolumeFeatureRenderer(nn.Module):
         sdf = torch.empty(B, H, W, N, 1, device=dev) if self.return_sdf else None
         xyz = torch.empty(B, 3, H, W, device=dev) if self.return_xyz else None
         mask = torch.empty(B, 1, H, W, device=dev) if self.return_xyz else None
-        siren = kind == 1
-        if kind == 2:
-            ws_bytes = _lib.lib().sdfr_render_fc_workspace_bytes(B, H, W, N)
-        elif siren:
-            ws_bytes = _lib.lib().sdfr_render_siren_workspace_bytes(B)
-        else:
-            L = self.network.encoder.num_levels
-            ws_bytes = _lib.lib().sdfr_render_ngp_workspace_bytes(B, H, W, N, L)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        pix_x = self.i[0, 0, :].contiguous()
-        pix_y = self.j[0, :, 0].contiguous()
-        t_vals = self.t_vals.reshape(-1).contiguous()
-
-        a = _lib.NgpRenderArgs()
-        a.B, a.H, a.W, a.N = B, H, W, N
-        a.cam, a.focal, a.near_, a.far_ = (_lib.ptr(cam), _lib.ptr(focal), _lib.ptr(near),
-                                           _lib.ptr(far))
-        a.styles = _lib.ptr(styles)
-        a.pix_x, a.pix_y, a.t_vals = _lib.ptr(pix_x), _lib.ptr(pix_y), _lib.ptr(t_vals)
-        a.t_rand, a.sigma_noise = _lib.ptr(t_rand), _lib.ptr(noise)
-        a.t_rand_per_sample = per_sample
-        a.offset_sampling = int(self.offset_sampling)
-        a.static_viewdirs = int(bool(self.static_viewdirs))
-        a.z_normalize = int(self.z_normalize)
-        a.force_background = int(bool(self.force_background))
-        a.with_sdf = int(self.with_sdf)
-        a.rgb, a.features, a.sdf = _lib.ptr(rgb), _lib.ptr(features), _lib.ptr(sdf)
-        a.xyz, a.mask = _lib.ptr(xyz), _lib.ptr(mask)
-        a.workspace, a.workspace_bytes = _lib.ptr(ws), ws_bytes
-        if self.field_precision not in ("f16x3", "fp32"):
-            raise ValueError(f"field_precision must be 'f16x3' or 'fp32', "
-                             f"got {self.field_precision!r}")
-        a.field_precision = _lib.FIELD_FP32 if self.field_precision == "fp32" else _lib.FIELD_F16X3
-        a.max_field_segments = int(self.max_field_segments)
+        num_levels = self.network.encoder.num_levels if kind == 0 else 0
+        ws = torch.empty(ops.workspace_bytes(kind, B, H, W, N, num_levels), dtype=torch.uint8,
+                         device=dev)
+        a = ops.render_args(B, H, W, N, cam, focal, near, far, styles, pix_x, pix_y, t_vals,
+                            t_rand, noise, flags, rgb, features, sdf, xyz, mask, ws, prepacked)
         if self.stage_events is not None:
             for k, ev in enumerate(self.stage_events):
                 a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)
@@ -687,23 +663,14 @@ class VolumeFeatureRenderer(nn.Module):
             feat_mod = feat_mod.detach().float().contiguous()
             a.features_split, a.features_mod = _lib.ptr(feat_split), _lib.ptr(feat_mod)
             features = feat_split
-        if self.field_precision == "f16x3":
-            a.prepacked = _lib.ptr(self._prepacked(kind, cam))
-        if kind:
-            if encode_only:
-                raise RuntimeError("only the ngp renderer has a hash-grid encode stage")
-            w = self._weight_struct(kind)
-            name = "sdfr_render_siren_forward" if siren else "sdfr_render_fc_forward"
-            _lib.check(getattr(_lib.lib(), name)(ctypes.byref(w), ctypes.byref(a),
-                                                 _lib.stream_of(cam)), name)
-            return rgb, features, sdf, mask, xyz, None
-        w = self._ngp_weight_struct()
-        fn = (_lib.lib().sdfr_render_ngp_encode_only if encode_only
-              else _lib.lib().sdfr_render_ngp_forward)
-        _lib.check(fn(ctypes.byref(w), ctypes.byref(a), _lib.stream_of(cam)),
-                   "sdfr_render_ngp_forward")
+        w = self._weight_struct(kind)
         if encode_only:
+            _lib.check(_lib.lib().sdfr_render_ngp_encode_only(
+                ctypes.byref(w), ctypes.byref(a), _lib.stream_of(cam)), "sdfr_render_ngp_encode_only")
             return ws
+        name = ops.FORWARD_FN[kind]
+        _lib.check(getattr(_lib.lib(), name)(ctypes.byref(w), ctypes.byref(a), _lib.stream_of(cam)),
+                   name)
         return rgb, features, sdf, mask, xyz, None
 
     def _prepacked(self, kind, like):
