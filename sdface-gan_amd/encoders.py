@@ -55,9 +55,12 @@ class _GridEncode(Function):
         # autograd.grad, which returns the points' gradient only; linear._wanted, scoped to
         # that graph task) would discard it: skip it (binned table gradient, csrc/encoders.hip)
         want_table = not with_inputs or _wanted(ctx.needs_input_grad[1], ctx.table_edge)
-        grad_embeddings, grad_inputs = torch.ops.sdfr.grid_encode_backward(
-            grad, inputs, embeddings, offsets, dy_dx, S, H, want_table, int(gridtype),
-            bool(align_corners), int(interpolation))
+        # outside autograd, as the reference's backward (grid.py:65-89): under create_graph
+        # (the eikonal term) its results are constants, not nodes of the double backward
+        with torch.no_grad():
+            grad_embeddings, grad_inputs = torch.ops.sdfr.grid_encode_backward(
+                grad, inputs, embeddings, offsets, dy_dx, S, H, want_table, int(gridtype),
+                bool(align_corners), int(interpolation))
         grad_embeddings = grad_embeddings if want_table else None
         grad_inputs = grad_inputs.to(inputs.dtype) if with_inputs else None
         return grad_inputs, grad_embeddings, None, None, None, None, None, None, None
@@ -152,7 +155,9 @@ class _SHEncode(Function):
         inputs, dy_dx = ctx.saved_tensors
         if dy_dx.numel() == 0:
             return None, None, None
-        return torch.ops.sdfr.sh_encode_backward(grad, inputs, dy_dx, int(ctx.degree)), None, None
+        with torch.no_grad():                   # (as _GridEncode.backward)
+            gi = torch.ops.sdfr.sh_encode_backward(grad, inputs, dy_dx, int(ctx.degree))
+        return gi, None, None
 
 
 sh_encode = _SHEncode.apply

@@ -30,6 +30,7 @@ An absent optional output is a 0-element tensor (a custom op returns tensors onl
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -275,7 +276,6 @@ def render_fused(kind: int, params: List[Tensor], cam: Tensor, focal: Tensor, ne
     a = render_args(B, H, W, N, cam, focal, near, far, styles, pix_x, pix_y, t_vals, t_rand,
                     sigma_noise, f, rgb, _none_if_empty(features), _none_if_empty(sdf),
                     _none_if_empty(xyz), _none_if_empty(mask), ws, prepacked)
-    import ctypes
     name = FORWARD_FN[kind]
     _lib.check(getattr(_lib.lib(), name)(ctypes.byref(w), ctypes.byref(a), _lib.stream_of(cam)),
                name)

@@ -61,7 +61,11 @@ def test_grid_encoder_module_through_op(sdfr, grid):
     ge, gi = torch.ops.sdfr.grid_encode_backward(
         g.view(-1, 16, 2).permute(1, 0, 2).contiguous(), ((xi.detach() * 2 - 1) + 1) / 2,
         enc.embeddings.detach(), enc.offsets, dydx, S, 16, True, 0, False, 0)
-    assert torch.equal(enc.embeddings.grad, ge)
+    # (the table gradient is a sum over samples in hardware atomic order, as the
+    # reference's atomicAdd: equal up to fp32 reassociation)
+    err = (enc.embeddings.grad - ge).abs().max() / ge.abs().max()
+    assert err <= 1e-5, err
+    assert torch.equal(xi.grad, gi)     # d/dxi of (2 xi - 1 + 1) / 2 is exactly 1
 
 
 def test_opcheck_sh_encode(sdfr):
