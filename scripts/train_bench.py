@@ -88,6 +88,17 @@ def main():
     tr.generator_test.renderer.rng_device = "device"
     torch.manual_seed(1000 + rank)
     real = [torch.rand(a.batch, 3, size, size, device=dev) * 2 - 1 for _ in range(4)]
+    if a.miopen_find and rank == 0:
+        # MIOpen's find can run for minutes inside one warmup step without a line of
+        # output: a heartbeat keeps the run visibly alive (gpurun kills silent runs)
+        import threading
+        t_start = time.perf_counter()
+
+        def beat():
+            while True:
+                time.sleep(30)
+                print(f"  ... {time.perf_counter() - t_start:.0f} s", flush=True)
+        threading.Thread(target=beat, daemon=True).start()
     for k in range(a.warmup):
         t0 = time.perf_counter()
         tr.step(real[k % 4])

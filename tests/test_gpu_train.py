@@ -180,7 +180,7 @@ def _beta_term_sum():
     sdf_model.py:227-229): the scale of the reordering error of that scalar's sum."""
     from sdface_gan_amd.renderer import VolumeFeatureRenderer as VR
     orig = VR.sdf_activation
-    acc = {"abs": 0.0}
+    acc = {"abs": 0.0, "n": 0}
 
     def sdf_activation(self, input):
         out = orig(self, input)
@@ -191,6 +191,7 @@ def _beta_term_sum():
 
             def hook(g):
                 acc["abs"] += float((g * dsdb).abs().sum(dtype=torch.float64))
+                acc["n"] += g.numel()
             out.register_hook(hook)
         return out
     VR.sdf_activation = sdf_activation
@@ -246,7 +247,7 @@ def test_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path, ngp):
     runs = []
     try:
         for _ in range(2):                 # twice: the single process's own run-to-run spread
-            beta_terms["abs"] = 0.0
+            beta_terms["abs"], beta_terms["n"] = 0.0, 0
             tr = RendererTrainer(opt, DEV, seed=5)
             runs.append(_ngp_grads(tr, noise, cams, real, chunks))
     finally:
@@ -277,15 +278,20 @@ def test_stage1_ddp_gradients_equal_single_process(sdfr, tmp_path, ngp):
                 want = ref[k] * scale
                 # fp32 sums in a different order (atomics / binned table gradient,
                 # the all-reduce): relative to the tensor's largest entry; for
-                # renderer.sigmoid_beta -- one cancelling sum over every sample, |g| ~ 3e-7
-                # against sum |t_i| ~ 1e-3 -- a recursive-summation bound on that sum,
-                # 64 u sum |t_i| (u = 2^-24), from the terms measured in this run
+                # renderer.sigmoid_beta -- one cancelling sum of n = 8192 terms t_i,
+                # |g| ~ 3e-7 against sum |t_i| ~ 3e-5 -- a reordered-sum bound
+                # c sqrt(n) u sum |t_i| (u = 2^-24) from the terms measured in this run;
+                # c = 16: the world-2 value landed up to ~9.4 sqrt(n) u sum |t_i| from the
+                # single process's over round 6's runs (the single process is bit-stable,
+                # profiles/round6_beta_grad_ab.txt)
                 tol = 2e-5 * float(want.abs().max())
                 if k == "renderer.sigmoid_beta":
-                    tol = max(tol, 64 * 2.0 ** -24 * beta_terms["abs"] * scale)
+                    tol = max(tol, 16 * beta_terms["n"] ** 0.5 * 2.0 ** -24
+                              * beta_terms["abs"] * scale)
                 assert torch.allclose(v, want, rtol=2e-4, atol=tol), \
                     (f"{what} {k}: max |diff| {float((v - want).abs().max()):.3e} "
-                     f"(max |ref| {float(want.abs().max()):.3e})")
+                     f"(max |ref| {float(want.abs().max()):.3e}, tol {tol:.3e}, "
+                     f"beta terms {beta_terms})")
         if not ngp:
             continue
         # the hashed levels (5-15) carry most of the table's gradient rows
