@@ -15,8 +15,8 @@
 #   trace | trace_b1          rocprofv3 --kernel-trace --stats of bench_quick / bench_b1
 #   counters                  SQ counter passes: field kernels (ngp, fc, siren), decoder convs
 #   traffic                   FETCH_SIZE / WRITE_SIZE passes over bench (one pass each)
-#   train1 | train2 | train2find   scripts/train_bench.py (stage 1 ngp / stage 2 /
-#                             stage 2 with MIOpen find)
+#   train1 | train2 | train2find | train2fast   scripts/train_bench.py (stage 1 ngp /
+#                             stage 2 / stage 2 with MIOpen find / the same in FAST find mode)
 #   prof2 | prof2find         scripts/train_prof.py --stage 2 (torch.profiler breakdown)
 #   ddp                       scripts/ddp_cost.py (RCCL world-1 DDP cost)
 #   mesh                      scripts/bench_mesh.py
@@ -81,6 +81,8 @@ for task in "$@"; do
     train1) step train1 400 python scripts/train_bench.py --stage 1 --net ngp ;;
     train2) step train2 400 python scripts/train_bench.py --stage 2 ;;
     train2find) step train2find 600 python scripts/train_bench.py --stage 2 --miopen-find ;;
+    train2fast) MIOPEN_FIND_MODE=2 step train2fast 600 python scripts/train_bench.py --stage 2 \
+               --miopen-find ;;
     prof2) step prof2 400 python scripts/train_prof.py --stage 2 --steps 4 --out "$O/prof2.txt" ;;
     prof2find) step prof2find 600 python scripts/train_prof.py --stage 2 --steps 4 --miopen-find \
                --out "$O/prof2find.txt" ;;

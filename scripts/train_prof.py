@@ -60,7 +60,10 @@ def main():
             for ev in sorted(ranges, key=lambda e: e.key):
                 f.write(f"{ev.key:24s} {ev.cpu_time_total / 1e3 / a.steps:9.2f} "
                         f"{ev.device_time_total / 1e3 / a.steps:9.2f}  x{ev.count / a.steps:.2f}\n")
-        tot = sum(ev.self_device_time_total for ev in prof.key_averages()) / 1e3 / a.steps
+        # (the record_function ranges carry their whole span as self device time: left out)
+        names = {ev.key for ev in ranges} if ranges else set()
+        tot = sum(ev.self_device_time_total for ev in prof.key_averages()
+                  if ev.key not in names) / 1e3 / a.steps
         f.write(f"# device time, all kernels: {tot:.2f} ms per step\n\n")
         f.write(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=70,
                                           max_name_column_width=70))
