@@ -69,7 +69,7 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip the B=1/8 and host-copy measurements")
     p.add_argument("--traffic-json", default=str(REPO / "profiles" / "field_traffic.json"))
-    p.add_argument("--counters-json", default=str(REPO / "profiles" / "round5_counters.json"),
+    p.add_argument("--counters-json", default=str(REPO / "profiles" / "round6_counters.json"),
                    help="committed SQ counter summary (scripts/summarize_counters.py) quoted "
                         "as the field kernel's MFMA-busy fraction")
     return p.parse_args()
