@@ -38,6 +38,8 @@ def make_kernel(k):
     return k / k.sum()
 
 
+_EMPTY = {}                      # device -> a 0-element tensor (fused_ready's probe)
+
 class Upsample(nn.Module):
     def __init__(self, kernel, factor=2):
         super().__init__()
@@ -396,7 +398,10 @@ class Decoder(nn.Module):
         before the features exist, so that prepare_fused can run beside the renderer.)"""
         if device.type != "cuda":
             return False
-        return self._fused_ok(torch.empty(0, device=device), rgbd_in, transform)
+        probe = _EMPTY.get(device)
+        if probe is None:
+            probe = _EMPTY[device] = torch.empty(0, device=device)
+        return self._fused_ok(probe, rgbd_in, transform)
 
     def prepare_fused(self, styles, B, device, noise=None, inject_index=None, truncation=1,
                       truncation_latent=None, input_is_latent=False, randomize_noise=True):

@@ -25,6 +25,7 @@ differ, so a replay never mixes a new renderer with a stale decoder.
 """
 from __future__ import annotations
 
+import operator
 import weakref
 from collections import OrderedDict
 
@@ -145,12 +146,16 @@ class GraphedGenerator:
         return out
 
 
+_PLAIN = (bool, int, float, str, type(None))
+_VERSION = operator.attrgetter("_version")
+_DATA_PTR = torch.Tensor.data_ptr
+
+
 def _plain_config(m):
     """A module's public plain-valued attributes (flags such as rng_device,
     field_precision, use_fused, N_samples): anything that can change which kernels
     a forward enqueues or with which constants."""
-    return tuple((k, v) for k, v in m.__dict__.items()
-                 if not k.startswith("_") and isinstance(v, (bool, int, float, str, type(None))))
+    return tuple([(k, v) for k, v in m.__dict__.items() if k[0] != "_" and isinstance(v, _PLAIN)])
 
 
 def _arg_key(v):
@@ -215,15 +220,18 @@ class ForwardGraphCache:
         if torch.cuda.is_current_stream_capturing():
             return False                        # inside a caller's own capture
         z = styles[0]
-        if not r._fused_ok(cam_poses, z if kw["input_is_latent"] else
-                           z.new_empty(z.shape[0], 256), False):
+        # (the renderer's styles are the mapped latent [B, 256]: z stands in for it
+        # whenever it has that shape, without an allocation per call)
+        lat = z if kw["input_is_latent"] or (z.dim() == 2 and z.shape[1] == 256) else \
+            z.new_empty(z.shape[0], 256)
+        if not r._fused_ok(cam_poses, lat, False):
             return False
         return not g.full_pipeline or g.decoder.fused_ready(cam_poses.device)
 
     def _weights(self, g):
         if self.tensors is None:
             self.tensors = list(g.parameters()) + list(g.buffers())
-        return [(t.data_ptr(), t._version) for t in self.tensors]
+        return tuple(map(_VERSION, self.tensors)), tuple(map(_DATA_PTR, self.tensors))
 
     def call_key(self, g, z, cam_poses, focals, near, far, kw):
         tl = kw["truncation_latent"]
@@ -264,10 +272,13 @@ class ForwardGraphCache:
             self.graphs.move_to_end(key)
         graph, static, outs, shape = entry
         dev = cam_poses.device
+        dst, src = [], []
         for name, v in (("z", z), ("cam", cam_poses), ("focal", focals), ("near", near),
                         ("far", far)):
             if name in static:
-                static[name].copy_(v, non_blocking=True)
+                dst.append(static[name])
+                src.append(v)
+        torch._foreach_copy_(dst, src, non_blocking=True)   # (one launch for the five)
         if shape is not None and g.renderer.rng_device == "cpu":
             # the eager path's draw (renderer._draw_t_rand), same CPU stream position;
             # staged through pinned memory so the copy does not block the host
