@@ -111,6 +111,22 @@ def load_file(path, map_location="cpu"):
     return torch.load(path, map_location=map_location, weights_only=True)
 
 
+def merge_param_groups(state, optimizer):
+    """An optimizer state saved with one param group per parameter (the reference's
+    generator optimizer layout, config.py:206-215, and this trainer's before round 6)
+    as the single group ``optimizer`` has: parameter ids in group order, the
+    hyperparameters of the first group (identical in every group there)."""
+    groups = state["param_groups"]
+    if len(optimizer.param_groups) != 1 or len(groups) <= 1:
+        return state
+    keys = {k for g in groups for k in g if k != "params"}
+    for k in keys:
+        if any(g.get(k) != groups[0].get(k) for g in groups):
+            raise ValueError(f"g_optim: param groups differ in {k!r}; cannot merge them")
+    merged = dict(groups[0], params=[i for g in groups for i in g["params"]])
+    return {"state": state["state"], "param_groups": [merged]}
+
+
 def load_into(trainer, ckpt):
     """Restore g / d / g_ema (and the optimizers, iteration and path-length EMA when
     the file has them) into ``trainer`` (training_utils.py:220-225)."""
@@ -118,7 +134,8 @@ def load_into(trainer, ckpt):
     trainer.d_module.load_state_dict(ckpt["d"])
     trainer.generator_test.load_state_dict(ckpt["g_ema"])
     if "g_optim" in ckpt:
-        trainer.optimizer.load_state_dict(ckpt["g_optim"])
+        trainer.optimizer.load_state_dict(merge_param_groups(ckpt["g_optim"],
+                                                             trainer.optimizer))
         trainer.optimizer_d.load_state_dict(ckpt["d_optim"])
     if "iteration" in ckpt:
         trainer.iteration = int(ckpt["iteration"])

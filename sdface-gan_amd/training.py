@@ -255,9 +255,13 @@ class FullPipelineTrainer:
         t = self.t
         g_ratio = t.g_reg_every / (t.g_reg_every + 1) if t.g_reg_every > 0 else 1
         d_ratio = t.d_reg_every / (t.d_reg_every + 1)
-        self.optimizer = torch.optim.Adam([{"params": [p], "lr": t.lr * g_ratio}
-                                           for p in self.g_train],
-                                          lr=t.lr * g_ratio, betas=(0 ** g_ratio, 0.99 ** g_ratio))
+        # The reference builds one param group per decoder parameter, every one at the
+        # same lr and betas (config.py:206-215).  Adam is elementwise, so a single group
+        # gives the same update bit for bit (test_train_step.py::test_g_adam_one_group_
+        # equals_per_parameter_groups) with ~6 foreach launches per step instead of ~6
+        # per parameter.  checkpoint.load_into folds a per-group state into it.
+        self.optimizer = torch.optim.Adam(self.g_train, lr=t.lr * g_ratio,
+                                          betas=(0 ** g_ratio, 0.99 ** g_ratio))
         self.optimizer_d = torch.optim.Adam(self.discriminator.parameters(), lr=t.lr * d_ratio,
                                             betas=(0 ** d_ratio, 0.99 ** d_ratio))
         accumulate(self.generator_test, self.generator, 0)

@@ -108,6 +108,48 @@ def test_stage2_resume_ema(sdfr, tmp_path, reference_resume_ema):
         assert torch.equal(got[k], want[k]), k
 
 
+@pytest.mark.parametrize("foreach", [True, False])
+def test_g_adam_one_group_equals_per_parameter_groups(foreach):
+    """The stage-2 generator optimizer as one param group gives the reference's
+    per-parameter groups' update (config.py:206-215) bit for bit, and a state saved in
+    the per-group layout loads into it (checkpoint.merge_param_groups)."""
+    from sdface_gan_amd import checkpoint as ck
+    g = torch.Generator().manual_seed(0)
+    shapes = [(64, 32, 3, 3), (64,), (1, 3, 64, 1, 1), (512, 512), (3,)]
+    p0 = [torch.randn(s, generator=g) for s in shapes]
+    grads = [[torch.randn(s, generator=g) for s in shapes] for _ in range(4)]
+    ratio = 4 / 5
+    kw = dict(lr=2e-3 * ratio, betas=(0 ** ratio, 0.99 ** ratio), foreach=foreach)
+
+    def run(grouped, steps, params=None, opt=None):
+        ps = params or [p.clone().requires_grad_() for p in p0]
+        if opt is None:
+            opt = torch.optim.Adam([{"params": [p], "lr": kw["lr"]} for p in ps] if grouped
+                                   else ps, **kw)
+        for gs in steps:
+            for p, gr in zip(ps, gs):
+                p.grad = gr.clone()
+            opt.step()
+        return ps, opt
+
+    ref, ref_opt = run(True, grads)
+    one, _ = run(False, grads)
+    for a, b in zip(ref, one):
+        assert torch.equal(a, b)
+    # two steps in the per-group layout, saved; two more in the single group
+    half, half_opt = run(True, grads[:2])
+    ps = [p.detach().clone().requires_grad_() for p in half]
+    opt = torch.optim.Adam(ps, **kw)
+    opt.load_state_dict(ck.merge_param_groups(half_opt.state_dict(), opt))
+    run(False, grads[2:], ps, opt)
+    for a, b in zip(ref, ps):
+        assert torch.equal(a, b)
+    bad = ref_opt.state_dict()
+    bad["param_groups"][1]["lr"] = 1.0
+    with pytest.raises(ValueError, match="differ"):
+        ck.merge_param_groups(bad, opt)
+
+
 def test_load_size_matched(sdfr):
     from sdface_gan_amd import checkpoint as ck
     opt = _stage2_opt(sdfr)
