@@ -160,7 +160,25 @@ def accumulate(model1, model2, decay=0.999):
     """EMA of model2's parameters into model1 (sdf_utils.py:64-69).  The update runs
     on the parameters themselves (not ``.data``), so it bumps their version
     counters: the fused decoder's packed-weight caches and GraphedGenerator key on
-    (data_ptr, version) and must see every EMA step."""
+    (data_ptr, version) and must see every EMA step.  Two foreach launches per
+    device / dtype instead of two per parameter: the same mul-then-add per element
+    (test_gpu_train.py::test_accumulate_foreach_bit_identical pins it against the
+    per-parameter loop)."""
+    par2 = dict(model2.named_parameters())
+    p1, p2 = [], []
+    for k, p in model1.named_parameters():
+        p1.append(p)
+        p2.append(par2[k].detach())
+    if not p1:
+        return
+    torch._foreach_mul_(p1, decay)
+    torch._foreach_add_(p1, p2, alpha=1 - decay)
+
+
+@torch.no_grad()
+def accumulate_loop(model1, model2, decay=0.999):
+    """The per-parameter form of ``accumulate`` (sdf_utils.py:64-69 verbatim in
+    operations): the pin for the foreach one."""
     par1 = dict(model1.named_parameters())
     par2 = dict(model2.named_parameters())
     for k in par1.keys():

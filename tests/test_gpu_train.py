@@ -61,6 +61,45 @@ def test_stage2_full_size_step(sdfr, ngp):
                if k.startswith("decoder.") and k.endswith("weight"))
 
 
+def test_accumulate_foreach_bit_identical(sdfr):
+    """The EMA as two foreach launches == the reference's per-parameter mul_ / add_
+    (sdf_utils.py:64-69) on the GPU's kernels, and it bumps every parameter's version
+    (the decoder's weight caches key on it); the stage-2 generator Adam as one group ==
+    the reference's per-parameter groups (config.py:206-215), foreach kernels."""
+    import copy
+    from sdface_gan_amd.training import accumulate, accumulate_loop
+    opt = sdfr.vol_render_opt(ngp=True)
+    torch.manual_seed(0)
+    g = sdfr.Generator(opt.model, opt.rendering).to(DEV)
+    e1 = copy.deepcopy(g)
+    with torch.no_grad():
+        for p in g.parameters():
+            p.add_(torch.randn_like(p))
+    e2 = copy.deepcopy(e1)
+    v0 = [p._version for p in e1.parameters()]
+    for decay in (0.5 ** (32 / 10000), 0.999):
+        accumulate(e1, g, decay)
+        accumulate_loop(e2, g, decay)
+    assert all(p._version > v for p, v in zip(e1.parameters(), v0))
+    for (k, a), b in zip(e1.named_parameters(), e2.parameters()):
+        assert torch.equal(a, b), k
+    params = [p for n, p in g.named_parameters() if n.startswith("decoder.")]
+    r = 4 / 5
+    kw = dict(lr=2e-3 * r, betas=(0 ** r, 0.99 ** r))
+    pa = [p.detach().clone().requires_grad_() for p in params]
+    pb = [p.detach().clone().requires_grad_() for p in params]
+    oa = torch.optim.Adam([{"params": [p], "lr": kw["lr"]} for p in pa], **kw)
+    ob = torch.optim.Adam(pb, **kw)
+    for _ in range(3):
+        grads = [torch.randn_like(p) for p in pa]
+        for x, y, gr in zip(pa, pb, grads):
+            x.grad, y.grad = gr.clone(), gr.clone()
+        oa.step()
+        ob.step()
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("ngp", [True, False], ids=["ngp", "siren"])
 def test_stage1_step_64(sdfr, ngp):
     from sdface_gan_amd.training import RendererTrainer
