@@ -48,9 +48,22 @@
 /* ------------------------------------------------------------------ */
 /* per-level parameters (gridencoder.cu:137-139)                       */
 /* ------------------------------------------------------------------ */
+/* Sensitivity probe (tests only): exp2f's result moved by g_exp2_ulp[level]
+ * ulps, standing in for a CUDA exp2f that is off by that much (<= 2 documented).
+ * All zero by default: the correctly rounded value. */
+static int32_t g_exp2_ulp[32];
+
+void orc_set_exp2_ulp(const int32_t *off, uint32_t n) {
+    for (uint32_t i = 0; i < 32; i++) g_exp2_ulp[i] = (off && i < n) ? off[i] : 0;
+}
+
 float orc_level_scale(uint32_t level, float S, uint32_t H) {
     float ls = (float)level * S;             /* level * S in fp32         */
     float e = (float)exp2((double)ls);       /* correctly rounded exp2f   */
+    /* (an integer exponent is an exact power of two for any exp2f: not moved) */
+    int32_t k = (level < 32 && ls != floorf(ls)) ? g_exp2_ulp[level] : 0;
+    for (; k > 0; k--) e = nextafterf(e, INFINITY);
+    for (; k < 0; k++) e = nextafterf(e, 0.0f);
     return e * (float)H - 1.0f;              /* *16 exact; one rounding   */
 }
 

@@ -54,6 +54,7 @@ def lib():
         L = ctypes.CDLL(str(LIB_PATH))
         L.orc_level_scale.restype = ctypes.c_float
         L.orc_level_scale.argtypes = [_u32, ctypes.c_float, _u32]
+        L.orc_set_exp2_ulp.argtypes = [_i32p, _u32]
         L.orc_level_resolution.restype = _u32
         L.orc_level_resolution.argtypes = [ctypes.c_float]
         L.orc_grid_index.restype = _u32
@@ -111,6 +112,17 @@ def level_table(L, S, H, offsets):
         out.append((np.float32(sc), int(lb.orc_level_resolution(ctypes.c_float(sc))),
                     int(offsets[level + 1] - offsets[level])))
     return out
+
+
+def set_exp2_ulp(offsets=None):
+    """Move the oracle's per-level exp2f result by ``offsets[level]`` ulps (None: back
+    to the correctly rounded value) -- the exp2f sensitivity test's probe for a CUDA
+    exp2f that differs from the correctly rounded one (documented <= 2 ulp)."""
+    if offsets is None:
+        lib().orc_set_exp2_ulp(ctypes.cast(None, _i32p), 0)
+        return
+    off = np.ascontiguousarray(offsets, dtype=np.int32)
+    lib().orc_set_exp2_ulp(_p(off, _i32p), off.shape[0])
 
 
 def grid_index(pos_grid, hashmap_size, resolution, gridtype=0, align_corners=False, C=2):

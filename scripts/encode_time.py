@@ -1,8 +1,8 @@
-"""Hash-grid encode stage: median time per 32-face launch and an exact checksum of
-its [L][S][2] output, for each ngp_encode_kernel mode (SDFR_ENC_MODE, one
+"""Hash-grid encode stage: median time per launch (32 faces, or SDFR_ENC_B faces) and an
+exact checksum of its [L][S][2] output, for each ngp_encode_kernel mode (SDFR_ENC_MODE, one
 subprocess per mode).  Profiling aid, not a test; the checksums of all modes must
 agree (the modes change scheduling and load width, never arithmetic).
-    python scripts/encode_time.py [modes...]"""
+    [SDFR_ENC_B=<faces>] python scripts/encode_time.py [modes...]"""
 import os
 import subprocess
 import sys
@@ -15,7 +15,8 @@ import statistics, sys, torch
 sys.path.insert(0, sys.argv[1])
 from sdfr_loader import load
 sdfr = load()
-dev = "cuda:0"; B = 32
+import os
+dev = "cuda:0"; B = int(os.environ.get("SDFR_ENC_B", "32"))
 opt = sdfr.vol_render_opt()
 torch.manual_seed(0)
 g = sdfr.Generator(opt.model, opt.rendering).to(dev).eval()

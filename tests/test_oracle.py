@@ -254,3 +254,52 @@ def test_det_uniform_platform_independent():
     assert v.dtype == np.float32
     assert np.all(np.abs(v) < 1)
     np.testing.assert_array_equal(v, W.det_uniform((4,), -1.0, 1.0, 7))
+
+
+def test_exp2f_ulp_sensitivity_bounded(oracle_mod):
+    """The per-level scale exp2f(l*S)*16 - 1 (gridencoder.cu:138) is computed here with a
+    correctly rounded exp2f; nvcc's exp2f is documented to <= 2 ulp and cannot run in
+    this container.  What a 1-2 ulp different exp2f would change:
+    (a) no level's resolution, hence no dense / hashed decision or dense stride -- the
+        index structure is the same for any exp2f within 2 ulp;
+    (b) levels 0 and 15 not at all (l*S rounds to 0 and 8.0 in fp32: exact powers of 2);
+    (c) the features by at most k * ulp(e) * 16 * max(u) * (cell difference bound) per
+        level -- a bound this test checks on 20k samples over the measured u range
+        [0.23, 0.78] and reports for a table at the reference's init amplitude (1e-4)
+        and at a trained amplitude (1)."""
+    offsets, pls = oracle_mod.grid_offsets()
+    S = np.float32(np.log2(pls))
+    base = oracle_mod.level_table(16, S, 16, offsets)
+    rng = np.random.default_rng(5)
+    x = rng.uniform(0.23, 0.78, size=(20000, 3)).astype(np.float32)
+    worst = {}
+    try:
+        for amp in (1e-4, 1.0):
+            emb = rng.uniform(-amp, amp, size=(int(offsets[-1]), 2)).astype(np.float32)
+            ref, _ = oracle_mod.grid_encode_forward(x, emb, offsets, pls, 16)
+            for k in (-2, -1, 1, 2):
+                oracle_mod.set_exp2_ulp([k] * 16)
+                lt = oracle_mod.level_table(16, S, 16, offsets)
+                assert [r for _, r, _ in lt] == [r for _, r, _ in base], k
+                assert lt[0][0] == base[0][0] and lt[15][0] == base[15][0]
+                out, _ = oracle_mod.grid_encode_forward(x, emb, offsets, pls, 16)
+                oracle_mod.set_exp2_ulp(None)
+                d = np.abs(out - ref).max(axis=(1, 2))          # per level
+                assert d[0] == 0 and d[15] == 0
+                for lvl in range(1, 15):
+                    e = np.float32((base[lvl][0] + 1) / 16)
+                    # |d pos| <= |k| ulp(e) * 16 * max u (+ one ulp of pos for the fma's
+                    # rounding); |d feature| <= 3 dims * |d pos| * 2 amp (a cell's largest
+                    # corner difference), + the 8-term sum's rounding
+                    dpos = abs(k) * float(np.spacing(e)) * 16 * 0.78 + \
+                        float(np.spacing(np.float32(base[lvl][0])))
+                    bound = 3 * dpos * 2 * amp + 16 * float(np.spacing(np.float32(amp)))
+                    assert d[lvl] <= bound, (amp, k, lvl, d[lvl], bound)
+                worst[(amp, k)] = float(d.max())
+    finally:
+        oracle_mod.set_exp2_ulp(None)
+    # at the init amplitude a 2-ulp exp2f moves features by < 2e-7 absolute (the
+    # renderer's feature bound vs the reference goldens is 4e-5, test_gpu_render.py)
+    assert worst[(1e-4, 2)] < 2e-7 and worst[(1e-4, -2)] < 2e-7
+    print("exp2f ulp sensitivity (max |d feature| over levels):",
+          {f"amp={a:g} k={k:+d}": f"{v:.2e}" for (a, k), v in worst.items()})
