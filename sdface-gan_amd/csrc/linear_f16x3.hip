@@ -367,6 +367,12 @@ __global__ void __launch_bounds__(kLinThreads) lin_fwd_kernel(const LinArgs a) {
 //   per-block column sums  du y (-> dgamma[f]),  du (-> dbeta[f]),  dy (-> db)
 // Block (f, j) covers rows [f R + j rpb, ...) of face f; thread = column (N = 256).
 // ----------------------------------------------------------------------------
+// rows per thread whose loads are issued together (film_bwd / film_bwd2_kernel)
+#ifndef SDFR_FILM_ROWS
+#define SDFR_FILM_ROWS 4
+#endif
+constexpr int kFilmRows = SDFR_FILM_ROWS;
+
 __global__ void __launch_bounds__(256) film_bwd_kernel(const float *__restrict__ ds,
                                                        const float *__restrict__ y,
                                                        const float *__restrict__ gamma,
@@ -380,15 +386,15 @@ __global__ void __launch_bounds__(256) film_bwd_kernel(const float *__restrict__
     float sg = 0.0f, sb = 0.0f, sd = 0.0f;
     const size_t base = (size_t)f * rows_per_face;
     uint32_t r = r0;
-    for (; r + 4 <= r1; r += 4) {
-        float dsv[4], yv[4];
+    for (; r + kFilmRows <= r1; r += kFilmRows) {
+        float dsv[kFilmRows], yv[kFilmRows];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kFilmRows; ++k) {
             dsv[k] = ds[(base + r + k) * N + c];
             yv[k] = y[(base + r + k) * N + c];
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kFilmRows; ++k) {
             const float u = __fadd_rn(__fmul_rn(gm, yv[k]), bt);
             const float du = __fmul_rn(dsv[k], cos_hw(u));
             const float d = __fmul_rn(du, gm);
@@ -470,9 +476,8 @@ __global__ void __launch_bounds__(256) film_bwd2_kernel(
     const float gg = gdg ? gdg[fc] : 0.0f, gb = gdb ? gdb[fc] : 0.0f;
     float sg = 0.0f, sb = 0.0f;
     const size_t base = (size_t)f * rows_per_face;
-    for (uint32_t r = r0; r < r1; ++r) {
-        const size_t e = (base + r) * N + c;
-        const float dsv = ds[e], yv = y[e], gd = gdy ? gdy[e] : 0.0f;
+    // one row's arithmetic; the column sums run over the rows in order
+    auto row = [&](size_t e, float dsv, float yv, float gd) {
         const float u = __fadd_rn(__fmul_rn(gm, yv), bt);
         const float cu = cos_hw(u), su = sin_hw(u);
         const float h = __fadd_rn(__fadd_rn(__fmul_rn(gd, gm), __fmul_rn(gg, yv)), gb);
@@ -482,6 +487,25 @@ __global__ void __launch_bounds__(256) film_bwd2_kernel(
         d_y[e] = __fadd_rn(__fmul_rn(du_, gm), __fmul_rn(gg, dsc));
         sg = __fadd_rn(sg, __fadd_rn(__fmul_rn(du_, yv), __fmul_rn(gd, dsc)));
         sb = __fadd_rn(sb, du_);
+    };
+    uint32_t r = r0;
+    // kFilmRows rows' loads in flight per thread (two waves per SIMD run this kernel:
+    // one row at a time left it at ~3.0 TB/s of its 1 GB per call)
+    for (; r + kFilmRows <= r1; r += kFilmRows) {
+        float dsv[kFilmRows], yv[kFilmRows], gd[kFilmRows];
+#pragma unroll
+        for (int k = 0; k < kFilmRows; ++k) {
+            const size_t e = (base + r + k) * N + c;
+            dsv[k] = ds[e];
+            yv[k] = y[e];
+            gd[k] = gdy ? gdy[e] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < kFilmRows; ++k) row((base + r + k) * N + c, dsv[k], yv[k], gd[k]);
+    }
+    for (; r < r1; ++r) {
+        const size_t e = (base + r) * N + c;
+        row(e, ds[e], y[e], gdy ? gdy[e] : 0.0f);
     }
     float *p = part + ((size_t)f * gridDim.x + j) * 3 * N;
     p[c] = sg;
