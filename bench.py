@@ -292,23 +292,34 @@ def main():
     for _ in range(args.warmup):
         step()
 
+    # every timed step times the field kernel (the roofline kernel); the first n_full
+    # also the render, the gather and the decoder's regular convs (each event the
+    # library records costs the stream a few microseconds: the other steps carry two)
+    n_full = min(args.steps, 5)
+    n_conv = 0
+
     def set_events(k):
-        if k > 0:
+        nonlocal n_conv
+        if 0 < k <= n_full:                   # step k - 1's decoder FLOPs / launches
             conv_flops.append(g.decoder.conv_flops)
-        g.renderer.stage_events = evs[k][:4]
+            n_conv = g.decoder._conv_ev
+        full = k < n_full
+        g.renderer.stage_events = evs[k][:4] if full else [None, None, None, evs[k][3]]
         g.renderer.field_event = evs[k][4]
-        g.decoder.profile_convs(dev_evs[k])
+        g.decoder.profile_convs(dev_evs[k] if full else None)
     elapsed = timed_steps(step, args.steps, world, device, before_step=set_events)
-    conv_flops.append(g.decoder.conv_flops)
-    n_conv = g.decoder._conv_ev
+    if args.steps <= n_full:
+        conv_flops.append(g.decoder.conv_flops)
+        n_conv = g.decoder._conv_ev
     g.renderer.stage_events = None
     g.renderer.field_event = None
     g.decoder.profile_convs(None)
 
-    conv_ms = sum(a_.elapsed_time(b_) for pairs in dev_evs for a_, b_ in pairs[:n_conv]) / args.steps
-    enc_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    conv_ms = sum(a_.elapsed_time(b_) for pairs in dev_evs[:n_full]
+                  for a_, b_ in pairs[:n_conv]) / n_full
+    enc_ms = sum(e[1].elapsed_time(e[2]) for e in evs[:n_full]) / n_full
     field_ms = sum(e[4].elapsed_time(e[3]) for e in evs) / args.steps
-    render_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args.steps
+    render_ms = sum(e[0].elapsed_time(e[3]) for e in evs[:n_full]) / n_full
     samples = B * res * res * N
     f16x3 = args.field_precision == "f16x3"
     flop = (FLOP_PER_SAMPLE_FC if fc else FLOP_PER_SAMPLE_SIREN) if siren else (

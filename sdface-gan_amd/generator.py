@@ -942,8 +942,10 @@ class Generator(nn.Module):
                 cam_poses, focals, near, far, styles=lat0, return_eikonal=return_eikonal,
                 t_rand=t_rand, styles_event=styles_ev, feat_mod=feat_mod)
         if self.full_pipeline:
-            if side is not None:
-                torch.cuda.current_stream(cam_poses.device).wait_stream(side)
+            # (the side stream's work ends at styles_ev, which the renderer made this
+            # stream wait on before its FiLM prep -- every render entry does, ABI 11 --
+            # so the decoder needs no second join: one right here would sit behind the
+            # field kernel as a barrier packet, ~10 us of idle GPU per call)
             rgb, decoder_latent = self.decoder(
                 features, latent, transform=cam_poses if project_noise else None,
                 return_latents=return_latents, inject_index=inject_index, truncation=truncation,

@@ -654,7 +654,8 @@ class VolumeFeatureRenderer(nn.Module):
                             t_rand, noise, flags, rgb, features, sdf, xyz, mask, ws, prepacked)
         if self.stage_events is not None:
             for k, ev in enumerate(self.stage_events):
-                a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)
+                if ev is not None:               # (None: that point is not timed)
+                    a.stage_events[k] = ctypes.c_void_p(ev.cuda_event)
         if self.field_event is not None:
             a.field_event = ctypes.c_void_p(self.field_event.cuda_event)
         if styles_event is not None:
