@@ -46,6 +46,11 @@ def main():
     p.add_argument("--miopen-find", action="store_true",
                    help="torch.backends.cudnn.benchmark = True (MIOpen find per conv shape "
                         "during warmup instead of its heuristics)")
+    p.add_argument("--miopen-db", default=None,
+                   help="MIOpen user find / perf database directory (MIOPEN_USER_DB_PATH), "
+                        "e.g. sdface-gan_amd/miopen_db: the stage-2 convolutions' find results "
+                        "recorded on an MI355X (ROCm 7.2 image), so --miopen-find skips its "
+                        "~12 min search")
     p.add_argument("--train-gemm", default="f16x3", choices=["f16x3", "torch"],
                    help="stage 1: renderer-MLP GEMMs on the split-fp16 MFMA kernels or on "
                         "rocBLAS fp32 (linear.py)")
@@ -56,6 +61,8 @@ def main():
     p.add_argument("--no-skip-identity", action="store_true",
                    help="LinearLayer computes the literal 1 * y + 0 (A/B aid)")
     a = p.parse_args()
+    if a.miopen_db:                      # before MIOpen's first handle (the first convolution)
+        os.environ["MIOPEN_USER_DB_PATH"] = str(Path(a.miopen_db).resolve())
     torch.backends.cudnn.benchmark = a.miopen_find
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
